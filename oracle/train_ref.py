@@ -1,0 +1,102 @@
+"""Oracle: the mean-teacher + CowMix training step on torch-CPU fp32.  TEST INFRASTRUCTURE ONLY.
+
+Restates reference/train.py:41-130 (one epoch of steps) for plain torch.nn models on the CPU:
+  supervised forward + CalculateLoss (interp -> BCE * weight)         train.py:47-61, losses.py:15-22
+  teacher forwards (no_grad, eval) + interp to the image size         train.py:69-75
+  CowMix mask (oracle.cowmix_ref, RNG order of cowmix.py:44-55) + mix train.py:77-86
+  student consistency forward in eval() with grads on                 train.py:90-94
+  consistency loss + gate float(epoch > 25) + backward                train.py:97-115
+  optimizer step skipped at step 0; clip_grad_norm_ before SGD         train.py:121-124
+  EMA of parameters, buffers aliased                                  train.py:130, mean_teacher.py:5-18
+It is pinned by tests/golden trainsteps.npz (G7) and consistency_*.npz (G3).
+"""
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import cowmix_ref
+
+
+def calculate_loss(pred_list, target, weights=(0.5,)):
+    """CalculateLoss([{'loss_fn': DenseBinaryCrossEntropyLossWithLogits('mean'), 'weight': weights}])."""
+    loss = 0
+    for i, p in enumerate(pred_list):
+        p = F.interpolate(p, size=(target.size(2), target.size(3)), mode='bilinear', align_corners=False)
+        loss = loss + F.binary_cross_entropy_with_logits(p, target, reduction='mean') * weights[i]
+    return loss
+
+
+def cowmix_mask_like(example, prop_range, sigma_range):
+    B, _, H, W = example.shape
+    p, sig, noise = cowmix_ref.draw_inputs(B, H, W, prop_range, sigma_range)
+    m, *_ = cowmix_ref.cowmix_masks(noise, sig, p)
+    return torch.from_numpy(m).view(B, 1, H, W).to(example.dtype)
+
+
+def consistency_loss(student_up, teacher_mixed, thr):
+    pt = torch.sigmoid(teacher_mixed)
+    ps = torch.sigmoid(student_up)
+    cm = (pt.max(dim=1).values > thr).to(pt)
+    loss = ((ps - pt).pow(2.0).sum(dim=1) * cm).sum() / cm.sum()
+    return loss.mean(), cm.mean()
+
+
+@torch.no_grad()
+def ema_update(model, ema_model, alpha):
+    for e, p in zip(ema_model.parameters(), model.parameters()):
+        e.mul_(alpha).add_(p, alpha=1.0 - alpha)
+    for eb, b in zip(ema_model.buffers(), model.buffers()):
+        eb.data = b.data
+
+
+def train_epoch(model, ema_model, optimizer, batches, unsup_iter, epoch, cfg, loss_weights=(0.5,),
+                on_step=None):
+    """Run len(batches) steps; returns per-step dict(sup_loss, unsup_loss, cm_mean)."""
+    tc = cfg
+    model.train()
+    optimizer.zero_grad()
+    logs = []
+    for step, (image, mask) in enumerate(batches):
+        _, preds = model(image)
+        sup = calculate_loss(preds, mask, loss_weights)
+        (sup / tc['virtual_batch_size_multiplier']).backward()
+        rec = dict(sup_loss=float(sup.detach()))
+        if tc['use_semi_supervised']:
+            ua = next(unsup_iter)
+            ub = next(unsup_iter)
+            with torch.no_grad():
+                ta = F.interpolate(ema_model(ua)[-1][-1], ua.shape[2:4], mode='bilinear', align_corners=False)
+                tb = F.interpolate(ema_model(ub)[-1][-1], ua.shape[2:4], mode='bilinear', align_corners=False)
+                m = cowmix_mask_like(ua, tc['mask_proportion_range'], tc['sigma_range'])
+                t_mix = ta * m + tb * (1. - m)
+                x_mix = ua * m + ub * (1. - m)
+            model.eval()
+            s = model(x_mix)[-1][-1]
+            model.train()
+            s = F.interpolate(s, x_mix.shape[2:4], mode='bilinear', align_corners=False)
+            cons, cm_mean = consistency_loss(s, t_mix, tc['confidence_threshold'])
+            unsup = cons * tc['consistency_loss_weight'] * float(epoch > 25)
+            unsup.backward()
+            rec.update(unsup_loss=float(unsup), cm_mean=float(cm_mean))
+        if step % tc['virtual_batch_size_multiplier'] == 0 and step != 0:
+            torch.nn.utils.clip_grad_norm_(model.parameters(), tc['gradient_clip_value'])
+            optimizer.step()
+            optimizer.zero_grad()
+        if tc['use_semi_supervised']:
+            ema_update(model, ema_model, tc['ema_model_alpha'])
+        logs.append(rec)
+        if on_step is not None:
+            on_step(step, rec)
+    return logs
+
+
+def default_cfg(**over):
+    cfg = dict(virtual_batch_size_multiplier=1, use_semi_supervised=True, mask_proportion_range=(0.45, 0.55),
+               sigma_range=(8, 32), consistency_loss_weight=10, ema_model_alpha=0.99,
+               confidence_threshold=0.97, gradient_clip_value=5.0)
+    cfg.update(over)
+    return cfg
+
+
+def as_np(t):
+    return t.detach().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t)

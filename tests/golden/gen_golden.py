@@ -1,0 +1,339 @@
+"""Generate golden vectors from the reference (Luonic/semi-supervised_semantic_segmentation).
+
+RUNS ONLY IN THE BUILD CONTAINER, where the reference is mounted read-only at /root/reference.
+It imports the reference's own Python modules (with an empty `kornia` stub, which train.py imports
+but never calls: reference/train.py:5, reversible_augmentations.py) and writes small .npz
+fixtures next to this file. The fixtures are data (inputs + expected outputs); nothing from the
+reference travels with them. Tests on the GPU box read only the .npz files.
+
+Fixture index:
+  G1  cowmix_*.npz      generate_cowmix_masks_like / generate_gaussian      (reference/cowmix.py:6-69)
+  G2  mix.npz           mix_with_mask                                     (reference/cowmix.py:72-73)
+  G3  consistency_*.npz train.train one step with stub models: BCE(+interp) loss, CowMix,
+                        consistency loss value + gradients, EMA (reference/train.py:41-130)
+  G4  lovasz.npz        binary_lovasz_loss_with_logits + lovasz_grad        (reference/losses.py:239-250, lovasz.py)
+  G5  ema.npz           update_ema_variables                              (reference/mean_teacher.py:5-18)
+  G6  model_*.npz       SimpleUNet / UNet(MobileNetV2) forwards            (reference/models/*.py)
+  G7  trainsteps.npz    3 steps of train.train on a tiny SimpleUNet (DDP, gloo world 1)
+
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+"""
+import os
+import sys
+import types
+import hashlib
+
+import numpy as np
+
+REF = '/root/reference'
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+sys.dont_write_bytecode = True
+sys.path.insert(0, REF)
+sys.modules.setdefault('kornia', types.ModuleType('kornia'))
+
+import torch  # noqa: E402
+import torch.nn as nn  # noqa: E402
+
+import cowmix  # noqa: E402  (reference)
+import losses  # noqa: E402
+import lovasz  # noqa: E402
+import mean_teacher  # noqa: E402
+import train as ref_train  # noqa: E402
+from models import simple_unet, unet  # noqa: E402
+from models.encoders import mobilenetv2  # noqa: E402
+
+torch.set_num_threads(8)
+META = dict(torch_version=torch.__version__)
+
+
+def sha(t):
+    return hashlib.sha256(np.ascontiguousarray(t.detach().cpu().numpy()).tobytes()).hexdigest()
+
+
+def save(name, **arrays):
+    path = os.path.join(OUT, name)
+    out = {}
+    for k, v in arrays.items():
+        if isinstance(v, torch.Tensor):
+            v = v.detach().cpu().numpy()
+        out[k] = np.asarray(v)
+    out['torch_version'] = np.asarray(META['torch_version'])
+    np.savez_compressed(path, **out)
+    print(f'wrote {name}: {os.path.getsize(path) / 1024:.1f} KiB')
+
+
+def state_arrays(prefix, module):
+    d = {}
+    for k, v in module.state_dict().items():
+        d[prefix + k] = v.detach().clone()
+    return d
+
+
+# ----------------------------------------------------------------------------------------------
+# G1: CowMix masks
+# ----------------------------------------------------------------------------------------------
+def gen_cowmix():
+    cases = [
+        # (tag, seed, shape, mask_proportion_range, sigma_range, keep_field)
+        ('a0', 0, (4, 3, 128, 128), (0.45, 0.55), (8, 32), True),
+        ('a1', 1, (4, 3, 128, 128), (0.45, 0.55), (8, 32), False),
+        ('a2', 2, (4, 3, 128, 128), (0.45, 0.55), (8, 32), False),
+        ('b3', 3, (2, 3, 96, 80), (0.4, 0.6), (4, 16), True),
+        ('c0', 0, (2, 3, 512, 512), (0.45, 0.55), (8, 32), False),
+    ]
+    for tag, seed, shape, pr, sr, keep_field in cases:
+        example = torch.zeros(shape)
+        torch.manual_seed(seed)
+        mask = cowmix.generate_cowmix_masks_like(example, pr, sr)
+        # Replay the reference RNG order (cowmix.py:44-55): rand(B) for p, rand(B) for sigma, normal.
+        torch.manual_seed(seed)
+        B = shape[0]
+        p = torch.distributions.Uniform(torch.tensor(pr[0]), torch.tensor(pr[1])).rsample([B])
+        import math
+        sig = torch.exp(torch.distributions.Uniform(torch.tensor(math.log(float(sr[0]))),
+                                                    torch.tensor(math.log(float(sr[1])))).rsample([B]))
+        noise = torch.normal(mean=0, std=1, size=(B, 1) + tuple(shape[2:]), dtype=torch.float32)
+        field = cowmix.dual_pass_gaussian_fileter2d(noise.transpose(0, 1), sig).transpose(1, 0)
+        mean = field.mean(dim=(1, 2, 3))
+        std = field.std(dim=(1, 2, 3))
+        thr = torch.erfinv(2 * p - 1) * math.sqrt(2.0) * std + mean
+        replay = (field > thr.view(B, 1, 1, 1)).float()
+        assert torch.equal(replay, mask), 'RNG replay does not reproduce the reference mask'
+        K = int(round(sig.max().item() * 3) * 2) + 1
+        d = dict(seed=seed, shape=np.array(shape), prop_range=np.array(pr, dtype=np.float64),
+                 sigma_range=np.array(sr, dtype=np.float64), p=p, sigma=sig, K=K,
+                 noise_sha256=np.asarray(sha(noise)), mean=mean, std=std, thr=thr,
+                 mask_bits=np.packbits(mask.numpy().astype(np.uint8).reshape(-1)),
+                 # distance of every pixel to its threshold in units of std: the tie band
+                 tie_band_count=int(((field - thr.view(B, 1, 1, 1)).abs()
+                                     < 1e-5 * std.view(B, 1, 1, 1)).sum()))
+        if keep_field:
+            d['field'] = field
+            d['noise'] = noise
+        save(f'cowmix_{tag}.npz', **d)
+
+    # generate_gaussian (cowmix.py:6-11): odd and even window sizes
+    gs = {}
+    for K, s in [(7, 1.3), (8, 2.0), (49, 8.0), (193, 31.7), (97, 16.2)]:
+        gs[f'g_{K}'] = cowmix.generate_gaussian(K, torch.tensor(s))
+        gs[f'sigma_{K}'] = np.float32(s)
+    save('cowmix_gaussian.npz', **gs)
+
+
+# ----------------------------------------------------------------------------------------------
+# G2: mix_with_mask
+# ----------------------------------------------------------------------------------------------
+def gen_mix():
+    g = torch.Generator().manual_seed(11)
+    a = torch.randn(2, 3, 16, 24, generator=g)
+    b = torch.randn(2, 3, 16, 24, generator=g)
+    m = (torch.rand(2, 1, 16, 24, generator=g) > 0.5).float()
+    save('mix.npz', a=a, b=b, mask=m, out=cowmix.mix_with_mask(a, b, m))
+
+
+# ----------------------------------------------------------------------------------------------
+# helpers for driving reference train.train
+# ----------------------------------------------------------------------------------------------
+class ScalarLog:
+    def __init__(self):
+        self.rows = []
+
+    def add_scalar(self, name, value, step):
+        self.rows.append((name, float(value), int(step)))
+
+
+def ensure_pg():
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', '29533')
+        dist.init_process_group('gloo', rank=0, world_size=1)
+
+
+class StubLogits(nn.Module):
+    """A 'model' whose logits are a learnable tensor (+0*x so autograd sees the input)."""
+
+    def __init__(self, init):
+        super().__init__()
+        self.logits = nn.Parameter(init.clone())
+
+    def forward(self, x):
+        y = self.logits + 0.0 * x.sum()
+        return [y], [y]
+
+
+# ----------------------------------------------------------------------------------------------
+# G3: one train.train step with stub models -> BCE/CalculateLoss, CowMix, consistency, EMA
+# ----------------------------------------------------------------------------------------------
+def gen_consistency():
+    ensure_pg()
+    cases = [
+        # tag, seed, B, H, W, h, w, thr, epoch, logit_scale
+        ('thr05', 5, 2, 64, 64, 32, 32, 0.5, 30, 3.0),
+        ('thr097', 6, 3, 48, 40, 24, 20, 0.97, 30, 4.0),
+        ('nan', 7, 2, 32, 32, 16, 16, 0.97, 30, 0.1),   # sigmoid < 0.97 everywhere -> 0/0 = NaN
+        ('gated', 8, 2, 32, 32, 16, 16, 0.5, 10, 3.0),   # epoch <= 25 -> unsup loss * 0
+    ]
+    for tag, seed, B, H, W, h, w, thr, epoch, scale in cases:
+        g = torch.Generator().manual_seed(seed)
+        s_init = torch.randn(B, 2, h, w, generator=g) * scale
+        t_init = torch.randn(B, 2, h, w, generator=g) * scale
+        image = torch.rand(B, 3, H, W, generator=g)
+        target_fg = (torch.rand(B, 1, H, W, generator=g) > 0.6).float()
+        semantic_mask = torch.cat([1 - target_fg, target_fg], dim=1)
+        ua = torch.rand(B, 3, H, W, generator=g)
+        ub = torch.rand(B, 3, H, W, generator=g)
+        student = StubLogits(s_init)
+        teacher = StubLogits(t_init)
+        mean_teacher.detach_model_parameters(teacher)
+        teacher.eval()
+        opt = torch.optim.SGD(student.parameters(), lr=0.0)
+        cfg = {'train': dict(loss=losses.CalculateLoss([
+            {'loss_fn': losses.DenseBinaryCrossEntropyLossWithLogits(reduction='mean'), 'weight': [0.5]}]),
+            virtual_batch_size_multiplier=1, use_semi_supervised=True,
+            mask_proportion_range=(0.45, 0.55), sigma_range=(4, 8), confidence_threshold=thr,
+            consistency_loss_weight=10, ema_model_alpha=0.99, print_freq=1, gradient_clip_value=5.0)}
+        log = ScalarLog()
+        torch.manual_seed(1000 + seed)
+        ref_train.train(student, teacher, opt, [{'image': image, 'semantic_mask': semantic_mask}],
+                        iter([{'image': ua}, {'image': ub}]), epoch, 0, log, cfg, 'cpu')
+        vals = {n: v for n, v, _ in log.rows}
+        save(f'consistency_{tag}.npz', seed=seed, rng_seed=1000 + seed, thr=thr, epoch=epoch,
+             s_logits=s_init, t_logits=t_init, image=image, semantic_mask=semantic_mask, ua=ua, ub=ub,
+             sup_loss=np.float32(vals['train_classification_loss']),
+             unsup_loss=np.float32(vals['train_unsupervised_loss']),
+             grad=student.logits.grad, ema_after=teacher.logits.detach())
+
+
+# ----------------------------------------------------------------------------------------------
+# G4: Lovasz
+# ----------------------------------------------------------------------------------------------
+def gen_lovasz():
+    g = torch.Generator().manual_seed(21)
+    B, H, W = 3, 64, 64
+    logits = (torch.randn(B, 2, H, W, generator=g) * 2.0).requires_grad_(True)
+    fg = (torch.rand(B, 1, H, W, generator=g) > 0.55).float()
+    fg[1] = 0.0  # an all-background image: valid = 0 path (losses.py:247)
+    target = torch.cat([1 - fg, fg], dim=1)
+    loss = losses.binary_lovasz_loss_with_logits(logits, target)
+    loss.backward()
+    gt = torch.tensor([1, 0, 1, 1, 0, 0, 1, 0], dtype=torch.float32)
+    save('lovasz.npz', logits=logits.detach(), target=target, loss=loss.detach(), grad=logits.grad,
+         gt_sorted=gt, lovasz_grad=lovasz.lovasz_grad(gt),
+         lovasz_grad_1=lovasz.lovasz_grad(torch.tensor([1.0])))
+
+
+# ----------------------------------------------------------------------------------------------
+# G5: EMA
+# ----------------------------------------------------------------------------------------------
+def gen_ema():
+    torch.manual_seed(31)
+    student = simple_unet.UNet(2, num_blocks=2, first_channels=4, max_width=8)
+    teacher = simple_unet.UNet(2, num_blocks=2, first_channels=4, max_width=8)
+    for b in student.buffers():
+        if torch.is_floating_point(b):
+            b.uniform_(0.5, 1.5)
+    before_t = state_arrays('t.', teacher)
+    before_s = state_arrays('s.', student)
+    mean_teacher.update_ema_variables(student, teacher, alpha=0.99)
+    alias = all(eb.data_ptr() == sb.data_ptr() for eb, sb in zip(teacher.buffers(), student.buffers()))
+    assert alias
+    after = state_arrays('after.', teacher)
+    save('ema.npz', alpha=0.99, buffers_aliased=alias, **before_t, **before_s, **after)
+
+
+# ----------------------------------------------------------------------------------------------
+# G6: model forwards
+# ----------------------------------------------------------------------------------------------
+def gen_models():
+    specs = [
+        ('simple_unet_t', lambda: simple_unet.UNet(2, num_blocks=3, first_channels=8, max_width=32,
+                                                   train_upsampling=True), (2, 3, 32, 32)),
+        ('simple_unet_b', lambda: simple_unet.UNet(2, num_blocks=3, first_channels=8, max_width=32,
+                                                   train_upsampling=False), (2, 3, 36, 36)),
+        ('unet_mbv2_t', lambda: unet.UNet(2, mobilenetv2.mobilenet_v2(width_mult=0.35), 32,
+                                          train_upsampling=True), (2, 3, 64, 64)),
+        ('unet_mbv2_b', lambda: unet.UNet(2, mobilenetv2.mobilenet_v2(width_mult=0.35), 32,
+                                          train_upsampling=False), (2, 3, 64, 64)),
+    ]
+    for i, (tag, fn, shape) in enumerate(specs):
+        torch.manual_seed(41 + i)
+        m = fn()
+        # non-trivial BN affine + running stats so eval mode is a real test
+        with torch.no_grad():
+            for mod in m.modules():
+                if isinstance(mod, nn.BatchNorm2d):
+                    mod.weight.uniform_(0.5, 1.5)
+                    mod.bias.uniform_(-0.2, 0.2)
+                    mod.running_mean.uniform_(-0.1, 0.1)
+                    mod.running_var.uniform_(0.5, 2.0)
+        init = state_arrays('init.', m)
+        x = torch.rand(*shape)
+        m.eval()
+        with torch.no_grad():
+            y_eval = m(x)
+        m.train()
+        y_train = m(x)
+        # after the train-mode forward only the BN buffers change
+        after = {k: v for k, v in state_arrays('after.', m).items() if 'running' in k or 'num_batches' in k}
+        save(f'model_{tag}.npz', x=x, y_eval=y_eval, y_train=y_train.detach(), **init, **after)
+
+
+# ----------------------------------------------------------------------------------------------
+# G7: three reference train steps, tiny SimpleUNet, DDP on gloo world 1
+# ----------------------------------------------------------------------------------------------
+class ListOutput(nn.Module):
+    def __init__(self, model):
+        super().__init__()
+        self.model = model
+
+    def forward(self, x):
+        y = self.model(x)
+        return [y], [y]
+
+
+def gen_trainsteps():
+    ensure_pg()
+    torch.manual_seed(51)
+    fn = lambda: ListOutput(simple_unet.UNet(2, num_blocks=2, first_channels=4, max_width=8))  # noqa: E731
+    student = fn()
+    teacher = fn()
+    teacher.load_state_dict(student.state_dict())
+    init = state_arrays('init.', student)
+    ddp = torch.nn.parallel.DistributedDataParallel(student)
+    mean_teacher.detach_model_parameters(teacher)
+    teacher.eval()
+    opt = torch.optim.SGD(ddp.parameters(), lr=0.05, momentum=0.9, weight_decay=0.0005)
+    g = torch.Generator().manual_seed(52)
+    B, H, W, steps = 2, 32, 32, 3
+    imgs = torch.rand(steps, B, 3, H, W, generator=g)
+    fg = (torch.rand(steps, B, 1, H, W, generator=g) > 0.5).float()
+    masks = torch.cat([1 - fg, fg], dim=2)
+    unl = torch.rand(2 * steps, B, 3, H, W, generator=g)
+    cfg = {'train': dict(loss=losses.CalculateLoss([
+        {'loss_fn': losses.DenseBinaryCrossEntropyLossWithLogits(reduction='mean'), 'weight': [0.5]}]),
+        virtual_batch_size_multiplier=1, use_semi_supervised=True,
+        mask_proportion_range=(0.45, 0.55), sigma_range=(2, 4), confidence_threshold=0.5,
+        consistency_loss_weight=10, ema_model_alpha=0.99, print_freq=1, gradient_clip_value=5.0)}
+    log = ScalarLog()
+    torch.manual_seed(53)
+    ref_train.train(ddp, teacher, opt, [{'image': imgs[i], 'semantic_mask': masks[i]} for i in range(steps)],
+                    iter([{'image': unl[i]} for i in range(2 * steps)]), 30, 0, log, cfg, 'cpu')
+    sup = [v for n, v, _ in log.rows if n == 'train_classification_loss'][:steps]
+    uns = [v for n, v, _ in log.rows if n == 'train_unsupervised_loss'][:steps]
+    final_s = state_arrays('final_s.', student)
+    final_t = state_arrays('final_t.', teacher)
+    save('trainsteps.npz', imgs=imgs, masks=masks, unl=unl, rng_seed=53, lr=0.05,
+         sup_loss=np.array(sup, np.float32), unsup_loss=np.array(uns, np.float32),
+         **init, **final_s, **final_t)
+
+
+if __name__ == '__main__':
+    gen_cowmix()
+    gen_mix()
+    gen_consistency()
+    gen_lovasz()
+    gen_ema()
+    gen_models()
+    gen_trainsteps()
