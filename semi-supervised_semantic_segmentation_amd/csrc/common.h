@@ -1,0 +1,77 @@
+// Shared device helpers for the ssseg HIP kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ssseg.h"
+
+#define SSSEG_WAVE 64
+
+// Launch-error check: every extern "C" entry returns 0 or a hipError_t / SSSEG_E* code.
+#define SSSEG_LAUNCH_CHECK()                                   \
+  do {                                                         \
+    hipError_t _e = hipGetLastError();                         \
+    if (_e != hipSuccess) return (int)_e;                      \
+  } while (0)
+
+#define SSSEG_TRY(expr)                                        \
+  do {                                                         \
+    hipError_t _e = (expr);                                    \
+    if (_e != hipSuccess) return (int)_e;                      \
+  } while (0)
+
+typedef unsigned short bf16_t;   // raw bfloat16 bits
+
+__device__ __forceinline__ float bf16_to_f32(bf16_t v) {
+  return __uint_as_float(((unsigned)v) << 16);
+}
+
+// round-to-nearest-even f32 -> bf16 (NaN kept a NaN)
+__device__ __forceinline__ bf16_t f32_to_bf16(float f) {
+  unsigned u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+template <typename T> struct io;
+template <> struct io<float> {
+  __device__ __forceinline__ static float ld(const float* p, int64_t i) { return p[i]; }
+  __device__ __forceinline__ static void st(float* p, int64_t i, float v) { p[i] = v; }
+};
+template <> struct io<bf16_t> {
+  __device__ __forceinline__ static float ld(const bf16_t* p, int64_t i) { return bf16_to_f32(p[i]); }
+  __device__ __forceinline__ static void st(bf16_t* p, int64_t i, float v) { p[i] = f32_to_bf16(v); }
+};
+
+// wave64 reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// block-wide sum; `scratch` needs blockDim.x/64 entries; result valid in every thread
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  T t = 0;
+  for (int i = 0; i < nw; ++i) t += scratch[i];
+  return t;
+}
+
+static inline int ssseg_grid(int64_t n, int block, int cap = 256 * 16) {
+  int64_t g = (n + block - 1) / block;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}

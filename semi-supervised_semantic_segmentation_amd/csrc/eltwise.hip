@@ -1,0 +1,342 @@
+// HBM-bound elementwise / reduction kernels of the training step:
+//   layout + dtype conversion at the model boundary, BCE-with-logits (losses.py:41-48),
+//   consistency loss (train.py:97-108), teacher EMA (mean_teacher.py:5-18),
+//   clip_grad_norm_ + SGD momentum step (train.py:122-124, default_config.py:151-154).
+// Reductions: grid-strided partials in fp64 -> one finalize block (deterministic, no atomics).
+#include "common.h"
+
+namespace {
+
+constexpr int RED_BLOCKS = 1024;
+constexpr int RED_THREADS = 256;
+
+template <typename TI, typename TO>
+__global__ void nchw_to_nhwc_kernel(const TI* x, TO* y, int64_t C, int64_t HW, int64_t Cp, int64_t total) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = i % Cp, pix = (i / Cp) % HW, n = i / (Cp * HW);
+    const float v = c < C ? io<TI>::ld(x, (n * C + c) * HW + pix) : 0.f;
+    io<TO>::st(y, i, v);
+  }
+}
+
+template <typename TI, typename TO>
+__global__ void nhwc_to_nchw_kernel(const TI* x, TO* y, int64_t C, int64_t HW, int64_t ldc, int64_t total) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t pix = i % HW, c = (i / HW) % C, n = i / (C * HW);
+    io<TO>::st(y, i, io<TI>::ld(x, (n * HW + pix) * ldc + c));
+  }
+}
+
+template <typename TI, typename TO>
+__global__ void cast_kernel(const TI* x, TO* y, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    io<TO>::st(y, i, io<TI>::ld(x, i));
+}
+
+__device__ __forceinline__ float sigmoidf_ref(float x) { return 1.f / (1.f + expf(-x)); }
+
+// ---- BCE with logits ----
+__global__ void __launch_bounds__(RED_THREADS) bce_partial_kernel(const float* x, const float* t, int64_t n,
+                                                                  double* part) {
+  __shared__ double red[RED_THREADS / 64];
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = x[i], tt = t[i];
+    const float l = fmaxf(v, 0.f) - v * tt + log1pf(expf(-fabsf(v)));
+    acc += (double)l;
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+__global__ void __launch_bounds__(RED_THREADS) bce_final_kernel(const double* part, int nparts, int64_t n, float* out) {
+  __shared__ double red[RED_THREADS / 64];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) acc += part[i];
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) out[0] = (float)(acc / (double)n);
+}
+
+__global__ void bce_bwd_kernel(const float* x, const float* t, int64_t n, const float* gout, float* gx) {
+  const float scale = gout[0] / (float)n;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    gx[i] = (sigmoidf_ref(x[i]) - t[i]) * scale;
+}
+
+// ---- consistency loss ----
+__global__ void __launch_bounds__(RED_THREADS) cons_partial_kernel(const float* s, const float* t, int64_t C,
+                                                                   int64_t HW, int64_t npix, float thr,
+                                                                   double* part) {
+  __shared__ double red[RED_THREADS / 64];
+  double num = 0.0, cnt = 0.0;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < npix; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = q / HW, pix = q % HW;
+    const float* sp = s + b * C * HW + pix;
+    const float* tp = t + b * C * HW + pix;
+    float mx = -INFINITY, d2 = 0.f;
+    for (int64_t c = 0; c < C; ++c) {
+      const float pt = sigmoidf_ref(tp[c * HW]);
+      const float ps = sigmoidf_ref(sp[c * HW]);
+      const float d = ps - pt;
+      d2 += d * d;
+      mx = fmaxf(mx, pt);
+    }
+    if (mx > thr) {
+      num += (double)d2;
+      cnt += 1.0;
+    }
+  }
+  num = block_sum(num, red);
+  cnt = block_sum(cnt, red);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = num;
+    part[2 * blockIdx.x + 1] = cnt;
+  }
+}
+
+__global__ void __launch_bounds__(RED_THREADS) cons_final_kernel(const double* part, int nparts, int64_t npix,
+                                                                 float* out3) {
+  __shared__ double red[RED_THREADS / 64];
+  double num = 0.0, cnt = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
+    num += part[2 * i];
+    cnt += part[2 * i + 1];
+  }
+  num = block_sum(num, red);
+  cnt = block_sum(cnt, red);
+  if (threadIdx.x == 0) {
+    out3[0] = (float)num / (float)cnt;   // 0/0 = NaN when no pixel is confident (train.py:106)
+    out3[1] = (float)(cnt / (double)npix);
+    out3[2] = (float)cnt;
+  }
+}
+
+__global__ void cons_bwd_kernel(const float* s, const float* t, int64_t C, int64_t HW, int64_t npix, float thr,
+                                const float* out3, const float* gout, float* gs) {
+  const float scale = gout[0] / out3[2];
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < npix; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = q / HW, pix = q % HW;
+    const float* sp = s + b * C * HW + pix;
+    const float* tp = t + b * C * HW + pix;
+    float mx = -INFINITY;
+    for (int64_t c = 0; c < C; ++c) mx = fmaxf(mx, sigmoidf_ref(tp[c * HW]));
+    const float cm = mx > thr ? 1.f : 0.f;
+    float* gp = gs + b * C * HW + pix;
+    for (int64_t c = 0; c < C; ++c) {
+      const float ps = sigmoidf_ref(sp[c * HW]);
+      const float pt = sigmoidf_ref(tp[c * HW]);
+      gp[c * HW] = 2.f * (ps - pt) * cm * scale * (ps * (1.f - ps));
+    }
+  }
+}
+
+// ---- EMA: t = round(ema*a); ema = fma(p, 1-a, t)  (bit-exact with torch CPU mul_().add_(alpha=)) ----
+__global__ void ema_kernel(float* __restrict__ ema, const float* __restrict__ p, int64_t n, float a, float beta) {
+  const int64_t n4 = n / 4;
+  float4* e4 = reinterpret_cast<float4*>(ema);
+  const float4* p4 = reinterpret_cast<const float4*>(p);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 e = e4[i];
+    const float4 q = p4[i];
+    e.x = fmaf(q.x, beta, __fmul_rn(e.x, a));
+    e.y = fmaf(q.y, beta, __fmul_rn(e.y, a));
+    e.z = fmaf(q.z, beta, __fmul_rn(e.z, a));
+    e.w = fmaf(q.w, beta, __fmul_rn(e.w, a));
+    e4[i] = e;
+  }
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    ema[i] = fmaf(p[i], beta, __fmul_rn(ema[i], a));
+}
+
+// ---- squared norm ----
+__global__ void __launch_bounds__(RED_THREADS) sq_partial_kernel(const float* x, int64_t n, double* part) {
+  __shared__ double red[RED_THREADS / 64];
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double v = x[i];
+    acc += v * v;
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+__global__ void __launch_bounds__(RED_THREADS) sq_final_kernel(const double* part, int nparts, float* out) {
+  __shared__ double red[RED_THREADS / 64];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) acc += part[i];
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) out[0] += (float)acc;
+}
+
+// ---- clip + SGD ----
+__global__ void sgd_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ buf, bf16_t* shadow,
+                           int64_t n, float lr, float mom, float wd, float max_norm, const float* sqnorm, int first) {
+  float coef = 1.f;
+  if (max_norm > 0.f) {
+    const float total = sqrtf(sqnorm[0]);
+    coef = fminf(max_norm / (total + 1e-6f), 1.f);
+  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = __fmul_rn(g[i], coef);
+    g[i] = gi;
+    const float pi = p[i];
+    const float d = wd != 0.f ? fmaf(pi, wd, gi) : gi;
+    float b;
+    if (mom != 0.f) {
+      b = first ? d : __fadd_rn(__fmul_rn(buf[i], mom), d);
+      buf[i] = b;
+    } else {
+      b = d;
+    }
+    const float np = fmaf(b, -lr, pi);
+    p[i] = np;
+    if (shadow) shadow[i] = f32_to_bf16(np);
+  }
+}
+
+}  // namespace
+
+extern "C" size_t ssseg_reduce_workspace_bytes(int64_t) { return sizeof(double) * 2 * RED_BLOCKS; }
+
+static int red_blocks(int64_t n) { return ssseg_grid(n, RED_THREADS, RED_BLOCKS); }
+
+extern "C" int ssseg_nchw_to_nhwc(const void* x, void* y, int64_t N, int64_t C, int64_t H, int64_t W, int64_t Cp,
+                                  int dt_in, int dt_out, ssseg_stream_t stream) {
+  if (!x || !y || Cp < C) return SSSEG_EINVAL;
+  const int64_t total = N * H * W * Cp;
+  if (total == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g(ssseg_grid(total, 256)), b(256);
+  if (dt_in == SSSEG_F32 && dt_out == SSSEG_F32)
+    hipLaunchKernelGGL((nchw_to_nhwc_kernel<float, float>), g, b, 0, s, (const float*)x, (float*)y, C, H * W, Cp, total);
+  else if (dt_in == SSSEG_F32 && dt_out == SSSEG_BF16)
+    hipLaunchKernelGGL((nchw_to_nhwc_kernel<float, bf16_t>), g, b, 0, s, (const float*)x, (bf16_t*)y, C, H * W, Cp, total);
+  else if (dt_in == SSSEG_BF16 && dt_out == SSSEG_BF16)
+    hipLaunchKernelGGL((nchw_to_nhwc_kernel<bf16_t, bf16_t>), g, b, 0, s, (const bf16_t*)x, (bf16_t*)y, C, H * W, Cp, total);
+  else if (dt_in == SSSEG_BF16 && dt_out == SSSEG_F32)
+    hipLaunchKernelGGL((nchw_to_nhwc_kernel<bf16_t, float>), g, b, 0, s, (const bf16_t*)x, (float*)y, C, H * W, Cp, total);
+  else
+    return SSSEG_EUNSUPPORTED;
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_nhwc_to_nchw(const void* x, void* y, int64_t N, int64_t C, int64_t H, int64_t W, int64_t ldc,
+                                  int dt_in, int dt_out, ssseg_stream_t stream) {
+  if (!x || !y || ldc < C) return SSSEG_EINVAL;
+  const int64_t total = N * H * W * C;
+  if (total == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g(ssseg_grid(total, 256)), b(256);
+  if (dt_in == SSSEG_F32 && dt_out == SSSEG_F32)
+    hipLaunchKernelGGL((nhwc_to_nchw_kernel<float, float>), g, b, 0, s, (const float*)x, (float*)y, C, H * W, ldc, total);
+  else if (dt_in == SSSEG_BF16 && dt_out == SSSEG_F32)
+    hipLaunchKernelGGL((nhwc_to_nchw_kernel<bf16_t, float>), g, b, 0, s, (const bf16_t*)x, (float*)y, C, H * W, ldc, total);
+  else if (dt_in == SSSEG_F32 && dt_out == SSSEG_BF16)
+    hipLaunchKernelGGL((nhwc_to_nchw_kernel<float, bf16_t>), g, b, 0, s, (const float*)x, (bf16_t*)y, C, H * W, ldc, total);
+  else if (dt_in == SSSEG_BF16 && dt_out == SSSEG_BF16)
+    hipLaunchKernelGGL((nhwc_to_nchw_kernel<bf16_t, bf16_t>), g, b, 0, s, (const bf16_t*)x, (bf16_t*)y, C, H * W, ldc, total);
+  else
+    return SSSEG_EUNSUPPORTED;
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_cast(const void* x, void* y, int64_t n, int dt_in, int dt_out, ssseg_stream_t stream) {
+  if (!x || !y || n < 0) return SSSEG_EINVAL;
+  if (n == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g(ssseg_grid(n, 256)), b(256);
+  if (dt_in == SSSEG_F32 && dt_out == SSSEG_BF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16_t>), g, b, 0, s, (const float*)x, (bf16_t*)y, n);
+  else if (dt_in == SSSEG_BF16 && dt_out == SSSEG_F32)
+    hipLaunchKernelGGL((cast_kernel<bf16_t, float>), g, b, 0, s, (const bf16_t*)x, (float*)y, n);
+  else if (dt_in == SSSEG_F32 && dt_out == SSSEG_F32)
+    hipLaunchKernelGGL((cast_kernel<float, float>), g, b, 0, s, (const float*)x, (float*)y, n);
+  else if (dt_in == SSSEG_BF16 && dt_out == SSSEG_BF16)
+    hipLaunchKernelGGL((cast_kernel<bf16_t, bf16_t>), g, b, 0, s, (const bf16_t*)x, (bf16_t*)y, n);
+  else
+    return SSSEG_EUNSUPPORTED;
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_bce_logits_fwd(const float* x, const float* t, int64_t n, float* loss_out, void* ws,
+                                    size_t ws_bytes, ssseg_stream_t stream) {
+  if (!x || !t || !loss_out || n <= 0) return SSSEG_EINVAL;
+  if (!ws || ws_bytes < ssseg_reduce_workspace_bytes(n)) return SSSEG_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = red_blocks(n);
+  hipLaunchKernelGGL(bce_partial_kernel, dim3(nb), dim3(RED_THREADS), 0, s, x, t, n, (double*)ws);
+  hipLaunchKernelGGL(bce_final_kernel, dim3(1), dim3(RED_THREADS), 0, s, (const double*)ws, nb, n, loss_out);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_bce_logits_bwd(const float* x, const float* t, int64_t n, const float* gout, float* gx,
+                                    ssseg_stream_t stream) {
+  if (!x || !t || !gout || !gx || n <= 0) return SSSEG_EINVAL;
+  hipLaunchKernelGGL(bce_bwd_kernel, dim3(ssseg_grid(n, 256)), dim3(256), 0, (hipStream_t)stream, x, t, n, gout, gx);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_consistency_fwd(const float* s, const float* t, int64_t B, int64_t C, int64_t HW, float thr,
+                                     float* out3, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
+  if (!s || !t || !out3 || B <= 0 || C <= 0 || HW <= 0) return SSSEG_EINVAL;
+  if (!ws || ws_bytes < ssseg_reduce_workspace_bytes(B * HW)) return SSSEG_EWORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t npix = B * HW;
+  const int nb = red_blocks(npix);
+  hipLaunchKernelGGL(cons_partial_kernel, dim3(nb), dim3(RED_THREADS), 0, st, s, t, C, HW, npix, thr, (double*)ws);
+  hipLaunchKernelGGL(cons_final_kernel, dim3(1), dim3(RED_THREADS), 0, st, (const double*)ws, nb, npix, out3);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_consistency_bwd(const float* s, const float* t, int64_t B, int64_t C, int64_t HW, float thr,
+                                     const float* out3, const float* gout, float* gs, ssseg_stream_t stream) {
+  if (!s || !t || !out3 || !gout || !gs || B <= 0 || C <= 0 || HW <= 0) return SSSEG_EINVAL;
+  const int64_t npix = B * HW;
+  hipLaunchKernelGGL(cons_bwd_kernel, dim3(ssseg_grid(npix, 256)), dim3(256), 0, (hipStream_t)stream, s, t, C, HW,
+                     npix, thr, out3, gout, gs);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_ema_update(float* ema, const float* param, int64_t n, double alpha, ssseg_stream_t stream) {
+  if (!ema || !param || n < 0) return SSSEG_EINVAL;
+  if (n == 0) return 0;
+  if ((((uintptr_t)ema) | ((uintptr_t)param)) & 15) return SSSEG_EINVAL;
+  const float a = (float)alpha, beta = (float)(1.0 - alpha);
+  hipLaunchKernelGGL(ema_kernel, dim3(ssseg_grid(n / 4 + 1, 256, 256 * 8)), dim3(256), 0, (hipStream_t)stream, ema,
+                     param, n, a, beta);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_sqnorm_accum(const float* x, int64_t n, float* out, void* ws, size_t ws_bytes,
+                                  ssseg_stream_t stream) {
+  if (!x || !out || n < 0) return SSSEG_EINVAL;
+  if (n == 0) return 0;
+  if (!ws || ws_bytes < ssseg_reduce_workspace_bytes(n)) return SSSEG_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = red_blocks(n);
+  hipLaunchKernelGGL(sq_partial_kernel, dim3(nb), dim3(RED_THREADS), 0, s, x, n, (double*)ws);
+  hipLaunchKernelGGL(sq_final_kernel, dim3(1), dim3(RED_THREADS), 0, s, (const double*)ws, nb, out);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_sgd_step(float* param, float* grad, float* momentum_buf, uint16_t* bf16_shadow, int64_t n,
+                              float lr, float momentum, float weight_decay, float max_norm, const float* sqnorm,
+                              int first_step, ssseg_stream_t stream) {
+  if (!param || !grad || n < 0 || (momentum != 0.f && !momentum_buf) || (max_norm > 0.f && !sqnorm))
+    return SSSEG_EINVAL;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(sgd_kernel, dim3(ssseg_grid(n, 256, 256 * 8)), dim3(256), 0, (hipStream_t)stream, param, grad,
+                     momentum_buf, (bf16_t*)bf16_shadow, n, lr, momentum, weight_decay, max_norm, sqnorm,
+                     first_step);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}

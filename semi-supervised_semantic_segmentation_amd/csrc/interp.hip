@@ -1,0 +1,173 @@
+// Bilinear interpolation forward/backward (F.interpolate mode='bilinear'), gfx950.
+// Call sites: losses.py:18 and train.py:71,74,93 (align_corners=False, to the image size),
+// unet.py:26 / simple_unet.py:71 (nn.Upsample(scale_factor=2, align_corners=True)).
+// Source-index arithmetic follows PyTorch's area_pixel_compute_source_index in fp32; the 2-D blend
+// is evaluated as (x00*w0 + x01*w1)*h0 + (x10*w0 + x11*w1)*h1 with explicit roundings, the order of
+// the CPU kernel.  Backward is a deterministic gather over the outputs that read each input pixel.
+#include "common.h"
+
+namespace {
+
+struct Strides {
+  int64_t n, c, h, w;
+};
+
+struct Axis {
+  int in, out;
+  float scale;
+  bool align;
+};
+
+__device__ __forceinline__ void src_index(const Axis& a, int d, int& i0, int& i1, float& l0, float& l1) {
+  float src;
+  if (a.align) {
+    src = a.scale * (float)d;
+  } else {
+    src = a.scale * ((float)d + 0.5f) - 0.5f;
+    src = src < 0.f ? 0.f : src;
+  }
+  i0 = min((int)src, a.in - 1);
+  l1 = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
+  i1 = i0 + (i0 < a.in - 1 ? 1 : 0);
+  l0 = 1.f - l1;
+}
+
+static Axis make_axis(int64_t in, int64_t out, bool align) {
+  Axis a;
+  a.in = (int)in;
+  a.out = (int)out;
+  a.align = align;
+  if (align)
+    a.scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+  else
+    a.scale = (float)in / (float)out;
+  return a;
+}
+
+template <typename T>
+__global__ void bilinear_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t N, int64_t C, Axis ah, Axis aw,
+                                    Strides xs, Strides ys, int c_fastest) {
+  const int64_t Ho = ah.out, Wo = aw.out, total = N * C * Ho * Wo;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t n, c, oh, ow;
+    if (c_fastest) {
+      c = i % C; ow = (i / C) % Wo; oh = (i / (C * Wo)) % Ho; n = i / (C * Wo * Ho);
+    } else {
+      ow = i % Wo; oh = (i / Wo) % Ho; c = (i / (Wo * Ho)) % C; n = i / (Wo * Ho * C);
+    }
+    int h0, h1, w0, w1;
+    float lh0, lh1, lw0, lw1;
+    src_index(ah, (int)oh, h0, h1, lh0, lh1);
+    src_index(aw, (int)ow, w0, w1, lw0, lw1);
+    const T* xb = x + n * xs.n + c * xs.c;
+    const float x00 = io<T>::ld(xb, h0 * xs.h + w0 * xs.w), x01 = io<T>::ld(xb, h0 * xs.h + w1 * xs.w);
+    const float x10 = io<T>::ld(xb, h1 * xs.h + w0 * xs.w), x11 = io<T>::ld(xb, h1 * xs.h + w1 * xs.w);
+    const float t0 = __fadd_rn(__fmul_rn(x00, lw0), __fmul_rn(x01, lw1));
+    const float t1 = __fadd_rn(__fmul_rn(x10, lw0), __fmul_rn(x11, lw1));
+    const float v = __fadd_rn(__fmul_rn(t0, lh0), __fmul_rn(t1, lh1));
+    io<T>::st(y, n * ys.n + c * ys.c + oh * ys.h + ow * ys.w, v);
+  }
+}
+
+// outputs o whose source pair (i0, i1) contains input i lie within [lo, hi]
+__device__ __forceinline__ void out_window(const Axis& a, int i, int& lo, int& hi) {
+  if (a.scale <= 0.f) {
+    lo = 0;
+    hi = a.out - 1;
+    return;
+  }
+  const float inv = 1.f / a.scale;
+  float c0, c1;
+  if (a.align) {
+    c0 = (float)(i - 1) * inv;
+    c1 = (float)(i + 1) * inv;
+  } else {
+    c0 = ((float)(i - 1) + 0.5f) * inv - 0.5f;
+    c1 = ((float)(i + 1) + 0.5f) * inv - 0.5f;
+  }
+  lo = max((int)floorf(c0) - 1, 0);
+  hi = min((int)ceilf(c1) + 1, a.out - 1);
+}
+
+template <typename T>
+__global__ void bilinear_bwd_kernel(const T* __restrict__ gy, T* __restrict__ gx, int64_t N, int64_t C, Axis ah,
+                                    Axis aw, Strides gys, Strides gxs, int c_fastest) {
+  const int64_t H = ah.in, W = aw.in, total = N * C * H * W;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t n, c, h, w;
+    if (c_fastest) {
+      c = i % C; w = (i / C) % W; h = (i / (C * W)) % H; n = i / (C * W * H);
+    } else {
+      w = i % W; h = (i / W) % H; c = (i / (W * H)) % C; n = i / (W * H * C);
+    }
+    int ohlo, ohhi, owlo, owhi;
+    out_window(ah, (int)h, ohlo, ohhi);
+    out_window(aw, (int)w, owlo, owhi);
+    const T* gb = gy + n * gys.n + c * gys.c;
+    float acc = 0.f;
+    for (int oh = ohlo; oh <= ohhi; ++oh) {
+      int h0, h1;
+      float l0, l1;
+      src_index(ah, oh, h0, h1, l0, l1);
+      const float wh = (h0 == h ? l0 : 0.f) + (h1 == h ? l1 : 0.f);
+      if (wh == 0.f) continue;
+      float row = 0.f;
+      for (int ow = owlo; ow <= owhi; ++ow) {
+        int w0, w1;
+        float m0, m1;
+        src_index(aw, ow, w0, w1, m0, m1);
+        const float ww = (w0 == w ? m0 : 0.f) + (w1 == w ? m1 : 0.f);
+        if (ww != 0.f) row = fmaf(io<T>::ld(gb, oh * gys.h + ow * gys.w), ww, row);
+      }
+      acc = fmaf(row, wh, acc);
+    }
+    io<T>::st(gx, n * gxs.n + c * gxs.c + h * gxs.h + w * gxs.w, acc);
+  }
+}
+
+static Strides to_strides(const int64_t* s) { return Strides{s[0], s[1], s[2], s[3]}; }
+
+}  // namespace
+
+extern "C" int ssseg_bilinear_fwd(const void* x, void* y, int64_t N, int64_t C, int64_t H, int64_t W, int64_t Ho,
+                                  int64_t Wo, const int64_t* xs4, const int64_t* ys4, int align_corners, int dt,
+                                  ssseg_stream_t stream) {
+  if (!x || !y || !xs4 || !ys4 || N < 0 || C < 0 || H < 1 || W < 1 || Ho < 1 || Wo < 1) return SSSEG_EINVAL;
+  const int64_t total = N * C * Ho * Wo;
+  if (total == 0) return 0;
+  const Axis ah = make_axis(H, Ho, align_corners), aw = make_axis(W, Wo, align_corners);
+  const Strides xs = to_strides(xs4), ys = to_strides(ys4);
+  const int cf = ys.c == 1 && C > 1;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g(ssseg_grid(total, 256, 256 * 32)), b(256);
+  if (dt == SSSEG_F32)
+    hipLaunchKernelGGL(bilinear_fwd_kernel<float>, g, b, 0, s, (const float*)x, (float*)y, N, C, ah, aw, xs, ys, cf);
+  else if (dt == SSSEG_BF16)
+    hipLaunchKernelGGL(bilinear_fwd_kernel<bf16_t>, g, b, 0, s, (const bf16_t*)x, (bf16_t*)y, N, C, ah, aw, xs, ys, cf);
+  else
+    return SSSEG_EUNSUPPORTED;
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_bilinear_bwd(const void* gy, void* gx, int64_t N, int64_t C, int64_t H, int64_t W, int64_t Ho,
+                                  int64_t Wo, const int64_t* gys4, const int64_t* gxs4, int align_corners, int dt,
+                                  ssseg_stream_t stream) {
+  if (!gy || !gx || !gys4 || !gxs4 || N < 0 || C < 0 || H < 1 || W < 1 || Ho < 1 || Wo < 1) return SSSEG_EINVAL;
+  const int64_t total = N * C * H * W;
+  if (total == 0) return 0;
+  const Axis ah = make_axis(H, Ho, align_corners), aw = make_axis(W, Wo, align_corners);
+  const Strides gys = to_strides(gys4), gxs = to_strides(gxs4);
+  const int cf = gxs.c == 1 && C > 1;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g(ssseg_grid(total, 256, 256 * 32)), b(256);
+  if (dt == SSSEG_F32)
+    hipLaunchKernelGGL(bilinear_bwd_kernel<float>, g, b, 0, s, (const float*)gy, (float*)gx, N, C, ah, aw, gys, gxs, cf);
+  else if (dt == SSSEG_BF16)
+    hipLaunchKernelGGL(bilinear_bwd_kernel<bf16_t>, g, b, 0, s, (const bf16_t*)gy, (bf16_t*)gx, N, C, ah, aw, gys, gxs,
+                       cf);
+  else
+    return SSSEG_EUNSUPPORTED;
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,107 @@
+"""ctypes binding of libssseg.so (the C ABI declared in include/ssseg.h).
+
+The library is built in-tree (`make -C semi-supervised_semantic_segmentation_amd/csrc`, or
+`__graft_entry__.build()`).  There is no fallback: if the library is missing, or a tensor handed to
+an op is not on the HIP device, the call raises.
+"""
+import ctypes
+import os
+import re
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libssseg.so')
+HEADER = os.path.join(_HERE, '..', '..', 'include', 'ssseg.h')
+
+F32, BF16 = 0, 1
+_ERRS = {-1: 'SSSEG_EINVAL', -2: 'SSSEG_EUNSUPPORTED', -3: 'SSSEG_EWORKSPACE'}
+
+vp, i64, i32, f32, f64, sz, u64 = (ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_double,
+                                   ctypes.c_size_t, ctypes.c_uint64)
+I64P = ctypes.POINTER(ctypes.c_int64)
+
+# name -> (restype, argtypes); every entry must match include/ssseg.h
+SIGS = {
+    'ssseg_version': (ctypes.c_char_p, []),
+    'ssseg_cowmix_workspace_bytes': (sz, [i64, i64, i64]),
+    'ssseg_cowmix_mask': (i32, [vp, vp, vp, i64, i64, i64, vp, vp, vp, vp, sz, vp]),
+    'ssseg_normal_f32': (i32, [vp, i64, u64, u64, vp]),
+    'ssseg_mix': (i32, [vp, vp, vp, vp, i64, i64, i64, i32, vp]),
+    'ssseg_nchw_to_nhwc': (i32, [vp, vp, i64, i64, i64, i64, i64, i32, i32, vp]),
+    'ssseg_nhwc_to_nchw': (i32, [vp, vp, i64, i64, i64, i64, i64, i32, i32, vp]),
+    'ssseg_cast': (i32, [vp, vp, i64, i32, i32, vp]),
+    'ssseg_bilinear_fwd': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, I64P, I64P, i32, i32, vp]),
+    'ssseg_bilinear_bwd': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, I64P, I64P, i32, i32, vp]),
+    'ssseg_reduce_workspace_bytes': (sz, [i64]),
+    'ssseg_bce_logits_fwd': (i32, [vp, vp, i64, vp, vp, sz, vp]),
+    'ssseg_bce_logits_bwd': (i32, [vp, vp, i64, vp, vp, vp]),
+    'ssseg_consistency_fwd': (i32, [vp, vp, i64, i64, i64, f32, vp, vp, sz, vp]),
+    'ssseg_consistency_bwd': (i32, [vp, vp, i64, i64, i64, f32, vp, vp, vp, vp]),
+    'ssseg_lovasz_workspace_bytes': (sz, [i64, i64]),
+    'ssseg_lovasz_fwd': (i32, [vp, vp, i64, i64, i64, vp, vp, sz, vp]),
+    'ssseg_lovasz_bwd': (i32, [vp, vp, i64, i64, i64, vp, vp, vp, sz, vp]),
+    'ssseg_ema_update': (i32, [vp, vp, i64, f64, vp]),
+    'ssseg_sqnorm_accum': (i32, [vp, i64, vp, vp, sz, vp]),
+    'ssseg_sgd_step': (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]),
+}
+
+_lib = None
+
+
+def header_symbols():
+    """Function names declared in include/ssseg.h."""
+    with open(HEADER) as f:
+        text = f.read()
+    text = re.sub(r'/\*.*?\*/', '', text, flags=re.S)
+    return sorted(set(re.findall(r'\b(ssseg_[a-z0-9_]+)\s*\(', text)))
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f'ssseg: native library not built ({LIB_PATH}); run __graft_entry__.build() '
+                               'or make -C semi-supervised_semantic_segmentation_amd/csrc. There is no CPU fallback.')
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f'ssseg: {name} failed with {_ERRS.get(rc, "hipError " + str(rc))}')
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def dev_ptr(t, name='tensor'):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError(f'ssseg: {name} must be a HIP device tensor (no CPU fallback), got {t.device}')
+    return t.data_ptr()
+
+
+def dt_code(t):
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise RuntimeError(f'ssseg: unsupported dtype {t.dtype}')
+
+
+def workspace(nbytes, device):
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+def strides4(t):
+    arr = (ctypes.c_int64 * 4)(*t.stride())
+    return arr

@@ -1,0 +1,168 @@
+"""Autograd-aware wrappers over libssseg.so for the loss / CowMix / EMA part of the hot path.
+
+Each function documents the reference call site it replaces.  Inputs must be HIP tensors.
+"""
+import torch
+
+from . import native as N
+
+
+def _c(t):
+    return t if t.is_contiguous() else t.contiguous()
+
+
+# ------------------------------------------------------------------------------------------------
+# CowMix (cowmix.py)
+# ------------------------------------------------------------------------------------------------
+def cowmix_mask(noise, sigma, p, return_field=False):
+    """Mask arithmetic of generate_cowmix_masks_like (cowmix.py:40-69).
+
+    noise [B,1,H,W] or [B,H,W] f32, sigma [B], p [B] (device tensors) -> mask [B,1,H,W] f32.
+    """
+    B = noise.shape[0]
+    H, W = noise.shape[-2:]
+    noise = _c(noise.float())
+    sigma = _c(sigma.float().to(noise.device))
+    p = _c(p.float().to(noise.device))
+    mask = torch.empty(B, 1, H, W, device=noise.device, dtype=torch.float32)
+    field = torch.empty_like(mask) if return_field else None
+    thr = torch.empty(B, device=noise.device, dtype=torch.float32) if return_field else None
+    nb = N.lib().ssseg_cowmix_workspace_bytes(B, H, W)
+    ws = N.workspace(nb, noise.device)
+    N.call('ssseg_cowmix_mask', N.dev_ptr(noise, 'noise'), N.dev_ptr(sigma), N.dev_ptr(p), B, H, W, N.dev_ptr(mask),
+           N.dev_ptr(field) if field is not None else None, N.dev_ptr(thr) if thr is not None else None,
+           N.dev_ptr(ws), nb, N.stream())
+    if return_field:
+        return mask, field, thr
+    return mask
+
+
+def normal_(out, seed, offset):
+    N.call('ssseg_normal_f32', N.dev_ptr(out, 'out'), out.numel(), int(seed) & (2 ** 64 - 1),
+           int(offset) & (2 ** 64 - 1), N.stream())
+    return out
+
+
+def mix(a, b, mask):
+    """mix_with_mask (cowmix.py:72-73): a*m + b*(1-m), mask [B,1,H,W] broadcast over channels."""
+    a, b = _c(a), _c(b)
+    m = _c(mask.float())
+    out = torch.empty_like(a)
+    B, C = a.shape[0], a.shape[1]
+    HW = a[0, 0].numel()
+    N.call('ssseg_mix', N.dev_ptr(a, 'a'), N.dev_ptr(b, 'b'), N.dev_ptr(m, 'mask'), N.dev_ptr(out), B, C, HW,
+           N.dt_code(a), N.stream())
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# Bilinear interpolation (F.interpolate mode='bilinear')
+# ------------------------------------------------------------------------------------------------
+class _Bilinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, size, align_corners):
+        Nn, C, H, W = x.shape
+        Ho, Wo = int(size[0]), int(size[1])
+        fmt = torch.channels_last if (x.is_contiguous(memory_format=torch.channels_last) and C > 1
+                                      and not x.is_contiguous()) else torch.contiguous_format
+        y = torch.empty((Nn, C, Ho, Wo), device=x.device, dtype=x.dtype, memory_format=fmt)
+        N.call('ssseg_bilinear_fwd', N.dev_ptr(x, 'x'), N.dev_ptr(y), Nn, C, H, W, Ho, Wo, N.strides4(x),
+               N.strides4(y), int(bool(align_corners)), N.dt_code(x), N.stream())
+        ctx.meta = (Nn, C, H, W, Ho, Wo, bool(align_corners), fmt)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        Nn, C, H, W, Ho, Wo, ac, fmt = ctx.meta
+        gx = torch.empty((Nn, C, H, W), device=gy.device, dtype=gy.dtype, memory_format=fmt)
+        N.call('ssseg_bilinear_bwd', N.dev_ptr(gy, 'gy'), N.dev_ptr(gx), Nn, C, H, W, Ho, Wo, N.strides4(gy),
+               N.strides4(gx), int(ac), N.dt_code(gy), N.stream())
+        return gx, None, None
+
+
+def interpolate_bilinear(x, size, align_corners=False):
+    return _Bilinear.apply(x, tuple(size), align_corners)
+
+
+# ------------------------------------------------------------------------------------------------
+# Losses
+# ------------------------------------------------------------------------------------------------
+class _BCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, t):
+        x, t = _c(x.float()), _c(t.float())
+        out = torch.empty((), device=x.device, dtype=torch.float32)
+        nb = N.lib().ssseg_reduce_workspace_bytes(x.numel())
+        ws = N.workspace(nb, x.device)
+        N.call('ssseg_bce_logits_fwd', N.dev_ptr(x, 'x'), N.dev_ptr(t, 'target'), x.numel(), N.dev_ptr(out),
+               N.dev_ptr(ws), nb, N.stream())
+        ctx.save_for_backward(x, t)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, t = ctx.saved_tensors
+        gx = torch.empty_like(x)
+        g = _c(g.float())
+        N.call('ssseg_bce_logits_bwd', N.dev_ptr(x), N.dev_ptr(t), x.numel(), N.dev_ptr(g), N.dev_ptr(gx), N.stream())
+        return gx, None
+
+
+def bce_with_logits_mean(x, t):
+    """F.binary_cross_entropy_with_logits(x, t, reduction='mean') (losses.py:47)."""
+    return _BCE.apply(x, t)
+
+
+class _Consistency(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, s, t, thr):
+        s, t = _c(s.float()), _c(t.float())
+        B, C = s.shape[:2]
+        HW = s[0, 0].numel()
+        out = torch.empty(3, device=s.device, dtype=torch.float32)
+        nb = N.lib().ssseg_reduce_workspace_bytes(B * HW)
+        ws = N.workspace(nb, s.device)
+        N.call('ssseg_consistency_fwd', N.dev_ptr(s, 'student'), N.dev_ptr(t, 'teacher'), B, C, HW, float(thr),
+               N.dev_ptr(out), N.dev_ptr(ws), nb, N.stream())
+        ctx.save_for_backward(s, t, out)
+        ctx.meta = (B, C, HW, float(thr))
+        ctx.mark_non_differentiable(out)
+        return out[0], out[1]
+
+    @staticmethod
+    def backward(ctx, g_loss, g_cm):
+        s, t, out = ctx.saved_tensors
+        B, C, HW, thr = ctx.meta
+        gs = torch.empty_like(s)
+        g = _c(g_loss.float())
+        N.call('ssseg_consistency_bwd', N.dev_ptr(s), N.dev_ptr(t), B, C, HW, thr, N.dev_ptr(out), N.dev_ptr(g),
+               N.dev_ptr(gs), N.stream())
+        return gs, None, None
+
+
+def consistency_loss(student_logits, teacher_logits, thr):
+    """train.py:97-108: returns (loss, confidence_modulator.mean()); loss is NaN when no pixel is confident."""
+    return _Consistency.apply(student_logits, teacher_logits, thr)
+
+
+# ------------------------------------------------------------------------------------------------
+# EMA / optimiser over flat arenas
+# ------------------------------------------------------------------------------------------------
+def ema_update_(ema_flat, param_flat, alpha):
+    """mean_teacher.update_ema_variables parameter loop (mean_teacher.py:10-11), one launch."""
+    assert ema_flat.numel() == param_flat.numel() and ema_flat.dtype == torch.float32
+    N.call('ssseg_ema_update', N.dev_ptr(ema_flat, 'ema'), N.dev_ptr(param_flat, 'param'), ema_flat.numel(),
+           float(alpha), N.stream())
+
+
+def sqnorm_(x_flat, out):
+    nb = N.lib().ssseg_reduce_workspace_bytes(x_flat.numel())
+    ws = N.workspace(nb, x_flat.device)
+    N.call('ssseg_sqnorm_accum', N.dev_ptr(x_flat, 'x'), x_flat.numel(), N.dev_ptr(out), N.dev_ptr(ws), nb, N.stream())
+
+
+def sgd_step_(param, grad, buf, shadow, lr, momentum, wd, max_norm, sqnorm, first):
+    N.call('ssseg_sgd_step', N.dev_ptr(param, 'param'), N.dev_ptr(grad, 'grad'),
+           N.dev_ptr(buf) if buf is not None else None, N.dev_ptr(shadow) if shadow is not None else None,
+           param.numel(), float(lr), float(momentum), float(wd), float(max_norm),
+           N.dev_ptr(sqnorm) if sqnorm is not None else None, int(bool(first)), N.stream())

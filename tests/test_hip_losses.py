@@ -1,0 +1,159 @@
+"""GPU parity of the CowMix / loss / interpolation / EMA / SGD kernels against the oracle and the
+reference golden vectors.  Tolerances are stated per test."""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import cowmix_ref, losses_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def ops():
+    from ssseg import ops as o
+    return o
+
+
+@pytest.mark.parametrize('tag', ['a0', 'a1', 'a2', 'b3', 'c0'])
+def test_cowmix_mask_bit_exact_outside_tie_band(hip_device, tag):
+    g = golden(f'cowmix_{tag}.npz')
+    B, _, H, W = [int(v) for v in g['shape']]
+    torch.manual_seed(int(g['seed']))
+    p, sig, noise = cowmix_ref.draw_inputs(B, H, W, g['prop_range'], g['sigma_range'])
+    assert hashlib.sha256(noise.reshape(B, 1, H, W).tobytes()).hexdigest() == str(g['noise_sha256'])
+    dev = hip_device
+    mask, field, thr = ops().cowmix_mask(torch.from_numpy(noise).to(dev), torch.from_numpy(sig).to(dev),
+                                         torch.from_numpy(p).to(dev), return_field=True)
+    mask = mask.cpu().numpy().reshape(B, H, W)
+    field = field.cpu().numpy().reshape(B, H, W)
+    ref = np.unpackbits(g['mask_bits'])[:B * H * W].reshape(B, H, W)
+    std = g['std'].reshape(B, 1, 1)
+    np.testing.assert_allclose(thr.cpu().numpy(), g['thr'], rtol=1e-5, atol=1e-6)
+    if 'field' in g.files:
+        np.testing.assert_allclose(field, g['field'].reshape(B, H, W), rtol=0, atol=2e-6)
+    band = np.abs(field - g['thr'].reshape(B, 1, 1)) < 1e-5 * std
+    diff = mask.astype(np.uint8) != ref
+    assert not (diff & ~band).any(), f'{int((diff & ~band).sum())} pixels differ outside the tie band'
+    assert set(np.unique(mask)) <= {0.0, 1.0}
+
+
+def test_cowmix_device_noise_statistics(hip_device):
+    out = torch.empty(1 << 22, device=hip_device)
+    ops().normal_(out, seed=1234, offset=0)
+    x = out.double()
+    assert abs(float(x.mean())) < 3e-3 and abs(float(x.std()) - 1) < 3e-3
+    out2 = torch.empty_like(out)
+    ops().normal_(out2, seed=1234, offset=0)
+    assert torch.equal(out, out2)
+
+
+def test_mix_bit_exact(hip_device):
+    g = golden('mix.npz')
+    a, b, m = (torch.from_numpy(g[k]).to(hip_device) for k in ('a', 'b', 'mask'))
+    assert np.array_equal(ops().mix(a, b, m).cpu().numpy(), g['out'])
+
+
+@pytest.mark.parametrize('shape,size,ac', [((2, 2, 32, 32), (64, 64), False), ((2, 3, 17, 23), (40, 31), False),
+                                           ((1, 4, 8, 8), (16, 16), True), ((2, 2, 64, 48), (32, 24), False),
+                                           ((1, 2, 9, 9), (9, 9), False)])
+def test_bilinear_fwd_bwd(hip_device, shape, size, ac):
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal(shape).astype(np.float32)
+    gy = rng.standard_normal(shape[:2] + size).astype(np.float32)
+    xt = torch.from_numpy(x).to(hip_device).requires_grad_(True)
+    y = ops().interpolate_bilinear(xt, size, align_corners=ac)
+    y.backward(torch.from_numpy(gy).to(hip_device))
+    ref = torch.nn.functional.interpolate(torch.from_numpy(x), size=size, mode='bilinear', align_corners=ac)
+    np.testing.assert_allclose(y.detach().cpu().numpy(), ref.numpy(), rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(y.detach().cpu().numpy(), losses_ref.bilinear(x, size, ac), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(xt.grad.cpu().numpy(), losses_ref.bilinear_backward(gy, shape[2:], ac),
+                               rtol=1e-5, atol=1e-5)
+
+
+def test_bilinear_channels_last_bf16(hip_device):
+    x = torch.randn(2, 8, 16, 16, device=hip_device).to(memory_format=torch.channels_last)
+    y32 = ops().interpolate_bilinear(x, (32, 32), True)
+    yb = ops().interpolate_bilinear(x.bfloat16(), (32, 32), True)
+    assert yb.is_contiguous(memory_format=torch.channels_last)
+    ref = torch.nn.functional.interpolate(x.cpu(), size=(32, 32), mode='bilinear', align_corners=True)
+    np.testing.assert_allclose(y32.cpu().numpy(), ref.numpy(), rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(yb.float().cpu().numpy(), ref.numpy(), rtol=2e-2, atol=2e-2)
+
+
+def test_bce_fwd_bwd(hip_device):
+    rng = np.random.default_rng(1)
+    x = (rng.standard_normal((4, 2, 64, 64)) * 3).astype(np.float32)
+    t = (rng.random((4, 2, 64, 64)) > 0.5).astype(np.float32)
+    xt = torch.from_numpy(x).to(hip_device).requires_grad_(True)
+    loss = ops().bce_with_logits_mean(xt, torch.from_numpy(t).to(hip_device))
+    (loss * 0.5).backward()
+    ref_l, ref_g = losses_ref.bce_logits_mean(x, t)
+    np.testing.assert_allclose(float(loss), ref_l, rtol=1e-6)
+    np.testing.assert_allclose(xt.grad.cpu().numpy(), ref_g * 0.5, rtol=1e-5, atol=1e-10)
+
+
+@pytest.mark.parametrize('tag', ['thr05', 'thr097', 'nan', 'gated'])
+def test_consistency_chain_vs_golden(hip_device, tag):
+    """G3 through the HIP ops: interp -> BCE, CowMix (CPU-generator inputs) -> mix -> consistency."""
+    o = ops()
+    g = golden(f'consistency_{tag}.npz')
+    dev = hip_device
+    s = torch.from_numpy(g['s_logits']).to(dev).requires_grad_(True)
+    t = torch.from_numpy(g['t_logits']).to(dev)
+    B, _, H, W = g['image'].shape
+    sm = torch.from_numpy(g['semantic_mask']).to(dev)
+    sup = o.bce_with_logits_mean(o.interpolate_bilinear(s, (H, W)), sm) * 0.5
+    torch.manual_seed(int(g['rng_seed']))
+    p, sig, noise = cowmix_ref.draw_inputs(B, H, W, (0.45, 0.55), (4, 8))
+    m = o.cowmix_mask(torch.from_numpy(noise).to(dev), torch.from_numpy(sig).to(dev), torch.from_numpy(p).to(dev))
+    tu = o.interpolate_bilinear(t, (H, W))
+    t_mix = o.mix(tu, tu, m)
+    loss, cm = o.consistency_loss(o.interpolate_bilinear(s, (H, W)), t_mix, float(g['thr']))
+    unsup = loss * (10.0 * float(int(g['epoch']) > 25))
+    (sup + unsup).backward()
+    np.testing.assert_allclose(float(sup), g['sup_loss'], rtol=1e-5)
+    if tag == 'nan':
+        assert np.isnan(float(unsup)) and torch.isnan(s.grad).all()
+        return
+    np.testing.assert_allclose(float(unsup), g['unsup_loss'], rtol=2e-5, atol=1e-7)
+    np.testing.assert_allclose(s.grad.cpu().numpy(), g['grad'], rtol=2e-4, atol=2e-8)
+
+
+def test_ema_bit_exact(hip_device):
+    g = golden('ema.npz')
+    keys = [k[2:] for k in g.files if k.startswith('t.') and 'running' not in k and 'num_batches' not in k]
+    e = torch.cat([torch.from_numpy(g['t.' + k]).reshape(-1) for k in keys]).to(hip_device)
+    p = torch.cat([torch.from_numpy(g['s.' + k]).reshape(-1) for k in keys]).to(hip_device)
+    ref = np.concatenate([g['after.' + k].reshape(-1) for k in keys])
+    ops().ema_update_(e, p, float(g['alpha']))
+    assert np.array_equal(e.cpu().numpy(), ref)
+
+
+def test_clip_sgd_matches_torch(hip_device):
+    torch.manual_seed(3)
+    params = [torch.randn(37, 5), torch.randn(1000), torch.randn(3, 3, 4)]
+    grads = [torch.randn_like(q) * 3 for q in params]
+    ref_p = [q.clone().requires_grad_(True) for q in params]
+    for q, gr in zip(ref_p, grads):
+        q.grad = gr.clone()
+    opt = torch.optim.SGD(ref_p, lr=0.05, momentum=0.9, weight_decay=5e-4)
+    flat_p = torch.cat([q.reshape(-1) for q in params]).to(hip_device)
+    flat_g = torch.cat([q.reshape(-1) for q in grads]).to(hip_device)
+    buf = torch.zeros_like(flat_p)
+    shadow = torch.empty(flat_p.numel(), dtype=torch.bfloat16, device=hip_device)
+    o = ops()
+    for step in range(3):
+        torch.nn.utils.clip_grad_norm_(ref_p, 5.0)
+        opt.step()
+        sq = torch.zeros(1, device=hip_device)
+        o.sqnorm_(flat_g, sq)
+        o.sgd_step_(flat_p, flat_g, buf, shadow, 0.05, 0.9, 5e-4, 5.0, sq, step == 0)
+        for q, gr in zip(ref_p, grads):
+            q.grad = gr.clone()
+        flat_g = torch.cat([q.reshape(-1) for q in grads]).to(hip_device)
+    ref = torch.cat([q.detach().reshape(-1) for q in ref_p]).numpy()
+    np.testing.assert_allclose(flat_p.cpu().numpy(), ref, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(shadow.float().cpu().numpy(), ref, rtol=1e-2, atol=1e-2)
