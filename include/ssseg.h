@@ -139,6 +139,95 @@ int ssseg_sgd_step(float* param, float* grad, float* momentum_buf, uint16_t* bf1
                    float lr, float momentum, float weight_decay, float max_norm, const float* sqnorm,
                    int first_step, ssseg_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Convolution engine (implicit GEMM on MFMA).  Replaces the cuDNN/MIOpen convolutions behind
+ * nn.Conv2d / nn.ConvTranspose2d in unet.py:8,21,27,85, simple_unet.py:64,72,138, the encoders,
+ * and their autograd backward (train.py:61,115).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+  int64_t N, H, W, C, ldx;        /* input activations NHWC; C = physical channels (multiple of 8 bf16 / 4 f32),
+                                     ldx = pixel stride in elements */
+  int64_t OH, OW;                 /* GEMM spatial grid (per image) */
+  int64_t K;                      /* output channels (GEMM N) */
+  int64_t R, S;                   /* taps */
+  int64_t sy, sx, dy, dx, py, px; /* input row = oy*sy + r*dy + py (zero outside), same for columns */
+  int64_t outH, outW;             /* output map; pixel written = (oy*osy + ooy, ox*osx + oox) */
+  int64_t osy, osx, ooy, oox;
+  int64_t ldy;                    /* output pixel stride (elements) */
+  int64_t ldw;                    /* packed weight row stride (rows = K, row = [R][S][C]) */
+} ssseg_conv_desc;
+
+/* y[m][n] = act(sum_k A[m][k] * W[n][k] + bias[n]).  Used for the forward conv, the stride-1 dgrad
+ * (flipped packing), every phase of a strided dgrad and of ConvTranspose2d(4,2,1) (dilation -1 and
+ * strided output), and the ConvTranspose2d input gradient.  dt: input/weight dtype; dt_out: output.
+ * When R*S == 0 (an output phase no tap reaches) the phase is zero-filled. */
+int ssseg_conv_igemm(const void* x, const void* w, void* y, const ssseg_conv_desc* desc_host, int dt, int dt_out,
+                     const float* bias, int relu, ssseg_stream_t stream);
+
+/* dW = sum over output pixels of dY[p][k] * x_col[p][(r,s,c)] (split-K fp32 slabs + deterministic
+ * reduce).  dy is [N][OH][OW] with pixel stride desc.ldy.  layout 0: dw [K][R][S][C];
+ * layout 1: dw [k_real][c_real][R][S] (PyTorch OIHW / ConvTranspose2d [Cin][Cout][R][S]).
+ * accumulate != 0 adds into dw (the reference accumulates the two backward passes, train.py:61,115). */
+size_t ssseg_conv_wgrad_workspace_bytes(const ssseg_conv_desc* desc_host, int dt);
+int ssseg_conv_wgrad(const void* x, const void* dy, float* dw, const ssseg_conv_desc* desc_host, int dt, int64_t c_real,
+                     int64_t k_real, int layout, int accumulate, void* ws, size_t ws_bytes, ssseg_stream_t stream);
+
+/* Pack fp32 master weights into the engine's [Kd][Rn][Sn][Cp] layout (dtype dt; rows >= Kr and
+ * channels >= Cd zero): layout 0 reads src[k][c][r][s] (src is [Kr][Cd][Rs][Ss]), layout 1 reads
+ * src[c][k][r][s] (src is [Cd][Kr][Rs][Ss]); r = r0 + rr*rstep, s = s0 + ss*sstep. */
+int ssseg_weight_pack(const float* src, void* dst, int64_t Kd, int64_t Kr, int64_t Cd, int64_t Rs, int64_t Ss,
+                      int64_t Cp, int layout, int64_t r0, int64_t rstep, int64_t Rn, int64_t s0, int64_t sstep,
+                      int64_t Sn, int dt, ssseg_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * BatchNorm2d / SyncBatchNorm (nn.BatchNorm2d in every ConvBlock, unet.py:9; distributed_trainer.py:36)
+ * NHWC [P][ld] activations, C % 4 == 0.  Training: stats -> (all-reduce sums for SyncBN) -> finalize.
+ * ------------------------------------------------------------------------------------------- */
+size_t ssseg_bn_workspace_bytes(int64_t C);
+/* sums[0:C] = sum_p x, sums[C:2C] = sum_p x^2 (fp64) */
+int ssseg_bn_stats(const void* x, int64_t P, int64_t C, int64_t ldx, int dt, double* sums, void* ws, size_t ws_bytes,
+                   ssseg_stream_t stream);
+/* mean, invstd = 1/sqrt(biased var + eps) from sums over `count` pixels; running stats updated with
+ * momentum and the unbiased variance when running_mean != NULL; *num_batches_tracked += 1 if non-NULL. */
+int ssseg_bn_finalize(const double* sums, int64_t C, double count, float eps, float momentum, float* mean_out,
+                      float* invstd_out, float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                      ssseg_stream_t stream);
+/* eval mode: mean = running_mean, invstd = 1/sqrt(running_var + eps) */
+int ssseg_bn_eval_params(const float* running_mean, const float* running_var, float eps, int64_t C, float* mean_out,
+                         float* invstd_out, ssseg_stream_t stream);
+/* y = act(gamma*(x-mean)*invstd + beta [+ residual]); relu = 1 for ReLU (unet.py:10, Bottleneck add+relu) */
+int ssseg_bn_apply(const void* x, const void* residual, void* y, int64_t P, int64_t C, int64_t ldx, int64_t ldr,
+                   int64_t ldy, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu,
+                   int dt, ssseg_stream_t stream);
+/* backward pass 1: sums[0:C] = sum dyr, sums[C:2C] = sum dyr*xhat, dyr = dy*[y>0] (y recomputed) */
+int ssseg_bn_bwd_reduce(const void* dy, const void* x, const void* residual, int64_t P, int64_t C, int64_t ldx,
+                        int64_t ldr, int64_t lddy, const float* mean, const float* invstd, const float* gamma,
+                        const float* beta, int relu, int dt, double* sums, void* ws, size_t ws_bytes,
+                        ssseg_stream_t stream);
+/* dgamma += sums[C:2C], dbeta += sums[0:C] (local sums, before any SyncBN all-reduce) */
+int ssseg_bn_param_grad(const double* sums, int64_t C, float* dgamma, float* dbeta, ssseg_stream_t stream);
+/* backward pass 2: dx = gamma*invstd*(dyr - [train]*(sum_dyr + xhat*sum_dyr_xhat)/count); dres = dyr */
+int ssseg_bn_bwd_apply(const void* dy, const void* x, const void* residual, void* dx, void* dres, int64_t P, int64_t C,
+                       int64_t ldx, int64_t ldr, int64_t lddy, int64_t lddx, const float* mean, const float* invstd,
+                       const float* gamma, const float* beta, int relu, int train, const double* sums, double count,
+                       int dt, ssseg_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Pooling and NHWC window copies (torch.cat / _center_crop, unet.py:40-60)
+ * ------------------------------------------------------------------------------------------- */
+/* MaxPool2d(k, s, p): y and argmax idx (tap index within the window, PyTorch tie order) */
+int ssseg_maxpool_fwd(const void* x, void* y, uint8_t* idx, int64_t N, int64_t H, int64_t W, int64_t C, int64_t OH,
+                      int64_t OW, int64_t k, int64_t s, int64_t p, int dt, ssseg_stream_t stream);
+int ssseg_maxpool_bwd(const void* gy, const uint8_t* idx, void* gx, int64_t N, int64_t H, int64_t W, int64_t C,
+                      int64_t OH, int64_t OW, int64_t k, int64_t s, int64_t p, int dt, ssseg_stream_t stream);
+/* dst[n][h+doy][w+dox][c] = src[n][h+soy][w+sox][c] for h<H, w<W, c<C (pixel strides sld/dld) */
+int ssseg_nhwc_copy(const void* src, void* dst, int64_t N, int64_t H, int64_t W, int64_t C, int64_t sH, int64_t sW,
+                    int64_t sld, int64_t soy, int64_t sox, int64_t dH, int64_t dW, int64_t dld, int64_t doy, int64_t dox,
+                    int dt, ssseg_stream_t stream);
+int ssseg_zero(void* p, size_t bytes, ssseg_stream_t stream);
+/* gx = gy * [y > 0]  (ReLU backward from the saved output; ConvTranspose2d+ReLU upsampler unet.py:21-22) */
+int ssseg_relu_bwd(const void* gy, const void* y, void* gx, int64_t n, int dt, ssseg_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

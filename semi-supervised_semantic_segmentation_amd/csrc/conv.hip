@@ -1,0 +1,616 @@
+// Implicit-GEMM convolution engine for gfx950 (MFMA 16x16x32 bf16 / 16x16x4 f32), NHWC activations.
+//
+// One gather-GEMM kernel covers every contraction of the conv layers on the hot path
+// (unet.py:8,21-22,27,85; simple_unet.py:64-72,118; encoder convs):
+//   y[m][n] = sum_k A[m][k] * B[n][k]
+//   m = output position (img, oy, ox) of a GEMM grid OHxOW, written to pixel (oy*osy+ooy, ox*osx+oox)
+//   k = (r, s, c):  A = x[img][oy*sy + r*dy + py][ox*sx + s*dx + px][c]  (0 outside),  B = packed weights
+// Forward conv, stride-1 dgrad (flipped taps), strided dgrad and ConvTranspose2d(4,2,1) forward
+// (stride-phase decomposition: one launch per output phase, dilation -1) are all this kernel with
+// different descriptors and weight packings (ssseg_weight_pack).
+// Weight gradients use a second kernel (split-K over pixels, fp32 slabs, deterministic reduce).
+//
+// Tiling: 256 threads = 4 waves; block tile BM pixels x BN channels x 64 bytes of k; LDS double
+// buffer with register-staged global loads (issue next tile's loads before the MFMAs, write them to
+// the other buffer after), one barrier per k-tile.  The MFMA A operand is the weight tile and the B
+// operand the pixel tile, so each lane's accumulator holds 4 consecutive output channels of one
+// pixel: the NHWC epilogue stores them with one 8/16-byte write.
+#include <algorithm>
+
+#include "common.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+struct ConvGeom {
+  int N, H, W, C, ldx;
+  int OH, OW, K;
+  int R, S, sy, sx, dy, dx, py, px;
+  int outH, outW, osy, osx, ooy, oox, ldy;
+  int ldw;
+  long long M;   // N*OH*OW
+  int KK;        // R*S*C
+};
+
+static bool make_geom(const ssseg_conv_desc* d, ConvGeom& g) {
+  if (!d) return false;
+  const int64_t vals[] = {d->N, d->H, d->W, d->C, d->ldx, d->OH, d->OW, d->K, d->R, d->S, d->outH, d->outW, d->ldy,
+                          d->ldw};
+  for (int64_t v : vals)
+    if (v < 0 || v > (int64_t)0x7fffffff) return false;
+  g.N = (int)d->N; g.H = (int)d->H; g.W = (int)d->W; g.C = (int)d->C; g.ldx = (int)d->ldx;
+  g.OH = (int)d->OH; g.OW = (int)d->OW; g.K = (int)d->K;
+  g.R = (int)d->R; g.S = (int)d->S; g.sy = (int)d->sy; g.sx = (int)d->sx; g.dy = (int)d->dy; g.dx = (int)d->dx;
+  g.py = (int)d->py; g.px = (int)d->px;
+  g.outH = (int)d->outH; g.outW = (int)d->outW; g.osy = (int)d->osy; g.osx = (int)d->osx; g.ooy = (int)d->ooy;
+  g.oox = (int)d->oox; g.ldy = (int)d->ldy; g.ldw = (int)d->ldw;
+  g.M = (long long)d->N * d->OH * d->OW;
+  g.KK = (int)(d->R * d->S * d->C);
+  return true;
+}
+
+template <typename T> struct MF;
+template <> struct MF<bf16_t> {
+  static constexpr int VEC = 8;
+  typedef bf16x8 frag;
+  __device__ __forceinline__ static void mma(const frag& a, const frag& b, f32x4& c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct MF<float> {
+  static constexpr int VEC = 4;
+  typedef f32x4 frag;
+  // k inside a 16-element chunk is permuted consistently for A and B: MFMA e consumes element e
+  __device__ __forceinline__ static void mma(const frag& a, const frag& b, f32x4& c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], c, 0, 0, 0);
+  }
+};
+
+template <typename TO> struct Store4;
+template <> struct Store4<float> {
+  __device__ __forceinline__ static void st(float* p, const float (&v)[4]) { *(float4*)p = make_float4(v[0], v[1], v[2], v[3]); }
+};
+template <> struct Store4<bf16_t> {
+  __device__ __forceinline__ static void st(bf16_t* p, const float (&v)[4]) {
+    uint2 u;
+    u.x = (unsigned)f32_to_bf16(v[0]) | ((unsigned)f32_to_bf16(v[1]) << 16);
+    u.y = (unsigned)f32_to_bf16(v[2]) | ((unsigned)f32_to_bf16(v[3]) << 16);
+    *(uint2*)p = u;
+  }
+};
+
+constexpr int ROWB = 80;   // 64 data bytes + 16 pad per LDS row
+
+// ------------------------------------------------------------------------------------------------
+// forward / dgrad / transposed-conv gather GEMM
+// ------------------------------------------------------------------------------------------------
+template <typename T, typename TO, int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256) igemm_kernel(const T* __restrict__ x, const T* __restrict__ w,
+                                                    TO* __restrict__ y, ConvGeom g, const float* __restrict__ bias,
+                                                    int relu) {
+  constexpr int VEC = MF<T>::VEC;
+  constexpr int BK = 64 / (int)sizeof(T);
+  constexpr int A_PER = BM / 64;                 // pixel rows per thread (4 chunks per row)
+  constexpr int B_IT = (BN * 4 + 255) / 256;
+  constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
+  static_assert(WM * WN == 4 && FM >= 1 && FN >= 1, "tile");
+  __shared__ __attribute__((aligned(16))) char smem[2 * (BM + BN) * ROWB];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const long long m0 = (long long)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int chunk = t & 3;
+  const int RS = g.R * g.S;
+
+  int a_n[A_PER], a_oy[A_PER], a_ox[A_PER];
+  bool a_ok[A_PER];
+#pragma unroll
+  for (int i = 0; i < A_PER; ++i) {
+    const long long m = m0 + (t >> 2) + 64 * i;
+    a_ok[i] = m < g.M;
+    const long long mm = a_ok[i] ? m : 0;
+    a_ox[i] = (int)(mm % g.OW);
+    const long long q = mm / g.OW;
+    a_oy[i] = (int)(q % g.OH);
+    a_n[i] = (int)(q / g.OH);
+  }
+  // k-state of this thread's chunk: k = tap*C + kc, tap = r*S + s
+  int kc = chunk * VEC, tap = 0, r = 0, s = 0;
+  while (kc >= g.C && tap < RS) {
+    kc -= g.C; ++tap;
+    if (++s == g.S) { s = 0; ++r; }
+  }
+  const int nk = (g.KK + BK - 1) / BK;
+
+  uint4 ra[A_PER], rb[B_IT];
+  auto load = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int iy = a_oy[i] * g.sy + r * g.dy + g.py;
+      const int ix = a_ox[i] * g.sx + s * g.dx + g.px;
+      const bool ok = a_ok[i] && tap < RS && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+      ra[i] = ok ? *(const uint4*)(x + ((long long)(a_n[i] * g.H + iy) * g.W + ix) * g.ldx + kc) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < B_IT; ++j) {
+      const int id = t + 256 * j;
+      rb[j] = make_uint4(0, 0, 0, 0);
+      if (id < BN * 4) {
+        const int n = n0 + (id >> 2);
+        const int k = kt * BK + (id & 3) * VEC;
+        if (n < g.K && k < g.KK) rb[j] = *(const uint4*)(w + (long long)n * g.ldw + k);
+      }
+    }
+    kc += BK;
+    while (kc >= g.C && tap < RS) {
+      kc -= g.C; ++tap;
+      if (++s == g.S) { s = 0; ++r; }
+    }
+  };
+  auto store = [&](int buf) {
+    char* As = smem + buf * (BM + BN) * ROWB;
+    char* Bs = As + BM * ROWB;
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) *(uint4*)(As + ((t >> 2) + 64 * i) * ROWB + chunk * 16) = ra[i];
+#pragma unroll
+    for (int j = 0; j < B_IT; ++j) {
+      const int id = t + 256 * j;
+      if (id < BN * 4) *(uint4*)(Bs + (id >> 2) * ROWB + (id & 3) * 16) = rb[j];
+    }
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    load(0);
+    store(0);
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) load(kt + 1);
+    const char* As = smem + buf * (BM + BN) * ROWB;
+    const char* Bs = As + BM * ROWB;
+    typename MF<T>::frag af[FN], bfr[FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+      af[i] = *(const typename MF<T>::frag*)(Bs + (wn * WTN + i * 16 + (lane & 15)) * ROWB + (lane >> 4) * 16);
+#pragma unroll
+    for (int j = 0; j < FM; ++j)
+      bfr[j] = *(const typename MF<T>::frag*)(As + (wm * WTM + j * 16 + (lane & 15)) * ROWB + (lane >> 4) * 16);
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) MF<T>::mma(af[i], bfr[j], acc[i][j]);
+    if (kt + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane holds channels n..n+3 (n = 4*(lane>>4) within a 16-wide fragment) of pixel lane&15
+#pragma unroll
+  for (int j = 0; j < FM; ++j) {
+    const long long m = m0 + wm * WTM + j * 16 + (lane & 15);
+    if (m >= g.M) continue;
+    const int ox = (int)(m % g.OW);
+    const long long q = m / g.OW;
+    const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
+    const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+    TO* yp = y + op * g.ldy;
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      const int n = n0 + wn * WTN + i * 16 + (lane >> 4) * 4;
+      if (n >= g.K) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float a = acc[i][j][e];
+        if (bias && n + e < g.K) a += bias[n + e];
+        if (relu) a = fmaxf(a, 0.f);
+        v[e] = a;
+      }
+      if (n + 3 < g.K && (g.ldy & 3) == 0) {
+        Store4<TO>::st(yp + n, v);
+      } else {
+        for (int e = 0; e < 4 && n + e < g.K; ++e) io<TO>::st(yp, n + e, v[e]);
+      }
+    }
+  }
+}
+
+// zero the output pixels of a phase whose tap set is empty (e.g. odd rows of a 1x1/s2 dgrad)
+template <typename TO>
+__global__ void phase_zero_kernel(TO* y, ConvGeom g) {
+  const long long total = g.M * g.K;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int n = (int)(i % g.K);
+    const long long m = i / g.K;
+    const int ox = (int)(m % g.OW);
+    const long long q = m / g.OW;
+    const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
+    const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+    io<TO>::st(y, op * g.ldy + n, 0.f);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// weight gradient: dW[co][kk] = sum_p dY[p][co] * x_col[p][kk], kk = (r, s, c)
+// MFMA A = x_col^T (rows kk), B = dY (cols co).  LDS tiles are stored pixel-major as loaded and the
+// k-contiguous fragments come from ds_read_b64_tr_b16 (bf16) / strided ds_read_b32 (f32).
+// Split-K over pixels; every split writes an fp32 slab tile, a reduce kernel sums the slabs.
+// ------------------------------------------------------------------------------------------------
+template <typename T> struct WG;
+template <> struct WG<bf16_t> {
+  static constexpr int BKP = 32;                   // pixels per k-tile
+  static constexpr int PADB = 32;                  // row pad bytes (row stride == 8 dwords mod 64)
+};
+template <> struct WG<float> {
+  static constexpr int BKP = 16;
+  static constexpr int PADB = 64;                  // row stride == 16 dwords mod 32
+};
+
+// MFMA k index (8g + j) -> LDS row, conflict-free for the transpose reads
+__device__ __forceinline__ int kperm(int g, int j) { return 16 * (g >> 1) + 8 * (j >> 2) + 4 * (g & 1) + (j & 3); }
+
+template <typename T, int BMW, int BNW>
+__global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                    float* __restrict__ slab, ConvGeom g, long long pix_per_split) {
+  constexpr int VEC = MF<T>::VEC;
+  constexpr int BKP = WG<T>::BKP;
+  constexpr int ROWX = BMW * (int)sizeof(T) + WG<T>::PADB;
+  constexpr int ROWD = BNW * (int)sizeof(T) + WG<T>::PADB;
+  constexpr int XCH = BMW / VEC, DCH = BNW / VEC;          // 16-byte chunks per row
+  constexpr int X_IT = BKP * XCH / 256, D_IT = BKP * DCH / 256;
+  static_assert(X_IT >= 1 && D_IT >= 1 && (256 % XCH) == 0 && (256 % DCH) == 0, "wgrad tile");
+  constexpr int WTM = BMW / 2, WTN = BNW / 2, FM = WTM / 16, FN = WTN / 16;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BKP * (ROWX + ROWD)];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int kk0 = blockIdx.x * BMW, co0 = blockIdx.y * BNW;
+  const long long p_begin = (long long)blockIdx.z * pix_per_split;
+  const long long p_end = min(p_begin + pix_per_split, g.M);
+
+  // x_col chunk of this thread: fixed (r, s, c)
+  const int xc = t % XCH;
+  const int kkx = kk0 + xc * VEC;
+  const bool kk_ok = kkx < g.KK;
+  const int tapx = kk_ok ? kkx / g.C : 0, cx = kk_ok ? kkx % g.C : 0;
+  const int rx = tapx / g.S, sx_ = tapx % g.S;
+  const int dc = t % DCH;
+  const int cod = co0 + dc * VEC;
+  const bool co_ok = cod < g.K;
+
+  // pixel state per loaded row
+  long long xp[X_IT];
+  long long dp[D_IT];
+#pragma unroll
+  for (int i = 0; i < X_IT; ++i) xp[i] = p_begin + t / XCH + i * (256 / XCH);
+#pragma unroll
+  for (int i = 0; i < D_IT; ++i) dp[i] = p_begin + t / DCH + i * (256 / DCH);
+
+  uint4 rx_[X_IT], rd_[D_IT];
+  auto load = [&]() {
+#pragma unroll
+    for (int i = 0; i < X_IT; ++i) {
+      const long long p = xp[i];
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (p < p_end && kk_ok) {
+        const int ox = (int)(p % g.OW);
+        const long long q = p / g.OW;
+        const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
+        const int iy = oy * g.sy + rx * g.dy + g.py, ix = ox * g.sx + sx_ * g.dx + g.px;
+        if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
+          v = *(const uint4*)(x + ((long long)(img * g.H + iy) * g.W + ix) * g.ldx + cx);
+      }
+      rx_[i] = v;
+      xp[i] += BKP;
+    }
+#pragma unroll
+    for (int i = 0; i < D_IT; ++i) {
+      const long long p = dp[i];
+      rd_[i] = (p < p_end && co_ok) ? *(const uint4*)(dy + p * g.ldy + cod) : make_uint4(0, 0, 0, 0);
+      dp[i] += BKP;
+    }
+  };
+  auto store = [&](int buf) {
+    char* Xs = smem + buf * BKP * (ROWX + ROWD);
+    char* Ds = Xs + BKP * ROWX;
+#pragma unroll
+    for (int i = 0; i < X_IT; ++i) *(uint4*)(Xs + (t / XCH + i * (256 / XCH)) * ROWX + xc * 16) = rx_[i];
+#pragma unroll
+    for (int i = 0; i < D_IT; ++i) *(uint4*)(Ds + (t / DCH + i * (256 / DCH)) * ROWD + dc * 16) = rd_[i];
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const long long npix = p_end > p_begin ? p_end - p_begin : 0;
+  const int nk = (int)((npix + BKP - 1) / BKP);
+  if (nk > 0) {
+    load();
+    store(0);
+    __syncthreads();
+  }
+  const int gq = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) load();
+    const char* Xs = smem + buf * BKP * (ROWX + ROWD);
+    const char* Ds = Xs + BKP * ROWX;
+    if constexpr (sizeof(T) == 2) {
+      bf16x8 af[FM], bfr[FN];
+      const int r0 = kperm(gq, q4), r1 = kperm(gq, 4 + q4);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int col = wm * WTM + i * 16 + 4 * p4;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Xs + r0 * ROWX + col * 2));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Xs + r1 * ROWX + col * 2));
+        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = wn * WTN + j * 16 + 4 * p4;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ds + r0 * ROWD + col * 2));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ds + r1 * ROWD + col * 2));
+        bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < BKP / 4; ++ks) {
+        const int row = ks * 4 + gq;
+        float af[FM], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = *(const float*)(Xs + row * ROWX + (wm * WTM + i * 16 + li) * 4);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfr[j] = *(const float*)(Ds + row * ROWD + (wn * WTN + j * 16 + li) * 4);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  // slab[split][co][kk]: lane holds kk .. kk+3 (rows) of channel co (column)
+  float* sl = slab + (long long)blockIdx.z * g.K * g.KK;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int kk = kk0 + wm * WTM + i * 16 + 4 * gq;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int co = co0 + wn * WTN + j * 16 + li;
+      if (co >= g.K || kk >= g.KK) continue;
+      float* p = sl + (long long)co * g.KK + kk;
+      if (kk + 3 < g.KK) {
+        *(float4*)p = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      } else {
+        for (int e = 0; e < 4 && kk + e < g.KK; ++e) p[e] = acc[i][j][e];
+      }
+    }
+  }
+}
+
+// sum the split slabs and write dW in the requested layout: 0 = [K][R][S][C] (packed, C = physical),
+// 1 = [K][C_real][R][S] (PyTorch OIHW).  accumulate: dst += sum.
+__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int K, int R, int S, int C, int c_real,
+                                    int k_real, float* __restrict__ dst, int layout, int accumulate) {
+  const long long KK = (long long)R * S * C;
+  const long long total = (long long)K * KK;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int kk = (int)(i % KK), k = (int)(i / KK);
+    const int c = kk % C, tap = kk / C, r = tap / S, s = tap % S;
+    if (c >= c_real || k >= k_real) continue;
+    float sum = 0.f;
+    for (int z = 0; z < splits; ++z) sum += slab[(long long)z * total + i];
+    long long o;
+    if (layout == 0) o = ((long long)k * R * S + tap) * C + c;
+    else o = (((long long)k * c_real + c) * R + r) * S + s;
+    dst[o] = accumulate ? dst[o] + sum : sum;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// weight packing: dst[k][rr][ss][c] (c < Cp; zero for c >= Cd) from an fp32 source
+//   layout 0: src[k][c][r][s]  (Conv2d OIHW; ConvTranspose2d used as a conv over its output grad)
+//   layout 1: src[c][k][r][s]  (transposed roles: conv dgrad, ConvTranspose2d forward)
+//   r = r0 + rr*rstep, s = s0 + ss*sstep
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void weight_pack_kernel(const float* __restrict__ src, T* __restrict__ dst, int Kd, int Kr, int Cd, int Rs,
+                                   int Ss, int Cp, int layout, int r0, int rstep, int Rn, int s0, int sstep, int Sn) {
+  const long long total = (long long)Kd * Rn * Sn * Cp;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % Cp);
+    long long q = i / Cp;
+    const int ss = (int)(q % Sn);
+    q /= Sn;
+    const int rr = (int)(q % Rn);
+    const int k = (int)(q / Rn);
+    float v = 0.f;
+    if (c < Cd && k < Kr) {
+      const int r = r0 + rr * rstep, s = s0 + ss * sstep;
+      const long long idx = layout == 0 ? (((long long)k * Cd + c) * Rs + r) * Ss + s
+                                        : (((long long)c * Kr + k) * Rs + r) * Ss + s;
+      v = src[idx];
+    }
+    io<T>::st(dst, i, v);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+template <typename T, typename TO, int BM, int BN, int WM, int WN>
+void launch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, const float* bias, int relu,
+                  hipStream_t s) {
+  const dim3 grid((unsigned)((g.M + BM - 1) / BM), (unsigned)((g.K + BN - 1) / BN));
+  hipLaunchKernelGGL((igemm_kernel<T, TO, BM, BN, WM, WN>), grid, dim3(256), 0, s, (const T*)x, (const T*)w, (TO*)y,
+                     g, bias, relu);
+}
+
+template <typename T, typename TO>
+void dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, const float* bias, int relu,
+                    hipStream_t s) {
+  if (g.K <= 16)
+    launch_igemm<T, TO, 256, 16, 4, 1>(x, w, y, g, bias, relu, s);
+  else if (g.K <= 64)
+    launch_igemm<T, TO, 256, 64, 4, 1>(x, w, y, g, bias, relu, s);
+  else
+    launch_igemm<T, TO, 128, 128, 2, 2>(x, w, y, g, bias, relu, s);
+}
+
+struct WgradPlan {
+  int bmw, bnw, mt, nt, splits;
+  long long pps;
+};
+
+template <typename T>
+WgradPlan plan_wgrad(const ConvGeom& g) {
+  WgradPlan p;
+  p.bmw = g.KK <= 64 ? 64 : 128;
+  p.bnw = g.K <= 64 ? 64 : 128;
+  p.mt = (g.KK + p.bmw - 1) / p.bmw;
+  p.nt = (g.K + p.bnw - 1) / p.bnw;
+  const long long tiles = (long long)p.mt * p.nt;
+  const int bkp = WG<T>::BKP;
+  const long long max_splits_by_work = std::max<long long>(1, g.M / (bkp * 8));   // >= 8 k-tiles per split
+  long long want = std::max<long long>(1, (1024 + tiles - 1) / tiles);
+  const long long slab_cap = std::max<long long>(1, (64ll << 20) / (4ll * g.K * g.KK + 1));  // <= 64 MiB of slabs
+  long long sp = std::min(std::min(want, max_splits_by_work), slab_cap);
+  sp = std::max<long long>(1, std::min<long long>(sp, 65535));
+  p.pps = (g.M + sp - 1) / sp;
+  p.pps = (p.pps + bkp - 1) / bkp * bkp;
+  p.splits = (int)((g.M + p.pps - 1) / p.pps);
+  if (p.splits < 1) p.splits = 1;
+  return p;
+}
+
+template <typename T>
+void launch_wgrad(const void* x, const void* dy, float* slab, const ConvGeom& g, const WgradPlan& p, hipStream_t s) {
+  const dim3 grid(p.mt, p.nt, p.splits);
+  if (p.bmw == 64 && p.bnw == 64)
+    hipLaunchKernelGGL((wgrad_kernel<T, 64, 64>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, g, p.pps);
+  else if (p.bmw == 64)
+    hipLaunchKernelGGL((wgrad_kernel<T, 64, 128>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, g, p.pps);
+  else if (p.bnw == 64)
+    hipLaunchKernelGGL((wgrad_kernel<T, 128, 64>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, g, p.pps);
+  else
+    hipLaunchKernelGGL((wgrad_kernel<T, 128, 128>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, g, p.pps);
+}
+
+bool geom_ok(const ConvGeom& g, int dt) {
+  const int vec = dt == SSSEG_BF16 ? 8 : 4;
+  if (g.C % vec || g.ldx % vec || g.ldw % vec) return false;
+  if (g.N < 1 || g.OH < 1 || g.OW < 1 || g.K < 1 || g.C < 1) return false;
+  if (g.R < 0 || g.S < 0) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" int ssseg_conv_igemm(const void* x, const void* w, void* y, const ssseg_conv_desc* d, int dt, int dt_out,
+                                const float* bias, int relu, ssseg_stream_t stream) {
+  ConvGeom g;
+  if (!make_geom(d, g) || !y) return SSSEG_EINVAL;
+  if (!geom_ok(g, dt)) return SSSEG_EINVAL;
+  if (g.M == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (g.KK == 0) {   // no taps reach this output phase: the contribution is zero
+    if (dt_out == SSSEG_F32)
+      hipLaunchKernelGGL(phase_zero_kernel<float>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, (float*)y, g);
+    else
+      hipLaunchKernelGGL(phase_zero_kernel<bf16_t>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, (bf16_t*)y, g);
+    SSSEG_LAUNCH_CHECK();
+    return 0;
+  }
+  if (!x || !w) return SSSEG_EINVAL;
+  if (dt == SSSEG_BF16 && dt_out == SSSEG_BF16)
+    dispatch_igemm<bf16_t, bf16_t>(x, w, y, g, bias, relu, s);
+  else if (dt == SSSEG_BF16 && dt_out == SSSEG_F32)
+    dispatch_igemm<bf16_t, float>(x, w, y, g, bias, relu, s);
+  else if (dt == SSSEG_F32 && dt_out == SSSEG_F32)
+    dispatch_igemm<float, float>(x, w, y, g, bias, relu, s);
+  else
+    return SSSEG_EUNSUPPORTED;
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" size_t ssseg_conv_wgrad_workspace_bytes(const ssseg_conv_desc* d, int dt) {
+  ConvGeom g;
+  if (!make_geom(d, g)) return 0;
+  const WgradPlan p = dt == SSSEG_BF16 ? plan_wgrad<bf16_t>(g) : plan_wgrad<float>(g);
+  return (size_t)p.splits * g.K * g.KK * sizeof(float) + 256;
+}
+
+extern "C" int ssseg_conv_wgrad(const void* x, const void* dy, float* dw, const ssseg_conv_desc* d, int dt,
+                                int64_t c_real, int64_t k_real, int layout, int accumulate, void* ws, size_t ws_bytes,
+                                ssseg_stream_t stream) {
+  ConvGeom g;
+  if (!make_geom(d, g) || !x || !dy || !dw) return SSSEG_EINVAL;
+  if (!geom_ok(g, dt) || g.ldy % (dt == SSSEG_BF16 ? 8 : 4) || g.K % (dt == SSSEG_BF16 ? 8 : 4)) return SSSEG_EINVAL;
+  if (c_real < 1 || c_real > g.C || k_real < 1 || k_real > g.K || (layout != 0 && layout != 1)) return SSSEG_EINVAL;
+  if (!ws || ws_bytes < ssseg_conv_wgrad_workspace_bytes(d, dt)) return SSSEG_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  float* slab = (float*)ws;
+  WgradPlan p;
+  if (dt == SSSEG_BF16) {
+    p = plan_wgrad<bf16_t>(g);
+    launch_wgrad<bf16_t>(x, dy, slab, g, p, s);
+  } else if (dt == SSSEG_F32) {
+    p = plan_wgrad<float>(g);
+    launch_wgrad<float>(x, dy, slab, g, p, s);
+  } else {
+    return SSSEG_EUNSUPPORTED;
+  }
+  const long long total = (long long)g.K * g.KK;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ssseg_grid(total, 256)), dim3(256), 0, s, slab, p.splits, g.K, g.R, g.S,
+                     g.C, (int)c_real, (int)k_real, dw, layout, accumulate);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_weight_pack(const float* src, void* dst, int64_t Kd, int64_t Kr, int64_t Cd, int64_t Rs, int64_t Ss,
+                                 int64_t Cp, int layout, int64_t r0, int64_t rstep, int64_t Rn, int64_t s0, int64_t sstep,
+                                 int64_t Sn, int dt, ssseg_stream_t stream) {
+  if (!src || !dst || Cp < Cd || Kd < 1 || Kr < 1 || Kr > Kd || Rn < 0 || Sn < 0 || (layout != 0 && layout != 1))
+    return SSSEG_EINVAL;
+  if (Rn > 0 && (r0 < 0 || r0 >= Rs || r0 + (Rn - 1) * rstep < 0 || r0 + (Rn - 1) * rstep >= Rs)) return SSSEG_EINVAL;
+  if (Sn > 0 && (s0 < 0 || s0 >= Ss || s0 + (Sn - 1) * sstep < 0 || s0 + (Sn - 1) * sstep >= Ss)) return SSSEG_EINVAL;
+  const long long total = Kd * Rn * Sn * Cp;
+  if (total == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (dt == SSSEG_BF16)
+    hipLaunchKernelGGL(weight_pack_kernel<bf16_t>, dim3(ssseg_grid(total, 256)), dim3(256), 0, s, src, (bf16_t*)dst,
+                       (int)Kd, (int)Kr, (int)Cd, (int)Rs, (int)Ss, (int)Cp, layout, (int)r0, (int)rstep, (int)Rn,
+                       (int)s0, (int)sstep, (int)Sn);
+  else if (dt == SSSEG_F32)
+    hipLaunchKernelGGL(weight_pack_kernel<float>, dim3(ssseg_grid(total, 256)), dim3(256), 0, s, src, (float*)dst,
+                       (int)Kd, (int)Kr, (int)Cd, (int)Rs, (int)Ss, (int)Cp, layout, (int)r0, (int)rstep, (int)Rn,
+                       (int)s0, (int)sstep, (int)Sn);
+  else
+    return SSSEG_EUNSUPPORTED;
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,200 @@
+// Max pooling (ResNet stem MaxPool2d(3,2,1); simple_unet.py:18 MaxPool2d(2,2,ceil_mode=True)) and the
+// NHWC window copy used for torch.cat / _center_crop (unet.py:40-45, simple_unet.py:86-91), gfx950.
+#include "common.h"
+
+namespace {
+
+template <typename T>
+__global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, uint8_t* __restrict__ idx, int N, int H,
+                                   int W, int C, int OH, int OW, int k, int s, int p) {
+  const int64_t total = (int64_t)N * OH * OW * C;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    int64_t q = i / C;
+    const int ow = (int)(q % OW);
+    q /= OW;
+    const int oh = (int)(q % OH);
+    const int n = (int)(q / OH);
+    // PyTorch CPU order: maxval = -inf, maxindex = first valid tap; update when v > maxval or v is NaN
+    float m = -INFINITY;
+    int best = -1;
+    for (int kh = 0; kh < k; ++kh) {
+      const int ih = oh * s - p + kh;
+      if (ih < 0 || ih >= H) continue;
+      for (int kw = 0; kw < k; ++kw) {
+        const int iw = ow * s - p + kw;
+        if (iw < 0 || iw >= W) continue;
+        const float v = io<T>::ld(x, (((int64_t)n * H + ih) * W + iw) * C + c);
+        if (best < 0) best = kh * k + kw;
+        if (v > m || v != v) {
+          m = v;
+          best = kh * k + kw;
+        }
+      }
+    }
+    io<T>::st(y, i, m);
+    idx[i] = (uint8_t)best;
+  }
+}
+
+template <typename T>
+__global__ void maxpool_bwd_kernel(const T* __restrict__ gy, const uint8_t* __restrict__ idx, T* __restrict__ gx, int N,
+                                   int H, int W, int C, int OH, int OW, int k, int s, int p) {
+  const int64_t total = (int64_t)N * H * W * C;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    int64_t q = i / C;
+    const int iw = (int)(q % W);
+    q /= W;
+    const int ih = (int)(q % H);
+    const int n = (int)(q / H);
+    const int oh0 = max(0, (ih + p - k + s) / s), oh1 = min(OH - 1, (ih + p) / s);
+    const int ow0 = max(0, (iw + p - k + s) / s), ow1 = min(OW - 1, (iw + p) / s);
+    float acc = 0.f;
+    for (int oh = oh0; oh <= oh1; ++oh) {
+      const int kh = ih - (oh * s - p);
+      if (kh < 0 || kh >= k) continue;
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        const int kw = iw - (ow * s - p);
+        if (kw < 0 || kw >= k) continue;
+        const int64_t o = (((int64_t)n * OH + oh) * OW + ow) * C + c;
+        if (idx[o] == kh * k + kw) acc += io<T>::ld(gy, o);
+      }
+    }
+    io<T>::st(gx, i, acc);
+  }
+}
+
+template <typename T>
+__global__ void nhwc_copy_kernel(const T* __restrict__ src, T* __restrict__ dst, int N, int H, int W, int C, int sH,
+                                 int sW, int64_t sld, int soy, int sox, int dH, int dW, int64_t dld, int doy, int dox) {
+  const int64_t total = (int64_t)N * H * W * C;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    int64_t q = i / C;
+    const int w = (int)(q % W);
+    q /= W;
+    const int h = (int)(q % H);
+    const int n = (int)(q / H);
+    const T v = src[(((int64_t)n * sH + h + soy) * sW + w + sox) * sld + c];
+    dst[(((int64_t)n * dH + h + doy) * dW + w + dox) * dld + c] = v;
+  }
+}
+
+// 16-byte vector variant (C, sld, dld multiples of 16/sizeof(T) elements)
+__global__ void nhwc_copy_v16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, int N, int H, int W, int C4,
+                                     int sH, int sW, int64_t sld4, int soy, int sox, int dH, int dW, int64_t dld4, int doy,
+                                     int dox) {
+  const int64_t total = (int64_t)N * H * W * C4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4);
+    int64_t q = i / C4;
+    const int w = (int)(q % W);
+    q /= W;
+    const int h = (int)(q % H);
+    const int n = (int)(q / H);
+    dst[(((int64_t)n * dH + h + doy) * dW + w + dox) * dld4 + c] = src[(((int64_t)n * sH + h + soy) * sW + w + sox) * sld4 + c];
+  }
+}
+
+}  // namespace
+
+extern "C" int ssseg_maxpool_fwd(const void* x, void* y, uint8_t* idx, int64_t N, int64_t H, int64_t W, int64_t C,
+                                 int64_t OH, int64_t OW, int64_t k, int64_t s, int64_t p, int dt, ssseg_stream_t stream) {
+  if (!x || !y || !idx || k < 1 || k > 15 || s < 1 || p < 0) return SSSEG_EINVAL;
+  const int64_t total = N * OH * OW * C;
+  if (total == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 g(ssseg_grid(total, 256, 256 * 16)), b(256);
+  if (dt == SSSEG_BF16)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)x, (bf16_t*)y, idx, (int)N, (int)H,
+                       (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
+  else if (dt == SSSEG_F32)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<float>, g, b, 0, st, (const float*)x, (float*)y, idx, (int)N, (int)H, (int)W,
+                       (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
+  else
+    return SSSEG_EUNSUPPORTED;
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_maxpool_bwd(const void* gy, const uint8_t* idx, void* gx, int64_t N, int64_t H, int64_t W,
+                                 int64_t C, int64_t OH, int64_t OW, int64_t k, int64_t s, int64_t p, int dt,
+                                 ssseg_stream_t stream) {
+  if (!gy || !gx || !idx || k < 1 || s < 1 || p < 0) return SSSEG_EINVAL;
+  const int64_t total = N * H * W * C;
+  if (total == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 g(ssseg_grid(total, 256, 256 * 16)), b(256);
+  if (dt == SSSEG_BF16)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)gy, idx, (bf16_t*)gx, (int)N, (int)H,
+                       (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
+  else if (dt == SSSEG_F32)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, g, b, 0, st, (const float*)gy, idx, (float*)gx, (int)N, (int)H,
+                       (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
+  else
+    return SSSEG_EUNSUPPORTED;
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_nhwc_copy(const void* src, void* dst, int64_t N, int64_t H, int64_t W, int64_t C, int64_t sH,
+                               int64_t sW, int64_t sld, int64_t soy, int64_t sox, int64_t dH, int64_t dW, int64_t dld,
+                               int64_t doy, int64_t dox, int dt, ssseg_stream_t stream) {
+  if (!src || !dst || C < 0 || soy < 0 || sox < 0 || doy < 0 || dox < 0 || H + soy > sH || W + sox > sW ||
+      H + doy > dH || W + dox > dW)
+    return SSSEG_EINVAL;
+  const int64_t total = N * H * W * C;
+  if (total == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const int esz = dt == SSSEG_BF16 ? 2 : 4;
+  const int v = 16 / esz;
+  if (C % v == 0 && sld % v == 0 && dld % v == 0 && (((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+    const int64_t t4 = total / v;
+    hipLaunchKernelGGL(nhwc_copy_v16_kernel, dim3(ssseg_grid(t4, 256, 256 * 16)), dim3(256), 0, st, (const uint4*)src,
+                       (uint4*)dst, (int)N, (int)H, (int)W, (int)(C / v), (int)sH, (int)sW, sld / v, (int)soy, (int)sox,
+                       (int)dH, (int)dW, dld / v, (int)doy, (int)dox);
+  } else if (dt == SSSEG_BF16) {
+    hipLaunchKernelGGL(nhwc_copy_kernel<bf16_t>, dim3(ssseg_grid(total, 256, 256 * 16)), dim3(256), 0, st,
+                       (const bf16_t*)src, (bf16_t*)dst, (int)N, (int)H, (int)W, (int)C, (int)sH, (int)sW, sld, (int)soy,
+                       (int)sox, (int)dH, (int)dW, dld, (int)doy, (int)dox);
+  } else if (dt == SSSEG_F32) {
+    hipLaunchKernelGGL(nhwc_copy_kernel<float>, dim3(ssseg_grid(total, 256, 256 * 16)), dim3(256), 0, st,
+                       (const float*)src, (float*)dst, (int)N, (int)H, (int)W, (int)C, (int)sH, (int)sW, sld, (int)soy,
+                       (int)sox, (int)dH, (int)dW, dld, (int)doy, (int)dox);
+  } else {
+    return SSSEG_EUNSUPPORTED;
+  }
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_zero(void* p, size_t bytes, ssseg_stream_t stream) {
+  if (!p) return SSSEG_EINVAL;
+  if (bytes == 0) return 0;
+  SSSEG_TRY(hipMemsetAsync(p, 0, bytes, (hipStream_t)stream));
+  return 0;
+}
+
+namespace {
+template <typename T>
+__global__ void relu_bwd_kernel(const T* __restrict__ gy, const T* __restrict__ y, T* __restrict__ gx, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    io<T>::st(gx, i, io<T>::ld(y, i) > 0.f ? io<T>::ld(gy, i) : 0.f);
+}
+}  // namespace
+
+extern "C" int ssseg_relu_bwd(const void* gy, const void* y, void* gx, int64_t n, int dt, ssseg_stream_t stream) {
+  if (!gy || !y || !gx || n < 0) return SSSEG_EINVAL;
+  if (n == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 g(ssseg_grid(n, 256, 256 * 16)), b(256);
+  if (dt == SSSEG_BF16)
+    hipLaunchKernelGGL(relu_bwd_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)gy, (const bf16_t*)y, (bf16_t*)gx, n);
+  else if (dt == SSSEG_F32)
+    hipLaunchKernelGGL(relu_bwd_kernel<float>, g, b, 0, st, (const float*)gy, (const float*)y, (float*)gx, n);
+  else
+    return SSSEG_EUNSUPPORTED;
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}

@@ -44,7 +44,35 @@ SIGS = {
     'ssseg_ema_update': (i32, [vp, vp, i64, f64, vp]),
     'ssseg_sqnorm_accum': (i32, [vp, i64, vp, vp, sz, vp]),
     'ssseg_sgd_step': (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]),
+    # convolution engine
+    'ssseg_conv_igemm': (i32, [vp, vp, vp, vp, i32, i32, vp, i32, vp]),
+    'ssseg_conv_wgrad_workspace_bytes': (sz, [vp, i32]),
+    'ssseg_conv_wgrad': (i32, [vp, vp, vp, vp, i32, i64, i64, i32, i32, vp, sz, vp]),
+    'ssseg_weight_pack': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, i32, i64, i64, i64, i64, i64, i64, i32, vp]),
+    # batch norm
+    'ssseg_bn_workspace_bytes': (sz, [i64]),
+    'ssseg_bn_stats': (i32, [vp, i64, i64, i64, i32, vp, vp, sz, vp]),
+    'ssseg_bn_finalize': (i32, [vp, i64, f64, f32, f32, vp, vp, vp, vp, vp, vp]),
+    'ssseg_bn_eval_params': (i32, [vp, vp, f32, i64, vp, vp, vp]),
+    'ssseg_bn_apply': (i32, [vp, vp, vp, i64, i64, i64, i64, i64, vp, vp, vp, vp, i32, i32, vp]),
+    'ssseg_bn_bwd_reduce': (i32, [vp, vp, vp, i64, i64, i64, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp, sz, vp]),
+    'ssseg_bn_param_grad': (i32, [vp, i64, vp, vp, vp]),
+    'ssseg_bn_bwd_apply': (i32, [vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, vp, vp, vp, vp, i32, i32, vp, f64,
+                                 i32, vp]),
+    # pooling / copies
+    'ssseg_maxpool_fwd': (i32, [vp, vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, i32, vp]),
+    'ssseg_maxpool_bwd': (i32, [vp, vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, i32, vp]),
+    'ssseg_nhwc_copy': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i32, vp]),
+    'ssseg_zero': (i32, [vp, sz, vp]),
+    'ssseg_relu_bwd': (i32, [vp, vp, vp, i64, i32, vp]),
 }
+
+
+class ConvDesc(ctypes.Structure):
+    """Mirror of ssseg_conv_desc (include/ssseg.h)."""
+    _fields_ = [(n, ctypes.c_int64) for n in (
+        'N', 'H', 'W', 'C', 'ldx', 'OH', 'OW', 'K', 'R', 'S', 'sy', 'sx', 'dy', 'dx', 'py', 'px',
+        'outH', 'outW', 'osy', 'osx', 'ooy', 'oox', 'ldy', 'ldw')]
 
 _lib = None
 

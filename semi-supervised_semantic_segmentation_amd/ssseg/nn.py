@@ -1,0 +1,590 @@
+"""MI355X-native layers: drop-in subclasses of torch.nn's Conv2d / ConvTranspose2d / BatchNorm2d /
+MaxPool2d whose forward and backward run libssseg.so kernels.
+
+Activation convention inside a network: a 4-D tensor [N, Cp, H, W] in channels_last memory format
+(physically NHWC), Cp = channels rounded up to the MFMA vector (8 for bf16, 4 for fp32), padded
+channels zero.  Parameter names, shapes and layouts are PyTorch's, so reference state_dicts load.
+
+Gradients of parameters are accumulated by the kernels directly into `param.grad` (the flat
+gradient arena when one is attached, ssseg.arena) and the autograd Functions return None for them;
+a registered reducer (ssseg.ddp) is told when each parameter's gradient is complete so the RCCL
+all-reduce of its bucket can start during the rest of the backward pass.
+"""
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from . import native as N
+
+_CFG = {'dtype': torch.bfloat16, 'sync_bn': True}
+
+
+def set_compute_dtype(dtype):
+    assert dtype in (torch.bfloat16, torch.float32)
+    _CFG['dtype'] = dtype
+
+
+def compute_dtype():
+    return _CFG['dtype']
+
+
+def set_sync_bn(flag):
+    _CFG['sync_bn'] = bool(flag)
+
+
+def vec(dtype=None):
+    return 8 if (dtype or _CFG['dtype']) == torch.bfloat16 else 4
+
+
+def rup(c, v):
+    return (c + v - 1) // v * v
+
+
+def _zero_(t):
+    N.call('ssseg_zero', N.dev_ptr(t), t.numel() * t.element_size(), N.stream())
+    return t
+
+
+def new_act(n, c, h, w, dtype, device, zero=False):
+    t = torch.empty((n, c, h, w), dtype=dtype, device=device, memory_format=torch.channels_last)
+    return _zero_(t) if zero else t
+
+
+def _is_act(x, c_phys=None):
+    return (x.is_cuda and x.dim() == 4 and (c_phys is None or x.shape[1] == c_phys)
+            and x.dtype == _CFG['dtype'] and x.is_contiguous(memory_format=torch.channels_last))
+
+
+def _need_act(x, c_phys, what):
+    if not _is_act(x, c_phys):
+        raise RuntimeError(f'ssseg: {what} expects a {_CFG["dtype"]} channels_last HIP activation with {c_phys} '
+                           f'channels, got {tuple(x.shape)} {x.dtype} {x.device} strides {x.stride()}')
+
+
+# ------------------------------------------------------------------------------------------------
+# parameter gradient plumbing
+# ------------------------------------------------------------------------------------------------
+def _grad_of(p):
+    if p.grad is None:
+        p.grad = torch.zeros_like(p)
+    return p.grad
+
+
+def _ready(*params):
+    for p in params:
+        r = getattr(p, '_ssseg_reducer', None)
+        if r is not None:
+            r.mark_ready(p)
+
+
+# ------------------------------------------------------------------------------------------------
+# model input / output boundary
+# ------------------------------------------------------------------------------------------------
+class _ToAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        n, c, h, w = x.shape
+        cp = rup(c, vec())
+        y = new_act(n, cp, h, w, _CFG['dtype'], x.device)
+        xc = x if x.is_contiguous() else x.contiguous()
+        N.call('ssseg_nchw_to_nhwc', N.dev_ptr(xc, 'image'), N.dev_ptr(y), n, c, h, w, cp, N.dt_code(xc),
+               N.dt_code(y), N.stream())
+        ctx.meta = (n, c, h, w, cp, x.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        n, c, h, w, cp, dt = ctx.meta
+        gx = torch.empty((n, c, h, w), dtype=dt, device=gy.device)
+        N.call('ssseg_nhwc_to_nchw', N.dev_ptr(gy), N.dev_ptr(gx), n, c, h, w, cp, N.dt_code(gy), N.dt_code(gx),
+               N.stream())
+        return gx
+
+
+def to_act(x):
+    """NCHW image batch (any float dtype the kernels take) -> compute-dtype NHWC activation."""
+    if _is_act(x) and x.shape[1] % vec() == 0:
+        return x
+    return _ToAct.apply(x)
+
+
+# ------------------------------------------------------------------------------------------------
+# convolution
+# ------------------------------------------------------------------------------------------------
+def _desc(**kw):
+    d = N.ConvDesc()
+    for k, v in kw.items():
+        setattr(d, k, int(v))
+    return d
+
+
+def _phases(stride, pad, R, in_full, dil=1):
+    """Output-phase decomposition of a strided transposed contraction (conv dgrad / ConvTranspose2d
+    forward): map X (size in_full) gathers from map Y with x[s*q + phi] = sum_j y[q - j + delta] w[r0 + s*j].
+    Returns [(phi, r0, Rn, delta, Q)]."""
+    assert dil == 1, 'strided transposed contraction with dilation is not supported'
+    out = []
+    for phi in range(stride):
+        r0 = (phi + pad) % stride
+        rn = 0 if r0 >= R else (R - r0 + stride - 1) // stride
+        delta = (phi + pad - r0) // stride
+        q = (in_full - phi + stride - 1) // stride
+        out.append((phi, r0, rn, delta, max(q, 0)))
+    return out
+
+
+class _ConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, mod, relu):
+        y = mod._ssseg_forward(x, relu)
+        ctx.mod, ctx.relu = mod, relu
+        ctx.save_for_backward(x, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, y = ctx.saved_tensors
+        mod = ctx.mod
+        gy = mod._grad_in(gy)
+        if ctx.relu:
+            gm = torch.empty_like(gy)
+            N.call('ssseg_relu_bwd', N.dev_ptr(gy), N.dev_ptr(y), N.dev_ptr(gm), gy.numel(), N.dt_code(gy), N.stream())
+            gy = gm
+        mod._ssseg_wgrad(x, gy)
+        dx = mod._ssseg_dgrad(gy, x.shape) if ctx.needs_input_grad[0] else None
+        return dx, None, None, None, None
+
+
+def _bias_grad(mod, gy):
+    """d bias += per-channel sum of gy (NHWC)."""
+    if mod.bias is None or not mod.bias.requires_grad:
+        return
+    n, cp, h, w = gy.shape
+    C = mod.bias.numel()
+    sums = torch.empty(2 * C, dtype=torch.float64, device=gy.device)
+    nb = N.lib().ssseg_bn_workspace_bytes(C)
+    ws = N.workspace(nb, gy.device)
+    N.call('ssseg_bn_stats', N.dev_ptr(gy), n * h * w, C, cp, N.dt_code(gy), N.dev_ptr(sums), N.dev_ptr(ws), nb,
+           N.stream())
+    N.call('ssseg_bn_param_grad', N.dev_ptr(sums), C, None, N.dev_ptr(_grad_of(mod.bias)), N.stream())
+
+
+class _ConvBase:
+    """Shared host logic of Conv2d / ConvTranspose2d: packed-weight cache and launches."""
+
+    def _ssseg_init(self, head=False):
+        self._ssseg_head = head           # writes fp32 logits with the real channel count visible
+        self._ssseg_packs = {}
+
+    def invalidate_packed(self):
+        self._ssseg_packs = {}
+
+    def _pack(self, key, Kd, Kr, Cd, Cp, layout, r0, rstep, Rn, s0, sstep, Sn):
+        t = self._ssseg_packs.get(key)
+        if t is None:
+            w = self.weight.detach()
+            w = w if w.is_contiguous() else w.contiguous()
+            Rs, Ss = self.weight.shape[2], self.weight.shape[3]
+            t = torch.empty(max(Kd * Rn * Sn * Cp, 1), dtype=_CFG['dtype'], device=w.device)
+            N.call('ssseg_weight_pack', N.dev_ptr(w, 'weight'), N.dev_ptr(t), Kd, Kr, Cd, Rs, Ss, Cp, layout, r0,
+                   rstep, Rn, s0, sstep, Sn, N.dt_code(t), N.stream())
+            self._ssseg_packs[key] = t
+        return t
+
+    def _igemm(self, x, w, y, desc, out_dt, bias=None, relu=False):
+        N.call('ssseg_conv_igemm', N.dev_ptr(x), N.dev_ptr(w), N.dev_ptr(y), ctypes_ref(desc), N.dt_code(x), out_dt,
+               N.dev_ptr(bias) if bias is not None else None, int(bool(relu)), N.stream())
+
+
+def ctypes_ref(d):
+    import ctypes
+    return ctypes.byref(d)
+
+
+class Conv2d(nn.Conv2d, _ConvBase):
+    """nn.Conv2d on the implicit-GEMM engine (groups == 1)."""
+
+    def __init__(self, *args, head=False, **kw):
+        super().__init__(*args, **kw)
+        if self.groups != 1:
+            raise NotImplementedError('ssseg.nn.Conv2d: grouped/depthwise convolution is not implemented')
+        if self.padding_mode != 'zeros':
+            raise NotImplementedError('ssseg.nn.Conv2d: only zero padding')
+        self._ssseg_init(head)
+
+    # geometry helpers
+    def _dims(self):
+        v = vec()
+        return rup(self.in_channels, v), rup(self.out_channels, v)
+
+    def _out_hw(self, H, W):
+        (R, S), (sh, sw), (ph, pw), (dh, dw) = self.kernel_size, self.stride, self.padding, self.dilation
+        return (H + 2 * ph - dh * (R - 1) - 1) // sh + 1, (W + 2 * pw - dw * (S - 1) - 1) // sw + 1
+
+    def _fwd_desc(self, n, H, W):
+        cin, cout = self._dims()
+        (R, S), (sh, sw), (ph, pw), (dh, dw) = self.kernel_size, self.stride, self.padding, self.dilation
+        OH, OW = self._out_hw(H, W)
+        return _desc(N=n, H=H, W=W, C=cin, ldx=cin, OH=OH, OW=OW, K=cout, R=R, S=S, sy=sh, sx=sw, dy=dh, dx=dw,
+                     py=-ph, px=-pw, outH=OH, outW=OW, osy=1, osx=1, ooy=0, oox=0, ldy=cout, ldw=R * S * cin)
+
+    def forward(self, x):
+        if not _is_act(x):
+            x = to_act(x)
+        return _ConvFn.apply(x, self.weight, self.bias, self, False)
+
+    def _ssseg_forward(self, x, relu):
+        cin, cout = self._dims()
+        _need_act(x, cin, 'Conv2d')
+        n, _, H, W = x.shape
+        d = self._fwd_desc(n, H, W)
+        R, S = self.kernel_size
+        w = self._pack('fwd', cout, self.out_channels, self.in_channels, cin, 0, 0, 1, R, 0, 1, S)
+        if self._ssseg_head:
+            y = torch.empty((n, cout, d.OH, d.OW), dtype=torch.float32, device=x.device,
+                            memory_format=torch.channels_last)
+            self._igemm(x, w, y, d, N.F32, self.bias, relu)
+            return y[:, :self.out_channels]
+        y = new_act(n, cout, d.OH, d.OW, _CFG['dtype'], x.device)
+        self._igemm(x, w, y, d, N.dt_code(y), self.bias, relu)
+        return y
+
+    def _grad_in(self, gy):
+        """Incoming output gradient -> physical NHWC compute-dtype tensor."""
+        cin, cout = self._dims()
+        if self._ssseg_head:
+            n, c, h, w = gy.shape
+            g = new_act(n, cout, h, w, _CFG['dtype'], gy.device)
+            gc = gy if gy.is_contiguous() else gy.contiguous()
+            N.call('ssseg_nchw_to_nhwc', N.dev_ptr(gc), N.dev_ptr(g), n, c, h, w, cout, N.dt_code(gc), N.dt_code(g),
+                   N.stream())
+            return g
+        _need_act(gy, cout, 'Conv2d backward')
+        return gy
+
+    def _ssseg_wgrad(self, x, gy):
+        _bias_grad(self, gy)
+        if not self.weight.requires_grad:
+            return
+        n, _, H, W = x.shape
+        d = self._fwd_desc(n, H, W)
+        nb = N.lib().ssseg_conv_wgrad_workspace_bytes(ctypes_ref(d), N.dt_code(x))
+        ws = N.workspace(nb, x.device)
+        N.call('ssseg_conv_wgrad', N.dev_ptr(x), N.dev_ptr(gy), N.dev_ptr(_grad_of(self.weight)), ctypes_ref(d),
+               N.dt_code(x), self.in_channels, self.out_channels, 1, 1, N.dev_ptr(ws), nb, N.stream())
+        if self.bias is not None:
+            _ready(self.weight, self.bias)
+        else:
+            _ready(self.weight)
+
+    def _ssseg_dgrad(self, gy, xshape):
+        cin, cout = self._dims()
+        n, _, H, W = xshape
+        (R, S), (sh, sw), (ph, pw), (dh, dw) = self.kernel_size, self.stride, self.padding, self.dilation
+        OH, OW = gy.shape[2], gy.shape[3]
+        dx = new_act(n, cin, H, W, _CFG['dtype'], gy.device)
+        if sh == 1 and sw == 1:
+            w = self._pack('dgrad', cin, self.in_channels, self.out_channels, cout, 1, R - 1, -1, R, S - 1, -1, S)
+            d = _desc(N=n, H=OH, W=OW, C=cout, ldx=cout, OH=H, OW=W, K=cin, R=R, S=S, sy=1, sx=1, dy=dh, dx=dw,
+                      py=ph - (R - 1) * dh, px=pw - (S - 1) * dw, outH=H, outW=W, osy=1, osx=1, ooy=0, oox=0,
+                      ldy=cin, ldw=R * S * cout)
+            self._igemm(gy, w, dx, d, N.dt_code(dx))
+            return dx
+        for (phy, ry0, rny, dly, qy) in _phases(sh, ph, R, H, dh):
+            for (phx, rx0, rnx, dlx, qx) in _phases(sw, pw, S, W, dw):
+                if qy == 0 or qx == 0:
+                    continue
+                rr, ss = (rny, rnx) if rny * rnx > 0 else (0, 0)
+                w = self._pack(('dgrad', phy, phx), cin, self.in_channels, self.out_channels, cout, 1, ry0, sh,
+                               rny, rx0, sw, rnx) if rr else None
+                d = _desc(N=n, H=OH, W=OW, C=cout, ldx=cout, OH=qy, OW=qx, K=cin, R=rr, S=ss, sy=1, sx=1, dy=-1,
+                          dx=-1, py=dly, px=dlx, outH=H, outW=W, osy=sh, osx=sw, ooy=phy, oox=phx, ldy=cin,
+                          ldw=max(rr * ss * cout, cout))
+                self._igemm(gy, w, dx, d, N.dt_code(dx))
+        return dx
+
+
+class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
+    """nn.ConvTranspose2d (output_padding 0, groups 1, dilation 1) with an optional fused ReLU."""
+
+    def __init__(self, *args, **kw):
+        super().__init__(*args, **kw)
+        if self.groups != 1 or self.dilation != (1, 1) or self.output_padding != (0, 0):
+            raise NotImplementedError('ssseg.nn.ConvTranspose2d: groups/dilation/output_padding not implemented')
+        self._ssseg_init(False)
+        self._fuse_relu = False
+
+    def _dims(self):
+        v = vec()
+        return rup(self.in_channels, v), rup(self.out_channels, v)
+
+    def forward(self, x, output_size=None):
+        if output_size is not None:
+            raise NotImplementedError('ssseg.nn.ConvTranspose2d: output_size')
+        if not _is_act(x):
+            x = to_act(x)
+        return _ConvFn.apply(x, self.weight, self.bias, self, self._fuse_relu)
+
+    def forward_relu(self, x):
+        """ConvTranspose2d followed by ReLU, fused into the epilogue (unet.py:20-23)."""
+        return _ConvFn.apply(x, self.weight, self.bias, self, True)
+
+    def _out_hw(self, H, W):
+        (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
+        return (H - 1) * sh - 2 * ph + R, (W - 1) * sw - 2 * pw + S
+
+    def _ssseg_forward(self, x, relu):
+        cin, cout = self._dims()
+        _need_act(x, cin, 'ConvTranspose2d')
+        n, _, H, W = x.shape
+        (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
+        OH, OW = self._out_hw(H, W)
+        y = new_act(n, cout, OH, OW, _CFG['dtype'], x.device)
+        for (phy, ry0, rny, dly, qy) in _phases(sh, ph, R, OH):
+            for (phx, rx0, rnx, dlx, qx) in _phases(sw, pw, S, OW):
+                if qy == 0 or qx == 0:
+                    continue
+                rr, ss = (rny, rnx) if rny * rnx > 0 else (0, 0)
+                w = self._pack(('fwd', phy, phx), cout, self.out_channels, self.in_channels, cin, 1, ry0, sh, rny,
+                               rx0, sw, rnx) if rr else None
+                d = _desc(N=n, H=H, W=W, C=cin, ldx=cin, OH=qy, OW=qx, K=cout, R=rr, S=ss, sy=1, sx=1, dy=-1, dx=-1,
+                          py=dly, px=dlx, outH=OH, outW=OW, osy=sh, osx=sw, ooy=phy, oox=phx, ldy=cout,
+                          ldw=max(rr * ss * cin, cin))
+                self._igemm(x, w, y, d, N.dt_code(y), self.bias, relu)
+        return y
+
+    def _grad_in(self, gy):
+        _need_act(gy, self._dims()[1], 'ConvTranspose2d backward')
+        return gy
+
+    def _ssseg_wgrad(self, x, gy):
+        _bias_grad(self, gy)
+        if self.weight.requires_grad:
+            cin, cout = self._dims()
+            n, _, H, W = x.shape
+            (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
+            OH, OW = gy.shape[2], gy.shape[3]
+            # dW[ci][co][r][s] = sum_p x[p][ci] * gy[p*s - pad + r][co]: a conv over gy with x as its output grad
+            d = _desc(N=n, H=OH, W=OW, C=cout, ldx=cout, OH=H, OW=W, K=cin, R=R, S=S, sy=sh, sx=sw, dy=1, dx=1,
+                      py=-ph, px=-pw, outH=H, outW=W, osy=1, osx=1, ooy=0, oox=0, ldy=cin, ldw=R * S * cout)
+            nb = N.lib().ssseg_conv_wgrad_workspace_bytes(ctypes_ref(d), N.dt_code(x))
+            ws = N.workspace(nb, x.device)
+            N.call('ssseg_conv_wgrad', N.dev_ptr(gy), N.dev_ptr(x), N.dev_ptr(_grad_of(self.weight)), ctypes_ref(d),
+                   N.dt_code(x), self.out_channels, self.in_channels, 1, 1, N.dev_ptr(ws), nb, N.stream())
+        _ready(*[p for p in (self.weight, self.bias) if p is not None])
+
+    def _ssseg_dgrad(self, gy, xshape):
+        cin, cout = self._dims()
+        n, _, H, W = xshape
+        (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
+        OH, OW = gy.shape[2], gy.shape[3]
+        dx = new_act(n, cin, H, W, _CFG['dtype'], gy.device)
+        w = self._pack('dgrad', cin, self.in_channels, self.out_channels, cout, 0, 0, 1, R, 0, 1, S)
+        d = _desc(N=n, H=OH, W=OW, C=cout, ldx=cout, OH=H, OW=W, K=cin, R=R, S=S, sy=sh, sx=sw, dy=1, dx=1, py=-ph,
+                  px=-pw, outH=H, outW=W, osy=1, osx=1, ooy=0, oox=0, ldy=cin, ldw=R * S * cout)
+        self._igemm(gy, w, dx, d, N.dt_code(dx))
+        return dx
+
+
+# ------------------------------------------------------------------------------------------------
+# batch norm (+ReLU, +residual)
+# ------------------------------------------------------------------------------------------------
+def _sync_group(training):
+    return (training and _CFG['sync_bn'] and dist.is_available() and dist.is_initialized()
+            and dist.get_world_size() > 1)
+
+
+class _BNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, mod, relu):
+        C = mod.num_features
+        n, cp, h, w = x.shape
+        P = n * h * w
+        dev = x.device
+        mean = torch.empty(C, dtype=torch.float32, device=dev)
+        invstd = torch.empty(C, dtype=torch.float32, device=dev)
+        training = mod.training or not mod.track_running_stats
+        count = float(P)
+        if training:
+            sums = torch.empty(2 * C, dtype=torch.float64, device=dev)
+            nb = N.lib().ssseg_bn_workspace_bytes(C)
+            ws = N.workspace(nb, dev)
+            N.call('ssseg_bn_stats', N.dev_ptr(x), P, C, cp, N.dt_code(x), N.dev_ptr(sums), N.dev_ptr(ws), nb,
+                   N.stream())
+            if _sync_group(True):
+                dist.all_reduce(sums)
+                count = float(P * dist.get_world_size())
+            track = mod.track_running_stats and mod.training
+            if track and mod.momentum is None:
+                raise NotImplementedError('ssseg BatchNorm2d: momentum=None (cumulative average)')
+            N.call('ssseg_bn_finalize', N.dev_ptr(sums), C, count, float(mod.eps),
+                   float(mod.momentum if mod.momentum is not None else 0.0), N.dev_ptr(mean), N.dev_ptr(invstd),
+                   N.dev_ptr(mod.running_mean) if track else None, N.dev_ptr(mod.running_var) if track else None,
+                   N.dev_ptr(mod.num_batches_tracked) if track else None, N.stream())
+        else:
+            N.call('ssseg_bn_eval_params', N.dev_ptr(mod.running_mean), N.dev_ptr(mod.running_var), float(mod.eps), C,
+                   N.dev_ptr(mean), N.dev_ptr(invstd), N.stream())
+        y = new_act(n, cp, h, w, x.dtype, dev, zero=cp != C)
+        wt = weight.detach() if weight is not None else None
+        bs = bias.detach() if bias is not None else None
+        N.call('ssseg_bn_apply', N.dev_ptr(x), N.dev_ptr(residual) if residual is not None else None, N.dev_ptr(y),
+               P, C, cp, cp, cp, N.dev_ptr(mean), N.dev_ptr(invstd), N.dev_ptr(wt) if wt is not None else None,
+               N.dev_ptr(bs) if bs is not None else None, int(bool(relu)), N.dt_code(x), N.stream())
+        ctx.save_for_backward(x, residual, mean, invstd)
+        ctx.mod, ctx.relu, ctx.training, ctx.count = mod, relu, training, count
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, residual, mean, invstd = ctx.saved_tensors
+        mod = ctx.mod
+        C = mod.num_features
+        n, cp, h, w = x.shape
+        P = n * h * w
+        _need_act(gy, cp, 'BatchNorm2d backward')
+        dev = x.device
+        wt = mod.weight.detach() if mod.weight is not None else None
+        bs = mod.bias.detach() if mod.bias is not None else None
+        sums = torch.empty(2 * C, dtype=torch.float64, device=dev)
+        nb = N.lib().ssseg_bn_workspace_bytes(C)
+        ws = N.workspace(nb, dev)
+        res_p = N.dev_ptr(residual) if residual is not None else None
+        N.call('ssseg_bn_bwd_reduce', N.dev_ptr(gy), N.dev_ptr(x), res_p, P, C, cp, cp, cp, N.dev_ptr(mean),
+               N.dev_ptr(invstd), N.dev_ptr(wt) if wt is not None else None,
+               N.dev_ptr(bs) if bs is not None else None, int(bool(ctx.relu)), N.dt_code(x), N.dev_ptr(sums),
+               N.dev_ptr(ws), nb, N.stream())
+        if mod.weight is not None and mod.weight.requires_grad:
+            N.call('ssseg_bn_param_grad', N.dev_ptr(sums), C, N.dev_ptr(_grad_of(mod.weight)),
+                   N.dev_ptr(_grad_of(mod.bias)), N.stream())
+            _ready(mod.weight, mod.bias)
+        count = ctx.count
+        if ctx.training and _sync_group(True):
+            dist.all_reduce(sums)
+        dx = new_act(n, cp, h, w, x.dtype, dev, zero=cp != C)
+        want_res = residual is not None and ctx.needs_input_grad[3]
+        dres = new_act(n, cp, h, w, x.dtype, dev, zero=cp != C) if want_res else None
+        N.call('ssseg_bn_bwd_apply', N.dev_ptr(gy), N.dev_ptr(x), res_p, N.dev_ptr(dx),
+               N.dev_ptr(dres) if dres is not None else None, P, C, cp, cp, cp, cp, N.dev_ptr(mean),
+               N.dev_ptr(invstd), N.dev_ptr(wt) if wt is not None else None,
+               N.dev_ptr(bs) if bs is not None else None, int(bool(ctx.relu)), int(bool(ctx.training)),
+               N.dev_ptr(sums), float(count), N.dt_code(x), N.stream())
+        return dx, None, None, dres, None, None
+
+
+class BatchNorm2d(nn.BatchNorm2d):
+    """nn.BatchNorm2d (acts as SyncBatchNorm across the process group when one is initialised)."""
+
+    def forward(self, x, residual=None, relu=False):
+        _need_act(x, rup(self.num_features, vec()), 'BatchNorm2d')
+        return _BNFn.apply(x, self.weight, self.bias, residual, self, relu)
+
+
+def bn_act(x, bn, relu=True, residual=None):
+    """act(bn(x) [+ residual]) in one pass: ConvBlock's BN+ReLU (unet.py:9-10), Bottleneck's bn3+add+relu."""
+    if not isinstance(bn, BatchNorm2d):
+        raise TypeError('ssseg.nn.bn_act needs an ssseg BatchNorm2d')
+    _need_act(x, rup(bn.num_features, vec()), 'BatchNorm2d')
+    return _BNFn.apply(x, bn.weight, bn.bias, residual, bn, relu)
+
+
+# ------------------------------------------------------------------------------------------------
+# pooling, upsampling, concat / crop
+# ------------------------------------------------------------------------------------------------
+class _MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p, ceil_mode):
+        n, c, h, w = x.shape
+
+        def osz(L):
+            o = (L + 2 * p - k + (s - 1 if ceil_mode else 0)) // s + 1
+            if ceil_mode and (o - 1) * s >= L + p:
+                o -= 1
+            return o
+        oh, ow = osz(h), osz(w)
+        y = new_act(n, c, oh, ow, x.dtype, x.device)
+        idx = torch.empty((n, oh, ow, c), dtype=torch.uint8, device=x.device)
+        N.call('ssseg_maxpool_fwd', N.dev_ptr(x), N.dev_ptr(y), N.dev_ptr(idx), n, h, w, c, oh, ow, k, s, p,
+               N.dt_code(x), N.stream())
+        ctx.save_for_backward(idx)
+        ctx.meta = (n, c, h, w, oh, ow, k, s, p, x.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (idx,) = ctx.saved_tensors
+        n, c, h, w, oh, ow, k, s, p, dt = ctx.meta
+        _need_act(gy, c, 'MaxPool2d backward')
+        gx = new_act(n, c, h, w, dt, gy.device)
+        N.call('ssseg_maxpool_bwd', N.dev_ptr(gy), N.dev_ptr(idx), N.dev_ptr(gx), n, h, w, c, oh, ow, k, s, p,
+               N.dt_code(gy), N.stream())
+        return gx, None, None, None, None
+
+
+class MaxPool2d(nn.MaxPool2d):
+    def forward(self, x):
+        k, s, p = (self.kernel_size, self.stride, self.padding)
+        k = k if isinstance(k, int) else k[0]
+        s = s if isinstance(s, int) else s[0]
+        p = p if isinstance(p, int) else p[0]
+        if self.dilation not in (1, (1, 1)) or self.return_indices:
+            raise NotImplementedError('ssseg MaxPool2d: dilation / return_indices')
+        _need_act(x, None, 'MaxPool2d')
+        return _MaxPoolFn.apply(x, k, s, p, bool(self.ceil_mode))
+
+
+class Upsample(nn.Upsample):
+    """nn.Upsample(scale_factor, mode='bilinear') on NHWC activations (unet.py:26, simple_unet.py:71)."""
+
+    def forward(self, x):
+        if self.mode != 'bilinear' or self.size is not None:
+            raise NotImplementedError('ssseg Upsample: bilinear with scale_factor only')
+        from .ops import interpolate_bilinear
+        sf = self.scale_factor if isinstance(self.scale_factor, (tuple, list)) else (self.scale_factor,) * 2
+        oh, ow = int(x.shape[2] * sf[0]), int(x.shape[3] * sf[1])
+        return interpolate_bilinear(x, (oh, ow), align_corners=bool(self.align_corners))
+
+
+class _CatFn(torch.autograd.Function):
+    """torch.cat((a, b), 1) with a center-crop of whichever map is larger (unet.py:40-45)."""
+
+    @staticmethod
+    def forward(ctx, a, b, ca, cb):
+        n = a.shape[0]
+        H, W = min(a.shape[2], b.shape[2]), min(a.shape[3], b.shape[3])
+        v = vec()
+        cp = rup(ca + cb, v)
+        y = new_act(n, cp, H, W, a.dtype, a.device, zero=cp != ca + cb)
+        offs = []
+        for t, c, c0 in ((a, ca, 0), (b, cb, ca)):
+            oy, ox = (t.shape[2] - H) // 2, (t.shape[3] - W) // 2
+            offs.append((oy, ox))
+            N.call('ssseg_nhwc_copy', N.dev_ptr(t), N.dev_ptr(y) + c0 * y.element_size(), n, H, W, c, t.shape[2],
+                   t.shape[3], t.shape[1], oy, ox, H, W, cp, 0, 0, N.dt_code(t), N.stream())
+        ctx.meta = (a.shape, b.shape, ca, cb, offs, H, W, cp)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        ash, bsh, ca, cb, offs, H, W, cp = ctx.meta
+        n = gy.shape[0]
+        grads = []
+        for sh, c, c0, (oy, ox) in ((ash, ca, 0, offs[0]), (bsh, cb, ca, offs[1])):
+            cropped = (sh[2], sh[3]) != (H, W)
+            g = new_act(n, sh[1], sh[2], sh[3], gy.dtype, gy.device, zero=cropped or sh[1] != c)
+            N.call('ssseg_nhwc_copy', N.dev_ptr(gy) + c0 * gy.element_size(), N.dev_ptr(g), n, H, W, c, H, W, cp, 0,
+                   0, sh[2], sh[3], sh[1], oy, ox, N.dt_code(gy), N.stream())
+            grads.append(g)
+        return grads[0], grads[1], None, None
+
+
+def cat_crop(a, b, ca, cb):
+    """Concatenate NHWC activations a (ca real channels) and b (cb) along channels; the larger map is
+    center-cropped to the smaller (unet.py:40-45 compares dim 2; both dims are cropped to match here)."""
+    return _CatFn.apply(a, b, ca, cb)
+
+
+def invalidate_packed(model):
+    """Drop cached packed weights (call after the master weights change: optimizer step, EMA, load)."""
+    for m in model.modules():
+        if isinstance(m, _ConvBase):
+            m.invalidate_packed()

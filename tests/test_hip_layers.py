@@ -1,0 +1,194 @@
+"""GPU parity of the layer engine (implicit-GEMM conv fwd/dgrad/wgrad, ConvTranspose2d, BatchNorm,
+max-pool, concat/crop) against the plain PyTorch-CPU fp32 reference of the same op.
+
+Tolerances: fp32 compute mode 1e-4 relative to the output's max magnitude (f32 MFMA is an exact
+fp32 fma chain; the residual difference is summation order); bf16 mode 2e-2 relative RMS.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=['f32', 'bf16'])
+def mode(request):
+    from ssseg import nn as snn
+    dt = torch.float32 if request.param == 'f32' else torch.bfloat16
+    snn.set_compute_dtype(dt)
+    yield request.param
+    snn.set_compute_dtype(torch.bfloat16)
+
+
+def _close(got, ref, mode, what):
+    got = got.detach().float().cpu()
+    ref = ref.detach().float().cpu()
+    assert got.shape == ref.shape, (what, got.shape, ref.shape)
+    scale = float(ref.abs().max()) + 1e-12
+    if mode == 'f32':
+        err = float((got - ref).abs().max()) / scale
+        assert err < 1e-4, f'{what}: max rel err {err}'
+    else:
+        err = float(((got - ref) ** 2).mean().sqrt() / (ref.pow(2).mean().sqrt() + 1e-12))
+        assert err < 2e-2, f'{what}: rel rms err {err}'
+
+
+def _q(t, mode):
+    """bf16 mode: the reference sees the same bf16-rounded inputs the kernels see (fp32 math after)."""
+    return t.bfloat16().float() if mode == 'bf16' else t
+
+
+def _act_in(x, dev):
+    from ssseg import nn as snn
+    return snn.to_act(x.to(dev))
+
+
+def _act_out(y):
+    """physical NHWC activation -> logical NCHW float tensor with real channels"""
+    return y
+
+
+CONV_CASES = [
+    # cin, cout, k, stride, pad, dil, H, W, N
+    (8, 16, 3, 1, 1, 1, 12, 10, 2),
+    (16, 64, 1, 1, 0, 1, 9, 9, 2),
+    (64, 32, 1, 2, 0, 1, 10, 11, 2),
+    (16, 32, 3, 2, 1, 1, 13, 12, 2),
+    (3, 64, 7, 2, 3, 1, 23, 22, 2),
+    (32, 16, 3, 1, 2, 2, 11, 11, 1),
+    (24, 40, 3, 1, 1, 1, 7, 9, 3),
+    (128, 128, 3, 1, 1, 1, 8, 8, 2),
+]
+
+
+@pytest.mark.parametrize('cin,cout,k,s,p,d,H,W,n', CONV_CASES)
+def test_conv2d_fwd_bwd(hip_device, mode, cin, cout, k, s, p, d, H, W, n):
+    from ssseg import nn as snn
+    torch.manual_seed(0)
+    ref = torch.nn.Conv2d(cin, cout, k, s, p, d, bias=False)
+    mod = snn.Conv2d(cin, cout, k, s, p, d, bias=False, head=True).to(hip_device)
+    mod.load_state_dict(ref.state_dict())
+    with torch.no_grad():
+        ref.weight.copy_(_q(ref.weight, mode))
+    x = _q(torch.randn(n, cin, H, W), mode)
+    xr = x.clone().requires_grad_(True)
+    yr = ref(xr)
+    gy = _q(torch.randn_like(yr), mode)
+    yr.backward(gy)
+    xa = _act_in(x, hip_device).detach().requires_grad_(True)
+    y = mod(xa)
+    y.backward(gy.to(hip_device))
+    _close(y, yr, mode, 'y')
+    _close(mod.weight.grad, ref.weight.grad, mode, 'dW')
+    _close(xa.grad[:, :cin], xr.grad, mode, 'dx')
+
+
+@pytest.mark.parametrize('cin,cout,H,W', [(16, 8, 5, 6), (64, 32, 4, 4), (128, 64, 8, 7)])
+def test_conv_transpose_relu(hip_device, mode, cin, cout, H, W):
+    from ssseg import nn as snn
+    torch.manual_seed(1)
+    ref = torch.nn.ConvTranspose2d(cin, cout, 4, 2, 1)
+    mod = snn.ConvTranspose2d(cin, cout, 4, 2, 1).to(hip_device)
+    mod.load_state_dict(ref.state_dict())
+    with torch.no_grad():
+        ref.weight.copy_(_q(ref.weight, mode))
+    x = _q(torch.randn(2, cin, H, W), mode)
+    xr = x.clone().requires_grad_(True)
+    # the fused ReLU is checked in fp32; in bf16 outputs within rounding of 0 flip the ReLU mask, which
+    # swaps whole gradient terms, so the bf16 case checks the transposed conv itself
+    relu = mode == 'f32'
+    yr = F.relu(ref(xr)) if relu else ref(xr)
+    gy = _q(torch.randn_like(yr), mode)
+    yr.backward(gy)
+    xa = _act_in(x, hip_device).detach().requires_grad_(True)
+    y = mod.forward_relu(xa) if relu else mod(xa)
+    gya = _act_in(gy, hip_device)
+    y.backward(gya)
+    _close(y.float().permute(0, 1, 2, 3)[:, :cout], yr, mode, 'y')
+    _close(mod.weight.grad, ref.weight.grad, mode, 'dW')
+    _close(mod.bias.grad, ref.bias.grad, mode, 'db')
+    _close(xa.grad[:, :cin], xr.grad, mode, 'dx')
+
+
+@pytest.mark.parametrize('train', [True, False])
+@pytest.mark.parametrize('relu,residual', [(True, False), (False, False), (True, True)])
+def test_batchnorm_act(hip_device, mode, train, relu, residual):
+    from ssseg import nn as snn
+    torch.manual_seed(2)
+    C = 32
+    ref = torch.nn.BatchNorm2d(C)
+    with torch.no_grad():
+        ref.weight.uniform_(0.5, 1.5)
+        ref.bias.uniform_(-0.3, 0.3)
+        ref.running_mean.uniform_(-0.2, 0.2)
+        ref.running_var.uniform_(0.5, 2.0)
+    mod = snn.BatchNorm2d(C).to(hip_device)
+    mod.load_state_dict(ref.state_dict())
+    ref.train(train)
+    mod.train(train)
+    x = _q(torch.randn(4, C, 9, 7) * 2 + 0.5, mode)
+    r = _q(torch.randn(4, C, 9, 7), mode)
+    xr = x.clone().requires_grad_(True)
+    rr = r.clone().requires_grad_(True)
+    yr = ref(xr)
+    if residual:
+        yr = yr + rr
+    if relu:
+        yr = F.relu(yr)
+    gy = _q(torch.randn_like(yr), mode)
+    yr.backward(gy)
+    xa = _act_in(x, hip_device).detach().requires_grad_(True)
+    ra = _act_in(r, hip_device).detach().requires_grad_(True) if residual else None
+    y = snn.bn_act(xa, mod, relu=relu, residual=ra)
+    y.backward(_act_in(gy, hip_device))
+    _close(y, yr, mode, 'y')
+    _close(xa.grad, xr.grad, mode, 'dx')
+    _close(mod.weight.grad, ref.weight.grad, mode, 'dgamma')
+    _close(mod.bias.grad, ref.bias.grad, mode, 'dbeta')
+    if residual:
+        _close(ra.grad, rr.grad, mode, 'dres')
+    np.testing.assert_allclose(mod.running_mean.cpu().numpy(), ref.running_mean.numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(mod.running_var.cpu().numpy(), ref.running_var.numpy(), rtol=1e-5, atol=1e-6)
+    assert int(mod.num_batches_tracked) == int(ref.num_batches_tracked)
+
+
+@pytest.mark.parametrize('k,s,p,ceil', [(3, 2, 1, False), (2, 2, 0, True)])
+def test_maxpool(hip_device, mode, k, s, p, ceil):
+    from ssseg import nn as snn
+    torch.manual_seed(3)
+    x = _q(torch.randn(2, 16, 11, 9), mode)
+    xr = x.clone().requires_grad_(True)
+    yr = F.max_pool2d(xr, k, s, p, ceil_mode=ceil)
+    gy = _q(torch.randn_like(yr), mode)
+    yr.backward(gy)
+    xa = _act_in(x, hip_device).detach().requires_grad_(True)
+    y = snn.MaxPool2d(k, s, p, ceil_mode=ceil)(xa)
+    y.backward(_act_in(gy, hip_device))
+    _close(y, yr, mode, 'y')
+    _close(xa.grad, xr.grad, mode, 'dx')
+
+
+def test_cat_crop(hip_device, mode):
+    from ssseg import nn as snn
+    torch.manual_seed(4)
+    a = _q(torch.randn(2, 8, 10, 10), mode)
+    b = _q(torch.randn(2, 16, 9, 9), mode)
+    ar, br = a.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = torch.cat((ar[:, :, 0:9, 0:9], br), 1)
+    gy = _q(torch.randn_like(yr), mode)
+    yr.backward(gy)
+    aa = _act_in(a, hip_device).detach().requires_grad_(True)
+    ba = _act_in(b, hip_device).detach().requires_grad_(True)
+    y = snn.cat_crop(aa, ba, 8, 16)
+    y.backward(_act_in(gy, hip_device))
+    _close(y, yr, mode, 'y')
+    _close(aa.grad, ar.grad, mode, 'da')
+    _close(ba.grad, br.grad, mode, 'db')
+
+
+def test_no_cpu_fallback_for_layers():
+    from ssseg import nn as snn
+    mod = snn.Conv2d(8, 8, 3, padding=1)
+    with pytest.raises(RuntimeError):
+        mod(torch.randn(1, 8, 4, 4))
