@@ -56,6 +56,13 @@ int ssseg_cowmix_mask(const float* noise, const float* sigma, const float* p, in
  * Box-Muller): out[i] for i in [0,n).  Parity mode instead uploads the CPU generator's draws. */
 int ssseg_normal_f32(float* out, int64_t n, uint64_t seed, uint64_t offset, ssseg_stream_t stream);
 
+/* Throughput-mode draws of generate_cowmix_masks_like's random inputs (cowmix.py:44-55), all on device
+ * so a captured step replays fresh masks: p ~ U(prop_lo, prop_hi), sigma = exp(U(log lo, log hi)),
+ * noise ~ N(0,1) [B*HW]; Philox counter = offset (+B for the noise).  Parity mode instead draws the
+ * same quantities from the CPU torch generator in the reference's order and uploads them. */
+int ssseg_cowmix_draw(float* p, float* sigma, float* noise, int64_t B, int64_t HW, double prop_lo, double prop_hi,
+                      double sigma_lo, double sigma_hi, uint64_t seed, uint64_t offset, ssseg_stream_t stream);
+
 /* mix_with_mask (cowmix.py:72-73): out = a*m + b*(1-m), m [B,1,HW] broadcast over C.
  * a, b, out: [B,C,HW] (NCHW) of dtype `dt`; mask f32. */
 int ssseg_mix(const void* a, const void* b, const float* mask, void* out, int64_t B, int64_t C,

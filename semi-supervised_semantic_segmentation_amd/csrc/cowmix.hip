@@ -235,6 +235,24 @@ __global__ void normal_kernel(float* out, int64_t n, uint64_t seed, uint64_t off
   }
 }
 
+// p_b = lo + u*(hi-lo), sigma_b = exp(llo + u'*(lhi-llo)) from Philox uniforms (stream 1 of the key)
+__global__ void cowmix_draw_kernel(float* p, float* sigma, int B, float lo, float hi, float llo, float lhi, uint64_t seed,
+                                   uint64_t offset) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  unsigned c[4] = {(unsigned)(offset + b), (unsigned)((offset + b) >> 32), 1u, 0u};
+  unsigned k0 = (unsigned)seed, k1 = (unsigned)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    philox_round(c, k0, k1);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  const float u1 = (float)(c[0] >> 8) * (1.0f / 16777216.0f), u2 = (float)(c[1] >> 8) * (1.0f / 16777216.0f);
+  p[b] = lo + u1 * (hi - lo);
+  sigma[b] = expf(llo + u2 * (lhi - llo));
+}
+
 template <typename T>
 __global__ void mix_kernel(const T* a, const T* b, const float* m, T* out, int64_t C, int64_t HW, int64_t total) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -281,6 +299,20 @@ extern "C" int ssseg_normal_f32(float* out, int64_t n, uint64_t seed, uint64_t o
   if (n == 0) return 0;
   hipLaunchKernelGGL(normal_kernel, dim3(ssseg_grid((n + 3) / 4, 256)), dim3(256), 0, (hipStream_t)stream, out, n,
                      seed, offset);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_cowmix_draw(float* p, float* sigma, float* noise, int64_t B, int64_t HW, double prop_lo,
+                                 double prop_hi, double sigma_lo, double sigma_hi, uint64_t seed, uint64_t offset,
+                                 ssseg_stream_t stream) {
+  if (!p || !sigma || !noise || B < 1 || HW < 1 || sigma_lo <= 0 || sigma_hi <= 0) return SSSEG_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(cowmix_draw_kernel, dim3((B + 63) / 64), dim3(64), 0, s, p, sigma, (int)B, (float)prop_lo,
+                     (float)prop_hi, (float)log(sigma_lo), (float)log(sigma_hi), seed, offset);
+  const int64_t n = B * HW;
+  hipLaunchKernelGGL(normal_kernel, dim3(ssseg_grid((n + 3) / 4, 256)), dim3(256), 0, s, noise, n, seed,
+                     offset + (uint64_t)B);
   SSSEG_LAUNCH_CHECK();
   return 0;
 }

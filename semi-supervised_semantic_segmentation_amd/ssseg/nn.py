@@ -233,6 +233,12 @@ class Conv2d(nn.Conv2d, _ConvBase):
             x = to_act(x)
         return _ConvFn.apply(x, self.weight, self.bias, self, False)
 
+    def forward_relu(self, x):
+        """Conv2d followed by ReLU, fused into the GEMM epilogue (unet.py:27-28 with no norm)."""
+        if not _is_act(x):
+            x = to_act(x)
+        return _ConvFn.apply(x, self.weight, self.bias, self, True)
+
     def _ssseg_forward(self, x, relu):
         cin, cout = self._dims()
         _need_act(x, cin, 'Conv2d')

@@ -166,3 +166,41 @@ def sgd_step_(param, grad, buf, shadow, lr, momentum, wd, max_norm, sqnorm, firs
            N.dev_ptr(buf) if buf is not None else None, N.dev_ptr(shadow) if shadow is not None else None,
            param.numel(), float(lr), float(momentum), float(wd), float(max_norm),
            N.dev_ptr(sqnorm) if sqnorm is not None else None, int(bool(first)), N.stream())
+
+
+# ------------------------------------------------------------------------------------------------
+# Lovász (losses.py:239-250)
+# ------------------------------------------------------------------------------------------------
+class _Lovasz(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target):
+        logits, target = _c(logits.float()), _c(target.float())
+        B, C = logits.shape[:2]
+        HW = logits[0, 0].numel()
+        out = torch.empty((), device=logits.device, dtype=torch.float32)
+        nb = N.lib().ssseg_lovasz_workspace_bytes(B, HW)
+        ws = N.workspace(nb, logits.device)
+        N.call('ssseg_lovasz_fwd', N.dev_ptr(logits, 'logits'), N.dev_ptr(target, 'target'), B, C, HW,
+               N.dev_ptr(out), N.dev_ptr(ws), nb, N.stream())
+        ctx.save_for_backward(logits, target)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, target = ctx.saved_tensors
+        B, C = logits.shape[:2]
+        HW = logits[0, 0].numel()
+        gx = torch.empty_like(logits)
+        nb = N.lib().ssseg_lovasz_workspace_bytes(B, HW)
+        ws = N.workspace(nb, logits.device)
+        g = _c(g.float())
+        N.call('ssseg_lovasz_bwd', N.dev_ptr(logits), N.dev_ptr(target), B, C, HW, N.dev_ptr(g), N.dev_ptr(gx),
+               N.dev_ptr(ws), nb, N.stream())
+        return gx, None
+
+
+def lovasz_binary(logits, target, valid_weighted=True):
+    """binary_lovasz_loss_with_logits (losses.py:239-250) on the device."""
+    if not valid_weighted:
+        raise NotImplementedError('lovasz_softmax without the valid-sample weighting')
+    return _Lovasz.apply(logits, target)

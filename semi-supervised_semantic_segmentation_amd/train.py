@@ -1,0 +1,149 @@
+"""Training / validation loop — drop-in for reference train.py (train :25-147, validate :150-195).
+
+Same signatures and the same step semantics: supervised forward + CalculateLoss +
+backward; mean-teacher forwards (no_grad, eval) + bilinear resize; CowMix mask + mixing; the student's
+consistency forward in eval() with grads on; consistency loss gated by float(epoch > 25) (NaN when no
+pixel is confident, like the reference); clip_grad_norm_ + optimizer step skipped at step 0;
+EMA update every step.  Every tensor op of the step runs on the MI355X kernels.
+
+Deliberate differences: loss scalars stay on the device and are reduced / synced only on
+print steps (the reference syncs 4x per step for logging only); the DDP gradient all-reduce runs once
+per step, armed on the last backward pass (linear, so the averaged gradient is the same).
+"""
+import time
+
+import torch
+
+import cowmix
+import mean_teacher
+import metrics
+import utils.utils as utils
+from ssseg import nn as snn
+from ssseg import ops
+from ssseg.ddp import DistributedDataParallel as _DDP
+from ssseg.optim import SGD as _SGD
+
+
+def _inner(model):
+    return model.module if hasattr(model, 'module') else model
+
+
+def _world():
+    return torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
+
+
+def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch, step, config):
+    """One step of train.py:44-130.  Returns device scalars (classification loss, unsup loss, cm mean)."""
+    tc = config['train']
+    ddp = model if isinstance(model, _DDP) else None
+    semi = tc['use_semi_supervised']
+    features, pred_maps = model(image)
+    classification_loss = tc['loss'](pred_maps, mask)
+    sup_loss = classification_loss
+    if ddp is not None and not semi:
+        ddp.arm()
+    (sup_loss / tc['virtual_batch_size_multiplier']).backward()
+    del pred_maps, features
+    unsup_loss = cm_mean = None
+    if semi:
+        size = unsup_a.shape[2:4]
+        with torch.no_grad():
+            ema_pred_a = ops.interpolate_bilinear(ema_model(unsup_a)[-1][-1], size, align_corners=False)
+            ema_pred_b = ops.interpolate_bilinear(ema_model(unsup_b)[-1][-1], size, align_corners=False)
+            cmask = cowmix.generate_cowmix_masks_like(unsup_a, mask_proportion_range=tc['mask_proportion_range'],
+                                                      sigma_range=tc['sigma_range'])
+            mixed_ema_pred = cowmix.mix_with_mask(ema_pred_a, ema_pred_b, cmask)
+            mixed_images = cowmix.mix_with_mask(unsup_a, unsup_b, cmask)
+            del cmask, ema_pred_a, ema_pred_b
+        model.eval()
+        student_pred = model(mixed_images)[-1][-1]
+        model.train()
+        student_pred = ops.interpolate_bilinear(student_pred, mixed_images.shape[2:4], align_corners=False)
+        consistency, cm_mean = ops.consistency_loss(student_pred, mixed_ema_pred, tc['confidence_threshold'])
+        unsup_loss = consistency * tc['consistency_loss_weight'] * float(epoch > 25)
+        if ddp is not None:
+            ddp.arm()
+        unsup_loss.backward()
+    if ddp is not None:
+        ddp.finish()
+    if step % tc['virtual_batch_size_multiplier'] == 0 and step != 0:
+        clip = tc['gradient_clip_value']
+        if isinstance(optimizer, _SGD):
+            optimizer.step(max_norm=clip)
+        else:
+            torch.nn.utils.clip_grad_norm_(_inner(model).parameters(), clip)
+            optimizer.step()
+        optimizer.zero_grad()
+        snn.invalidate_packed(_inner(model))
+    if semi:
+        mean_teacher.update_ema_variables(model, ema_model, alpha=tc['ema_model_alpha'])
+    return classification_loss.detach(), (unsup_loss.detach() if unsup_loss is not None else None), \
+        (cm_mean.detach() if cm_mean is not None else None)
+
+
+def train(model, ema_model, optimizer, dataloader, unsupervised_dataloader, epoch, initial_step, summary_writer,
+          config, device):
+    model.train()
+    meters = {k: utils.AverageMeter() for k in ('cls', 'sup', 'unsup', 'cm', 'time')}
+    rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
+    world = _world()
+    optimizer.zero_grad()
+    tc = config['train']
+    for step, sample in enumerate(dataloader):
+        tic = time.time()
+        global_step = initial_step + step
+        image = sample['image'].to(device, non_blocking=True)
+        mask = sample['semantic_mask'].to(device, non_blocking=True)
+        ua = ub = None
+        if tc['use_semi_supervised']:
+            ua = next(unsupervised_dataloader)['image'].to(device, non_blocking=True)
+            ub = next(unsupervised_dataloader)['image'].to(device, non_blocking=True)
+        cls, unsup, cm = train_step(model, ema_model, optimizer, image, mask, ua, ub, epoch, step, config)
+        meters['cls'].update(cls)
+        meters['sup'].update(cls)
+        meters['unsup'].update(unsup if unsup is not None else 0.)
+        meters['cm'].update(cm if cm is not None else 0.)
+        meters['time'].update(time.time() - tic)
+        if step % tc['print_freq'] == 0:
+            red_cls = utils.reduce_tensor(cls.clone()) / world
+            red_uns = utils.reduce_tensor(unsup.clone()) / world if unsup is not None else torch.zeros(())
+            if rank == 0:
+                print(f'Epoch: {epoch} Step: {step} Batch time: {meters["time"].average()} '
+                      f'Loss: {meters["cls"].average()}')
+                if summary_writer is not None:
+                    summary_writer.add_scalar('train_classification_loss', float(red_cls), global_step)
+                    summary_writer.add_scalar('train_unsupervised_loss', float(red_uns), global_step)
+    if rank == 0 and summary_writer is not None and meters['sup'].initialized:
+        summary_writer.add_scalar('batch_time', meters['time'].average(), global_step)
+        summary_writer.add_scalar('train_loss_avg', meters['sup'].average() + meters['unsup'].average(), global_step)
+        summary_writer.add_scalar('train_supervised_loss_avg', meters['sup'].average(), global_step)
+        summary_writer.add_scalar('train_unsupervised_loss_avg', meters['unsup'].average(), global_step)
+        summary_writer.add_scalar('train_classification_loss', meters['cls'].average(), global_step)
+        summary_writer.add_scalar('train_confidence_modulator', meters['cm'].average(), global_step)
+
+
+def validate(model, dataloader, epoch, initial_step, summary_writer, config, device):
+    """train.py:150-195 (Dice on the argmax one-hot; validation is outside the MI355X hot path)."""
+    model.eval()
+    avg_loss, avg_metric = utils.AverageMeter(), utils.AverageMeter()
+    rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
+    world = _world()
+    with torch.no_grad():
+        for sample in dataloader:
+            image = sample['image'].to(device)
+            mask = sample['semantic_mask'].to(device)
+            features, pred_maps = model(image)
+            loss = config['train']['loss'](pred_maps, mask)
+            logits = pred_maps[-1]
+            one_hot = torch.nn.functional.one_hot(torch.argmax(logits, dim=1), num_classes=2).permute(0, 3, 1, 2)
+            pred_bin = torch.nn.functional.interpolate(one_hot.float(), size=mask.size()[2:4], mode='nearest')
+            metric = metrics.dice_metric(pred_bin[:, 1:], (mask > 0.5).to(mask)[:, 1:]).mean()
+            avg_loss.update(utils.reduce_tensor(loss.clone()) / world)
+            avg_metric.update(utils.reduce_tensor(metric.clone()) / world)
+    if rank == 0:
+        print(f'Eval: Epoch: {epoch} Val loss: {avg_loss.average()} Val metric: {avg_metric.average()}')
+        if summary_writer is not None:
+            summary_writer.add_scalar('val_loss_avg', avg_loss.average(), initial_step)
+            summary_writer.add_scalar('val_dice', avg_metric.average(), initial_step)
+    model.train()
+    return avg_loss.average(), avg_metric.average()
