@@ -1,0 +1,203 @@
+"""Benchmark: semi-supervised training throughput of UNet-ResNet50 512x512 (BASELINE.json config C2).
+
+One "step" = one full reference training step (reference train.py:44-130) on one batch per GPU:
+student forward + BCE loss + backward, two teacher forwards + resize, CowMix mask + mixing, student
+consistency forward (eval BN) + consistency loss + backward, clip + SGD step, EMA update — all on the
+libssseg.so kernels, bf16 activations/weights with fp32 accumulation, fp32 master weights and EMA.
+Inputs are synthetic and pre-generated in HBM (8 batches cycled); weights random-init.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--size S] [--no-cpu-baseline]
+
+N>1 is launched by torch.distributed.run (one rank per GPU, RCCL); value = images/sec of the whole job
+(labeled images, N*B*K / max-over-ranks time).  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, 'semi-supervised_semantic_segmentation_amd')
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+BF16_DENSE_PEAK = 2.5e15        # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, spec)
+FWD_GFLOP_PER_IMAGE = 95.94     # UNet-R50 mw128 ConvT @512 (verified by tests/test_models_host.py)
+
+
+def build(batch, size, device):
+    import losses
+    from models import unet
+    from models.adapters import ListOutput
+    from models.encoders import resnet
+    from ssseg import arena, optim
+    from ssseg.ddp import DistributedDataParallel
+    torch.manual_seed(0)
+    student = ListOutput(unet.UNet(2, resnet.resnet50_encoder(), max_width=128, train_upsampling=True)).to(device)
+    teacher = ListOutput(unet.UNet(2, resnet.resnet50_encoder(), max_width=128, train_upsampling=True)).to(device)
+    for p in teacher.parameters():
+        p.detach_()
+    teacher.eval()
+    model = DistributedDataParallel(student)
+    arena.attach(teacher, with_grads=False)
+    opt = optim.SGD(model.parameters(), lr=0.0001 * 9 / 4, momentum=0.9, weight_decay=0.0005)
+    cfg = {'train': dict(
+        loss=losses.CalculateLoss([{'loss_fn': losses.DenseBinaryCrossEntropyLossWithLogits('mean'), 'weight': [0.5]}]),
+        virtual_batch_size_multiplier=1, use_semi_supervised=True, mask_proportion_range=(0.45, 0.55),
+        sigma_range=(8, 32), consistency_loss_weight=10, ema_model_alpha=0.99, confidence_threshold=0.97,
+        gradient_clip_value=5.0, print_freq=10 ** 9)}
+    return model, teacher, opt, cfg
+
+
+def synthetic_batches(n_batches, batch, size, device, rank):
+    """images U[0,1); masks = one-hot of smoothed-noise blobs (sigma 16, p 0.4)."""
+    from ssseg import ops
+    g = torch.Generator().manual_seed(1000 + rank)
+    data = []
+    for _ in range(n_batches):
+        img = torch.rand(batch, 3, size, size, generator=g).to(device)
+        noise = torch.randn(batch, 1, size, size, generator=g).to(device)
+        fg = ops.cowmix_mask(noise, torch.full((batch,), 16.0, device=device), torch.full((batch,), 0.6, device=device))
+        mask = torch.cat([1 - fg, fg], 1)
+        ua = torch.rand(batch, 3, size, size, generator=g).to(device)
+        ub = torch.rand(batch, 3, size, size, generator=g).to(device)
+        data.append((img, mask.contiguous(), ua, ub))
+    return data
+
+
+def cpu_baseline(size, batch=2, steps=2):
+    """The oracle's torch-CPU restatement of the same step (oracle/train_ref.py), bounded sample."""
+    from oracle import models_ref, train_ref
+    threads = torch.get_num_threads()
+    torch.manual_seed(0)
+    s = models_ref.ListOutput(models_ref.UNet(2, models_ref.resnet50_encoder(), 128, train_upsampling=True))
+    t = models_ref.ListOutput(models_ref.UNet(2, models_ref.resnet50_encoder(), 128, train_upsampling=True))
+    for p in t.parameters():
+        p.detach_()
+    t.eval()
+    opt = torch.optim.SGD(s.parameters(), lr=0.0001 * 9 / 4, momentum=0.9, weight_decay=0.0005)
+    g = torch.Generator().manual_seed(7)
+    n = steps + 1
+    imgs = torch.rand(n, batch, 3, size, size, generator=g)
+    fg = (torch.rand(n, batch, 1, size, size, generator=g) > 0.5).float()
+    masks = torch.cat([1 - fg, fg], 2)
+    unl = torch.rand(2 * n, batch, 3, size, size, generator=g)
+    cfg = train_ref.default_cfg()
+    times = []
+
+    def on_step(step, rec):
+        times.append(time.perf_counter())
+
+    t0 = time.perf_counter()
+    train_ref.train_epoch(s, t, opt, list(zip(imgs, masks)), iter(unl), 30, cfg, on_step=on_step)
+    dt = (times[-1] - times[0]) / steps     # first step is warm-up
+    return {'value': round(batch / dt, 4), 'unit': 'images/sec', 'cores': threads, 'kind': 'port',
+            'sample': f'oracle/train_ref.py torch-CPU fp32 semi-supervised step, UNet-R50 {size}x{size}, batch {batch}, '
+                      f'{steps} timed steps after 1 warm-up ({time.perf_counter() - t0:.1f} s total)'}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--batch', type=int, default=16)
+    ap.add_argument('--size', type=int, default=512)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', rank=rank, world_size=world, device_id=torch.device('cuda', local))
+    device = torch.device('cuda', local)
+
+    import train
+    from ssseg import nn as snn
+    snn.set_compute_dtype(torch.bfloat16)
+    model, teacher, opt, cfg = build(args.batch, args.size, device)
+    data = synthetic_batches(8, args.batch, args.size, device, rank)
+
+    step_idx = [0]
+
+    def one_step():
+        img, mask, ua, ub = data[step_idx[0] % len(data)]
+        train.train_step(model, teacher, opt, img, mask, ua, ub, 30, step_idx[0], cfg)
+        step_idx[0] += 1
+
+    model.train()
+    opt.zero_grad()
+    for _ in range(max(args.warmup, 2)):
+        one_step()
+    torch.cuda.synchronize()
+
+    # instrumented step: HIP events around every conv-engine launch (dominant kernel family)
+    rows = snn.probe(True)
+    one_step()
+    snn.probe(False)
+    torch.cuda.synchronize()
+    conv_ms = sum(a.elapsed_time(b) for a, b, _, _ in rows)
+    conv_flops = sum(f for _, _, f, _ in rows)
+    n_launch = len(rows)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.steps):
+        one_step()
+    e1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    gpu_s = e0.elapsed_time(e1) / 1e3
+    elapsed = max(wall, gpu_s)
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+
+    images = world * args.batch * args.steps
+    value = images / elapsed
+    achieved = conv_flops / (conv_ms / 1e3)
+    result = {
+        'metric': 'images/sec (UNet-R50 512x512 bs=16/GPU, mean-teacher + CowMix semi-supervised training step)',
+        'value': round(value, 3), 'unit': 'images/sec', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16', 'data': 'synthetic (SURVEY §8d), random-init weights',
+        'config': {'workload': 'C2: UNet(ResNet-50 encoder, max_width=128, ConvT up) 512x512, semi-supervised '
+                               'mean-teacher + CowMix step (BCE sup loss w=0.5, consistency w=10, SGD m=0.9)',
+                   'global_batch': world * args.batch, 'per_gpu_batch': args.batch, 'image_size': args.size,
+                   'parallelism': f'dp{world}'},
+        'roofline': {'bound': 'mfma', 'kernel': 'conv engine (igemm fwd/dgrad/ConvT + wgrad), all launches of one step',
+                     'achieved': round(achieved / 1e12, 2), 'peak': BF16_DENSE_PEAK / 1e12, 'unit': 'TFLOP/s',
+                     'frac': round(achieved / BF16_DENSE_PEAK, 4), 'traffic': None,
+                     'conv_ms_per_step': round(conv_ms, 3), 'conv_gflop_per_step': round(conv_flops / 1e9, 1),
+                     'launches_per_step': n_launch},
+        'step_tflops': round(8 * FWD_GFLOP_PER_IMAGE * args.batch * world / (elapsed / args.steps) / 1e3, 2),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            result['cpu_baseline'] = cpu_baseline(args.size)
+        except Exception as exc:  # report, never hide
+            result['cpu_baseline'] = {'error': repr(exc)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

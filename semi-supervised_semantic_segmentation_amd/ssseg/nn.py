@@ -62,6 +62,41 @@ def _need_act(x, c_phys, what):
 
 
 # ------------------------------------------------------------------------------------------------
+# live kernel instrumentation (bench.py roofline): HIP events around every conv-engine launch
+# ------------------------------------------------------------------------------------------------
+_PROBE = {'on': False, 'rows': []}
+
+
+def probe(enable):
+    """Start/stop recording (start_event, end_event, algorithmic_flops, kind) per conv-engine call."""
+    _PROBE['on'] = bool(enable)
+    if enable:
+        _PROBE['rows'] = []
+    return _PROBE['rows']
+
+
+class _Timed:
+    def __init__(self, flops, kind):
+        self.flops, self.kind = flops, kind
+
+    def __enter__(self):
+        if _PROBE['on']:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+        return self
+
+    def __exit__(self, *a):
+        if _PROBE['on']:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            _PROBE['rows'].append((self.e0, e1, self.flops, self.kind))
+
+
+def _conv_flops(n, oh, ow, cout, cin, r, s):
+    return 2.0 * n * oh * ow * cout * cin * r * s
+
+
+# ------------------------------------------------------------------------------------------------
 # parameter gradient plumbing
 # ------------------------------------------------------------------------------------------------
 def _grad_of(p):
@@ -246,13 +281,16 @@ class Conv2d(nn.Conv2d, _ConvBase):
         d = self._fwd_desc(n, H, W)
         R, S = self.kernel_size
         w = self._pack('fwd', cout, self.out_channels, self.in_channels, cin, 0, 0, 1, R, 0, 1, S)
+        fl = _conv_flops(n, d.OH, d.OW, self.out_channels, self.in_channels, R, S)
         if self._ssseg_head:
             y = torch.empty((n, cout, d.OH, d.OW), dtype=torch.float32, device=x.device,
                             memory_format=torch.channels_last)
-            self._igemm(x, w, y, d, N.F32, self.bias, relu)
+            with _Timed(fl, 'fwd'):
+                self._igemm(x, w, y, d, N.F32, self.bias, relu)
             return y[:, :self.out_channels]
         y = new_act(n, cout, d.OH, d.OW, _CFG['dtype'], x.device)
-        self._igemm(x, w, y, d, N.dt_code(y), self.bias, relu)
+        with _Timed(fl, 'fwd'):
+            self._igemm(x, w, y, d, N.dt_code(y), self.bias, relu)
         return y
 
     def _grad_in(self, gy):
@@ -276,8 +314,10 @@ class Conv2d(nn.Conv2d, _ConvBase):
         d = self._fwd_desc(n, H, W)
         nb = N.lib().ssseg_conv_wgrad_workspace_bytes(ctypes_ref(d), N.dt_code(x))
         ws = N.workspace(nb, x.device)
-        N.call('ssseg_conv_wgrad', N.dev_ptr(x), N.dev_ptr(gy), N.dev_ptr(_grad_of(self.weight)), ctypes_ref(d),
-               N.dt_code(x), self.in_channels, self.out_channels, 1, 1, N.dev_ptr(ws), nb, N.stream())
+        R, S = self.kernel_size
+        with _Timed(_conv_flops(n, d.OH, d.OW, self.out_channels, self.in_channels, R, S), 'wgrad'):
+            N.call('ssseg_conv_wgrad', N.dev_ptr(x), N.dev_ptr(gy), N.dev_ptr(_grad_of(self.weight)), ctypes_ref(d),
+                   N.dt_code(x), self.in_channels, self.out_channels, 1, 1, N.dev_ptr(ws), nb, N.stream())
         if self.bias is not None:
             _ready(self.weight, self.bias)
         else:
@@ -289,13 +329,16 @@ class Conv2d(nn.Conv2d, _ConvBase):
         (R, S), (sh, sw), (ph, pw), (dh, dw) = self.kernel_size, self.stride, self.padding, self.dilation
         OH, OW = gy.shape[2], gy.shape[3]
         dx = new_act(n, cin, H, W, _CFG['dtype'], gy.device)
+        timer = _Timed(_conv_flops(n, OH, OW, self.out_channels, self.in_channels, R, S), 'dgrad')
         if sh == 1 and sw == 1:
             w = self._pack('dgrad', cin, self.in_channels, self.out_channels, cout, 1, R - 1, -1, R, S - 1, -1, S)
             d = _desc(N=n, H=OH, W=OW, C=cout, ldx=cout, OH=H, OW=W, K=cin, R=R, S=S, sy=1, sx=1, dy=dh, dx=dw,
                       py=ph - (R - 1) * dh, px=pw - (S - 1) * dw, outH=H, outW=W, osy=1, osx=1, ooy=0, oox=0,
                       ldy=cin, ldw=R * S * cout)
-            self._igemm(gy, w, dx, d, N.dt_code(dx))
+            with timer:
+                self._igemm(gy, w, dx, d, N.dt_code(dx))
             return dx
+        timer.__enter__()
         for (phy, ry0, rny, dly, qy) in _phases(sh, ph, R, H, dh):
             for (phx, rx0, rnx, dlx, qx) in _phases(sw, pw, S, W, dw):
                 if qy == 0 or qx == 0:
@@ -307,6 +350,7 @@ class Conv2d(nn.Conv2d, _ConvBase):
                           dx=-1, py=dly, px=dlx, outH=H, outW=W, osy=sh, osx=sw, ooy=phy, oox=phx, ldy=cin,
                           ldw=max(rr * ss * cout, cout))
                 self._igemm(gy, w, dx, d, N.dt_code(dx))
+        timer.__exit__()
         return dx
 
 
@@ -346,6 +390,8 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
         (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
         OH, OW = self._out_hw(H, W)
         y = new_act(n, cout, OH, OW, _CFG['dtype'], x.device)
+        timer = _Timed(_conv_flops(n, H, W, self.out_channels, self.in_channels, R, S), 'fwd')
+        timer.__enter__()
         for (phy, ry0, rny, dly, qy) in _phases(sh, ph, R, OH):
             for (phx, rx0, rnx, dlx, qx) in _phases(sw, pw, S, OW):
                 if qy == 0 or qx == 0:
@@ -357,6 +403,7 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
                           py=dly, px=dlx, outH=OH, outW=OW, osy=sh, osx=sw, ooy=phy, oox=phx, ldy=cout,
                           ldw=max(rr * ss * cin, cin))
                 self._igemm(x, w, y, d, N.dt_code(y), self.bias, relu)
+        timer.__exit__()
         return y
 
     def _grad_in(self, gy):
@@ -375,8 +422,10 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
                       py=-ph, px=-pw, outH=H, outW=W, osy=1, osx=1, ooy=0, oox=0, ldy=cin, ldw=R * S * cout)
             nb = N.lib().ssseg_conv_wgrad_workspace_bytes(ctypes_ref(d), N.dt_code(x))
             ws = N.workspace(nb, x.device)
-            N.call('ssseg_conv_wgrad', N.dev_ptr(gy), N.dev_ptr(x), N.dev_ptr(_grad_of(self.weight)), ctypes_ref(d),
-                   N.dt_code(x), self.out_channels, self.in_channels, 1, 1, N.dev_ptr(ws), nb, N.stream())
+            with _Timed(_conv_flops(n, H, W, self.out_channels, self.in_channels, R, S), 'wgrad'):
+                N.call('ssseg_conv_wgrad', N.dev_ptr(gy), N.dev_ptr(x), N.dev_ptr(_grad_of(self.weight)),
+                       ctypes_ref(d), N.dt_code(x), self.out_channels, self.in_channels, 1, 1, N.dev_ptr(ws), nb,
+                       N.stream())
         _ready(*[p for p in (self.weight, self.bias) if p is not None])
 
     def _ssseg_dgrad(self, gy, xshape):
@@ -388,7 +437,8 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
         w = self._pack('dgrad', cin, self.in_channels, self.out_channels, cout, 0, 0, 1, R, 0, 1, S)
         d = _desc(N=n, H=OH, W=OW, C=cout, ldx=cout, OH=H, OW=W, K=cin, R=R, S=S, sy=sh, sx=sw, dy=1, dx=1, py=-ph,
                   px=-pw, outH=H, outW=W, osy=1, osx=1, ooy=0, oox=0, ldy=cin, ldw=R * S * cout)
-        self._igemm(gy, w, dx, d, N.dt_code(dx))
+        with _Timed(_conv_flops(n, H, W, self.out_channels, self.in_channels, R, S), 'dgrad'):
+            self._igemm(gy, w, dx, d, N.dt_code(dx))
         return dx
 
 
