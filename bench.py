@@ -144,8 +144,8 @@ def main():
     one_step()
     snn.probe(False)
     torch.cuda.synchronize()
-    conv_ms = sum(a.elapsed_time(b) for a, b, _, _ in rows)
-    conv_flops = sum(f for _, _, f, _ in rows)
+    conv_ms = sum(r[0].elapsed_time(r[1]) for r in rows)
+    conv_flops = sum(r[2] for r in rows)
     n_launch = len(rows)
 
     if world > 1:

@@ -169,7 +169,14 @@ typedef struct {
  * strided output), and the ConvTranspose2d input gradient.  dt: input/weight dtype; dt_out: output.
  * When R*S == 0 (an output phase no tap reaches) the phase is zero-filled. */
 int ssseg_conv_igemm(const void* x, const void* w, void* y, const ssseg_conv_desc* desc_host, int dt, int dt_out,
-                     const float* bias, int relu, ssseg_stream_t stream);
+                     const float* bias, int relu, void* ws, size_t ws_bytes, ssseg_stream_t stream);
+/* Workspace for ssseg_conv_igemm: non-zero when the launch splits K across workgroups (few output tiles,
+ * long contraction: fp32 partials [M][K] + a finalize pass).  Passing no workspace disables the split. */
+size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* desc_host, int dt);
+
+/* Runtime variant switches for A/B measurement.  knob 0: igemm pipeline depth (0 = one k-tile in flight,
+ * default; 1 = two); knob 1: split-K cap (0 = heuristic, -1 = off, n = at most n).  Not thread-safe. */
+int ssseg_set_knob(int id, int value);
 
 /* dW = sum over output pixels of dY[p][k] * x_col[p][(r,s,c)] (split-K fp32 slabs + deterministic
  * reduce).  dy is [N][OH][OW] with pixel stride desc.ldy.  layout 0: dw [K][R][S][C];

@@ -126,16 +126,29 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x
   }
 }
 
-__global__ void bn_partial_final_kernel(const double* part, int nparts, int C, double* sums) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// sums over the per-block partials: block = 32 channels x 8 partial lanes
+__global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* part, int nparts, int C, double* sums) {
+  __shared__ double red[2][8][32];
+  const int cl = threadIdx.x & 31, pl = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
   double a = 0, b = 0;
-  for (int i = 0; i < nparts; ++i) {
-    a += part[(int64_t)(2 * i) * C + c];
-    b += part[(int64_t)(2 * i + 1) * C + c];
+  if (c < C) {
+    for (int i = pl; i < nparts; i += 8) {
+      a += part[(int64_t)(2 * i) * C + c];
+      b += part[(int64_t)(2 * i + 1) * C + c];
+    }
   }
-  sums[c] = a;
-  sums[C + c] = b;
+  red[0][pl][cl] = a;
+  red[1][pl][cl] = b;
+  __syncthreads();
+  if (pl == 0 && c < C) {
+    for (int k = 1; k < 8; ++k) {
+      a += red[0][k][cl];
+      b += red[1][k][cl];
+    }
+    sums[c] = a;
+    sums[C + c] = b;
+  }
 }
 
 __global__ void bn_finalize_kernel(const double* sums, int C, double count, float eps, float momentum, float* mean_out,
@@ -237,7 +250,7 @@ int run_partials(const T* x, const T* dy, const T* res, int64_t P, int64_t C, in
   gx = gx < 1 ? 1 : (gx > MAXG ? MAXG : gx);
   hipLaunchKernelGGL((bn_partial_kernel<T, MODE>), dim3((unsigned)gx, L.cblocks), dim3(256), 0, s, x, dy, res, P,
                      (int)C, ldx, lddy, ldr, L, mean, invstd, gamma, beta, relu, (double*)ws);
-  hipLaunchKernelGGL(bn_partial_final_kernel, dim3((C + 255) / 256), dim3(256), 0, s, (const double*)ws, (int)gx,
+  hipLaunchKernelGGL(bn_partial_final_kernel, dim3((C + 31) / 32), dim3(256), 0, s, (const double*)ws, (int)gx,
                      (int)C, sums);
   return 0;
 }

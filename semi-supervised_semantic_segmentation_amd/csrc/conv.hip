@@ -89,10 +89,13 @@ constexpr int ROWB = 80;   // 64 data bytes + 16 pad per LDS row
 // ------------------------------------------------------------------------------------------------
 // forward / dgrad / transposed-conv gather GEMM
 // ------------------------------------------------------------------------------------------------
-template <typename T, typename TO, int BM, int BN, int WM, int WN>
-__global__ void __launch_bounds__(256) igemm_kernel(const T* __restrict__ x, const T* __restrict__ w,
-                                                    TO* __restrict__ y, ConvGeom g, const float* __restrict__ bias,
-                                                    int relu) {
+int g_knobs[8] = {0, -1, 0, 0, 0, 0, 0, 0};   // runtime variant switches (ssseg_set_knob)
+
+template <typename T, typename TO, int BM, int BN, int WM, int WN, bool DEEP>
+__global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __restrict__ x, const T* __restrict__ w,
+                                                                  TO* __restrict__ y, ConvGeom g,
+                                                                  const float* __restrict__ bias, int relu,
+                                                                  int splits, float* __restrict__ ws) {
   constexpr int VEC = MF<T>::VEC;
   constexpr int BK = 64 / (int)sizeof(T);
   constexpr int A_PER = BM / 64;                 // pixel rows per thread (4 chunks per row)
@@ -103,10 +106,21 @@ __global__ void __launch_bounds__(256) igemm_kernel(const T* __restrict__ x, con
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const long long m0 = (long long)blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
+  // XCD-aware remap of the 1-D grid: consecutive tile ids (the N tiles of one M tile, then the next
+  // M tile) go to the same XCD so the gathered input rows are re-read from that XCD's L2.
+  const int nnt = (g.K + BN - 1) / BN;
+  const int ntiles = gridDim.x;
+  const int xcd = blockIdx.x & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+  const long long m0 = (long long)(tile / nnt) * BM;
+  const int n0 = (tile % nnt) * BN;
   const int chunk = t & 3;
   const int RS = g.R * g.S;
+  // split-K: this block reduces k-tiles [kt0, kt1) of the contraction (blockIdx.y = split index)
+  const int nk_all = (g.KK + BK - 1) / BK;
+  const int kper = (nk_all + splits - 1) / splits;
+  const int kt0 = blockIdx.y * kper;
+  const int kt1 = min(nk_all, kt0 + kper);
 
   int a_n[A_PER], a_oy[A_PER], a_ox[A_PER];
   bool a_ok[A_PER];
@@ -120,16 +134,12 @@ __global__ void __launch_bounds__(256) igemm_kernel(const T* __restrict__ x, con
     a_oy[i] = (int)(q % g.OH);
     a_n[i] = (int)(q / g.OH);
   }
-  // k-state of this thread's chunk: k = tap*C + kc, tap = r*S + s
-  int kc = chunk * VEC, tap = 0, r = 0, s = 0;
-  while (kc >= g.C && tap < RS) {
-    kc -= g.C; ++tap;
-    if (++s == g.S) { s = 0; ++r; }
-  }
-  const int nk = (g.KK + BK - 1) / BK;
+  // k-state of this thread's chunk: k = tap*C + kc, tap = r*S + s (advanced by every load, in order)
+  const int k_first = kt0 * BK + chunk * VEC;
+  int tap = min(k_first / g.C, RS), kc = k_first - tap * g.C, r = tap / max(g.S, 1), s = tap - r * g.S;
+  const int nk = max(kt1 - kt0, 0);
 
-  uint4 ra[A_PER], rb[B_IT];
-  auto load = [&](int kt) {
+  auto load = [&](uint4 (&ra)[A_PER], uint4 (&rb)[B_IT], int kt) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int iy = a_oy[i] * g.sy + r * g.dy + g.py;
@@ -143,7 +153,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(const T* __restrict__ x, con
       rb[j] = make_uint4(0, 0, 0, 0);
       if (id < BN * 4) {
         const int n = n0 + (id >> 2);
-        const int k = kt * BK + (id & 3) * VEC;
+        const int k = (kt0 + kt) * BK + (id & 3) * VEC;
         if (n < g.K && k < g.KK) rb[j] = *(const uint4*)(w + (long long)n * g.ldw + k);
       }
     }
@@ -153,7 +163,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(const T* __restrict__ x, con
       if (++s == g.S) { s = 0; ++r; }
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](const uint4 (&ra)[A_PER], const uint4 (&rb)[B_IT], int buf) {
     char* As = smem + buf * (BM + BN) * ROWB;
     char* Bs = As + BM * ROWB;
 #pragma unroll
@@ -171,14 +181,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(const T* __restrict__ x, con
 #pragma unroll
     for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) {
-    load(0);
-    store(0);
-    __syncthreads();
-  }
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) load(kt + 1);
+  auto compute = [&](int buf) {
     const char* As = smem + buf * (BM + BN) * ROWB;
     const char* Bs = As + BM * ROWB;
     typename MF<T>::frag af[FN], bfr[FM];
@@ -192,8 +195,40 @@ __global__ void __launch_bounds__(256) igemm_kernel(const T* __restrict__ x, con
     for (int i = 0; i < FN; ++i)
 #pragma unroll
       for (int j = 0; j < FM; ++j) MF<T>::mma(af[i], bfr[j], acc[i][j]);
-    if (kt + 1 < nk) store(buf ^ 1);
+  };
+
+  if constexpr (DEEP) {
+    // two register sets: tile kt+2 is in flight while tile kt is multiplied and tile kt+1 is staged
+    uint4 ra0[A_PER], rb0[B_IT], ra1[A_PER], rb1[B_IT];
+    if (nk > 0) load(ra0, rb0, 0);
+    if (nk > 1) load(ra1, rb1, 1);
+    if (nk > 0) store(ra0, rb0, 0);
     __syncthreads();
+    for (int kt = 0; kt < nk; kt += 2) {
+      if (kt + 2 < nk) load(ra0, rb0, kt + 2);
+      compute(0);
+      if (kt + 1 < nk) store(ra1, rb1, 1);
+      __syncthreads();
+      if (kt + 1 >= nk) break;
+      if (kt + 3 < nk) load(ra1, rb1, kt + 3);
+      compute(1);
+      if (kt + 2 < nk) store(ra0, rb0, 0);
+      __syncthreads();
+    }
+  } else {
+    // one register set: tile kt+1 is in flight while tile kt is multiplied
+    uint4 ra0[A_PER], rb0[B_IT];
+    if (nk > 0) {
+      load(ra0, rb0, 0);
+      store(ra0, rb0, 0);
+    }
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) load(ra0, rb0, kt + 1);
+      compute(kt & 1);
+      if (kt + 1 < nk) store(ra0, rb0, (kt + 1) & 1);
+      __syncthreads();
+    }
   }
 
   // epilogue: lane holds channels n..n+3 (n = 4*(lane>>4) within a 16-wide fragment) of pixel lane&15
@@ -206,6 +241,16 @@ __global__ void __launch_bounds__(256) igemm_kernel(const T* __restrict__ x, con
     const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
     const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
     TO* yp = y + op * g.ldy;
+    if (splits > 1) {   // fp32 partials into ws[m][K]; finalize adds bias/ReLU and writes y
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        const int n = n0 + wn * WTN + i * 16 + (lane >> 4) * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (n + e < g.K) atomicAdd(ws + m * g.K + n + e, acc[i][j][e]);
+      }
+      continue;
+    }
 #pragma unroll
     for (int i = 0; i < FN; ++i) {
       const int n = n0 + wn * WTN + i * 16 + (lane >> 4) * 4;
@@ -224,6 +269,24 @@ __global__ void __launch_bounds__(256) igemm_kernel(const T* __restrict__ x, con
         for (int e = 0; e < 4 && n + e < g.K; ++e) io<TO>::st(yp, n + e, v[e]);
       }
     }
+  }
+}
+
+// split-K finalize: y[pixel(m)][n] = act(ws[m][n] + bias[n])
+template <typename TO>
+__global__ void splitk_finalize_kernel(const float* __restrict__ ws, TO* __restrict__ y, ConvGeom g,
+                                       const float* __restrict__ bias, int relu) {
+  const long long total = g.M * g.K;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int n = (int)(i % g.K);
+    const long long m = i / g.K;
+    const int ox = (int)(m % g.OW);
+    const long long q = m / g.OW;
+    const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
+    const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+    float v = ws[i] + (bias ? bias[n] : 0.f);
+    if (relu) v = fmaxf(v, 0.f);
+    io<TO>::st(y, op * g.ldy + n, v);
   }
 }
 
@@ -419,8 +482,17 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, 
     const int kk = (int)(i % KK), k = (int)(i / KK);
     const int c = kk % C, tap = kk / C, r = tap / S, s = tap % S;
     if (c >= c_real || k >= k_real) continue;
-    float sum = 0.f;
-    for (int z = 0; z < splits; ++z) sum += slab[(long long)z * total + i];
+    // 4 independent accumulators keep several slab loads in flight (the loop is latency-bound)
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int z = 0;
+    for (; z + 4 <= splits; z += 4) {
+      s0 += slab[(long long)z * total + i];
+      s1 += slab[(long long)(z + 1) * total + i];
+      s2 += slab[(long long)(z + 2) * total + i];
+      s3 += slab[(long long)(z + 3) * total + i];
+    }
+    for (; z < splits; ++z) s0 += slab[(long long)z * total + i];
+    const float sum = (s0 + s1) + (s2 + s3);
     long long o;
     if (layout == 0) o = ((long long)k * R * S + tap) * C + c;
     else o = (((long long)k * c_real + c) * R + r) * S + s;
@@ -461,23 +533,43 @@ __global__ void weight_pack_kernel(const float* __restrict__ src, T* __restrict_
 // ------------------------------------------------------------------------------------------------
 namespace {
 
+template <typename T, int BM, int BN>
+int plan_splits(const ConvGeom& g) {
+  const long long tiles = ((g.M + BM - 1) / BM) * ((g.K + BN - 1) / BN);
+  const int nk = (g.KK + 64 / (int)sizeof(T) - 1) / (64 / (int)sizeof(T));
+  if (g_knobs[1] < 0 || tiles >= 512 || nk < 32) return 1;
+  long long sp = (1024 + tiles - 1) / tiles;
+  sp = std::min<long long>(sp, nk / 16);
+  if (g_knobs[1] > 0) sp = std::min<long long>(sp, g_knobs[1]);
+  return (int)std::max<long long>(1, std::min<long long>(sp, 64));
+}
+
 template <typename T, typename TO, int BM, int BN, int WM, int WN>
-void launch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, const float* bias, int relu,
-                  hipStream_t s) {
-  const dim3 grid((unsigned)((g.M + BM - 1) / BM), (unsigned)((g.K + BN - 1) / BN));
-  hipLaunchKernelGGL((igemm_kernel<T, TO, BM, BN, WM, WN>), grid, dim3(256), 0, s, (const T*)x, (const T*)w, (TO*)y,
-                     g, bias, relu);
+void launch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, const float* bias, int relu, float* ws,
+                  int splits, hipStream_t s) {
+  const long long tiles = ((g.M + BM - 1) / BM) * ((g.K + BN - 1) / BN);
+  const dim3 grid((unsigned)tiles, (unsigned)splits);
+  if (splits > 1) (void)hipMemsetAsync(ws, 0, sizeof(float) * g.M * g.K, s);
+  if (g_knobs[0] == 0)
+    hipLaunchKernelGGL((igemm_kernel<T, TO, BM, BN, WM, WN, false>), grid, dim3(256), 0, s, (const T*)x, (const T*)w,
+                       (TO*)y, g, bias, relu, splits, ws);
+  else
+    hipLaunchKernelGGL((igemm_kernel<T, TO, BM, BN, WM, WN, true>), grid, dim3(256), 0, s, (const T*)x, (const T*)w,
+                       (TO*)y, g, bias, relu, splits, ws);
+  if (splits > 1)
+    hipLaunchKernelGGL(splitk_finalize_kernel<TO>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, ws, (TO*)y, g,
+                       bias, relu);
 }
 
 template <typename T, typename TO>
-void dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, const float* bias, int relu,
+void dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, const float* bias, int relu, float* ws,
                     hipStream_t s) {
   if (g.K <= 16)
-    launch_igemm<T, TO, 256, 16, 4, 1>(x, w, y, g, bias, relu, s);
+    launch_igemm<T, TO, 256, 16, 4, 1>(x, w, y, g, bias, relu, ws, ws ? plan_splits<T, 256, 16>(g) : 1, s);
   else if (g.K <= 64)
-    launch_igemm<T, TO, 256, 64, 4, 1>(x, w, y, g, bias, relu, s);
+    launch_igemm<T, TO, 256, 64, 4, 1>(x, w, y, g, bias, relu, ws, ws ? plan_splits<T, 256, 64>(g) : 1, s);
   else
-    launch_igemm<T, TO, 128, 128, 2, 2>(x, w, y, g, bias, relu, s);
+    launch_igemm<T, TO, 128, 128, 2, 2>(x, w, y, g, bias, relu, ws, ws ? plan_splits<T, 128, 128>(g) : 1, s);
 }
 
 struct WgradPlan {
@@ -529,8 +621,24 @@ bool geom_ok(const ConvGeom& g, int dt) {
 
 }  // namespace
 
+extern "C" int ssseg_set_knob(int id, int value) {
+  if (id < 0 || id >= 8) return SSSEG_EINVAL;
+  g_knobs[id] = value;
+  return 0;
+}
+
+extern "C" size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* d, int dt) {
+  ConvGeom g;
+  if (!make_geom(d, g)) return 0;
+  int sp;
+  if (g.K <= 16) sp = dt == SSSEG_BF16 ? plan_splits<bf16_t, 256, 16>(g) : plan_splits<float, 256, 16>(g);
+  else if (g.K <= 64) sp = dt == SSSEG_BF16 ? plan_splits<bf16_t, 256, 64>(g) : plan_splits<float, 256, 64>(g);
+  else sp = dt == SSSEG_BF16 ? plan_splits<bf16_t, 128, 128>(g) : plan_splits<float, 128, 128>(g);
+  return sp > 1 ? (size_t)g.M * g.K * sizeof(float) : 0;
+}
+
 extern "C" int ssseg_conv_igemm(const void* x, const void* w, void* y, const ssseg_conv_desc* d, int dt, int dt_out,
-                                const float* bias, int relu, ssseg_stream_t stream) {
+                                const float* bias, int relu, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
   ConvGeom g;
   if (!make_geom(d, g) || !y) return SSSEG_EINVAL;
   if (!geom_ok(g, dt)) return SSSEG_EINVAL;
@@ -545,12 +653,14 @@ extern "C" int ssseg_conv_igemm(const void* x, const void* w, void* y, const sss
     return 0;
   }
   if (!x || !w) return SSSEG_EINVAL;
+  const size_t need = ssseg_conv_igemm_workspace_bytes(d, dt);
+  float* wsf = (need > 0 && ws && ws_bytes >= need) ? (float*)ws : nullptr;   // no workspace: no split-K
   if (dt == SSSEG_BF16 && dt_out == SSSEG_BF16)
-    dispatch_igemm<bf16_t, bf16_t>(x, w, y, g, bias, relu, s);
+    dispatch_igemm<bf16_t, bf16_t>(x, w, y, g, bias, relu, wsf, s);
   else if (dt == SSSEG_BF16 && dt_out == SSSEG_F32)
-    dispatch_igemm<bf16_t, float>(x, w, y, g, bias, relu, s);
+    dispatch_igemm<bf16_t, float>(x, w, y, g, bias, relu, wsf, s);
   else if (dt == SSSEG_F32 && dt_out == SSSEG_F32)
-    dispatch_igemm<float, float>(x, w, y, g, bias, relu, s);
+    dispatch_igemm<float, float>(x, w, y, g, bias, relu, wsf, s);
   else
     return SSSEG_EUNSUPPORTED;
   SSSEG_LAUNCH_CHECK();

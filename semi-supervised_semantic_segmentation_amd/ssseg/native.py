@@ -46,7 +46,9 @@ SIGS = {
     'ssseg_sqnorm_accum': (i32, [vp, i64, vp, vp, sz, vp]),
     'ssseg_sgd_step': (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]),
     # convolution engine
-    'ssseg_conv_igemm': (i32, [vp, vp, vp, vp, i32, i32, vp, i32, vp]),
+    'ssseg_conv_igemm': (i32, [vp, vp, vp, vp, i32, i32, vp, i32, vp, sz, vp]),
+    'ssseg_conv_igemm_workspace_bytes': (sz, [vp, i32]),
+    'ssseg_set_knob': (i32, [i32, i32]),
     'ssseg_conv_wgrad_workspace_bytes': (sz, [vp, i32]),
     'ssseg_conv_wgrad': (i32, [vp, vp, vp, vp, i32, i64, i64, i32, i32, vp, sz, vp]),
     'ssseg_weight_pack': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, i32, i64, i64, i64, i64, i64, i64, i32, vp]),

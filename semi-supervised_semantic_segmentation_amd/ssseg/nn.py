@@ -76,8 +76,8 @@ def probe(enable):
 
 
 class _Timed:
-    def __init__(self, flops, kind):
-        self.flops, self.kind = flops, kind
+    def __init__(self, flops, kind, tag=''):
+        self.flops, self.kind, self.tag = flops, kind, tag
 
     def __enter__(self):
         if _PROBE['on']:
@@ -89,11 +89,15 @@ class _Timed:
         if _PROBE['on']:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
-            _PROBE['rows'].append((self.e0, e1, self.flops, self.kind))
+            _PROBE['rows'].append((self.e0, e1, self.flops, self.kind, self.tag))
 
 
 def _conv_flops(n, oh, ow, cout, cin, r, s):
     return 2.0 * n * oh * ow * cout * cin * r * s
+
+
+def _tag(mod, n, h, w):
+    return f'{type(mod).__name__} {mod.in_channels}->{mod.out_channels} k{mod.kernel_size[0]} s{mod.stride[0]} @{n}x{h}x{w}'
 
 
 # ------------------------------------------------------------------------------------------------
@@ -227,8 +231,12 @@ class _ConvBase:
         return t
 
     def _igemm(self, x, w, y, desc, out_dt, bias=None, relu=False):
-        N.call('ssseg_conv_igemm', N.dev_ptr(x), N.dev_ptr(w), N.dev_ptr(y), ctypes_ref(desc), N.dt_code(x), out_dt,
-               N.dev_ptr(bias) if bias is not None else None, int(bool(relu)), N.stream())
+        dref = ctypes_ref(desc)
+        nb = N.lib().ssseg_conv_igemm_workspace_bytes(dref, N.dt_code(x)) if w is not None else 0
+        ws = N.workspace(nb, x.device) if nb else None
+        N.call('ssseg_conv_igemm', N.dev_ptr(x), N.dev_ptr(w), N.dev_ptr(y), dref, N.dt_code(x), out_dt,
+               N.dev_ptr(bias) if bias is not None else None, int(bool(relu)), N.dev_ptr(ws) if ws is not None else None,
+               nb, N.stream())
 
 
 def ctypes_ref(d):
@@ -282,14 +290,15 @@ class Conv2d(nn.Conv2d, _ConvBase):
         R, S = self.kernel_size
         w = self._pack('fwd', cout, self.out_channels, self.in_channels, cin, 0, 0, 1, R, 0, 1, S)
         fl = _conv_flops(n, d.OH, d.OW, self.out_channels, self.in_channels, R, S)
+        tg = _tag(self, n, H, W)
         if self._ssseg_head:
             y = torch.empty((n, cout, d.OH, d.OW), dtype=torch.float32, device=x.device,
                             memory_format=torch.channels_last)
-            with _Timed(fl, 'fwd'):
+            with _Timed(fl, 'fwd', tg):
                 self._igemm(x, w, y, d, N.F32, self.bias, relu)
             return y[:, :self.out_channels]
         y = new_act(n, cout, d.OH, d.OW, _CFG['dtype'], x.device)
-        with _Timed(fl, 'fwd'):
+        with _Timed(fl, 'fwd', tg):
             self._igemm(x, w, y, d, N.dt_code(y), self.bias, relu)
         return y
 
@@ -315,7 +324,7 @@ class Conv2d(nn.Conv2d, _ConvBase):
         nb = N.lib().ssseg_conv_wgrad_workspace_bytes(ctypes_ref(d), N.dt_code(x))
         ws = N.workspace(nb, x.device)
         R, S = self.kernel_size
-        with _Timed(_conv_flops(n, d.OH, d.OW, self.out_channels, self.in_channels, R, S), 'wgrad'):
+        with _Timed(_conv_flops(n, d.OH, d.OW, self.out_channels, self.in_channels, R, S), 'wgrad', _tag(self, n, H, W)):
             N.call('ssseg_conv_wgrad', N.dev_ptr(x), N.dev_ptr(gy), N.dev_ptr(_grad_of(self.weight)), ctypes_ref(d),
                    N.dt_code(x), self.in_channels, self.out_channels, 1, 1, N.dev_ptr(ws), nb, N.stream())
         if self.bias is not None:
@@ -329,7 +338,7 @@ class Conv2d(nn.Conv2d, _ConvBase):
         (R, S), (sh, sw), (ph, pw), (dh, dw) = self.kernel_size, self.stride, self.padding, self.dilation
         OH, OW = gy.shape[2], gy.shape[3]
         dx = new_act(n, cin, H, W, _CFG['dtype'], gy.device)
-        timer = _Timed(_conv_flops(n, OH, OW, self.out_channels, self.in_channels, R, S), 'dgrad')
+        timer = _Timed(_conv_flops(n, OH, OW, self.out_channels, self.in_channels, R, S), 'dgrad', _tag(self, n, H, W))
         if sh == 1 and sw == 1:
             w = self._pack('dgrad', cin, self.in_channels, self.out_channels, cout, 1, R - 1, -1, R, S - 1, -1, S)
             d = _desc(N=n, H=OH, W=OW, C=cout, ldx=cout, OH=H, OW=W, K=cin, R=R, S=S, sy=1, sx=1, dy=dh, dx=dw,
@@ -390,7 +399,7 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
         (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
         OH, OW = self._out_hw(H, W)
         y = new_act(n, cout, OH, OW, _CFG['dtype'], x.device)
-        timer = _Timed(_conv_flops(n, H, W, self.out_channels, self.in_channels, R, S), 'fwd')
+        timer = _Timed(_conv_flops(n, H, W, self.out_channels, self.in_channels, R, S), 'fwd', _tag(self, n, H, W))
         timer.__enter__()
         for (phy, ry0, rny, dly, qy) in _phases(sh, ph, R, OH):
             for (phx, rx0, rnx, dlx, qx) in _phases(sw, pw, S, OW):
@@ -422,7 +431,7 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
                       py=-ph, px=-pw, outH=H, outW=W, osy=1, osx=1, ooy=0, oox=0, ldy=cin, ldw=R * S * cout)
             nb = N.lib().ssseg_conv_wgrad_workspace_bytes(ctypes_ref(d), N.dt_code(x))
             ws = N.workspace(nb, x.device)
-            with _Timed(_conv_flops(n, H, W, self.out_channels, self.in_channels, R, S), 'wgrad'):
+            with _Timed(_conv_flops(n, H, W, self.out_channels, self.in_channels, R, S), 'wgrad', _tag(self, n, H, W)):
                 N.call('ssseg_conv_wgrad', N.dev_ptr(gy), N.dev_ptr(x), N.dev_ptr(_grad_of(self.weight)),
                        ctypes_ref(d), N.dt_code(x), self.out_channels, self.in_channels, 1, 1, N.dev_ptr(ws), nb,
                        N.stream())
@@ -437,7 +446,7 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
         w = self._pack('dgrad', cin, self.in_channels, self.out_channels, cout, 0, 0, 1, R, 0, 1, S)
         d = _desc(N=n, H=OH, W=OW, C=cout, ldx=cout, OH=H, OW=W, K=cin, R=R, S=S, sy=sh, sx=sw, dy=1, dx=1, py=-ph,
                   px=-pw, outH=H, outW=W, osy=1, osx=1, ooy=0, oox=0, ldy=cin, ldw=R * S * cout)
-        with _Timed(_conv_flops(n, H, W, self.out_channels, self.in_channels, R, S), 'dgrad'):
+        with _Timed(_conv_flops(n, H, W, self.out_channels, self.in_channels, R, S), 'dgrad', _tag(self, n, H, W)):
             self._igemm(gy, w, dx, d, N.dt_code(dx))
         return dx
 
