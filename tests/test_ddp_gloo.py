@@ -1,0 +1,68 @@
+"""World-size-2 gloo (CPU) test of the data-parallel gradient reducer (ssseg/ddp.py): buckets over the
+flat gradient arena, readiness-triggered launches, finish() joins, result = average over ranks."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from ssseg.ddp import DistributedDataParallel
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(torch.nn.Linear(64, 300), torch.nn.Linear(300, 70), torch.nn.Linear(70, 5))
+        if rank == 1:        # different init on rank 1: the constructor must broadcast rank 0's weights
+            with torch.no_grad():
+                for p in model.parameters():
+                    p.add_(1.0)
+        ddp = DistributedDataParallel(model, bucket_cap_mb=0.05)
+        assert len(ddp.buckets) > 1
+        params = list(model.parameters())
+        ref0 = [p.detach().clone() for p in params]
+        # weights equal across ranks after the broadcast
+        g = [torch.zeros_like(t) for t in range(world) for t in [ref0[0]]]
+        dist.all_gather(g, ref0[0])
+        assert torch.equal(g[0], g[1])
+        # each rank's gradient = (rank + 1) * index pattern; the average is 1.5 * pattern
+        for i, p in enumerate(params):
+            p.grad.copy_(torch.arange(p.numel(), dtype=torch.float32).view_as(p) * (rank + 1) + i)
+        ddp.arm()
+        for p in reversed(params):        # readiness in backward order
+            ddp.mark_ready(p)
+        ddp.finish()
+        ok = all(torch.allclose(p.grad, torch.arange(p.numel(), dtype=torch.float32).view_as(p) * 1.5 + i)
+                 for i, p in enumerate(params))
+        # an unarmed backward must not reduce
+        for p in params:
+            p.grad.fill_(float(rank))
+            ddp.mark_ready(p)
+        ok = ok and all(torch.all(p.grad == rank) for p in params)
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_reducer_gloo_world2():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    res = dict(q.get(timeout=5) for _ in range(2))
+    assert res == {0: True, 1: True}
