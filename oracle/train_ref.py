@@ -77,7 +77,7 @@ def train_epoch(model, ema_model, optimizer, batches, unsup_iter, epoch, cfg, lo
             cons, cm_mean = consistency_loss(s, t_mix, tc['confidence_threshold'])
             unsup = cons * tc['consistency_loss_weight'] * float(epoch > 25)
             unsup.backward()
-            rec.update(unsup_loss=float(unsup), cm_mean=float(cm_mean))
+            rec.update(unsup_loss=float(unsup.detach()), cm_mean=float(cm_mean))
         if step % tc['virtual_batch_size_multiplier'] == 0 and step != 0:
             torch.nn.utils.clip_grad_norm_(model.parameters(), tc['gradient_clip_value'])
             optimizer.step()

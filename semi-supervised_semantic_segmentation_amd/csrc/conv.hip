@@ -564,10 +564,14 @@ void launch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, cons
 template <typename T, typename TO>
 void dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, const float* bias, int relu, float* ws,
                     hipStream_t s) {
+  const long long t128 = ((g.M + 127) / 128) * ((g.K + 127) / 128);
+  const bool small = g_knobs[2] == 0 ? (t128 < 512) : (g_knobs[2] > 0);
   if (g.K <= 16)
     launch_igemm<T, TO, 256, 16, 4, 1>(x, w, y, g, bias, relu, ws, ws ? plan_splits<T, 256, 16>(g) : 1, s);
-  else if (g.K <= 64)
+  else if (g.K <= 64 && !small)
     launch_igemm<T, TO, 256, 64, 4, 1>(x, w, y, g, bias, relu, ws, ws ? plan_splits<T, 256, 64>(g) : 1, s);
+  else if (small)
+    launch_igemm<T, TO, 64, 64, 2, 2>(x, w, y, g, bias, relu, ws, ws ? plan_splits<T, 64, 64>(g) : 1, s);
   else
     launch_igemm<T, TO, 128, 128, 2, 2>(x, w, y, g, bias, relu, ws, ws ? plan_splits<T, 128, 128>(g) : 1, s);
 }
@@ -631,8 +635,11 @@ extern "C" size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* d, int
   ConvGeom g;
   if (!make_geom(d, g)) return 0;
   int sp;
+  const long long t128 = ((g.M + 127) / 128) * ((g.K + 127) / 128);
+  const bool small = g_knobs[2] == 0 ? (t128 < 512) : (g_knobs[2] > 0);
   if (g.K <= 16) sp = dt == SSSEG_BF16 ? plan_splits<bf16_t, 256, 16>(g) : plan_splits<float, 256, 16>(g);
-  else if (g.K <= 64) sp = dt == SSSEG_BF16 ? plan_splits<bf16_t, 256, 64>(g) : plan_splits<float, 256, 64>(g);
+  else if (g.K <= 64 && !small) sp = dt == SSSEG_BF16 ? plan_splits<bf16_t, 256, 64>(g) : plan_splits<float, 256, 64>(g);
+  else if (small) sp = dt == SSSEG_BF16 ? plan_splits<bf16_t, 64, 64>(g) : plan_splits<float, 64, 64>(g);
   else sp = dt == SSSEG_BF16 ? plan_splits<bf16_t, 128, 128>(g) : plan_splits<float, 128, 128>(g);
   return sp > 1 ? (size_t)g.M * g.K * sizeof(float) : 0;
 }
