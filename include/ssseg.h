@@ -170,6 +170,14 @@ typedef struct {
  * When R*S == 0 (an output phase no tap reaches) the phase is zero-filled. */
 int ssseg_conv_igemm(const void* x, const void* w, void* y, const ssseg_conv_desc* desc_host, int dt, int dt_out,
                      const float* bias, int relu, void* ws, size_t ws_bytes, ssseg_stream_t stream);
+/* Same contraction with the full fused epilogue
+ *   y[m][n] = act(acc[m][n] * scale[n] + shift[n] + residual[pixel(m)][n])
+ * scale NULL = 1, shift NULL = 0, residual NULL = 0 (dtype dt_out, pixel stride ldr).  Folds an eval-mode
+ * BatchNorm (ssseg_bn_fold) and the Bottleneck identity add + ReLU (unet.py:9-10 / encoder blocks) into the
+ * conv that produces them, so the teacher forwards (train.py:69-94, no grad) write each activation once. */
+int ssseg_conv_igemm_ex(const void* x, const void* w, void* y, const ssseg_conv_desc* desc_host, int dt, int dt_out,
+                        const float* scale, const float* shift, const void* residual, int64_t ldr, int relu, void* ws,
+                        size_t ws_bytes, ssseg_stream_t stream);
 /* Workspace for ssseg_conv_igemm: non-zero when the launch splits K across workgroups (few output tiles,
  * long contraction: fp32 partials [M][K] + a finalize pass).  Passing no workspace disables the split. */
 size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* desc_host, int dt);
@@ -209,7 +217,13 @@ int ssseg_bn_finalize(const double* sums, int64_t C, double count, float eps, fl
 /* eval mode: mean = running_mean, invstd = 1/sqrt(running_var + eps) */
 int ssseg_bn_eval_params(const float* running_mean, const float* running_var, float eps, int64_t C, float* mean_out,
                          float* invstd_out, ssseg_stream_t stream);
-/* y = act(gamma*(x-mean)*invstd + beta [+ residual]); relu = 1 for ReLU (unet.py:10, Bottleneck add+relu) */
+/* eval BatchNorm as a per-channel affine of the producing conv's accumulator (ssseg_conv_igemm_ex):
+ * scale = gamma/sqrt(running_var + eps), shift = beta + (conv_bias - running_mean)*scale for c < C,
+ * (0, 0) for C <= c < Cp (padding channels stay zero).  gamma/beta/conv_bias may be NULL. */
+int ssseg_bn_fold(const float* running_mean, const float* running_var, const float* gamma, const float* beta,
+                  const float* conv_bias, float eps, int64_t C, int64_t Cp, float* scale, float* shift,
+                  ssseg_stream_t stream);
+/* y = act(gamma*(x-mean)*invstd + beta [+ residual]); channels [C, rup(C, 16 bytes)) of y are written 0; relu = 1 for ReLU (unet.py:10, Bottleneck add+relu) */
 int ssseg_bn_apply(const void* x, const void* residual, void* y, int64_t P, int64_t C, int64_t ldx, int64_t ldr,
                    int64_t ldy, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu,
                    int dt, ssseg_stream_t stream);
@@ -220,7 +234,8 @@ int ssseg_bn_bwd_reduce(const void* dy, const void* x, const void* residual, int
                         ssseg_stream_t stream);
 /* dgamma += sums[C:2C], dbeta += sums[0:C] (local sums, before any SyncBN all-reduce) */
 int ssseg_bn_param_grad(const double* sums, int64_t C, float* dgamma, float* dbeta, ssseg_stream_t stream);
-/* backward pass 2: dx = gamma*invstd*(dyr - [train]*(sum_dyr + xhat*sum_dyr_xhat)/count); dres = dyr */
+/* backward pass 2: dx = gamma*invstd*(dyr - [train]*(sum_dyr + xhat*sum_dyr_xhat)/count); dres = dyr;
+ * padding channels of dx / dres written 0 as in ssseg_bn_apply */
 int ssseg_bn_bwd_apply(const void* dy, const void* x, const void* residual, void* dx, void* dres, int64_t P, int64_t C,
                        int64_t ldx, int64_t ldr, int64_t lddy, int64_t lddx, const float* mean, const float* invstd,
                        const float* gamma, const float* beta, int relu, int train, const double* sums, double count,

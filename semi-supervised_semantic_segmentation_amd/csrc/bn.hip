@@ -10,119 +10,178 @@
 //             apply   dx = gamma*invstd*(dyr - (sum_dyr + xhat*sum_dyr_xhat)/count)   (train)
 //                     dx = gamma*invstd*dyr                                            (eval)
 //             dres = dyr (residual branch gradient)
+#include <initializer_list>
+
 #include "common.h"
 
 namespace {
 
-constexpr int CH = 4;   // channels per thread chunk
+// A thread owns one chunk of V consecutive channels (16 bytes: 8 bf16 / 4 f32; 8-byte chunks when a
+// leading dimension is not 16-byte aligned) for the whole kernel, so the per-channel parameters sit in
+// registers; it walks pixels with U independent loads in flight.  Channels [C, rup(C, V)) of every
+// output are written as 0 (the NHWC channel padding), so callers need no memset.
+constexpr int U = 4;
+constexpr int CH = 4;   // ABI granularity: C and every leading dimension are multiples of 4
 
-template <typename T> struct V4;
-template <> struct V4<float> {
+template <typename T, int V> struct Vec;
+template <> struct Vec<float, 4> {
   __device__ __forceinline__ static void ld(const float* p, float (&v)[4]) {
     const float4 q = *(const float4*)p;
     v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
   }
   __device__ __forceinline__ static void st(float* p, const float (&v)[4]) { *(float4*)p = make_float4(v[0], v[1], v[2], v[3]); }
 };
-template <> struct V4<bf16_t> {
+template <> struct Vec<float, 2> {
+  __device__ __forceinline__ static void ld(const float* p, float (&v)[2]) {
+    const float2 q = *(const float2*)p;
+    v[0] = q.x; v[1] = q.y;
+  }
+  __device__ __forceinline__ static void st(float* p, const float (&v)[2]) { *(float2*)p = make_float2(v[0], v[1]); }
+};
+__device__ __forceinline__ void unpack2(unsigned u, float& a, float& b) {
+  a = __uint_as_float(u << 16);
+  b = __uint_as_float(u & 0xffff0000u);
+}
+__device__ __forceinline__ unsigned pack2(float a, float b) {
+  return (unsigned)f32_to_bf16(a) | ((unsigned)f32_to_bf16(b) << 16);
+}
+template <> struct Vec<bf16_t, 8> {
+  __device__ __forceinline__ static void ld(const bf16_t* p, float (&v)[8]) {
+    const uint4 q = *(const uint4*)p;
+    unpack2(q.x, v[0], v[1]); unpack2(q.y, v[2], v[3]); unpack2(q.z, v[4], v[5]); unpack2(q.w, v[6], v[7]);
+  }
+  __device__ __forceinline__ static void st(bf16_t* p, const float (&v)[8]) {
+    *(uint4*)p = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+  }
+};
+template <> struct Vec<bf16_t, 4> {
   __device__ __forceinline__ static void ld(const bf16_t* p, float (&v)[4]) {
     const uint2 q = *(const uint2*)p;
-    v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
-    v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+    unpack2(q.x, v[0], v[1]); unpack2(q.y, v[2], v[3]);
   }
   __device__ __forceinline__ static void st(bf16_t* p, const float (&v)[4]) {
-    uint2 u;
-    u.x = (unsigned)f32_to_bf16(v[0]) | ((unsigned)f32_to_bf16(v[1]) << 16);
-    u.y = (unsigned)f32_to_bf16(v[2]) | ((unsigned)f32_to_bf16(v[3]) << 16);
-    *(uint2*)p = u;
+    *(uint2*)p = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
   }
 };
 
 struct Layout {
   int cpb;        // chunks per block row (<= 256)
-  int ppb;        // pixels per block iteration
+  int ppb;        // pixel rows per block
   int cblocks;    // blocks along channels
 };
 
-static Layout layout_for(int64_t C) {
+static Layout layout_for(int64_t C, int V) {
   Layout l;
-  const int nch = (int)(C / CH);
+  const int nch = (int)((C + V - 1) / V);
   l.cpb = nch < 256 ? nch : 256;
   l.ppb = 256 / l.cpb;
   l.cblocks = (nch + l.cpb - 1) / l.cpb;
   return l;
 }
 
+// pixel blocks: enough workgroups to fill 256 CUs several times over, each walking >= U*ppb pixels
+static int64_t pixel_blocks(int64_t P, const Layout& L, int64_t cap) {
+  int64_t gx = (P + (int64_t)L.ppb * U - 1) / ((int64_t)L.ppb * U);
+  const int64_t want = (4096 + L.cblocks - 1) / L.cblocks;
+  gx = gx > want ? want : gx;
+  gx = gx > cap ? cap : gx;
+  return gx < 1 ? 1 : gx;
+}
+
+struct ChanParams {
+  const float *mean, *invstd, *gamma, *beta;
+};
+
+template <int V>
+__device__ __forceinline__ void load_params(const ChanParams& cp, int c0, int C, float (&mu)[V], float (&is)[V],
+                                            float (&ga)[V], float (&be)[V], bool (&live)[V]) {
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    const int c = c0 + e;
+    live[e] = c < C;
+    mu[e] = live[e] ? cp.mean[c] : 0.f;
+    is[e] = live[e] ? cp.invstd[c] : 0.f;
+    ga[e] = live[e] ? (cp.gamma ? cp.gamma[c] : 1.f) : 0.f;
+    be[e] = live[e] ? (cp.beta ? cp.beta[c] : 0.f) : 0.f;
+  }
+}
+
 constexpr int MAXG = 256;   // partial blocks along pixels
 
 // per-block partial sums of 2 per-channel quantities; mode 0: (x, x^2); mode 1: (dyr, dyr*xhat)
-template <typename T, int MODE>
+template <typename T, int V, int MODE>
 __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                                                          const T* __restrict__ res, int64_t P, int C, int64_t ldx,
-                                                         int64_t lddy, int64_t ldr, Layout L, const float* mean,
-                                                         const float* invstd, const float* gamma, const float* beta,
+                                                         int64_t lddy, int64_t ldr, Layout L, ChanParams prm,
                                                          int relu, double* part) {
-  __shared__ double red[2][256][CH];
+  __shared__ double red[2][256][V];
   const int t = threadIdx.x;
   const int cl = t % L.cpb, pl = t / L.cpb;
-  const int chunk = blockIdx.y * L.cpb + cl;
-  const int c0 = chunk * CH;
+  const int c0 = (blockIdx.y * L.cpb + cl) * V;
   const bool active = pl < L.ppb && c0 < C;
-  double s1[CH] = {0, 0, 0, 0}, s2[CH] = {0, 0, 0, 0};
+  double s1[V], s2[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) s1[e] = s2[e] = 0.0;
   if (active) {
-    float mu[CH], is[CH], ga[CH], be[CH];
-    if (MODE == 1) {
+    float mu[V], is[V], ga[V], be[V];
+    bool live[V];
+    if (MODE == 1) load_params<V>(prm, c0, C, mu, is, ga, be, live);
+    const int64_t stride = (int64_t)gridDim.x * L.ppb;
+    for (int64_t p0 = (int64_t)blockIdx.x * L.ppb + pl; p0 < P; p0 += stride * U) {
+      float v[U][V], g[U][V], r[U][V];
 #pragma unroll
-      for (int e = 0; e < CH; ++e) {
-        mu[e] = mean[c0 + e]; is[e] = invstd[c0 + e];
-        ga[e] = gamma ? gamma[c0 + e] : 1.f; be[e] = beta ? beta[c0 + e] : 0.f;
-      }
-    }
-    for (int64_t p = (int64_t)blockIdx.x * L.ppb + pl; p < P; p += (int64_t)gridDim.x * L.ppb) {
-      float v[CH];
-      V4<T>::ld(x + p * ldx + c0, v);
-      if (MODE == 0) {
+      for (int u = 0; u < U; ++u) {
+        const int64_t p = p0 + u * stride;
 #pragma unroll
-        for (int e = 0; e < CH; ++e) {
-          s1[e] += (double)v[e];
-          s2[e] += (double)v[e] * (double)v[e];
-        }
-      } else {
-        float g[CH];
-        V4<T>::ld(dy + p * lddy + c0, g);
-        float r[CH] = {0, 0, 0, 0};
-        if (res && relu) V4<T>::ld(res + p * ldr + c0, r);
-#pragma unroll
-        for (int e = 0; e < CH; ++e) {
-          const float xh = (v[e] - mu[e]) * is[e];
-          float gr = g[e];
-          if (relu) {
-            const float yv = fmaf(ga[e], xh, be[e]) + r[e];
-            gr = yv > 0.f ? gr : 0.f;
+        for (int e = 0; e < V; ++e) v[u][e] = g[u][e] = r[u][e] = 0.f;
+        if (p < P) {
+          Vec<T, V>::ld(x + p * ldx + c0, v[u]);
+          if (MODE == 1) {
+            Vec<T, V>::ld(dy + p * lddy + c0, g[u]);
+            if (res && relu) Vec<T, V>::ld(res + p * ldr + c0, r[u]);
           }
-          s1[e] += (double)gr;
-          s2[e] += (double)gr * (double)xh;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (p0 + u * stride >= P) continue;
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          if (MODE == 0) {
+            s1[e] += (double)v[u][e];
+            s2[e] += (double)v[u][e] * (double)v[u][e];
+          } else {
+            const float xh = (v[u][e] - mu[e]) * is[e];
+            float gr = g[u][e];
+            if (relu) {
+              const float yv = fmaf(ga[e], xh, be[e]) + r[u][e];
+              gr = yv > 0.f ? gr : 0.f;
+            }
+            s1[e] += (double)gr;
+            s2[e] += (double)gr * (double)xh;
+          }
         }
       }
     }
   }
 #pragma unroll
-  for (int e = 0; e < CH; ++e) {
+  for (int e = 0; e < V; ++e) {
     red[0][t][e] = s1[e];
     red[1][t][e] = s2[e];
   }
   __syncthreads();
-  if (t < L.cpb && c0 < C) {
-#pragma unroll
-    for (int e = 0; e < CH; ++e) {
-      double a = 0, b = 0;
-      for (int k = 0; k < L.ppb; ++k) {
-        a += red[0][k * L.cpb + t][e];
-        b += red[1][k * L.cpb + t][e];
-      }
-      part[((int64_t)blockIdx.x * 2) * C + c0 + e] = a;
-      part[((int64_t)blockIdx.x * 2 + 1) * C + c0 + e] = b;
+  // reduce over the ppb pixel rows: thread (chunk cl, element e) sums one column
+  for (int idx = t; idx < L.cpb * V; idx += 256) {
+    const int ch = idx / V, e = idx % V;
+    const int c = (blockIdx.y * L.cpb + ch) * V + e;
+    if (c >= C) continue;
+    double a = 0, b = 0;
+    for (int k = 0; k < L.ppb; ++k) {
+      a += red[0][k * L.cpb + ch][e];
+      b += red[1][k * L.cpb + ch][e];
     }
+    part[((int64_t)blockIdx.x * 2) * C + c] = a;
+    part[((int64_t)blockIdx.x * 2 + 1) * C + c] = b;
   }
 }
 
@@ -176,61 +235,116 @@ __global__ void bn_eval_params_kernel(const float* rmean, const float* rvar, flo
   invstd_out[c] = 1.f / sqrtf(rvar[c] + eps);
 }
 
-template <typename T>
-__global__ void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y, int64_t P, int C,
-                                int64_t ldx, int64_t ldr, int64_t ldy, const float* mean, const float* invstd,
-                                const float* gamma, const float* beta, int relu) {
-  const int nch = C / CH;
-  const int64_t total = P * nch;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % nch) * CH;
-    const int64_t p = i / nch;
-    float v[CH], r[CH] = {0, 0, 0, 0};
-    V4<T>::ld(x + p * ldx + c0, v);
-    if (res) V4<T>::ld(res + p * ldr + c0, r);
+// eval BN folded into a per-channel affine for a conv epilogue: scale = gamma*invstd,
+// shift = beta + (conv_bias - running_mean)*scale; channels [C, Cp) get (0, 0)
+__global__ void bn_fold_kernel(const float* rmean, const float* rvar, const float* gamma, const float* beta,
+                               const float* bias, float eps, int C, int Cp, float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= Cp) return;
+  if (c >= C) {
+    scale[c] = 0.f;
+    shift[c] = 0.f;
+    return;
+  }
+  const float is = 1.f / sqrtf(rvar[c] + eps);
+  const float sc = (gamma ? gamma[c] : 1.f) * is;
+  scale[c] = sc;
+  shift[c] = fmaf((bias ? bias[c] : 0.f) - rmean[c], sc, beta ? beta[c] : 0.f);
+}
+
+template <typename T, int V>
+__global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                       T* __restrict__ y, int64_t P, int C, int64_t ldx, int64_t ldr,
+                                                       int64_t ldy, Layout L, ChanParams prm, int relu) {
+  const int t = threadIdx.x;
+  const int cl = t % L.cpb, pl = t / L.cpb;
+  const int c0 = (blockIdx.y * L.cpb + cl) * V;
+  if (pl >= L.ppb || c0 >= C) return;
+  float mu[V], is[V], ga[V], be[V];
+  bool live[V];
+  load_params<V>(prm, c0, C, mu, is, ga, be, live);
+  const int64_t stride = (int64_t)gridDim.x * L.ppb;
+  for (int64_t p0 = (int64_t)blockIdx.x * L.ppb + pl; p0 < P; p0 += stride * U) {
+    float v[U][V], r[U][V];
 #pragma unroll
-    for (int e = 0; e < CH; ++e) {
-      const float xh = (v[e] - mean[c0 + e]) * invstd[c0 + e];
-      float o = fmaf(gamma ? gamma[c0 + e] : 1.f, xh, beta ? beta[c0 + e] : 0.f) + r[e];
-      if (relu) o = fmaxf(o, 0.f);
-      v[e] = o;
+    for (int u = 0; u < U; ++u) {
+      const int64_t p = p0 + u * stride;
+#pragma unroll
+      for (int e = 0; e < V; ++e) v[u][e] = r[u][e] = 0.f;
+      if (p < P) {
+        Vec<T, V>::ld(x + p * ldx + c0, v[u]);
+        if (res) Vec<T, V>::ld(res + p * ldr + c0, r[u]);
+      }
     }
-    V4<T>::st(y + p * ldy + c0, v);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t p = p0 + u * stride;
+      if (p >= P) continue;
+      float o[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const float xh = (v[u][e] - mu[e]) * is[e];
+        float a = fmaf(ga[e], xh, be[e]) + r[u][e];
+        if (relu) a = fmaxf(a, 0.f);
+        o[e] = live[e] ? a : 0.f;
+      }
+      Vec<T, V>::st(y + p * ldy + c0, o);
+    }
   }
 }
 
-template <typename T>
-__global__ void bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ res,
-                                    T* __restrict__ dx, T* __restrict__ dres, int64_t P, int C, int64_t ldx,
-                                    int64_t ldr, int64_t lddy, int64_t lddx, const float* mean, const float* invstd,
-                                    const float* gamma, const float* beta, int relu, int train, const double* sums,
-                                    double count) {
-  const int nch = C / CH;
-  const int64_t total = P * nch;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % nch) * CH;
-    const int64_t p = i / nch;
-    float v[CH], g[CH], r[CH] = {0, 0, 0, 0}, o[CH], od[CH];
-    V4<T>::ld(x + p * ldx + c0, v);
-    V4<T>::ld(dy + p * lddy + c0, g);
-    if (res && relu) V4<T>::ld(res + p * ldr + c0, r);
+template <typename T, int V>
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                           const T* __restrict__ res, T* __restrict__ dx,
+                                                           T* __restrict__ dres, int64_t P, int C, int64_t ldx,
+                                                           int64_t ldr, int64_t lddy, int64_t lddx, Layout L,
+                                                           ChanParams prm, int relu, int train, const double* sums,
+                                                           double count) {
+  const int t = threadIdx.x;
+  const int cl = t % L.cpb, pl = t / L.cpb;
+  const int c0 = (blockIdx.y * L.cpb + cl) * V;
+  if (pl >= L.ppb || c0 >= C) return;
+  float mu[V], is[V], ga[V], be[V], gi[V], mdy[V], mdyx[V];
+  bool live[V];
+  load_params<V>(prm, c0, C, mu, is, ga, be, live);
 #pragma unroll
-    for (int e = 0; e < CH; ++e) {
-      const int c = c0 + e;
-      const float is = invstd[c], ga = gamma ? gamma[c] : 1.f;
-      const float xh = (v[e] - mean[c]) * is;
-      float gr = g[e];
-      if (relu) gr = (fmaf(ga, xh, beta ? beta[c] : 0.f) + r[e]) > 0.f ? gr : 0.f;
-      od[e] = gr;
-      float d = gr;
-      if (train) {
-        const float mdy = (float)(sums[c] / count), mdyx = (float)(sums[C + c] / count);
-        d = gr - mdy - xh * mdyx;
+  for (int e = 0; e < V; ++e) {
+    gi[e] = ga[e] * is[e];
+    mdy[e] = (train && live[e]) ? (float)(sums[c0 + e] / count) : 0.f;
+    mdyx[e] = (train && live[e]) ? (float)(sums[C + c0 + e] / count) : 0.f;
+  }
+  const int64_t stride = (int64_t)gridDim.x * L.ppb;
+  for (int64_t p0 = (int64_t)blockIdx.x * L.ppb + pl; p0 < P; p0 += stride * U) {
+    float v[U][V], g[U][V], r[U][V];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t p = p0 + u * stride;
+#pragma unroll
+      for (int e = 0; e < V; ++e) v[u][e] = g[u][e] = r[u][e] = 0.f;
+      if (p < P) {
+        Vec<T, V>::ld(x + p * ldx + c0, v[u]);
+        Vec<T, V>::ld(dy + p * lddy + c0, g[u]);
+        if (res && relu) Vec<T, V>::ld(res + p * ldr + c0, r[u]);
       }
-      o[e] = ga * is * d;
     }
-    V4<T>::st(dx + p * lddx + c0, o);
-    if (dres) V4<T>::st(dres + p * lddx + c0, od);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t p = p0 + u * stride;
+      if (p >= P) continue;
+      float o[V], od[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const float xh = (v[u][e] - mu[e]) * is[e];
+        float gr = g[u][e];
+        if (relu) gr = (fmaf(ga[e], xh, be[e]) + r[u][e]) > 0.f ? gr : 0.f;
+        gr = live[e] ? gr : 0.f;
+        od[e] = gr;
+        const float d = train ? gr - mdy[e] - xh * mdyx[e] : gr;
+        o[e] = gi[e] * d;
+      }
+      Vec<T, V>::st(dx + p * lddx + c0, o);
+      if (dres) Vec<T, V>::st(dres + p * lddx + c0, od);
+    }
   }
 }
 
@@ -241,18 +355,68 @@ __global__ void bn_param_grad_kernel(const double* sums, int C, float* dgamma, f
   if (dgamma) dgamma[c] += (float)sums[C + c];
 }
 
-template <typename T, int MODE>
-int run_partials(const T* x, const T* dy, const T* res, int64_t P, int64_t C, int64_t ldx, int64_t lddy, int64_t ldr,
-                 const float* mean, const float* invstd, const float* gamma, const float* beta, int relu,
-                 double* sums, void* ws, hipStream_t s) {
-  const Layout L = layout_for(C);
-  int64_t gx = (P + (int64_t)L.ppb * 16 - 1) / ((int64_t)L.ppb * 16);
-  gx = gx < 1 ? 1 : (gx > MAXG ? MAXG : gx);
-  hipLaunchKernelGGL((bn_partial_kernel<T, MODE>), dim3((unsigned)gx, L.cblocks), dim3(256), 0, s, x, dy, res, P,
-                     (int)C, ldx, lddy, ldr, L, mean, invstd, gamma, beta, relu, (double*)ws);
+// 16-byte chunks when every leading dimension allows rup(C, V16) channels, else 8-byte chunks
+template <typename T>
+static bool wide_ok(int64_t C, std::initializer_list<int64_t> lds) {
+  constexpr int V16 = 16 / sizeof(T);
+  const int64_t cw = (C + V16 - 1) / V16 * V16;
+  for (int64_t ld : lds)
+    if (ld % V16 || ld < cw) return false;
+  return true;
+}
+
+template <typename T, int V, int MODE>
+void run_partials(const T* x, const T* dy, const T* res, int64_t P, int64_t C, int64_t ldx, int64_t lddy, int64_t ldr,
+                  ChanParams prm, int relu, double* sums, void* ws, hipStream_t s) {
+  const Layout L = layout_for(C, V);
+  const int64_t gx = pixel_blocks(P, L, MAXG);
+  hipLaunchKernelGGL((bn_partial_kernel<T, V, MODE>), dim3((unsigned)gx, L.cblocks), dim3(256), 0, s, x, dy, res, P,
+                     (int)C, ldx, lddy, ldr, L, prm, relu, (double*)ws);
   hipLaunchKernelGGL(bn_partial_final_kernel, dim3((C + 31) / 32), dim3(256), 0, s, (const double*)ws, (int)gx,
                      (int)C, sums);
-  return 0;
+}
+
+template <typename T, int MODE>
+void partials(const T* x, const T* dy, const T* res, int64_t P, int64_t C, int64_t ldx, int64_t lddy, int64_t ldr,
+              ChanParams prm, int relu, double* sums, void* ws, hipStream_t s) {
+  constexpr int V16 = 16 / sizeof(T);
+  if (wide_ok<T>(C, {ldx, MODE ? lddy : ldx, (MODE && res) ? ldr : ldx}))
+    run_partials<T, V16, MODE>(x, dy, res, P, C, ldx, lddy, ldr, prm, relu, sums, ws, s);
+  else
+    run_partials<T, V16 / 2, MODE>(x, dy, res, P, C, ldx, lddy, ldr, prm, relu, sums, ws, s);
+}
+
+template <typename T>
+void apply(const T* x, const T* res, T* y, int64_t P, int64_t C, int64_t ldx, int64_t ldr, int64_t ldy,
+           ChanParams prm, int relu, hipStream_t s) {
+  constexpr int V16 = 16 / sizeof(T);
+  if (wide_ok<T>(C, {ldx, ldy, res ? ldr : ldx})) {
+    const Layout L = layout_for(C, V16);
+    hipLaunchKernelGGL((bn_apply_kernel<T, V16>), dim3((unsigned)pixel_blocks(P, L, 1 << 20), L.cblocks), dim3(256),
+                       0, s, x, res, y, P, (int)C, ldx, ldr, ldy, L, prm, relu);
+  } else {
+    const Layout L = layout_for(C, V16 / 2);
+    hipLaunchKernelGGL((bn_apply_kernel<T, V16 / 2>), dim3((unsigned)pixel_blocks(P, L, 1 << 20), L.cblocks),
+                       dim3(256), 0, s, x, res, y, P, (int)C, ldx, ldr, ldy, L, prm, relu);
+  }
+}
+
+template <typename T>
+void bwd_apply(const T* dy, const T* x, const T* res, T* dx, T* dres, int64_t P, int64_t C, int64_t ldx, int64_t ldr,
+               int64_t lddy, int64_t lddx, ChanParams prm, int relu, int train, const double* sums, double count,
+               hipStream_t s) {
+  constexpr int V16 = 16 / sizeof(T);
+  if (wide_ok<T>(C, {ldx, lddy, lddx, (res && relu) ? ldr : ldx})) {
+    const Layout L = layout_for(C, V16);
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, V16>), dim3((unsigned)pixel_blocks(P, L, 1 << 20), L.cblocks),
+                       dim3(256), 0, s, dy, x, res, dx, dres, P, (int)C, ldx, ldr, lddy, lddx, L, prm, relu, train,
+                       sums, count);
+  } else {
+    const Layout L = layout_for(C, V16 / 2);
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, V16 / 2>), dim3((unsigned)pixel_blocks(P, L, 1 << 20), L.cblocks),
+                       dim3(256), 0, s, dy, x, res, dx, dres, P, (int)C, ldx, ldr, lddy, lddx, L, prm, relu, train,
+                       sums, count);
+  }
 }
 
 }  // namespace
@@ -265,11 +429,9 @@ extern "C" int ssseg_bn_stats(const void* x, int64_t P, int64_t C, int64_t ldx, 
   if (!ws || ws_bytes < ssseg_bn_workspace_bytes(C)) return SSSEG_EWORKSPACE;
   hipStream_t s = (hipStream_t)stream;
   if (dt == SSSEG_BF16)
-    run_partials<bf16_t, 0>((const bf16_t*)x, nullptr, nullptr, P, C, ldx, 0, 0, nullptr, nullptr, nullptr, nullptr, 0,
-                            sums, ws, s);
+    partials<bf16_t, 0>((const bf16_t*)x, nullptr, nullptr, P, C, ldx, 0, 0, ChanParams{}, 0, sums, ws, s);
   else if (dt == SSSEG_F32)
-    run_partials<float, 0>((const float*)x, nullptr, nullptr, P, C, ldx, 0, 0, nullptr, nullptr, nullptr, nullptr, 0,
-                           sums, ws, s);
+    partials<float, 0>((const float*)x, nullptr, nullptr, P, C, ldx, 0, 0, ChanParams{}, 0, sums, ws, s);
   else
     return SSSEG_EUNSUPPORTED;
   SSSEG_LAUNCH_CHECK();
@@ -296,20 +458,27 @@ extern "C" int ssseg_bn_eval_params(const float* running_mean, const float* runn
   return 0;
 }
 
+extern "C" int ssseg_bn_fold(const float* running_mean, const float* running_var, const float* gamma,
+                             const float* beta, const float* conv_bias, float eps, int64_t C, int64_t Cp, float* scale,
+                             float* shift, ssseg_stream_t stream) {
+  if (!running_mean || !running_var || !scale || !shift || C < 1 || Cp < C) return SSSEG_EINVAL;
+  hipLaunchKernelGGL(bn_fold_kernel, dim3((Cp + 255) / 256), dim3(256), 0, (hipStream_t)stream, running_mean,
+                     running_var, gamma, beta, conv_bias, eps, (int)C, (int)Cp, scale, shift);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int ssseg_bn_apply(const void* x, const void* residual, void* y, int64_t P, int64_t C, int64_t ldx,
                               int64_t ldr, int64_t ldy, const float* mean, const float* invstd, const float* gamma,
                               const float* beta, int relu, int dt, ssseg_stream_t stream) {
   if (!x || !y || !mean || !invstd || P < 1 || C < 1 || C % CH || ldx % CH || ldy % CH || (residual && ldr % CH))
     return SSSEG_EINVAL;
-  const int64_t total = P * (C / CH);
   hipStream_t s = (hipStream_t)stream;
-  const dim3 g(ssseg_grid(total, 256, 256 * 16)), b(256);
+  const ChanParams prm{mean, invstd, gamma, beta};
   if (dt == SSSEG_BF16)
-    hipLaunchKernelGGL(bn_apply_kernel<bf16_t>, g, b, 0, s, (const bf16_t*)x, (const bf16_t*)residual, (bf16_t*)y, P,
-                       (int)C, ldx, ldr, ldy, mean, invstd, gamma, beta, relu);
+    apply<bf16_t>((const bf16_t*)x, (const bf16_t*)residual, (bf16_t*)y, P, C, ldx, ldr, ldy, prm, relu, s);
   else if (dt == SSSEG_F32)
-    hipLaunchKernelGGL(bn_apply_kernel<float>, g, b, 0, s, (const float*)x, (const float*)residual, (float*)y, P,
-                       (int)C, ldx, ldr, ldy, mean, invstd, gamma, beta, relu);
+    apply<float>((const float*)x, (const float*)residual, (float*)y, P, C, ldx, ldr, ldy, prm, relu, s);
   else
     return SSSEG_EUNSUPPORTED;
   SSSEG_LAUNCH_CHECK();
@@ -324,11 +493,11 @@ extern "C" int ssseg_bn_bwd_reduce(const void* dy, const void* x, const void* re
   if (!ws || ws_bytes < ssseg_bn_workspace_bytes(C)) return SSSEG_EWORKSPACE;
   hipStream_t s = (hipStream_t)stream;
   if (dt == SSSEG_BF16)
-    run_partials<bf16_t, 1>((const bf16_t*)x, (const bf16_t*)dy, (const bf16_t*)residual, P, C, ldx, lddy, ldr, mean,
-                            invstd, gamma, beta, relu, sums, ws, s);
+    partials<bf16_t, 1>((const bf16_t*)x, (const bf16_t*)dy, (const bf16_t*)residual, P, C, ldx, lddy, ldr,
+                        ChanParams{mean, invstd, gamma, beta}, relu, sums, ws, s);
   else if (dt == SSSEG_F32)
-    run_partials<float, 1>((const float*)x, (const float*)dy, (const float*)residual, P, C, ldx, lddy, ldr, mean,
-                           invstd, gamma, beta, relu, sums, ws, s);
+    partials<float, 1>((const float*)x, (const float*)dy, (const float*)residual, P, C, ldx, lddy, ldr,
+                       ChanParams{mean, invstd, gamma, beta}, relu, sums, ws, s);
   else
     return SSSEG_EUNSUPPORTED;
   SSSEG_LAUNCH_CHECK();
@@ -350,17 +519,14 @@ extern "C" int ssseg_bn_bwd_apply(const void* dy, const void* x, const void* res
                                   const double* sums, double count, int dt, ssseg_stream_t stream) {
   if (!dy || !x || !dx || !mean || !invstd || P < 1 || C < 1 || C % CH || (train && (!sums || count <= 0)))
     return SSSEG_EINVAL;
-  const int64_t total = P * (C / CH);
   hipStream_t s = (hipStream_t)stream;
-  const dim3 g(ssseg_grid(total, 256, 256 * 16)), b(256);
+  const ChanParams prm{mean, invstd, gamma, beta};
   if (dt == SSSEG_BF16)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, g, b, 0, s, (const bf16_t*)dy, (const bf16_t*)x,
-                       (const bf16_t*)residual, (bf16_t*)dx, (bf16_t*)dres, P, (int)C, ldx, ldr, lddy, lddx, mean,
-                       invstd, gamma, beta, relu, train, sums, count);
+    bwd_apply<bf16_t>((const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)residual, (bf16_t*)dx, (bf16_t*)dres, P, C,
+                      ldx, ldr, lddy, lddx, prm, relu, train, sums, count, s);
   else if (dt == SSSEG_F32)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, g, b, 0, s, (const float*)dy, (const float*)x,
-                       (const float*)residual, (float*)dx, (float*)dres, P, (int)C, ldx, ldr, lddy, lddx, mean,
-                       invstd, gamma, beta, relu, train, sums, count);
+    bwd_apply<float>((const float*)dy, (const float*)x, (const float*)residual, (float*)dx, (float*)dres, P, C, ldx,
+                     ldr, lddy, lddx, prm, relu, train, sums, count, s);
   else
     return SSSEG_EUNSUPPORTED;
   SSSEG_LAUNCH_CHECK();

@@ -84,6 +84,32 @@ template <> struct Store4<bf16_t> {
   }
 };
 
+// epilogue: y = act(acc * scale[n] + shift[n] + res[pixel][n]); scale null = 1, shift null = 0
+// (conv bias -> shift; a folded eval BatchNorm -> scale/shift; Bottleneck identity -> res)
+template <typename TO>
+struct Epi {
+  const float* scale;
+  const float* shift;
+  const TO* res;
+  int ldr;
+  int relu;
+};
+
+template <typename TO> struct Load4;
+template <> struct Load4<float> {
+  __device__ __forceinline__ static void ld(const float* p, float (&v)[4]) {
+    const float4 q = *(const float4*)p;
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  }
+};
+template <> struct Load4<bf16_t> {
+  __device__ __forceinline__ static void ld(const bf16_t* p, float (&v)[4]) {
+    const uint2 q = *(const uint2*)p;
+    v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
+    v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+  }
+};
+
 constexpr int ROWB = 80;   // 64 data bytes + 16 pad per LDS row
 
 // ------------------------------------------------------------------------------------------------
@@ -93,8 +119,7 @@ int g_knobs[8] = {0, -1, 0, 0, 0, 0, 0, 0};   // runtime variant switches (ssseg
 
 template <typename T, typename TO, int BM, int BN, int WM, int WN, bool DEEP>
 __global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __restrict__ x, const T* __restrict__ w,
-                                                                  TO* __restrict__ y, ConvGeom g,
-                                                                  const float* __restrict__ bias, int relu,
+                                                                  TO* __restrict__ y, ConvGeom g, Epi<TO> ep,
                                                                   int splits, float* __restrict__ ws) {
   constexpr int VEC = MF<T>::VEC;
   constexpr int BK = 64 / (int)sizeof(T);
@@ -241,7 +266,7 @@ __global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __res
     const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
     const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
     TO* yp = y + op * g.ldy;
-    if (splits > 1) {   // fp32 partials into ws[m][K]; finalize adds bias/ReLU and writes y
+    if (splits > 1) {   // fp32 partials into ws[m][K]; finalize applies the epilogue and writes y
 #pragma unroll
       for (int i = 0; i < FN; ++i) {
         const int n = n0 + wn * WTN + i * 16 + (lane >> 4) * 4;
@@ -255,15 +280,26 @@ __global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __res
     for (int i = 0; i < FN; ++i) {
       const int n = n0 + wn * WTN + i * 16 + (lane >> 4) * 4;
       if (n >= g.K) continue;
-      float v[4];
+      const bool full = n + 3 < g.K;
+      float v[4], r[4] = {0.f, 0.f, 0.f, 0.f};
+      if (ep.res) {
+        const TO* rp = ep.res + op * ep.ldr + n;
+        if (full && (ep.ldr & 3) == 0)
+          Load4<TO>::ld(rp, r);
+        else
+          for (int e = 0; e < 4 && n + e < g.K; ++e) r[e] = io<TO>::ld(rp, e);
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float a = acc[i][j][e];
-        if (bias && n + e < g.K) a += bias[n + e];
-        if (relu) a = fmaxf(a, 0.f);
+        const bool in = n + e < g.K;
+        if (ep.scale && in) a *= ep.scale[n + e];
+        if (ep.shift && in) a += ep.shift[n + e];
+        a += r[e];
+        if (ep.relu) a = fmaxf(a, 0.f);
         v[e] = a;
       }
-      if (n + 3 < g.K && (g.ldy & 3) == 0) {
+      if (full && (g.ldy & 3) == 0) {
         Store4<TO>::st(yp + n, v);
       } else {
         for (int e = 0; e < 4 && n + e < g.K; ++e) io<TO>::st(yp, n + e, v[e]);
@@ -272,10 +308,9 @@ __global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __res
   }
 }
 
-// split-K finalize: y[pixel(m)][n] = act(ws[m][n] + bias[n])
+// split-K finalize: y[pixel(m)][n] = act(ws[m][n] * scale[n] + shift[n] + res[pixel(m)][n])
 template <typename TO>
-__global__ void splitk_finalize_kernel(const float* __restrict__ ws, TO* __restrict__ y, ConvGeom g,
-                                       const float* __restrict__ bias, int relu) {
+__global__ void splitk_finalize_kernel(const float* __restrict__ ws, TO* __restrict__ y, ConvGeom g, Epi<TO> ep) {
   const long long total = g.M * g.K;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
     const int n = (int)(i % g.K);
@@ -284,15 +319,18 @@ __global__ void splitk_finalize_kernel(const float* __restrict__ ws, TO* __restr
     const long long q = m / g.OW;
     const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
     const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
-    float v = ws[i] + (bias ? bias[n] : 0.f);
-    if (relu) v = fmaxf(v, 0.f);
+    float v = ws[i];
+    if (ep.scale) v *= ep.scale[n];
+    if (ep.shift) v += ep.shift[n];
+    if (ep.res) v += io<TO>::ld(ep.res, op * ep.ldr + n);
+    if (ep.relu) v = fmaxf(v, 0.f);
     io<TO>::st(y, op * g.ldy + n, v);
   }
 }
 
-// zero the output pixels of a phase whose tap set is empty (e.g. odd rows of a 1x1/s2 dgrad)
+// output pixels of a phase whose tap set is empty (e.g. odd rows of a 1x1/s2 dgrad): epilogue of 0
 template <typename TO>
-__global__ void phase_zero_kernel(TO* y, ConvGeom g) {
+__global__ void phase_zero_kernel(TO* y, ConvGeom g, Epi<TO> ep) {
   const long long total = g.M * g.K;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
     const int n = (int)(i % g.K);
@@ -301,7 +339,10 @@ __global__ void phase_zero_kernel(TO* y, ConvGeom g) {
     const long long q = m / g.OW;
     const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
     const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
-    io<TO>::st(y, op * g.ldy + n, 0.f);
+    float v = ep.shift ? ep.shift[n] : 0.f;
+    if (ep.res) v += io<TO>::ld(ep.res, op * ep.ldr + n);
+    if (ep.relu) v = fmaxf(v, 0.f);
+    io<TO>::st(y, op * g.ldy + n, v);
   }
 }
 
@@ -545,35 +586,35 @@ int plan_splits(const ConvGeom& g) {
 }
 
 template <typename T, typename TO, int BM, int BN, int WM, int WN>
-void launch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, const float* bias, int relu, float* ws,
-                  int splits, hipStream_t s) {
+void launch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, float* ws, int splits,
+                  hipStream_t s) {
   const long long tiles = ((g.M + BM - 1) / BM) * ((g.K + BN - 1) / BN);
   const dim3 grid((unsigned)tiles, (unsigned)splits);
   if (splits > 1) (void)hipMemsetAsync(ws, 0, sizeof(float) * g.M * g.K, s);
   if (g_knobs[0] == 0)
     hipLaunchKernelGGL((igemm_kernel<T, TO, BM, BN, WM, WN, false>), grid, dim3(256), 0, s, (const T*)x, (const T*)w,
-                       (TO*)y, g, bias, relu, splits, ws);
+                       (TO*)y, g, ep, splits, ws);
   else
     hipLaunchKernelGGL((igemm_kernel<T, TO, BM, BN, WM, WN, true>), grid, dim3(256), 0, s, (const T*)x, (const T*)w,
-                       (TO*)y, g, bias, relu, splits, ws);
+                       (TO*)y, g, ep, splits, ws);
   if (splits > 1)
     hipLaunchKernelGGL(splitk_finalize_kernel<TO>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, ws, (TO*)y, g,
-                       bias, relu);
+                       ep);
 }
 
 template <typename T, typename TO>
-void dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, const float* bias, int relu, float* ws,
+void dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, float* ws,
                     hipStream_t s) {
   const long long t128 = ((g.M + 127) / 128) * ((g.K + 127) / 128);
   const bool small = g_knobs[2] == 0 ? (t128 < 512) : (g_knobs[2] > 0);
   if (g.K <= 16)
-    launch_igemm<T, TO, 256, 16, 4, 1>(x, w, y, g, bias, relu, ws, ws ? plan_splits<T, 256, 16>(g) : 1, s);
+    launch_igemm<T, TO, 256, 16, 4, 1>(x, w, y, g, ep, ws, ws ? plan_splits<T, 256, 16>(g) : 1, s);
   else if (g.K <= 64 && !small)
-    launch_igemm<T, TO, 256, 64, 4, 1>(x, w, y, g, bias, relu, ws, ws ? plan_splits<T, 256, 64>(g) : 1, s);
+    launch_igemm<T, TO, 256, 64, 4, 1>(x, w, y, g, ep, ws, ws ? plan_splits<T, 256, 64>(g) : 1, s);
   else if (small)
-    launch_igemm<T, TO, 64, 64, 2, 2>(x, w, y, g, bias, relu, ws, ws ? plan_splits<T, 64, 64>(g) : 1, s);
+    launch_igemm<T, TO, 64, 64, 2, 2>(x, w, y, g, ep, ws, ws ? plan_splits<T, 64, 64>(g) : 1, s);
   else
-    launch_igemm<T, TO, 128, 128, 2, 2>(x, w, y, g, bias, relu, ws, ws ? plan_splits<T, 128, 128>(g) : 1, s);
+    launch_igemm<T, TO, 128, 128, 2, 2>(x, w, y, g, ep, ws, ws ? plan_splits<T, 128, 128>(g) : 1, s);
 }
 
 struct WgradPlan {
@@ -644,18 +685,22 @@ extern "C" size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* d, int
   return sp > 1 ? (size_t)g.M * g.K * sizeof(float) : 0;
 }
 
-extern "C" int ssseg_conv_igemm(const void* x, const void* w, void* y, const ssseg_conv_desc* d, int dt, int dt_out,
-                                const float* bias, int relu, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
+extern "C" int ssseg_conv_igemm_ex(const void* x, const void* w, void* y, const ssseg_conv_desc* d, int dt, int dt_out,
+                                   const float* scale, const float* shift, const void* residual, int64_t ldr, int relu,
+                                   void* ws, size_t ws_bytes, ssseg_stream_t stream) {
   ConvGeom g;
   if (!make_geom(d, g) || !y) return SSSEG_EINVAL;
   if (!geom_ok(g, dt)) return SSSEG_EINVAL;
+  if (residual && (ldr < g.K || ldr > 0x7fffffff)) return SSSEG_EINVAL;
   if (g.M == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  if (g.KK == 0) {   // no taps reach this output phase: the contribution is zero
+  if (g.KK == 0) {   // no taps reach this output phase: the contraction is zero
     if (dt_out == SSSEG_F32)
-      hipLaunchKernelGGL(phase_zero_kernel<float>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, (float*)y, g);
+      hipLaunchKernelGGL(phase_zero_kernel<float>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, (float*)y, g,
+                         Epi<float>{scale, shift, (const float*)residual, (int)ldr, relu});
     else
-      hipLaunchKernelGGL(phase_zero_kernel<bf16_t>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, (bf16_t*)y, g);
+      hipLaunchKernelGGL(phase_zero_kernel<bf16_t>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, (bf16_t*)y, g,
+                         Epi<bf16_t>{scale, shift, (const bf16_t*)residual, (int)ldr, relu});
     SSSEG_LAUNCH_CHECK();
     return 0;
   }
@@ -663,15 +708,21 @@ extern "C" int ssseg_conv_igemm(const void* x, const void* w, void* y, const sss
   const size_t need = ssseg_conv_igemm_workspace_bytes(d, dt);
   float* wsf = (need > 0 && ws && ws_bytes >= need) ? (float*)ws : nullptr;   // no workspace: no split-K
   if (dt == SSSEG_BF16 && dt_out == SSSEG_BF16)
-    dispatch_igemm<bf16_t, bf16_t>(x, w, y, g, bias, relu, wsf, s);
+    dispatch_igemm<bf16_t, bf16_t>(x, w, y, g, Epi<bf16_t>{scale, shift, (const bf16_t*)residual, (int)ldr, relu}, wsf,
+                                   s);
   else if (dt == SSSEG_BF16 && dt_out == SSSEG_F32)
-    dispatch_igemm<bf16_t, float>(x, w, y, g, bias, relu, wsf, s);
+    dispatch_igemm<bf16_t, float>(x, w, y, g, Epi<float>{scale, shift, (const float*)residual, (int)ldr, relu}, wsf, s);
   else if (dt == SSSEG_F32 && dt_out == SSSEG_F32)
-    dispatch_igemm<float, float>(x, w, y, g, bias, relu, wsf, s);
+    dispatch_igemm<float, float>(x, w, y, g, Epi<float>{scale, shift, (const float*)residual, (int)ldr, relu}, wsf, s);
   else
     return SSSEG_EUNSUPPORTED;
   SSSEG_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int ssseg_conv_igemm(const void* x, const void* w, void* y, const ssseg_conv_desc* d, int dt, int dt_out,
+                                const float* bias, int relu, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
+  return ssseg_conv_igemm_ex(x, w, y, d, dt, dt_out, nullptr, bias, nullptr, 0, relu, ws, ws_bytes, stream);
 }
 
 extern "C" size_t ssseg_conv_wgrad_workspace_bytes(const ssseg_conv_desc* d, int dt) {

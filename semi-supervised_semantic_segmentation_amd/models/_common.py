@@ -32,7 +32,7 @@ class ConvBlock(nn.Module):
         conv, norm, _ = self.conv_block
         if isinstance(norm, nn.Identity):
             return conv.forward_relu(x)
-        return snn.bn_act(conv(x), norm, relu=True)
+        return snn.conv_bn_act(conv, x, norm, relu=True)
 
 
 def center_crop(tensor, target_size):

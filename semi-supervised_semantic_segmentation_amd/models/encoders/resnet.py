@@ -28,12 +28,12 @@ class Bottleneck(nn.Module):
     def forward(self, x):
         if self.downsample is not None:
             conv, bn = self.downsample
-            shortcut = snn.bn_act(conv(x), bn, relu=False)
+            shortcut = snn.conv_bn_act(conv, x, bn, relu=False)
         else:
             shortcut = x
-        y = snn.bn_act(self.conv1(x), self.bn1)
-        y = snn.bn_act(self.conv2(y), self.bn2)
-        return snn.bn_act(self.conv3(y), self.bn3, relu=True, residual=shortcut)
+        y = snn.conv_bn_act(self.conv1, x, self.bn1)
+        y = snn.conv_bn_act(self.conv2, y, self.bn2)
+        return snn.conv_bn_act(self.conv3, y, self.bn3, relu=True, residual=shortcut)
 
 
 class Stem(nn.Sequential):
@@ -41,7 +41,7 @@ class Stem(nn.Sequential):
         super().__init__(snn.Conv2d(3, 64, 7, 2, 3, bias=False), snn.BatchNorm2d(64), nn.ReLU(inplace=True))
 
     def forward(self, x):
-        return snn.bn_act(self[0](x), self[1], relu=True)
+        return snn.conv_bn_act(self[0], x, self[1], relu=True)
 
 
 class Stage(nn.Sequential):

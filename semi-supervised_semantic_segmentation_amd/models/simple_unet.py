@@ -36,10 +36,10 @@ class UpBlock(nn.Module):
     def forward(self, x, skip):
         if self.train_upsampling:
             conv, bn, _ = self.upsampler
-            x = snn.bn_act(conv(x), bn, relu=True)
+            x = snn.conv_bn_act(conv, x, bn, relu=True)
         else:
             up, conv, bn, _ = self.upsampler
-            x = snn.bn_act(conv(up(x)), bn, relu=True)
+            x = snn.conv_bn_act(conv, up(x), bn, relu=True)
         x = snn.cat_crop(x, skip, self.out_channels, self.out_channels)
         return self.conv3_1(self.conv3_0(x))
 

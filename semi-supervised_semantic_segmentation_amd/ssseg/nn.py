@@ -230,13 +230,29 @@ class _ConvBase:
             self._ssseg_packs[key] = t
         return t
 
-    def _igemm(self, x, w, y, desc, out_dt, bias=None, relu=False):
+    def _igemm(self, x, w, y, desc, out_dt, bias=None, relu=False, fold=None):
+        """One engine launch; epilogue act(acc*scale + shift + residual) with shift = bias, or
+        fold = (scale, shift, residual) from a folded eval BatchNorm (conv_bn_act)."""
         dref = ctypes_ref(desc)
         nb = N.lib().ssseg_conv_igemm_workspace_bytes(dref, N.dt_code(x)) if w is not None else 0
         ws = N.workspace(nb, x.device) if nb else None
-        N.call('ssseg_conv_igemm', N.dev_ptr(x), N.dev_ptr(w), N.dev_ptr(y), dref, N.dt_code(x), out_dt,
-               N.dev_ptr(bias) if bias is not None else None, int(bool(relu)), N.dev_ptr(ws) if ws is not None else None,
+        scale, shift, res = fold if fold is not None else (None, bias, None)
+        N.call('ssseg_conv_igemm_ex', N.dev_ptr(x), N.dev_ptr(w) if w is not None else None, N.dev_ptr(y), dref,
+               N.dt_code(x), out_dt, N.dev_ptr(scale) if scale is not None else None,
+               N.dev_ptr(shift) if shift is not None else None, N.dev_ptr(res) if res is not None else None,
+               res.shape[1] if res is not None else 0, int(bool(relu)), N.dev_ptr(ws) if ws is not None else None,
                nb, N.stream())
+
+    def _fold(self, bn, residual, cout):
+        """Eval BatchNorm (+ this conv's bias) as the epilogue's per-channel scale/shift."""
+        if bn.num_features != self.out_channels:
+            raise ValueError('conv_bn_act: BatchNorm width != conv out_channels')
+        dev = self.weight.device
+        ss = torch.empty(2 * cout, dtype=torch.float32, device=dev)
+        opt = lambda t: N.dev_ptr(t.detach()) if t is not None else None  # noqa: E731
+        N.call('ssseg_bn_fold', N.dev_ptr(bn.running_mean), N.dev_ptr(bn.running_var), opt(bn.weight), opt(bn.bias),
+               opt(self.bias), float(bn.eps), bn.num_features, cout, N.dev_ptr(ss), N.dev_ptr(ss[cout:]), N.stream())
+        return ss[:cout], ss[cout:], residual
 
 
 def ctypes_ref(d):
@@ -282,7 +298,7 @@ class Conv2d(nn.Conv2d, _ConvBase):
             x = to_act(x)
         return _ConvFn.apply(x, self.weight, self.bias, self, True)
 
-    def _ssseg_forward(self, x, relu):
+    def _ssseg_forward(self, x, relu, bn=None, residual=None):
         cin, cout = self._dims()
         _need_act(x, cin, 'Conv2d')
         n, _, H, W = x.shape
@@ -291,6 +307,13 @@ class Conv2d(nn.Conv2d, _ConvBase):
         w = self._pack('fwd', cout, self.out_channels, self.in_channels, cin, 0, 0, 1, R, 0, 1, S)
         fl = _conv_flops(n, d.OH, d.OW, self.out_channels, self.in_channels, R, S)
         tg = _tag(self, n, H, W)
+        if bn is not None:
+            y = new_act(n, cout, d.OH, d.OW, _CFG['dtype'], x.device)
+            _need_res(residual, y)
+            fold = self._fold(bn, residual, cout)
+            with _Timed(fl, 'fwd', tg):
+                self._igemm(x, w, y, d, N.dt_code(y), relu=relu, fold=fold)
+            return y
         if self._ssseg_head:
             y = torch.empty((n, cout, d.OH, d.OW), dtype=torch.float32, device=x.device,
                             memory_format=torch.channels_last)
@@ -392,13 +415,17 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
         (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
         return (H - 1) * sh - 2 * ph + R, (W - 1) * sw - 2 * pw + S
 
-    def _ssseg_forward(self, x, relu):
+    def _ssseg_forward(self, x, relu, bn=None, residual=None):
         cin, cout = self._dims()
         _need_act(x, cin, 'ConvTranspose2d')
         n, _, H, W = x.shape
         (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
         OH, OW = self._out_hw(H, W)
         y = new_act(n, cout, OH, OW, _CFG['dtype'], x.device)
+        fold = None
+        if bn is not None:
+            _need_res(residual, y)
+            fold = self._fold(bn, residual, cout)
         timer = _Timed(_conv_flops(n, H, W, self.out_channels, self.in_channels, R, S), 'fwd', _tag(self, n, H, W))
         timer.__enter__()
         for (phy, ry0, rny, dly, qy) in _phases(sh, ph, R, OH):
@@ -411,7 +438,7 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
                 d = _desc(N=n, H=H, W=W, C=cin, ldx=cin, OH=qy, OW=qx, K=cout, R=rr, S=ss, sy=1, sx=1, dy=-1, dx=-1,
                           py=dly, px=dlx, outH=OH, outW=OW, osy=sh, osx=sw, ooy=phy, oox=phx, ldy=cout,
                           ldw=max(rr * ss * cin, cin))
-                self._igemm(x, w, y, d, N.dt_code(y), self.bias, relu)
+                self._igemm(x, w, y, d, N.dt_code(y), self.bias, relu, fold)
         timer.__exit__()
         return y
 
@@ -459,6 +486,12 @@ def _sync_group(training):
             and dist.get_world_size() > 1)
 
 
+def _pad16(C, dtype):
+    """Channels the BN kernels write (padding zeros included): C rounded up to a 16-byte chunk."""
+    v = 16 // torch.empty((), dtype=dtype).element_size()
+    return (C + v - 1) // v * v
+
+
 class _BNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, mod, relu):
@@ -489,7 +522,7 @@ class _BNFn(torch.autograd.Function):
         else:
             N.call('ssseg_bn_eval_params', N.dev_ptr(mod.running_mean), N.dev_ptr(mod.running_var), float(mod.eps), C,
                    N.dev_ptr(mean), N.dev_ptr(invstd), N.stream())
-        y = new_act(n, cp, h, w, x.dtype, dev, zero=cp != C)
+        y = new_act(n, cp, h, w, x.dtype, dev, zero=cp > _pad16(C, x.dtype))
         wt = weight.detach() if weight is not None else None
         bs = bias.detach() if bias is not None else None
         N.call('ssseg_bn_apply', N.dev_ptr(x), N.dev_ptr(residual) if residual is not None else None, N.dev_ptr(y),
@@ -525,9 +558,9 @@ class _BNFn(torch.autograd.Function):
         count = ctx.count
         if ctx.training and _sync_group(True):
             dist.all_reduce(sums)
-        dx = new_act(n, cp, h, w, x.dtype, dev, zero=cp != C)
+        dx = new_act(n, cp, h, w, x.dtype, dev, zero=cp > _pad16(C, x.dtype))
         want_res = residual is not None and ctx.needs_input_grad[3]
-        dres = new_act(n, cp, h, w, x.dtype, dev, zero=cp != C) if want_res else None
+        dres = new_act(n, cp, h, w, x.dtype, dev, zero=cp > _pad16(C, x.dtype)) if want_res else None
         N.call('ssseg_bn_bwd_apply', N.dev_ptr(gy), N.dev_ptr(x), res_p, N.dev_ptr(dx),
                N.dev_ptr(dres) if dres is not None else None, P, C, cp, cp, cp, cp, N.dev_ptr(mean),
                N.dev_ptr(invstd), N.dev_ptr(wt) if wt is not None else None,
@@ -542,6 +575,29 @@ class BatchNorm2d(nn.BatchNorm2d):
     def forward(self, x, residual=None, relu=False):
         _need_act(x, rup(self.num_features, vec()), 'BatchNorm2d')
         return _BNFn.apply(x, self.weight, self.bias, residual, self, relu)
+
+
+def _need_res(residual, y):
+    if residual is not None and (residual.shape != y.shape or residual.dtype != y.dtype or not _is_act(residual)):
+        raise ValueError(f'fused residual must match the output activation: {tuple(residual.shape)} vs {tuple(y.shape)}')
+
+
+def _no_grad(*ts):
+    return not torch.is_grad_enabled() or not any(t is not None and t.requires_grad for t in ts)
+
+
+def conv_bn_act(conv, x, bn, relu=True, residual=None):
+    """act(bn(conv(x)) [+ residual]).  With an eval-mode BatchNorm and nothing that needs a gradient
+    (the teacher forwards, reference train.py:69-94) the BN, residual add and ReLU run in the conv's
+    epilogue (ssseg_bn_fold + ssseg_conv_igemm_ex): one kernel, each activation written once.
+    Otherwise the conv and bn_act run as two steps (training BN needs the batch statistics first)."""
+    if (isinstance(conv, (Conv2d, ConvTranspose2d)) and not conv._ssseg_head and isinstance(bn, BatchNorm2d)
+            and not bn.training and bn.track_running_stats
+            and _no_grad(x, conv.weight, conv.bias, bn.weight, bn.bias, residual)):
+        if not _is_act(x):
+            x = to_act(x)
+        return conv._ssseg_forward(x, relu, bn=bn, residual=residual)
+    return bn_act(conv(x), bn, relu=relu, residual=residual)
 
 
 def bn_act(x, bn, relu=True, residual=None):

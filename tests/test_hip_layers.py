@@ -111,12 +111,13 @@ def test_conv_transpose_relu(hip_device, mode, cin, cout, H, W):
     _close(xa.grad[:, :cin], xr.grad, mode, 'dx')
 
 
+@pytest.mark.parametrize('C', [32, 12])
 @pytest.mark.parametrize('train', [True, False])
 @pytest.mark.parametrize('relu,residual', [(True, False), (False, False), (True, True)])
-def test_batchnorm_act(hip_device, mode, train, relu, residual):
+def test_batchnorm_act(hip_device, mode, train, relu, residual, C):
+    """C=12: 8-byte chunks in f32 mode, a 16-byte chunk half in padding in bf16 mode (pad written 0)."""
     from ssseg import nn as snn
     torch.manual_seed(2)
-    C = 32
     ref = torch.nn.BatchNorm2d(C)
     with torch.no_grad():
         ref.weight.uniform_(0.5, 1.5)
@@ -142,15 +143,56 @@ def test_batchnorm_act(hip_device, mode, train, relu, residual):
     ra = _act_in(r, hip_device).detach().requires_grad_(True) if residual else None
     y = snn.bn_act(xa, mod, relu=relu, residual=ra)
     y.backward(_act_in(gy, hip_device))
-    _close(y, yr, mode, 'y')
-    _close(xa.grad, xr.grad, mode, 'dx')
+    _close(y[:, :C], yr, mode, 'y')
+    _close(xa.grad[:, :C], xr.grad, mode, 'dx')
+    assert float(y.detach()[:, C:].abs().sum()) == 0 and float(xa.grad[:, C:].abs().sum()) == 0, 'padding channels'
     _close(mod.weight.grad, ref.weight.grad, mode, 'dgamma')
     _close(mod.bias.grad, ref.bias.grad, mode, 'dbeta')
     if residual:
-        _close(ra.grad, rr.grad, mode, 'dres')
+        _close(ra.grad[:, :C], rr.grad, mode, 'dres')
     np.testing.assert_allclose(mod.running_mean.cpu().numpy(), ref.running_mean.numpy(), rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(mod.running_var.cpu().numpy(), ref.running_var.numpy(), rtol=1e-5, atol=1e-6)
     assert int(mod.num_batches_tracked) == int(ref.num_batches_tracked)
+
+
+@pytest.mark.parametrize('kind,cin,cout,relu,residual', [
+    ('conv', 24, 20, True, True), ('conv', 16, 64, False, False), ('conv', 64, 128, True, False),
+    ('convT', 16, 12, True, False), ('convT', 32, 64, True, True)])
+def test_conv_bn_act_fused_eval(hip_device, mode, monkeypatch, kind, cin, cout, relu, residual):
+    """Eval BatchNorm (+ residual, ReLU) folded into the conv epilogue under no_grad (teacher forward)."""
+    from ssseg import nn as snn
+    torch.manual_seed(5)
+    if kind == 'conv':
+        rc, mc = torch.nn.Conv2d(cin, cout, 3, 1, 1, bias=True), snn.Conv2d(cin, cout, 3, 1, 1, bias=True)
+        H, W = 11, 9
+    else:
+        rc, mc = torch.nn.ConvTranspose2d(cin, cout, 4, 2, 1), snn.ConvTranspose2d(cin, cout, 4, 2, 1)
+        H, W = 5, 6
+    rb, mb = torch.nn.BatchNorm2d(cout), snn.BatchNorm2d(cout)
+    with torch.no_grad():
+        rc.weight.copy_(_q(rc.weight, mode))
+        rb.weight.uniform_(0.5, 1.5)
+        rb.bias.uniform_(-0.3, 0.3)
+        rb.running_mean.uniform_(-0.2, 0.2)
+        rb.running_var.uniform_(0.5, 2.0)
+    mc.load_state_dict(rc.state_dict())
+    mb.load_state_dict(rb.state_dict())
+    mc, mb = mc.to(hip_device), mb.to(hip_device)
+    rb.eval()
+    mb.eval()
+    x = _q(torch.randn(2, cin, H, W), mode)
+    with torch.no_grad():
+        yr = rb(rc(x))
+        r = _q(torch.randn_like(yr), mode)
+        if residual:
+            yr = yr + r
+        if relu:
+            yr = F.relu(yr)
+        monkeypatch.setattr(snn, 'bn_act', lambda *a, **k: (_ for _ in ()).throw(AssertionError('not fused')))
+        y = snn.conv_bn_act(mc, _act_in(x, hip_device), mb, relu=relu,
+                            residual=_act_in(r, hip_device) if residual else None)
+    _close(y[:, :cout], yr, mode, 'y')
+    assert float(y[:, cout:].abs().sum()) == 0, 'padding channels'
 
 
 @pytest.mark.parametrize('k,s,p,ceil', [(3, 2, 1, False), (2, 2, 0, True)])
