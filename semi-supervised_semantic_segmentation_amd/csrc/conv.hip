@@ -16,6 +16,8 @@
 // operand the pixel tile, so each lane's accumulator holds 4 consecutive output channels of one
 // pixel: the NHWC epilogue stores them with one 8/16-byte write.
 #include <algorithm>
+#include <mutex>
+#include <unordered_map>
 
 #include "common.h"
 
@@ -110,12 +112,66 @@ template <> struct Load4<bf16_t> {
   }
 };
 
+// Writes one wave's FN x FM fragments: y[pixel(m)][n..n+3] = act(acc*scale + shift + res), NHWC.
+template <typename TO, int FM, int FN>
+__device__ __forceinline__ void store_tile(const f32x4 (&acc)[FN][FM], long long mb, int nb, int lane,
+                                           const ConvGeom& g, TO* __restrict__ y, const Epi<TO>& ep) {
+#pragma unroll
+  for (int j = 0; j < FM; ++j) {
+    const long long m = mb + j * 16 + (lane & 15);
+    if (m >= g.M) continue;
+    const int ox = (int)(m % g.OW);
+    const long long q = m / g.OW;
+    const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
+    const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+    TO* yp = y + op * g.ldy;
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      const int n = nb + i * 16 + (lane >> 4) * 4;
+      if (n >= g.K) continue;
+      const bool full = n + 3 < g.K;
+      float v[4], r[4] = {0.f, 0.f, 0.f, 0.f};
+      if (ep.res) {
+        const TO* rp = ep.res + op * ep.ldr + n;
+        if (full && (ep.ldr & 3) == 0)
+          Load4<TO>::ld(rp, r);
+        else
+          for (int e = 0; e < 4 && n + e < g.K; ++e) r[e] = io<TO>::ld(rp, e);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float a = acc[i][j][e];
+        const bool in = n + e < g.K;
+        if (ep.scale && in) a *= ep.scale[n + e];
+        if (ep.shift && in) a += ep.shift[n + e];
+        a += r[e];
+        if (ep.relu) a = fmaxf(a, 0.f);
+        v[e] = a;
+      }
+      if (full && (g.ldy & 3) == 0) {
+        Store4<TO>::st(yp + n, v);
+      } else {
+        for (int e = 0; e < 4 && n + e < g.K; ++e) io<TO>::st(yp, n + e, v[e]);
+      }
+    }
+  }
+}
+
+// XCD-aware remap of a 1-D grid (bijective for any grid size): consecutive tile ids land on one XCD
+__device__ __forceinline__ int xcd_tile(int bid, int ntiles) {
+  const int xcd = bid & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+}
+
 constexpr int ROWB = 80;   // 64 data bytes + 16 pad per LDS row
 
 // ------------------------------------------------------------------------------------------------
 // forward / dgrad / transposed-conv gather GEMM
 // ------------------------------------------------------------------------------------------------
-int g_knobs[8] = {0, -1, 0, 0, 0, 0, 0, 0};   // runtime variant switches (ssseg_set_knob)
+int g_knobs[8] = {0, -1, 0, 0, 0, 1, 0, 0};   // runtime variant switches (ssseg_set_knob)
+// 0: reg-staged pipeline depth; 1: split-K cap (-1 off); 2: 64x64 small-M tiles (reg-staged path);
+// 3: bf16 LDS-DMA path (0 on, -1 off); 4: variant (0 auto, 1..10 LDS-DMA config, 11 register-staged);
+// 5: autotune unseen geometries (1 on, 0 = static heuristic); knob 6 = 1 clears the variant cache
 
 template <typename T, typename TO, int BM, int BN, int WM, int WN, bool DEEP>
 __global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __restrict__ x, const T* __restrict__ w,
@@ -134,9 +190,7 @@ __global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __res
   // XCD-aware remap of the 1-D grid: consecutive tile ids (the N tiles of one M tile, then the next
   // M tile) go to the same XCD so the gathered input rows are re-read from that XCD's L2.
   const int nnt = (g.K + BN - 1) / BN;
-  const int ntiles = gridDim.x;
-  const int xcd = blockIdx.x & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
-  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
   const long long m0 = (long long)(tile / nnt) * BM;
   const int n0 = (tile % nnt) * BN;
   const int chunk = t & 3;
@@ -257,16 +311,11 @@ __global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __res
   }
 
   // epilogue: lane holds channels n..n+3 (n = 4*(lane>>4) within a 16-wide fragment) of pixel lane&15
+  if (splits > 1) {   // fp32 partials into ws[m][K]; finalize applies the epilogue and writes y
 #pragma unroll
-  for (int j = 0; j < FM; ++j) {
-    const long long m = m0 + wm * WTM + j * 16 + (lane & 15);
-    if (m >= g.M) continue;
-    const int ox = (int)(m % g.OW);
-    const long long q = m / g.OW;
-    const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
-    const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
-    TO* yp = y + op * g.ldy;
-    if (splits > 1) {   // fp32 partials into ws[m][K]; finalize applies the epilogue and writes y
+    for (int j = 0; j < FM; ++j) {
+      const long long m = m0 + wm * WTM + j * 16 + (lane & 15);
+      if (m >= g.M) continue;
 #pragma unroll
       for (int i = 0; i < FN; ++i) {
         const int n = n0 + wn * WTN + i * 16 + (lane >> 4) * 4;
@@ -274,38 +323,163 @@ __global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __res
         for (int e = 0; e < 4; ++e)
           if (n + e < g.K) atomicAdd(ws + m * g.K + n + e, acc[i][j][e]);
       }
-      continue;
     }
+    return;
+  }
+  store_tile<TO, FM, FN>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, g, y, ep);
+}
+
+// ------------------------------------------------------------------------------------------------
+// bf16 gather GEMM, LDS-DMA pipeline (gfx950), for C % 64 == 0.  Same contraction and epilogue as
+// igemm_kernel.  k runs tap-major (k = tap*C + c) and a k-tile (BK = 64) never straddles a tap, so the
+// tap (r, s) and channel block c0 are wave-uniform scalars.  Tiles are staged by buffer_load ... lds
+// (16 B per lane straight into LDS, no VGPR round trip) into an NS-deep LDS ring: NS-1 tiles are in
+// flight while one is multiplied, one raw barrier per k-tile, counted vmcnt.  Per-lane byte offsets are
+// rebuilt only when the tap changes (padding pixels get an out-of-range offset: the buffer unit
+// returns zeros); inside a tap only the scalar soffset moves.  The LDS image is lane-linear (one
+// wave-instruction = 8 rows x 128 B); the bank swizzle (16-byte chunk c of row r stored at
+// c ^ ((r >> 1) & 7)) is applied on the per-lane source offset, and fragment reads apply the same XOR.
+// ------------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ void bldslds16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_base, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)lds_wave_base, 16, voff, soff, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void vmcnt_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+constexpr unsigned OOB = 0x80000000u;   // > any num_records we build: the load returns zeros
+
+template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS>
+__global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const bf16_t* __restrict__ x,
+                                                                const bf16_t* __restrict__ w, TO* __restrict__ y,
+                                                                ConvGeom g, Epi<TO> ep, unsigned xbytes,
+                                                                unsigned wbytes) {
+  constexpr int ROW = 128;                       // bytes per LDS row = 64 bf16 of k
+  constexpr int STAGE = (BM + BN) * ROW;
+  constexpr int AI = BM / 8 / NW;                // A (pixel) wave-instructions per wave per stage
+  constexpr int BI = BN / 8 / NW;                // B (weight) wave-instructions per wave per stage
+  constexpr int NL = AI + BI;
+  constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
+  static_assert(WM * WN == NW && FM >= 1 && FN >= 1 && AI >= 1 && BI >= 1 && NS >= 2 && NS <= 4, "tile");
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int nnt = (g.K + BN - 1) / BN;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const long long m0 = (long long)(tile / nnt) * BM;
+  const int n0 = (tile % nnt) * BN;
+  const int RS = g.R * g.S;
+  const int cpt = g.C >> 6;                      // k-tiles per tap
+  const int nk = RS * cpt;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, (int)wbytes, 0x00020000);
+
+  // lane rows: A row 8*(wave*AI + ii) + (lane>>3), B row 8*(wave*BI + jj) + (lane>>3); the lane loads
+  // logical chunk (lane & 7) ^ swz(row) = (lane & 7) ^ (lane >> 4) ^ 4*(instruction parity)
+  const int c_even = (lane & 7) ^ (lane >> 4);
+  int a_off[AI], a_iy[AI], a_ix[AI];
 #pragma unroll
-    for (int i = 0; i < FN; ++i) {
-      const int n = n0 + wn * WTN + i * 16 + (lane >> 4) * 4;
-      if (n >= g.K) continue;
-      const bool full = n + 3 < g.K;
-      float v[4], r[4] = {0.f, 0.f, 0.f, 0.f};
-      if (ep.res) {
-        const TO* rp = ep.res + op * ep.ldr + n;
-        if (full && (ep.ldr & 3) == 0)
-          Load4<TO>::ld(rp, r);
-        else
-          for (int e = 0; e < 4 && n + e < g.K; ++e) r[e] = io<TO>::ld(rp, e);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float a = acc[i][j][e];
-        const bool in = n + e < g.K;
-        if (ep.scale && in) a *= ep.scale[n + e];
-        if (ep.shift && in) a += ep.shift[n + e];
-        a += r[e];
-        if (ep.relu) a = fmaxf(a, 0.f);
-        v[e] = a;
-      }
-      if (full && (g.ldy & 3) == 0) {
-        Store4<TO>::st(yp + n, v);
-      } else {
-        for (int e = 0; e < 4 && n + e < g.K; ++e) io<TO>::st(yp, n + e, v[e]);
-      }
+  for (int ii = 0; ii < AI; ++ii) {
+    const int inst = wave * AI + ii;
+    const int ch = c_even ^ ((inst & 1) * 4);
+    const long long m = m0 + 8 * inst + (lane >> 3);
+    if (m < g.M) {
+      const int ox = (int)(m % g.OW);
+      const long long q = m / g.OW;
+      const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
+      a_iy[ii] = oy * g.sy + g.py;
+      a_ix[ii] = ox * g.sx + g.px;
+      a_off[ii] = ((img * g.H + a_iy[ii]) * g.W + a_ix[ii]) * g.ldx * 2 + ch * 16;
+    } else {
+      a_iy[ii] = -0x40000000;   // never in bounds
+      a_ix[ii] = 0;
+      a_off[ii] = 0;
     }
   }
+  unsigned b_off[BI];
+#pragma unroll
+  for (int jj = 0; jj < BI; ++jj) {
+    const int inst = wave * BI + jj;
+    const int ch = c_even ^ ((inst & 1) * 4);
+    const int n = n0 + 8 * inst + (lane >> 3);
+    b_off[jj] = n < g.K ? (unsigned)(n * g.ldw * 2 + ch * 16) : OOB;
+  }
+
+  unsigned a_cur[AI];   // byte offsets of this lane's A rows for the current tap (OOB = padding)
+  auto set_tap = [&](int tap) {
+    const int r = tap / g.S, s_ = tap - (tap / g.S) * g.S;
+    const int dyy = r * g.dy, dxx = s_ * g.dx;
+    const int toff = (dyy * g.W + dxx) * g.ldx * 2;
+#pragma unroll
+    for (int ii = 0; ii < AI; ++ii) {
+      const int iy = a_iy[ii] + dyy, ix = a_ix[ii] + dxx;
+      const bool ok = (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+      a_cur[ii] = ok ? (unsigned)(a_off[ii] + toff) : OOB;
+    }
+  };
+
+  int ld_tap = 0, ld_c = 0, ld_kt = 0;   // k-tile being staged next: tap, channel block, index
+  set_tap(0);
+  auto issue = [&](int buf) {
+    char* As = smem + buf * STAGE;
+    char* Bs = As + BM * ROW;
+    const unsigned sa = (unsigned)ld_c * 128u, sb = (unsigned)ld_kt * 128u;
+#pragma unroll
+    for (int ii = 0; ii < AI; ++ii) bldslds16(xr, As + (wave * AI + ii) * 1024, a_cur[ii], sa);
+#pragma unroll
+    for (int jj = 0; jj < BI; ++jj) bldslds16(wr, Bs + (wave * BI + jj) * 1024, b_off[jj], sb);
+    ++ld_kt;
+    if (++ld_c == cpt) {
+      ld_c = 0;
+      if (++ld_tap < RS) set_tap(ld_tap);
+    }
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int rsw = ((lane & 15) >> 1) & 7;   // read-side swizzle of this lane's fragment row
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + BM * ROW;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int pc = ((ks * 4 + (lane >> 4)) ^ rsw) * 16;
+      bf16x8 af[FN], bfr[FM];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) af[i] = *(const bf16x8*)(Bs + (wn * WTN + i * 16 + (lane & 15)) * ROW + pc);
+#pragma unroll
+      for (int j = 0; j < FM; ++j) bfr[j] = *(const bf16x8*)(As + (wm * WTM + j * 16 + (lane & 15)) * ROW + pc);
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  constexpr int D = NS - 1;   // tiles in flight ahead of the one being multiplied
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+    if (p < nk) issue(p);
+  for (int kt = 0; kt < nk; ++kt) {
+    // wait for tile kt: the tiles issued after it (at most D-1) may stay in flight
+    const int ahead = min(nk - 1, kt + D - 1) - kt;
+    if (D >= 3 && ahead >= 2) vmcnt_wait<2 * NL>();
+    else if (D >= 2 && ahead >= 1) vmcnt_wait<NL>();
+    else vmcnt_wait<0>();
+    __builtin_amdgcn_s_barrier();   // every wave's tile kt landed; ring slot (kt+D)%NS is free
+    if (kt + D < nk) issue((kt + D) % NS);
+    compute(kt % NS);
+  }
+  store_tile<TO, FM, FN>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, g, y, ep);
 }
 
 // split-K finalize: y[pixel(m)][n] = act(ws[m][n] * scale[n] + shift[n] + res[pixel(m)][n])
@@ -602,9 +776,34 @@ void launch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, cons
                        ep);
 }
 
+template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS>
+void launch_glds(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb, unsigned wb,
+                 hipStream_t s) {
+  const long long tiles = ((g.M + BM - 1) / BM) * ((g.K + BN - 1) / BN);
+  hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS>), dim3((unsigned)tiles), dim3(NW * 64), 0, s,
+                     (const bf16_t*)x, (const bf16_t*)w, (TO*)y, g, ep, xb, wb);
+}
+
+template <typename TO>
+void launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep,
+                     unsigned xb, unsigned wb, hipStream_t s) {
+  switch (cfg) {
+    case 1: launch_glds<TO, 256, 128, 2, 2, 4, 3>(x, w, y, g, ep, xb, wb, s); break;
+    case 2: launch_glds<TO, 256, 64, 4, 1, 4, 3>(x, w, y, g, ep, xb, wb, s); break;
+    case 3: launch_glds<TO, 128, 128, 2, 2, 4, 3>(x, w, y, g, ep, xb, wb, s); break;
+    case 4: launch_glds<TO, 128, 64, 2, 2, 4, 3>(x, w, y, g, ep, xb, wb, s); break;
+    case 5: launch_glds<TO, 64, 64, 2, 2, 4, 3>(x, w, y, g, ep, xb, wb, s); break;
+    case 6: launch_glds<TO, 256, 128, 4, 2, 8, 3>(x, w, y, g, ep, xb, wb, s); break;
+    case 7: launch_glds<TO, 256, 64, 4, 2, 8, 3>(x, w, y, g, ep, xb, wb, s); break;
+    case 8: launch_glds<TO, 128, 128, 2, 2, 4, 4>(x, w, y, g, ep, xb, wb, s); break;
+    case 9: launch_glds<TO, 128, 64, 2, 2, 4, 4>(x, w, y, g, ep, xb, wb, s); break;
+    default: launch_glds<TO, 64, 64, 2, 2, 4, 4>(x, w, y, g, ep, xb, wb, s); break;
+  }
+}
+
 template <typename T, typename TO>
-void dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, float* ws,
-                    hipStream_t s) {
+void dispatch_regstaged(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, float* ws,
+                        hipStream_t s) {
   const long long t128 = ((g.M + 127) / 128) * ((g.K + 127) / 128);
   const bool small = g_knobs[2] == 0 ? (t128 < 512) : (g_knobs[2] > 0);
   if (g.K <= 16)
@@ -615,6 +814,101 @@ void dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, co
     launch_igemm<T, TO, 64, 64, 2, 2>(x, w, y, g, ep, ws, ws ? plan_splits<T, 64, 64>(g) : 1, s);
   else
     launch_igemm<T, TO, 128, 128, 2, 2>(x, w, y, g, ep, ws, ws ? plan_splits<T, 128, 128>(g) : 1, s);
+}
+
+// ---- bf16 variant choice: per-geometry autotune cache ----------------------------------------
+// Every variant accumulates the same 32-deep MFMA k-sequence in the same order, so the choice changes
+// speed, never results (tests/test_hip_layers.py::test_conv_variants_bitwise).  Variant 0 is the
+// register-staged kernel, 1..10 the LDS-DMA configs.  With knob 5 on (default) an unseen geometry is
+// timed once over the candidates on the caller's stream (HIP events) and the fastest is cached.
+constexpr int kCandidates[] = {0, 1, 3, 5, 6, 7, 8, 10};
+std::unordered_map<unsigned long long, int> g_variant;
+std::mutex g_variant_mu;
+
+static unsigned long long geom_key(const ConvGeom& g, int tag) {
+  const long long v[] = {g.N, g.H, g.W, g.C, g.ldx, g.OH, g.OW, g.K, g.R, g.S, g.sy, g.sx, g.dy, g.dx, g.py, g.px,
+                         g.outH, g.outW, g.osy, g.osx, g.ldy, g.ldw, tag};
+  unsigned long long h = 1469598103934665603ull;
+  for (long long e : v) h = (h ^ (unsigned long long)e) * 1099511628211ull;
+  return h;
+}
+
+static int heuristic_variant(const ConvGeom& g) {
+  auto tiles = [&](int bm, int bn) { return ((g.M + bm - 1) / bm) * ((g.K + bn - 1) / bn); };
+  if (g.KK <= 128) return 0;
+  if (g.K > 64) return tiles(256, 128) >= 128 ? 6 : (tiles(128, 128) >= 256 ? 8 : 5);
+  return tiles(64, 64) < 512 ? 10 : 0;
+}
+
+template <typename T, typename TO>
+void run_variant(int v, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
+                 unsigned wb, hipStream_t s) {
+  if (v == 0)
+    dispatch_regstaged<T, TO>(x, w, y, g, ep, nullptr, s);
+  else
+    launch_glds_cfg<TO>(v, x, w, y, g, ep, xb, wb, s);
+}
+
+template <typename T, typename TO>
+int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
+                 unsigned wb, hipStream_t s) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return heuristic_variant(g);
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess) return heuristic_variant(g);
+  if (hipEventCreate(&e1) != hipSuccess) {
+    (void)hipEventDestroy(e0);
+    return heuristic_variant(g);
+  }
+  int best = heuristic_variant(g);
+  float best_ms = 1e30f;
+  for (int v : kCandidates) {
+    run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s);   // warm (code load, caches)
+    float ms = 1e30f;
+    for (int rep = 0; rep < 3; ++rep) {
+      (void)hipEventRecord(e0, s);
+      run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s);
+      (void)hipEventRecord(e1, s);
+      float t = 1e30f;
+      if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&t, e0, e1) == hipSuccess) ms = std::min(ms, t);
+    }
+    if (ms < best_ms) {
+      best_ms = ms;
+      best = v;
+    }
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return best;
+}
+
+template <typename T, typename TO>
+void dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, float* ws,
+                    hipStream_t s) {
+  if constexpr (sizeof(T) == 2) {
+    const long long xb = (long long)g.N * g.H * g.W * g.ldx * 2, wb = (long long)g.K * g.ldw * 2;
+    if (g_knobs[3] == 0 && !ws && g.C % 64 == 0 && g.ldx % 8 == 0 && g.ldw % 8 == 0 && g.ldw == g.KK &&
+        g.K > 16 && xb < 0x7fffffffLL && wb < 0x7fffffffLL) {
+      int v = g_knobs[4];
+      if (v < 0) v = 0;
+      if (v == 0) {
+        const unsigned long long key = geom_key(g, (int)sizeof(TO) * 4 + (ep.res ? 2 : 0) + (ep.scale ? 1 : 0));
+        std::lock_guard<std::mutex> lk(g_variant_mu);
+        auto it = g_variant.find(key);
+        if (it != g_variant.end()) {
+          v = it->second;
+        } else {
+          v = g_knobs[5] ? tune_variant<T, TO>(x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s) : heuristic_variant(g);
+          g_variant[key] = v;
+        }
+      } else if (g_knobs[4] == 11) {
+        v = 0;   // forced register-staged
+      }
+      run_variant<T, TO>(v, x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s);
+      return;
+    }
+  }
+  dispatch_regstaged<T, TO>(x, w, y, g, ep, ws, s);
 }
 
 struct WgradPlan {
@@ -668,6 +962,11 @@ bool geom_ok(const ConvGeom& g, int dt) {
 
 extern "C" int ssseg_set_knob(int id, int value) {
   if (id < 0 || id >= 8) return SSSEG_EINVAL;
+  if (id == 6 && value) {
+    std::lock_guard<std::mutex> lk(g_variant_mu);
+    g_variant.clear();
+    return 0;
+  }
   g_knobs[id] = value;
   return 0;
 }

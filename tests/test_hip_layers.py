@@ -195,6 +195,37 @@ def test_conv_bn_act_fused_eval(hip_device, mode, monkeypatch, kind, cin, cout, 
     assert float(y[:, cout:].abs().sum()) == 0, 'padding channels'
 
 
+@pytest.mark.parametrize('kind,cin,cout,k,H', [('conv', 64, 128, 3, 19), ('conv', 128, 64, 1, 17), ('conv', 192, 256, 3, 9),
+                                               ('convT', 128, 64, 4, 7)])
+def test_conv_variants_bitwise(hip_device, kind, cin, cout, k, H):
+    """Every bf16 engine variant (register-staged, LDS-DMA tile configs 1..10) accumulates the same
+    MFMA k-sequence: forward and input-gradient outputs are bit-identical, so autotuning never
+    changes results."""
+    from ssseg import native as N
+    from ssseg import nn as snn
+    snn.set_compute_dtype(torch.bfloat16)
+    torch.manual_seed(11)
+    if kind == 'conv':
+        mod = snn.Conv2d(cin, cout, k, 1, k // 2, bias=False).to(hip_device)
+    else:
+        mod = snn.ConvTranspose2d(cin, cout, k, 2, 1).to(hip_device)
+    x = _act_in(torch.randn(2, cin, H, H + 3), hip_device).detach().requires_grad_(True)
+    outs = []
+    try:
+        for v in [11] + list(range(1, 11)):
+            N.call('ssseg_set_knob', 4, v)
+            y = mod(x)
+            gy = torch.ones_like(y)
+            (gx,) = torch.autograd.grad(y, x, gy)
+            torch.cuda.synchronize()
+            outs.append((v, y.detach().clone(), gx.clone()))
+    finally:
+        N.call('ssseg_set_knob', 4, 0)
+    for v, y, gx in outs[1:]:
+        assert torch.equal(y, outs[0][1]), f'variant {v}: forward differs'
+        assert torch.equal(gx, outs[0][2]), f'variant {v}: input gradient differs'
+
+
 @pytest.mark.parametrize('k,s,p,ceil', [(3, 2, 1, False), (2, 2, 0, True)])
 def test_maxpool(hip_device, mode, k, s, p, ceil):
     from ssseg import nn as snn

@@ -1,7 +1,7 @@
 """Per-layer conv-engine timing on the C2 model (UNet-R50 512x512, bs16, bf16): one forward + backward,
 HIP events around every conv launch, interleaved over kernel variants (ssseg_set_knob) in ONE process.
 
-    python tools/bench_conv.py [--knobs 0:0,0:1] [--rounds 3] [--batch 16] [--size 512] [--top 25]
+    python tools/bench_conv.py [--knobs 3:-1,3:0/4:0,3:0/4:6] [--rounds 3] [--batch 16] [--size 512] [--top 25]
 """
 import argparse
 import collections
@@ -32,7 +32,8 @@ def main():
     model = unet.UNet(2, resnet.resnet50_encoder(), 128, train_upsampling=True).to(dev)
     x = torch.rand(args.batch, 3, args.size, args.size, device=dev)
     gy = torch.randn(args.batch, 2, args.size // 2, args.size // 2, device=dev)
-    variants = [tuple(int(v) for v in kv.split(':')) for kv in args.knobs.split(',')]
+    # a variant is one or more knob settings joined by '/': e.g. 3:-1,3:0/4:0,3:0/4:6
+    variants = [tuple(tuple(int(v) for v in kv.split(':')) for kv in var.split('/')) for var in args.knobs.split(',')]
 
     def run():
         y = model(x)
@@ -44,7 +45,8 @@ def main():
     tot = {v: [] for v in variants}
     for _ in range(args.rounds):
         for v in variants:
-            N.call('ssseg_set_knob', v[0], v[1])
+            for kid, kval in v:
+                N.call('ssseg_set_knob', kid, kval)
             run()
             torch.cuda.synchronize()
             rows = snn.probe(True)
