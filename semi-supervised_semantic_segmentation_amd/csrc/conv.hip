@@ -528,7 +528,7 @@ __global__ void phase_zero_kernel(TO* y, ConvGeom g, Epi<TO> ep) {
 // ------------------------------------------------------------------------------------------------
 template <typename T> struct WG;
 template <> struct WG<bf16_t> {
-  static constexpr int BKP = 32;                   // pixels per k-tile
+  static constexpr int BKP = 64;                   // pixels per k-tile (two 32-deep MFMA steps)
   static constexpr int PADB = 32;                  // row pad bytes (row stride == 8 dwords mod 64)
 };
 template <> struct WG<float> {
@@ -568,11 +568,20 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ x, con
   const int cod = co0 + dc * VEC;
   const bool co_ok = cod < g.K;
 
-  // pixel state per loaded row
+  // pixel state per loaded x row, advanced incrementally (no per-tile division): row pixel
+  // p = p_begin + t/XCH + i*(256/XCH) + kt*BKP, decoded once into (img, oy, ox)
   long long xp[X_IT];
+  int ximg[X_IT], xoy[X_IT], xox[X_IT];
   long long dp[D_IT];
 #pragma unroll
-  for (int i = 0; i < X_IT; ++i) xp[i] = p_begin + t / XCH + i * (256 / XCH);
+  for (int i = 0; i < X_IT; ++i) {
+    xp[i] = p_begin + t / XCH + i * (256 / XCH);
+    const long long pp = xp[i] < g.M ? xp[i] : 0;
+    xox[i] = (int)(pp % g.OW);
+    const long long q = pp / g.OW;
+    xoy[i] = (int)(q % g.OH);
+    ximg[i] = (int)(q / g.OH);
+  }
 #pragma unroll
   for (int i = 0; i < D_IT; ++i) dp[i] = p_begin + t / DCH + i * (256 / DCH);
 
@@ -580,18 +589,22 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ x, con
   auto load = [&]() {
 #pragma unroll
     for (int i = 0; i < X_IT; ++i) {
-      const long long p = xp[i];
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (p < p_end && kk_ok) {
-        const int ox = (int)(p % g.OW);
-        const long long q = p / g.OW;
-        const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
-        const int iy = oy * g.sy + rx * g.dy + g.py, ix = ox * g.sx + sx_ * g.dx + g.px;
+      if (xp[i] < p_end && kk_ok) {
+        const int iy = xoy[i] * g.sy + rx * g.dy + g.py, ix = xox[i] * g.sx + sx_ * g.dx + g.px;
         if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
-          v = *(const uint4*)(x + ((long long)(img * g.H + iy) * g.W + ix) * g.ldx + cx);
+          v = *(const uint4*)(x + ((long long)(ximg[i] * g.H + iy) * g.W + ix) * g.ldx + cx);
       }
       rx_[i] = v;
       xp[i] += BKP;
+      xox[i] += BKP;
+      while (xox[i] >= g.OW) {
+        xox[i] -= g.OW;
+        if (++xoy[i] == g.OH) {
+          xoy[i] = 0;
+          ++ximg[i];
+        }
+      }
     }
 #pragma unroll
     for (int i = 0; i < D_IT; ++i) {
@@ -629,8 +642,10 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ x, con
     const char* Xs = smem + buf * BKP * (ROWX + ROWD);
     const char* Ds = Xs + BKP * ROWX;
     if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int ks = 0; ks < BKP / 32; ++ks) {
       bf16x8 af[FM], bfr[FN];
-      const int r0 = kperm(gq, q4), r1 = kperm(gq, 4 + q4);
+      const int r0 = ks * 32 + kperm(gq, q4), r1 = ks * 32 + kperm(gq, 4 + q4);
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int col = wm * WTM + i * 16 + 4 * p4;
@@ -649,6 +664,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ x, con
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
     } else {
 #pragma unroll
       for (int ks = 0; ks < BKP / 4; ++ks) {
@@ -919,8 +935,8 @@ struct WgradPlan {
 template <typename T>
 WgradPlan plan_wgrad(const ConvGeom& g) {
   WgradPlan p;
-  p.bmw = g.KK <= 64 ? 64 : 128;
   p.bnw = g.K <= 64 ? 64 : 128;
+  p.bmw = g.KK <= 64 ? 64 : 128;   // (a 256x64 tile for Cout <= 64 measured slower: 263 -> 208 TF)
   p.mt = (g.KK + p.bmw - 1) / p.bmw;
   p.nt = (g.K + p.bnw - 1) / p.bnw;
   const long long tiles = (long long)p.mt * p.nt;
