@@ -170,14 +170,23 @@ typedef struct {
  * When R*S == 0 (an output phase no tap reaches) the phase is zero-filled. */
 int ssseg_conv_igemm(const void* x, const void* w, void* y, const ssseg_conv_desc* desc_host, int dt, int dt_out,
                      const float* bias, int relu, void* ws, size_t ws_bytes, ssseg_stream_t stream);
-/* Same contraction with the full fused epilogue
- *   y[m][n] = act(acc[m][n] * scale[n] + shift[n] + residual[pixel(m)][n])
- * scale NULL = 1, shift NULL = 0, residual NULL = 0 (dtype dt_out, pixel stride ldr).  Folds an eval-mode
- * BatchNorm (ssseg_bn_fold) and the Bottleneck identity add + ReLU (unet.py:9-10 / encoder blocks) into the
- * conv that produces them, so the teacher forwards (train.py:69-94, no grad) write each activation once. */
-int ssseg_conv_igemm_ex(const void* x, const void* w, void* y, const ssseg_conv_desc* desc_host, int dt, int dt_out,
-                        const float* scale, const float* shift, const void* residual, int64_t ldr, int relu, void* ws,
-                        size_t ws_bytes, ssseg_stream_t stream);
+/* Fused conv epilogue (ssseg_conv_igemm_epi):
+ *   y[m][n]   = act(acc[m][n] * scale[n] + shift[n] + residual[pixel(m)][n])
+ *   aux[m][n] = acc[m][n]                          (optional; same pixel stride as y)
+ * scale NULL = 1, shift NULL = 0, residual NULL = 0 (dtype dt_out, pixel stride ldr), aux NULL = not written.
+ * Folds an eval-mode BatchNorm (ssseg_bn_fold) and the Bottleneck identity add + ReLU (unet.py:9-10,
+ * encoder blocks) into the conv that produces them; aux keeps the pre-BN activation the BN backward
+ * needs when the eval pass is differentiated (consistency pass, train.py:90-92). */
+typedef struct ssseg_conv_epilogue {
+  const float* scale;
+  const float* shift;
+  const void* residual;
+  int64_t ldr;
+  void* aux;
+  int32_t relu;
+} ssseg_conv_epilogue;
+int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const ssseg_conv_desc* desc_host, int dt, int dt_out,
+                         const ssseg_conv_epilogue* epi, void* ws, size_t ws_bytes, ssseg_stream_t stream);
 /* Workspace for ssseg_conv_igemm: non-zero when the launch splits K across workgroups (few output tiles,
  * long contraction: fp32 partials [M][K] + a finalize pass).  Passing no workspace disables the split. */
 size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* desc_host, int dt);
@@ -221,12 +230,23 @@ int ssseg_bn_finalize(const double* sums, int64_t C, double count, float eps, fl
 /* eval mode: mean = running_mean, invstd = 1/sqrt(running_var + eps) */
 int ssseg_bn_eval_params(const float* running_mean, const float* running_var, float eps, int64_t C, float* mean_out,
                          float* invstd_out, ssseg_stream_t stream);
-/* eval BatchNorm as a per-channel affine of the producing conv's accumulator (ssseg_conv_igemm_ex):
- * scale = gamma/sqrt(running_var + eps), shift = beta + (conv_bias - running_mean)*scale for c < C,
- * (0, 0) for C <= c < Cp (padding channels stay zero).  gamma/beta/conv_bias may be NULL. */
+/* eval BatchNorm as a per-channel affine of the producing conv's accumulator (ssseg_conv_igemm_epi):
+ * scale = gamma*invstd, shift = beta + (conv_bias - running_mean)*scale, invstd = 1/sqrt(running_var + eps),
+ * mean_eff = running_mean - conv_bias (so xhat = (acc - mean_eff)*invstd); channels C <= c < Cp get
+ * zeros (padding stays zero).  gamma/beta/conv_bias may be NULL; mean_eff/invstd_out are optional. */
 int ssseg_bn_fold(const float* running_mean, const float* running_var, const float* gamma, const float* beta,
                   const float* conv_bias, float eps, int64_t C, int64_t Cp, float* scale, float* shift,
-                  ssseg_stream_t stream);
+                  float* mean_eff, float* invstd_out, ssseg_stream_t stream);
+/* backward of a folded eval BN (+residual, +ReLU): dyr = relu ? dy*[y > 0] : dy; dconv = scale*dyr (the
+ * conv's output gradient); dres = dyr (optional); sums[0:C] = sum dyr, sums[C:2C] = sum dyr*xhat with
+ * xhat = (aux - mean_eff)*invstd.  All tensors NHWC with pixel stride ld; padding channels written 0. */
+int ssseg_bn_eval_bwd(const void* dy, const void* y, const void* aux, void* dconv, void* dres, int64_t P, int64_t C,
+                      int64_t ld, const float* scale, const float* mean_eff, const float* invstd, int relu, int dt,
+                      double* sums, void* ws, size_t ws_bytes, ssseg_stream_t stream);
+/* parameter gradients of a folded eval BN: dgamma += sums[C:2C], dbeta += sums[0:C],
+ * dconv_bias += scale*sums[0:C] (any pointer may be NULL) */
+int ssseg_bn_eval_param_grad(const double* sums, int64_t C, const float* scale, float* dgamma, float* dbeta,
+                             float* dconv_bias, ssseg_stream_t stream);
 /* y = act(gamma*(x-mean)*invstd + beta [+ residual]); channels [C, rup(C, 16 bytes)) of y are written 0; relu = 1 for ReLU (unet.py:10, Bottleneck add+relu) */
 int ssseg_bn_apply(const void* x, const void* residual, void* y, int64_t P, int64_t C, int64_t ldx, int64_t ldr,
                    int64_t ldy, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu,

@@ -238,18 +238,112 @@ __global__ void bn_eval_params_kernel(const float* rmean, const float* rvar, flo
 // eval BN folded into a per-channel affine for a conv epilogue: scale = gamma*invstd,
 // shift = beta + (conv_bias - running_mean)*scale; channels [C, Cp) get (0, 0)
 __global__ void bn_fold_kernel(const float* rmean, const float* rvar, const float* gamma, const float* beta,
-                               const float* bias, float eps, int C, int Cp, float* scale, float* shift) {
+                               const float* bias, float eps, int C, int Cp, float* scale, float* shift,
+                               float* mean_eff, float* invstd) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= Cp) return;
   if (c >= C) {
     scale[c] = 0.f;
     shift[c] = 0.f;
+    if (mean_eff) mean_eff[c] = 0.f;
+    if (invstd) invstd[c] = 0.f;
     return;
   }
   const float is = 1.f / sqrtf(rvar[c] + eps);
   const float sc = (gamma ? gamma[c] : 1.f) * is;
+  const float me = rmean[c] - (bias ? bias[c] : 0.f);
   scale[c] = sc;
-  shift[c] = fmaf((bias ? bias[c] : 0.f) - rmean[c], sc, beta ? beta[c] : 0.f);
+  shift[c] = fmaf(-me, sc, beta ? beta[c] : 0.f);
+  if (mean_eff) mean_eff[c] = me;
+  if (invstd) invstd[c] = is;
+}
+
+// backward of a folded eval BN: dyr = relu ? dy*[y>0] : dy, dconv = scale*dyr, dres = dyr, and per-block
+// partial sums (dyr, dyr*xhat), xhat = (aux - mean_eff)*invstd
+template <typename T, int V>
+__global__ void __launch_bounds__(256) bn_eval_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+                                                          const T* __restrict__ aux, T* __restrict__ dconv,
+                                                          T* __restrict__ dres, int64_t P, int C, int64_t ld,
+                                                          Layout L, const float* scale, const float* mean_eff,
+                                                          const float* invstd, int relu, double* part) {
+  __shared__ double red[2][256][V];
+  const int t = threadIdx.x;
+  const int cl = t % L.cpb, pl = t / L.cpb;
+  const int c0 = (blockIdx.y * L.cpb + cl) * V;
+  const bool active = pl < L.ppb && c0 < C;
+  double s1[V], s2[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) s1[e] = s2[e] = 0.0;
+  if (active) {
+    float sc[V], me[V], is[V];
+    bool live[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      live[e] = c0 + e < C;
+      sc[e] = live[e] ? scale[c0 + e] : 0.f;
+      me[e] = live[e] ? mean_eff[c0 + e] : 0.f;
+      is[e] = live[e] ? invstd[c0 + e] : 0.f;
+    }
+    const int64_t stride = (int64_t)gridDim.x * L.ppb;
+    for (int64_t p0 = (int64_t)blockIdx.x * L.ppb + pl; p0 < P; p0 += stride * U) {
+      float g[U][V], yv[U][V], a[U][V];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t p = p0 + u * stride;
+#pragma unroll
+        for (int e = 0; e < V; ++e) g[u][e] = yv[u][e] = a[u][e] = 0.f;
+        if (p < P) {
+          Vec<T, V>::ld(dy + p * ld + c0, g[u]);
+          if (relu) Vec<T, V>::ld(y + p * ld + c0, yv[u]);
+          Vec<T, V>::ld(aux + p * ld + c0, a[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t p = p0 + u * stride;
+        if (p >= P) continue;
+        float od[V], oc[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          float gr = (relu && !(yv[u][e] > 0.f)) ? 0.f : g[u][e];
+          gr = live[e] ? gr : 0.f;
+          od[e] = gr;
+          oc[e] = sc[e] * gr;
+          s1[e] += (double)gr;
+          s2[e] += (double)gr * (double)((a[u][e] - me[e]) * is[e]);
+        }
+        Vec<T, V>::st(dconv + p * ld + c0, oc);
+        if (dres) Vec<T, V>::st(dres + p * ld + c0, od);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    red[0][t][e] = s1[e];
+    red[1][t][e] = s2[e];
+  }
+  __syncthreads();
+  for (int idx = t; idx < L.cpb * V; idx += 256) {
+    const int ch = idx / V, e = idx % V;
+    const int c = (blockIdx.y * L.cpb + ch) * V + e;
+    if (c >= C) continue;
+    double a = 0, b = 0;
+    for (int k = 0; k < L.ppb; ++k) {
+      a += red[0][k * L.cpb + ch][e];
+      b += red[1][k * L.cpb + ch][e];
+    }
+    part[((int64_t)blockIdx.x * 2) * C + c] = a;
+    part[((int64_t)blockIdx.x * 2 + 1) * C + c] = b;
+  }
+}
+
+__global__ void bn_eval_param_grad_kernel(const double* sums, int C, const float* scale, float* dgamma, float* dbeta,
+                                          float* dbias) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  if (dbeta) dbeta[c] += (float)sums[c];
+  if (dgamma) dgamma[c] += (float)sums[C + c];
+  if (dbias) dbias[c] += scale[c] * (float)sums[c];
 }
 
 template <typename T, int V>
@@ -460,10 +554,58 @@ extern "C" int ssseg_bn_eval_params(const float* running_mean, const float* runn
 
 extern "C" int ssseg_bn_fold(const float* running_mean, const float* running_var, const float* gamma,
                              const float* beta, const float* conv_bias, float eps, int64_t C, int64_t Cp, float* scale,
-                             float* shift, ssseg_stream_t stream) {
+                             float* shift, float* mean_eff, float* invstd_out, ssseg_stream_t stream) {
   if (!running_mean || !running_var || !scale || !shift || C < 1 || Cp < C) return SSSEG_EINVAL;
   hipLaunchKernelGGL(bn_fold_kernel, dim3((Cp + 255) / 256), dim3(256), 0, (hipStream_t)stream, running_mean,
-                     running_var, gamma, beta, conv_bias, eps, (int)C, (int)Cp, scale, shift);
+                     running_var, gamma, beta, conv_bias, eps, (int)C, (int)Cp, scale, shift, mean_eff, invstd_out);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+template <typename T>
+static void eval_bwd(const T* dy, const T* y, const T* aux, T* dconv, T* dres, int64_t P, int64_t C, int64_t ld,
+                     const float* scale, const float* mean_eff, const float* invstd, int relu, double* sums, void* ws,
+                     hipStream_t s) {
+  constexpr int V16 = 16 / sizeof(T);
+  const bool wide = wide_ok<T>(C, {ld});
+  const Layout L = layout_for(C, wide ? V16 : V16 / 2);
+  const int64_t gx = pixel_blocks(P, L, MAXG);
+  if (wide)
+    hipLaunchKernelGGL((bn_eval_bwd_kernel<T, V16>), dim3((unsigned)gx, L.cblocks), dim3(256), 0, s, dy, y, aux, dconv,
+                       dres, P, (int)C, ld, L, scale, mean_eff, invstd, relu, (double*)ws);
+  else
+    hipLaunchKernelGGL((bn_eval_bwd_kernel<T, V16 / 2>), dim3((unsigned)gx, L.cblocks), dim3(256), 0, s, dy, y, aux,
+                       dconv, dres, P, (int)C, ld, L, scale, mean_eff, invstd, relu, (double*)ws);
+  hipLaunchKernelGGL(bn_partial_final_kernel, dim3((C + 31) / 32), dim3(256), 0, s, (const double*)ws, (int)gx, (int)C,
+                     sums);
+}
+
+extern "C" int ssseg_bn_eval_bwd(const void* dy, const void* y, const void* aux, void* dconv, void* dres, int64_t P,
+                                 int64_t C, int64_t ld, const float* scale, const float* mean_eff, const float* invstd,
+                                 int relu, int dt, double* sums, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
+  if (!dy || !aux || !dconv || !sums || !scale || !mean_eff || !invstd || (relu && !y) || P < 1 || C < 1 ||
+      C % CH || ld % CH || ld < C)
+    return SSSEG_EINVAL;
+  if (!ws || ws_bytes < ssseg_bn_workspace_bytes(C)) return SSSEG_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  if (dt == SSSEG_BF16)
+    eval_bwd<bf16_t>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)aux, (bf16_t*)dconv, (bf16_t*)dres, P, C, ld,
+                     scale, mean_eff, invstd, relu, sums, ws, s);
+  else if (dt == SSSEG_F32)
+    eval_bwd<float>((const float*)dy, (const float*)y, (const float*)aux, (float*)dconv, (float*)dres, P, C, ld, scale,
+                    mean_eff, invstd, relu, sums, ws, s);
+  else
+    return SSSEG_EUNSUPPORTED;
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_bn_eval_param_grad(const double* sums, int64_t C, const float* scale, float* dgamma, float* dbeta,
+                                        float* dconv_bias, ssseg_stream_t stream) {
+  if (!sums || C < 1 || (dconv_bias && !scale)) return SSSEG_EINVAL;
+  if (!dgamma && !dbeta && !dconv_bias) return 0;
+  hipLaunchKernelGGL(bn_eval_param_grad_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, sums, (int)C,
+                     scale, dgamma, dbeta, dconv_bias);
   SSSEG_LAUNCH_CHECK();
   return 0;
 }

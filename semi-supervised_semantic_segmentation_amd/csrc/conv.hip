@@ -95,6 +95,7 @@ struct Epi {
   const TO* res;
   int ldr;
   int relu;
+  TO* aux;   // optional copy of the raw accumulator (pre-affine conv output), pixel stride ldy
 };
 
 template <typename TO> struct Load4;
@@ -137,6 +138,13 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[FN][FM], long long
           Load4<TO>::ld(rp, r);
         else
           for (int e = 0; e < 4 && n + e < g.K; ++e) r[e] = io<TO>::ld(rp, e);
+      }
+      if (ep.aux) {
+        const float a4[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (full && (g.ldy & 3) == 0)
+          Store4<TO>::st(ep.aux + op * g.ldy + n, a4);
+        else
+          for (int e = 0; e < 4 && n + e < g.K; ++e) io<TO>::st(ep.aux, op * g.ldy + n + e, a4[e]);
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -494,6 +502,7 @@ __global__ void splitk_finalize_kernel(const float* __restrict__ ws, TO* __restr
     const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
     const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
     float v = ws[i];
+    if (ep.aux) io<TO>::st(ep.aux, op * g.ldy + n, v);
     if (ep.scale) v *= ep.scale[n];
     if (ep.shift) v += ep.shift[n];
     if (ep.res) v += io<TO>::ld(ep.res, op * ep.ldr + n);
@@ -514,6 +523,7 @@ __global__ void phase_zero_kernel(TO* y, ConvGeom g, Epi<TO> ep) {
     const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
     const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
     float v = ep.shift ? ep.shift[n] : 0.f;
+    if (ep.aux) io<TO>::st(ep.aux, op * g.ldy + n, 0.f);
     if (ep.res) v += io<TO>::ld(ep.res, op * ep.ldr + n);
     if (ep.relu) v = fmaxf(v, 0.f);
     io<TO>::st(y, op * g.ldy + n, v);
@@ -1000,22 +1010,24 @@ extern "C" size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* d, int
   return sp > 1 ? (size_t)g.M * g.K * sizeof(float) : 0;
 }
 
-extern "C" int ssseg_conv_igemm_ex(const void* x, const void* w, void* y, const ssseg_conv_desc* d, int dt, int dt_out,
-                                   const float* scale, const float* shift, const void* residual, int64_t ldr, int relu,
-                                   void* ws, size_t ws_bytes, ssseg_stream_t stream) {
+extern "C" int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const ssseg_conv_desc* d, int dt, int dt_out,
+                                    const ssseg_conv_epilogue* epi, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
   ConvGeom g;
   if (!make_geom(d, g) || !y) return SSSEG_EINVAL;
   if (!geom_ok(g, dt)) return SSSEG_EINVAL;
-  if (residual && (ldr < g.K || ldr > 0x7fffffff)) return SSSEG_EINVAL;
+  const ssseg_conv_epilogue none = {nullptr, nullptr, nullptr, 0, nullptr, 0};
+  const ssseg_conv_epilogue& e = epi ? *epi : none;
+  if (e.residual && (e.ldr < g.K || e.ldr > 0x7fffffff)) return SSSEG_EINVAL;
   if (g.M == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
+  const Epi<float> ef{e.scale, e.shift, (const float*)e.residual, (int)e.ldr, e.relu, (float*)e.aux};
+  const Epi<bf16_t> eb{e.scale, e.shift, (const bf16_t*)e.residual, (int)e.ldr, e.relu, (bf16_t*)e.aux};
   if (g.KK == 0) {   // no taps reach this output phase: the contraction is zero
     if (dt_out == SSSEG_F32)
-      hipLaunchKernelGGL(phase_zero_kernel<float>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, (float*)y, g,
-                         Epi<float>{scale, shift, (const float*)residual, (int)ldr, relu});
+      hipLaunchKernelGGL(phase_zero_kernel<float>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, (float*)y, g, ef);
     else
       hipLaunchKernelGGL(phase_zero_kernel<bf16_t>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, (bf16_t*)y, g,
-                         Epi<bf16_t>{scale, shift, (const bf16_t*)residual, (int)ldr, relu});
+                         eb);
     SSSEG_LAUNCH_CHECK();
     return 0;
   }
@@ -1023,12 +1035,11 @@ extern "C" int ssseg_conv_igemm_ex(const void* x, const void* w, void* y, const 
   const size_t need = ssseg_conv_igemm_workspace_bytes(d, dt);
   float* wsf = (need > 0 && ws && ws_bytes >= need) ? (float*)ws : nullptr;   // no workspace: no split-K
   if (dt == SSSEG_BF16 && dt_out == SSSEG_BF16)
-    dispatch_igemm<bf16_t, bf16_t>(x, w, y, g, Epi<bf16_t>{scale, shift, (const bf16_t*)residual, (int)ldr, relu}, wsf,
-                                   s);
+    dispatch_igemm<bf16_t, bf16_t>(x, w, y, g, eb, wsf, s);
   else if (dt == SSSEG_BF16 && dt_out == SSSEG_F32)
-    dispatch_igemm<bf16_t, float>(x, w, y, g, Epi<float>{scale, shift, (const float*)residual, (int)ldr, relu}, wsf, s);
+    dispatch_igemm<bf16_t, float>(x, w, y, g, ef, wsf, s);
   else if (dt == SSSEG_F32 && dt_out == SSSEG_F32)
-    dispatch_igemm<float, float>(x, w, y, g, Epi<float>{scale, shift, (const float*)residual, (int)ldr, relu}, wsf, s);
+    dispatch_igemm<float, float>(x, w, y, g, ef, wsf, s);
   else
     return SSSEG_EUNSUPPORTED;
   SSSEG_LAUNCH_CHECK();
@@ -1037,7 +1048,8 @@ extern "C" int ssseg_conv_igemm_ex(const void* x, const void* w, void* y, const 
 
 extern "C" int ssseg_conv_igemm(const void* x, const void* w, void* y, const ssseg_conv_desc* d, int dt, int dt_out,
                                 const float* bias, int relu, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
-  return ssseg_conv_igemm_ex(x, w, y, d, dt, dt_out, nullptr, bias, nullptr, 0, relu, ws, ws_bytes, stream);
+  const ssseg_conv_epilogue e = {nullptr, bias, nullptr, 0, nullptr, relu};
+  return ssseg_conv_igemm_epi(x, w, y, d, dt, dt_out, &e, ws, ws_bytes, stream);
 }
 
 extern "C" size_t ssseg_conv_wgrad_workspace_bytes(const ssseg_conv_desc* d, int dt) {

@@ -47,7 +47,7 @@ SIGS = {
     'ssseg_sgd_step': (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]),
     # convolution engine
     'ssseg_conv_igemm': (i32, [vp, vp, vp, vp, i32, i32, vp, i32, vp, sz, vp]),
-    'ssseg_conv_igemm_ex': (i32, [vp, vp, vp, vp, i32, i32, vp, vp, vp, i64, i32, vp, sz, vp]),
+    'ssseg_conv_igemm_epi': (i32, [vp, vp, vp, vp, i32, i32, vp, vp, sz, vp]),
     'ssseg_conv_igemm_workspace_bytes': (sz, [vp, i32]),
     'ssseg_set_knob': (i32, [i32, i32]),
     'ssseg_conv_wgrad_workspace_bytes': (sz, [vp, i32]),
@@ -58,7 +58,9 @@ SIGS = {
     'ssseg_bn_stats': (i32, [vp, i64, i64, i64, i32, vp, vp, sz, vp]),
     'ssseg_bn_finalize': (i32, [vp, i64, f64, f32, f32, vp, vp, vp, vp, vp, vp]),
     'ssseg_bn_eval_params': (i32, [vp, vp, f32, i64, vp, vp, vp]),
-    'ssseg_bn_fold': (i32, [vp, vp, vp, vp, vp, f32, i64, i64, vp, vp, vp]),
+    'ssseg_bn_fold': (i32, [vp, vp, vp, vp, vp, f32, i64, i64, vp, vp, vp, vp, vp]),
+    'ssseg_bn_eval_bwd': (i32, [vp, vp, vp, vp, vp, i64, i64, i64, vp, vp, vp, i32, i32, vp, vp, sz, vp]),
+    'ssseg_bn_eval_param_grad': (i32, [vp, i64, vp, vp, vp, vp, vp]),
     'ssseg_bn_apply': (i32, [vp, vp, vp, i64, i64, i64, i64, i64, vp, vp, vp, vp, i32, i32, vp]),
     'ssseg_bn_bwd_reduce': (i32, [vp, vp, vp, i64, i64, i64, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp, sz, vp]),
     'ssseg_bn_param_grad': (i32, [vp, i64, vp, vp, vp]),
@@ -78,6 +80,13 @@ class ConvDesc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in (
         'N', 'H', 'W', 'C', 'ldx', 'OH', 'OW', 'K', 'R', 'S', 'sy', 'sx', 'dy', 'dx', 'py', 'px',
         'outH', 'outW', 'osy', 'osx', 'ooy', 'oox', 'ldy', 'ldw')]
+
+
+class ConvEpilogue(ctypes.Structure):
+    """Mirror of ssseg_conv_epilogue (include/ssseg.h)."""
+    _fields_ = [('scale', ctypes.c_void_p), ('shift', ctypes.c_void_p), ('residual', ctypes.c_void_p),
+                ('ldr', ctypes.c_int64), ('aux', ctypes.c_void_p), ('relu', ctypes.c_int32)]
+
 
 _lib = None
 

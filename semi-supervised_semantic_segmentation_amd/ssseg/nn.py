@@ -231,28 +231,33 @@ class _ConvBase:
         return t
 
     def _igemm(self, x, w, y, desc, out_dt, bias=None, relu=False, fold=None):
-        """One engine launch; epilogue act(acc*scale + shift + residual) with shift = bias, or
-        fold = (scale, shift, residual) from a folded eval BatchNorm (conv_bn_act)."""
+        """One engine launch; epilogue y = act(acc*scale + shift + residual) with shift = bias, or
+        fold = (scale, shift, residual, aux) from a folded eval BatchNorm (conv_bn_act); aux, when given,
+        receives the raw accumulator (the pre-BN activation the differentiated eval pass needs)."""
         dref = ctypes_ref(desc)
         nb = N.lib().ssseg_conv_igemm_workspace_bytes(dref, N.dt_code(x)) if w is not None else 0
         ws = N.workspace(nb, x.device) if nb else None
-        scale, shift, res = fold if fold is not None else (None, bias, None)
-        N.call('ssseg_conv_igemm_ex', N.dev_ptr(x), N.dev_ptr(w) if w is not None else None, N.dev_ptr(y), dref,
-               N.dt_code(x), out_dt, N.dev_ptr(scale) if scale is not None else None,
-               N.dev_ptr(shift) if shift is not None else None, N.dev_ptr(res) if res is not None else None,
-               res.shape[1] if res is not None else 0, int(bool(relu)), N.dev_ptr(ws) if ws is not None else None,
-               nb, N.stream())
+        scale, shift, res, aux = fold if fold is not None else (None, bias, None, None)
+        ep = N.ConvEpilogue(N.dev_ptr(scale) if scale is not None else None,
+                            N.dev_ptr(shift) if shift is not None else None,
+                            N.dev_ptr(res) if res is not None else None, res.shape[1] if res is not None else 0,
+                            N.dev_ptr(aux) if aux is not None else None, int(bool(relu)))
+        N.call('ssseg_conv_igemm_epi', N.dev_ptr(x), N.dev_ptr(w) if w is not None else None, N.dev_ptr(y), dref,
+               N.dt_code(x), out_dt, ctypes_ref(ep), N.dev_ptr(ws) if ws is not None else None, nb, N.stream())
 
-    def _fold(self, bn, residual, cout):
-        """Eval BatchNorm (+ this conv's bias) as the epilogue's per-channel scale/shift."""
+    def _fold(self, bn, residual, cout, aux=None):
+        """Eval BatchNorm (+ this conv's bias) as the epilogue's per-channel affine.  Returns the epilogue
+        tuple and the (scale, mean_eff, invstd) vectors the backward of a differentiated pass uses."""
         if bn.num_features != self.out_channels:
             raise ValueError('conv_bn_act: BatchNorm width != conv out_channels')
         dev = self.weight.device
-        ss = torch.empty(2 * cout, dtype=torch.float32, device=dev)
+        v = torch.empty(4 * cout, dtype=torch.float32, device=dev)
+        scale, shift, mean_eff, invstd = v[:cout], v[cout:2 * cout], v[2 * cout:3 * cout], v[3 * cout:]
         opt = lambda t: N.dev_ptr(t.detach()) if t is not None else None  # noqa: E731
         N.call('ssseg_bn_fold', N.dev_ptr(bn.running_mean), N.dev_ptr(bn.running_var), opt(bn.weight), opt(bn.bias),
-               opt(self.bias), float(bn.eps), bn.num_features, cout, N.dev_ptr(ss), N.dev_ptr(ss[cout:]), N.stream())
-        return ss[:cout], ss[cout:], residual
+               opt(self.bias), float(bn.eps), bn.num_features, cout, N.dev_ptr(scale), N.dev_ptr(shift),
+               N.dev_ptr(mean_eff), N.dev_ptr(invstd), N.stream())
+        return (scale, shift, residual, aux), (scale, mean_eff, invstd)
 
 
 def ctypes_ref(d):
@@ -298,7 +303,7 @@ class Conv2d(nn.Conv2d, _ConvBase):
             x = to_act(x)
         return _ConvFn.apply(x, self.weight, self.bias, self, True)
 
-    def _ssseg_forward(self, x, relu, bn=None, residual=None):
+    def _ssseg_forward(self, x, relu, bn=None, residual=None, keep_pre=False):
         cin, cout = self._dims()
         _need_act(x, cin, 'Conv2d')
         n, _, H, W = x.shape
@@ -310,10 +315,11 @@ class Conv2d(nn.Conv2d, _ConvBase):
         if bn is not None:
             y = new_act(n, cout, d.OH, d.OW, _CFG['dtype'], x.device)
             _need_res(residual, y)
-            fold = self._fold(bn, residual, cout)
+            aux = torch.empty_like(y) if keep_pre else None
+            fold, bwd = self._fold(bn, residual, cout, aux)
             with _Timed(fl, 'fwd', tg):
                 self._igemm(x, w, y, d, N.dt_code(y), relu=relu, fold=fold)
-            return y
+            return (y, aux, bwd) if keep_pre else y
         if self._ssseg_head:
             y = torch.empty((n, cout, d.OH, d.OW), dtype=torch.float32, device=x.device,
                             memory_format=torch.channels_last)
@@ -338,9 +344,12 @@ class Conv2d(nn.Conv2d, _ConvBase):
         _need_act(gy, cout, 'Conv2d backward')
         return gy
 
-    def _ssseg_wgrad(self, x, gy):
-        _bias_grad(self, gy)
+    def _ssseg_wgrad(self, x, gy, bias_grad=True):
+        if bias_grad:
+            _bias_grad(self, gy)
         if not self.weight.requires_grad:
+            if self.bias is not None:
+                _ready(self.bias)
             return
         n, _, H, W = x.shape
         d = self._fwd_desc(n, H, W)
@@ -415,17 +424,18 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
         (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
         return (H - 1) * sh - 2 * ph + R, (W - 1) * sw - 2 * pw + S
 
-    def _ssseg_forward(self, x, relu, bn=None, residual=None):
+    def _ssseg_forward(self, x, relu, bn=None, residual=None, keep_pre=False):
         cin, cout = self._dims()
         _need_act(x, cin, 'ConvTranspose2d')
         n, _, H, W = x.shape
         (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
         OH, OW = self._out_hw(H, W)
         y = new_act(n, cout, OH, OW, _CFG['dtype'], x.device)
-        fold = None
+        fold = aux = bwd = None
         if bn is not None:
             _need_res(residual, y)
-            fold = self._fold(bn, residual, cout)
+            aux = torch.empty_like(y) if keep_pre else None
+            fold, bwd = self._fold(bn, residual, cout, aux)
         timer = _Timed(_conv_flops(n, H, W, self.out_channels, self.in_channels, R, S), 'fwd', _tag(self, n, H, W))
         timer.__enter__()
         for (phy, ry0, rny, dly, qy) in _phases(sh, ph, R, OH):
@@ -440,14 +450,15 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
                           ldw=max(rr * ss * cin, cin))
                 self._igemm(x, w, y, d, N.dt_code(y), self.bias, relu, fold)
         timer.__exit__()
-        return y
+        return (y, aux, bwd) if keep_pre else y
 
     def _grad_in(self, gy):
         _need_act(gy, self._dims()[1], 'ConvTranspose2d backward')
         return gy
 
-    def _ssseg_wgrad(self, x, gy):
-        _bias_grad(self, gy)
+    def _ssseg_wgrad(self, x, gy, bias_grad=True):
+        if bias_grad:
+            _bias_grad(self, gy)
         if self.weight.requires_grad:
             cin, cout = self._dims()
             n, _, H, W = x.shape
@@ -586,17 +597,63 @@ def _no_grad(*ts):
     return not torch.is_grad_enabled() or not any(t is not None and t.requires_grad for t in ts)
 
 
+class _ConvBNEvalFn(torch.autograd.Function):
+    """Differentiated conv -> eval BatchNorm (-> + residual) (-> ReLU), the student's consistency pass
+    (reference train.py:90-92 runs model.eval() with autograd on).  Forward: one engine launch writes
+    y and the raw accumulator aux.  Backward: ssseg_bn_eval_bwd turns dy into the conv's output gradient
+    (and the residual's) plus the BN parameter sums in one pass; then the ordinary conv backward."""
+
+    @staticmethod
+    def forward(ctx, x, cweight, cbias, gamma, beta, residual, conv, bn, relu):
+        y, aux, (scale, mean_eff, invstd) = conv._ssseg_forward(x, relu, bn=bn, residual=residual, keep_pre=True)
+        ctx.save_for_backward(x, y, aux, scale, mean_eff, invstd)
+        ctx.conv, ctx.bn, ctx.relu, ctx.has_res = conv, bn, relu, residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, y, aux, scale, mean_eff, invstd = ctx.saved_tensors
+        conv, bn = ctx.conv, ctx.bn
+        n, cp, h, w = y.shape
+        C = bn.num_features
+        _need_act(gy, cp, 'conv_bn_act backward')
+        dev = y.device
+        dconv = new_act(n, cp, h, w, y.dtype, dev, zero=cp > _pad16(C, y.dtype))
+        want_res = ctx.has_res and ctx.needs_input_grad[5]
+        dres = new_act(n, cp, h, w, y.dtype, dev, zero=cp > _pad16(C, y.dtype)) if want_res else None
+        sums = torch.empty(2 * C, dtype=torch.float64, device=dev)
+        nb = N.lib().ssseg_bn_workspace_bytes(C)
+        ws = N.workspace(nb, dev)
+        N.call('ssseg_bn_eval_bwd', N.dev_ptr(gy), N.dev_ptr(y), N.dev_ptr(aux), N.dev_ptr(dconv),
+               N.dev_ptr(dres) if dres is not None else None, n * h * w, C, cp, N.dev_ptr(scale), N.dev_ptr(mean_eff),
+               N.dev_ptr(invstd), int(bool(ctx.relu)), N.dt_code(y), N.dev_ptr(sums), N.dev_ptr(ws), nb, N.stream())
+        want = lambda p: p is not None and p.requires_grad  # noqa: E731
+        if want(bn.weight) or want(bn.bias) or want(conv.bias):
+            N.call('ssseg_bn_eval_param_grad', N.dev_ptr(sums), C, N.dev_ptr(scale),
+                   N.dev_ptr(_grad_of(bn.weight)) if want(bn.weight) else None,
+                   N.dev_ptr(_grad_of(bn.bias)) if want(bn.bias) else None,
+                   N.dev_ptr(_grad_of(conv.bias)) if want(conv.bias) else None, N.stream())
+            _ready(*[p for p in (bn.weight, bn.bias) if want(p)])
+        conv._ssseg_wgrad(x, dconv, bias_grad=False)
+        dx = conv._ssseg_dgrad(dconv, x.shape) if ctx.needs_input_grad[0] else None
+        return dx, None, None, None, None, dres, None, None, None
+
+
 def conv_bn_act(conv, x, bn, relu=True, residual=None):
-    """act(bn(conv(x)) [+ residual]).  With an eval-mode BatchNorm and nothing that needs a gradient
-    (the teacher forwards, reference train.py:69-94) the BN, residual add and ReLU run in the conv's
-    epilogue (ssseg_bn_fold + ssseg_conv_igemm_ex): one kernel, each activation written once.
-    Otherwise the conv and bn_act run as two steps (training BN needs the batch statistics first)."""
-    if (isinstance(conv, (Conv2d, ConvTranspose2d)) and not conv._ssseg_head and isinstance(bn, BatchNorm2d)
-            and not bn.training and bn.track_running_stats
-            and _no_grad(x, conv.weight, conv.bias, bn.weight, bn.bias, residual)):
+    """act(bn(conv(x)) [+ residual]).  With an eval-mode BatchNorm the BN, residual add and ReLU run in
+    the conv's epilogue (ssseg_bn_fold + ssseg_conv_igemm_epi): one kernel, each activation written once.
+    Without gradients (the teacher forwards, reference train.py:69-94) that is all; when the eval pass
+    is differentiated (the consistency pass) the epilogue also keeps the raw accumulator and
+    _ConvBNEvalFn's backward runs the fused BN backward.  Training-mode BN needs the batch statistics
+    of the conv output first, so it runs as conv, then bn_act."""
+    fusable = (isinstance(conv, (Conv2d, ConvTranspose2d)) and not conv._ssseg_head and isinstance(bn, BatchNorm2d)
+               and not bn.training and bn.track_running_stats)
+    if fusable:
         if not _is_act(x):
             x = to_act(x)
-        return conv._ssseg_forward(x, relu, bn=bn, residual=residual)
+        if _no_grad(x, conv.weight, conv.bias, bn.weight, bn.bias, residual):
+            return conv._ssseg_forward(x, relu, bn=bn, residual=residual)
+        return _ConvBNEvalFn.apply(x, conv.weight, conv.bias, bn.weight, bn.bias, residual, conv, bn, relu)
     return bn_act(conv(x), bn, relu=relu, residual=residual)
 
 

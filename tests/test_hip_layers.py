@@ -195,6 +195,60 @@ def test_conv_bn_act_fused_eval(hip_device, mode, monkeypatch, kind, cin, cout, 
     assert float(y[:, cout:].abs().sum()) == 0, 'padding channels'
 
 
+@pytest.mark.parametrize('kind,cin,cout,relu,residual,bias', [
+    ('conv', 24, 20, True, True, False), ('conv', 64, 128, True, False, True), ('conv', 16, 64, False, False, False),
+    ('convT', 16, 12, True, False, True), ('convT', 32, 64, True, True, True)])
+def test_conv_bn_act_fused_eval_grad(hip_device, mode, monkeypatch, kind, cin, cout, relu, residual, bias):
+    """Differentiated conv -> eval BN (-> +residual) (-> ReLU) (the consistency pass): fused forward and the
+    ssseg_bn_eval_bwd backward against PyTorch fp32 autograd (dx, dres, dW, dbias, dgamma, dbeta)."""
+    from ssseg import nn as snn
+    torch.manual_seed(6)
+    if kind == 'conv':
+        rc, mc = torch.nn.Conv2d(cin, cout, 3, 1, 1, bias=bias), snn.Conv2d(cin, cout, 3, 1, 1, bias=bias)
+        H, W = 10, 9
+    else:
+        rc, mc = torch.nn.ConvTranspose2d(cin, cout, 4, 2, 1, bias=bias), snn.ConvTranspose2d(cin, cout, 4, 2, 1, bias=bias)
+        H, W = 5, 6
+    rb, mb = torch.nn.BatchNorm2d(cout), snn.BatchNorm2d(cout)
+    with torch.no_grad():
+        rc.weight.copy_(_q(rc.weight, mode))
+        rb.weight.uniform_(0.5, 1.5)
+        rb.bias.uniform_(-0.3, 0.3)
+        rb.running_mean.uniform_(-0.2, 0.2)
+        rb.running_var.uniform_(0.5, 2.0)
+    mc.load_state_dict(rc.state_dict())
+    mb.load_state_dict(rb.state_dict())
+    mc, mb = mc.to(hip_device), mb.to(hip_device)
+    rb.eval()
+    mb.eval()
+    x = _q(torch.randn(2, cin, H, W), mode)
+    xr = x.clone().requires_grad_(True)
+    yr = rb(rc(xr))
+    r = _q(torch.randn_like(yr), mode)
+    rr = r.clone().requires_grad_(True)
+    if residual:
+        yr = yr + rr
+    if relu:
+        yr = F.relu(yr)
+    gy = _q(torch.randn_like(yr), mode)
+    yr.backward(gy)
+    monkeypatch.setattr(snn, 'bn_act', lambda *a, **k: (_ for _ in ()).throw(AssertionError('not fused')))
+    xa = _act_in(x, hip_device).detach().requires_grad_(True)
+    ra = _act_in(r, hip_device).detach().requires_grad_(True) if residual else None
+    y = snn.conv_bn_act(mc, xa, mb, relu=relu, residual=ra)
+    y.backward(_act_in(gy, hip_device))
+    _close(y[:, :cout], yr, mode, 'y')
+    assert float(y.detach()[:, cout:].abs().sum()) == 0, 'padding channels'
+    _close(xa.grad[:, :cin], xr.grad, mode, 'dx')
+    if residual:
+        _close(ra.grad[:, :cout], rr.grad, mode, 'dres')
+    _close(mc.weight.grad, rc.weight.grad, mode, 'dW')
+    if bias:
+        _close(mc.bias.grad, rc.bias.grad, mode, 'dbias')
+    _close(mb.weight.grad, rb.weight.grad, mode, 'dgamma')
+    _close(mb.bias.grad, rb.bias.grad, mode, 'dbeta')
+
+
 @pytest.mark.parametrize('kind,cin,cout,k,H', [('conv', 64, 128, 3, 19), ('conv', 128, 64, 1, 17), ('conv', 192, 256, 3, 9),
                                                ('convT', 128, 64, 4, 7)])
 def test_conv_variants_bitwise(hip_device, kind, cin, cout, k, H):
