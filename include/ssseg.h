@@ -214,6 +214,17 @@ int ssseg_weight_pack(const float* src, void* dst, int64_t Kd, int64_t Kr, int64
                       int64_t Cp, int layout, int64_t r0, int64_t rstep, int64_t Rn, int64_t s0, int64_t sstep,
                       int64_t Sn, int dt, ssseg_stream_t stream);
 
+/* Batched repack: every conv's packed layouts refreshed by ONE launch after the master weights change
+ * (optimizer step, EMA; train.py:122-124, mean_teacher.py:10-11).  descs points to DEVICE memory
+ * holding n descriptors with the ssseg_weight_pack arguments. */
+typedef struct ssseg_pack_desc {
+  const float* src;
+  void* dst;
+  int64_t Kd, Kr, Cd, Rs, Ss, Cp;
+  int64_t layout, r0, rstep, Rn, s0, sstep, Sn;
+} ssseg_pack_desc;
+int ssseg_weight_pack_batch(const ssseg_pack_desc* descs, int64_t n, int dt, ssseg_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------------
  * BatchNorm2d / SyncBatchNorm (nn.BatchNorm2d in every ConvBlock, unet.py:9; distributed_trainer.py:36)
  * NHWC [P][ld] activations, C % 4 == 0.  Training: stats -> (all-reduce sums for SyncBN) -> finalize.
@@ -237,6 +248,19 @@ int ssseg_bn_eval_params(const float* running_mean, const float* running_var, fl
 int ssseg_bn_fold(const float* running_mean, const float* running_var, const float* gamma, const float* beta,
                   const float* conv_bias, float eps, int64_t C, int64_t Cp, float* scale, float* shift,
                   float* mean_eff, float* invstd_out, ssseg_stream_t stream);
+/* Batched ssseg_bn_fold: one launch folds every (conv, BN) pair of a model before an eval forward.
+ * descs points to DEVICE memory; out receives [scale | shift | mean_eff | invstd], Cp floats each. */
+typedef struct ssseg_fold_desc {
+  const float* running_mean;
+  const float* running_var;
+  const float* gamma;
+  const float* beta;
+  const float* conv_bias;
+  float* out;
+  int64_t C, Cp;
+  double eps;
+} ssseg_fold_desc;
+int ssseg_bn_fold_batch(const ssseg_fold_desc* descs, int64_t n, ssseg_stream_t stream);
 /* backward of a folded eval BN (+residual, +ReLU): dyr = relu ? dy*[y > 0] : dy; dconv = scale*dyr (the
  * conv's output gradient); dres = dyr (optional); sums[0:C] = sum dyr, sums[C:2C] = sum dyr*xhat with
  * xhat = (aux - mean_eff)*invstd.  All tensors NHWC with pixel stride ld; padding channels written 0. */

@@ -82,7 +82,7 @@ static Layout layout_for(int64_t C, int V) {
 // pixel blocks: enough workgroups to fill 256 CUs several times over, each walking >= U*ppb pixels
 static int64_t pixel_blocks(int64_t P, const Layout& L, int64_t cap) {
   int64_t gx = (P + (int64_t)L.ppb * U - 1) / ((int64_t)L.ppb * U);
-  const int64_t want = (4096 + L.cblocks - 1) / L.cblocks;
+  const int64_t want = (2048 + L.cblocks - 1) / L.cblocks;
   gx = gx > want ? want : gx;
   gx = gx > cap ? cap : gx;
   return gx < 1 ? 1 : gx;
@@ -106,7 +106,7 @@ __device__ __forceinline__ void load_params(const ChanParams& cp, int c0, int C,
   }
 }
 
-constexpr int MAXG = 256;   // partial blocks along pixels
+constexpr int MAXG = 1024;   // partial blocks along pixels (several per CU: the partial passes are HBM-bound)
 
 // per-block partial sums of 2 per-channel quantities; mode 0: (x, x^2); mode 1: (dyr, dyr*xhat)
 template <typename T, int V, int MODE>
@@ -185,23 +185,32 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x
   }
 }
 
-// sums over the per-block partials: block = 32 channels x 8 partial lanes
+// sums over the per-block partials: block = 8 channels x 32 partial lanes, two accumulator chains per
+// lane, then a fixed-order LDS reduction (deterministic)
 __global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* part, int nparts, int C, double* sums) {
-  __shared__ double red[2][8][32];
-  const int cl = threadIdx.x & 31, pl = threadIdx.x >> 5;
-  const int c = blockIdx.x * 32 + cl;
-  double a = 0, b = 0;
+  __shared__ double red[2][32][8];
+  const int cl = threadIdx.x & 7, pl = threadIdx.x >> 3;
+  const int c = blockIdx.x * 8 + cl;
+  double a0 = 0, a1 = 0, b0 = 0, b1 = 0;
   if (c < C) {
-    for (int i = pl; i < nparts; i += 8) {
-      a += part[(int64_t)(2 * i) * C + c];
-      b += part[(int64_t)(2 * i + 1) * C + c];
+    int i = pl;
+    for (; i + 32 < nparts; i += 64) {
+      a0 += part[(int64_t)(2 * i) * C + c];
+      b0 += part[(int64_t)(2 * i + 1) * C + c];
+      a1 += part[(int64_t)(2 * (i + 32)) * C + c];
+      b1 += part[(int64_t)(2 * (i + 32) + 1) * C + c];
+    }
+    if (i < nparts) {
+      a0 += part[(int64_t)(2 * i) * C + c];
+      b0 += part[(int64_t)(2 * i + 1) * C + c];
     }
   }
-  red[0][pl][cl] = a;
-  red[1][pl][cl] = b;
+  red[0][pl][cl] = a0 + a1;
+  red[1][pl][cl] = b0 + b1;
   __syncthreads();
   if (pl == 0 && c < C) {
-    for (int k = 1; k < 8; ++k) {
+    double a = 0, b = 0;
+    for (int k = 0; k < 32; ++k) {
       a += red[0][k][cl];
       b += red[1][k][cl];
     }
@@ -256,6 +265,28 @@ __global__ void bn_fold_kernel(const float* rmean, const float* rvar, const floa
   shift[c] = fmaf(-me, sc, beta ? beta[c] : 0.f);
   if (mean_eff) mean_eff[c] = me;
   if (invstd) invstd[c] = is;
+}
+
+__global__ void bn_fold_batch_kernel(const ssseg_fold_desc* __restrict__ descs) {
+  const ssseg_fold_desc& d = descs[blockIdx.y];
+  const int Cp = (int)d.Cp;
+  float* scale = d.out;
+  float* shift = d.out + Cp;
+  float* mean_eff = d.out + 2 * Cp;
+  float* invstd = d.out + 3 * Cp;
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < Cp; c += gridDim.x * blockDim.x) {
+    if (c >= d.C) {
+      scale[c] = shift[c] = mean_eff[c] = invstd[c] = 0.f;
+      continue;
+    }
+    const float is = 1.f / sqrtf(d.running_var[c] + (float)d.eps);
+    const float sc = (d.gamma ? d.gamma[c] : 1.f) * is;
+    const float me = d.running_mean[c] - (d.conv_bias ? d.conv_bias[c] : 0.f);
+    scale[c] = sc;
+    shift[c] = fmaf(-me, sc, d.beta ? d.beta[c] : 0.f);
+    mean_eff[c] = me;
+    invstd[c] = is;
+  }
 }
 
 // backward of a folded eval BN: dyr = relu ? dy*[y>0] : dy, dconv = scale*dyr, dres = dyr, and per-block
@@ -466,7 +497,7 @@ void run_partials(const T* x, const T* dy, const T* res, int64_t P, int64_t C, i
   const int64_t gx = pixel_blocks(P, L, MAXG);
   hipLaunchKernelGGL((bn_partial_kernel<T, V, MODE>), dim3((unsigned)gx, L.cblocks), dim3(256), 0, s, x, dy, res, P,
                      (int)C, ldx, lddy, ldr, L, prm, relu, (double*)ws);
-  hipLaunchKernelGGL(bn_partial_final_kernel, dim3((C + 31) / 32), dim3(256), 0, s, (const double*)ws, (int)gx,
+  hipLaunchKernelGGL(bn_partial_final_kernel, dim3((C + 7) / 8), dim3(256), 0, s, (const double*)ws, (int)gx,
                      (int)C, sums);
 }
 
@@ -562,6 +593,14 @@ extern "C" int ssseg_bn_fold(const float* running_mean, const float* running_var
   return 0;
 }
 
+extern "C" int ssseg_bn_fold_batch(const ssseg_fold_desc* descs, int64_t n, ssseg_stream_t stream) {
+  if (n < 0 || n > 65535 || (n > 0 && !descs)) return SSSEG_EINVAL;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(bn_fold_batch_kernel, dim3(2, (unsigned)n), dim3(256), 0, (hipStream_t)stream, descs);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
 template <typename T>
 static void eval_bwd(const T* dy, const T* y, const T* aux, T* dconv, T* dres, int64_t P, int64_t C, int64_t ld,
                      const float* scale, const float* mean_eff, const float* invstd, int relu, double* sums, void* ws,
@@ -576,7 +615,7 @@ static void eval_bwd(const T* dy, const T* y, const T* aux, T* dconv, T* dres, i
   else
     hipLaunchKernelGGL((bn_eval_bwd_kernel<T, V16 / 2>), dim3((unsigned)gx, L.cblocks), dim3(256), 0, s, dy, y, aux,
                        dconv, dres, P, (int)C, ld, L, scale, mean_eff, invstd, relu, (double*)ws);
-  hipLaunchKernelGGL(bn_partial_final_kernel, dim3((C + 31) / 32), dim3(256), 0, s, (const double*)ws, (int)gx, (int)C,
+  hipLaunchKernelGGL(bn_partial_final_kernel, dim3((C + 7) / 8), dim3(256), 0, s, (const double*)ws, (int)gx, (int)C,
                      sums);
 }
 

@@ -549,9 +549,15 @@ template <> struct WG<float> {
 // MFMA k index (8g + j) -> LDS row, conflict-free for the transpose reads
 __device__ __forceinline__ int kperm(int g, int j) { return 16 * (g >> 1) + 8 * (j >> 2) + 4 * (g & 1) + (j & 3); }
 
+struct WDirect {   // splits == 1: write dW in its final layout (no slab, no reduce launch)
+  float* dw;
+  int c_real, k_real, layout, accumulate;
+};
+
 template <typename T, int BMW, int BNW>
 __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy,
-                                                    float* __restrict__ slab, ConvGeom g, long long pix_per_split) {
+                                                    float* __restrict__ slab, ConvGeom g, long long pix_per_split,
+                                                    WDirect dd) {
   constexpr int VEC = MF<T>::VEC;
   constexpr int BKP = WG<T>::BKP;
   constexpr int ROWX = BMW * (int)sizeof(T) + WG<T>::PADB;
@@ -695,6 +701,29 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ x, con
   }
 
   // slab[split][co][kk]: lane holds kk .. kk+3 (rows) of channel co (column)
+  if (dd.dw) {   // single split: final layout directly (0 = [K][R][S][C], 1 = [k_real][c_real][R][S]), += if accumulate
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int kkb = kk0 + wm * WTM + i * 16 + 4 * gq;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int co = co0 + wn * WTN + j * 16 + li;
+        if (co >= dd.k_real) continue;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int kk = kkb + e;
+          if (kk >= g.KK) continue;
+          const int c = kk % g.C, tap = kk / g.C;
+          if (c >= dd.c_real) continue;
+          long long o;
+          if (dd.layout == 0) o = ((long long)co * g.R * g.S + tap) * g.C + c;
+          else o = (((long long)co * dd.c_real + c) * g.R + tap / g.S) * g.S + tap % g.S;
+          dd.dw[o] = dd.accumulate ? dd.dw[o] + acc[i][j][e] : acc[i][j][e];
+        }
+      }
+    }
+    return;
+  }
   float* sl = slab + (long long)blockIdx.z * g.K * g.KK;
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
@@ -764,6 +793,32 @@ __global__ void weight_pack_kernel(const float* __restrict__ src, T* __restrict_
       const long long idx = layout == 0 ? (((long long)k * Cd + c) * Rs + r) * Ss + s
                                         : (((long long)c * Kr + k) * Rs + r) * Ss + s;
       v = src[idx];
+    }
+    io<T>::st(dst, i, v);
+  }
+}
+
+// one launch repacks many convs: blockIdx.y = descriptor, blocks along x grid-stride over its elements
+template <typename T>
+__global__ void __launch_bounds__(256) weight_pack_batch_kernel(const ssseg_pack_desc* __restrict__ descs) {
+  // 32-bit index math (the host checks every pack < 2^31 elements)
+  const ssseg_pack_desc& d = descs[blockIdx.y];
+  const int Cp = (int)d.Cp, Sn = (int)d.Sn, Rn = (int)d.Rn, Cd = (int)d.Cd, Kr = (int)d.Kr, Rs = (int)d.Rs,
+            Ss = (int)d.Ss, r0 = (int)d.r0, rstep = (int)d.rstep, s0 = (int)d.s0, sstep = (int)d.sstep;
+  const int total = (int)d.Kd * Rn * Sn * Cp;
+  const bool l0 = d.layout == 0;
+  const float* src = d.src;
+  T* dst = (T*)d.dst;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c = i % Cp;
+    int q = i / Cp;
+    const int ss = q % Sn;
+    q /= Sn;
+    const int rr = q % Rn, k = q / Rn;
+    float v = 0.f;
+    if (c < Cd && k < Kr) {
+      const int r = r0 + rr * rstep, s = s0 + ss * sstep;
+      v = src[l0 ? ((k * Cd + c) * Rs + r) * Ss + s : ((c * Kr + k) * Rs + r) * Ss + s];
     }
     io<T>::st(dst, i, v);
   }
@@ -954,6 +1009,7 @@ WgradPlan plan_wgrad(const ConvGeom& g) {
   const long long max_splits_by_work = std::max<long long>(1, g.M / (bkp * 8));   // >= 8 k-tiles per split
   long long want = std::max<long long>(1, (1024 + tiles - 1) / tiles);
   const long long slab_cap = std::max<long long>(1, (64ll << 20) / (4ll * g.K * g.KK + 1));  // <= 64 MiB of slabs
+  // (capping splits by slab traffic measured slower: layer3/4 wgrads need the parallelism, 58 -> 150 us)
   long long sp = std::min(std::min(want, max_splits_by_work), slab_cap);
   sp = std::max<long long>(1, std::min<long long>(sp, 65535));
   p.pps = (g.M + sp - 1) / sp;
@@ -964,16 +1020,17 @@ WgradPlan plan_wgrad(const ConvGeom& g) {
 }
 
 template <typename T>
-void launch_wgrad(const void* x, const void* dy, float* slab, const ConvGeom& g, const WgradPlan& p, hipStream_t s) {
+void launch_wgrad(const void* x, const void* dy, float* slab, const ConvGeom& g, const WgradPlan& p, WDirect dd,
+                  hipStream_t s) {
   const dim3 grid(p.mt, p.nt, p.splits);
   if (p.bmw == 64 && p.bnw == 64)
-    hipLaunchKernelGGL((wgrad_kernel<T, 64, 64>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, g, p.pps);
+    hipLaunchKernelGGL((wgrad_kernel<T, 64, 64>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, g, p.pps, dd);
   else if (p.bmw == 64)
-    hipLaunchKernelGGL((wgrad_kernel<T, 64, 128>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, g, p.pps);
+    hipLaunchKernelGGL((wgrad_kernel<T, 64, 128>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, g, p.pps, dd);
   else if (p.bnw == 64)
-    hipLaunchKernelGGL((wgrad_kernel<T, 128, 64>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, g, p.pps);
+    hipLaunchKernelGGL((wgrad_kernel<T, 128, 64>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, g, p.pps, dd);
   else
-    hipLaunchKernelGGL((wgrad_kernel<T, 128, 128>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, g, p.pps);
+    hipLaunchKernelGGL((wgrad_kernel<T, 128, 128>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, g, p.pps, dd);
 }
 
 bool geom_ok(const ConvGeom& g, int dt) {
@@ -1070,18 +1127,34 @@ extern "C" int ssseg_conv_wgrad(const void* x, const void* dy, float* dw, const 
   hipStream_t s = (hipStream_t)stream;
   float* slab = (float*)ws;
   WgradPlan p;
-  if (dt == SSSEG_BF16) {
-    p = plan_wgrad<bf16_t>(g);
-    launch_wgrad<bf16_t>(x, dy, slab, g, p, s);
-  } else if (dt == SSSEG_F32) {
-    p = plan_wgrad<float>(g);
-    launch_wgrad<float>(x, dy, slab, g, p, s);
-  } else {
-    return SSSEG_EUNSUPPORTED;
+  if (dt != SSSEG_BF16 && dt != SSSEG_F32) return SSSEG_EUNSUPPORTED;
+  p = dt == SSSEG_BF16 ? plan_wgrad<bf16_t>(g) : plan_wgrad<float>(g);
+  const WDirect dd{p.splits == 1 ? dw : nullptr, (int)c_real, (int)k_real, layout, accumulate};
+  if (dt == SSSEG_BF16)
+    launch_wgrad<bf16_t>(x, dy, slab, g, p, dd, s);
+  else
+    launch_wgrad<float>(x, dy, slab, g, p, dd, s);
+  if (p.splits == 1) {
+    SSSEG_LAUNCH_CHECK();
+    return 0;
   }
   const long long total = (long long)g.K * g.KK;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ssseg_grid(total, 256)), dim3(256), 0, s, slab, p.splits, g.K, g.R, g.S,
                      g.C, (int)c_real, (int)k_real, dw, layout, accumulate);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_weight_pack_batch(const ssseg_pack_desc* descs, int64_t n, int dt, ssseg_stream_t stream) {
+  if (n < 0 || n > 65535 || (n > 0 && !descs)) return SSSEG_EINVAL;
+  if (n == 0) return 0;
+  const dim3 grid(256, (unsigned)n);
+  if (dt == SSSEG_BF16)
+    hipLaunchKernelGGL(weight_pack_batch_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, descs);
+  else if (dt == SSSEG_F32)
+    hipLaunchKernelGGL(weight_pack_batch_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, descs);
+  else
+    return SSSEG_EUNSUPPORTED;
   SSSEG_LAUNCH_CHECK();
   return 0;
 }

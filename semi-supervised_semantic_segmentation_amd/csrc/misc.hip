@@ -65,6 +65,151 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ gy, const uint8_t* __re
   }
 }
 
+// 16-byte channel-chunk variants (C % (16/sizeof(T)) == 0, < 2^31 chunks): one thread per (pixel, chunk),
+// 32-bit index math, the window's taps loaded as 16-byte vectors, argmax bytes stored 8/4 at a time.
+template <typename T> struct VC;
+template <> struct VC<bf16_t> {
+  static constexpr int V = 8;
+  __device__ __forceinline__ static void ld(const bf16_t* p, float (&v)[8]) {
+    const uint4 q = *(const uint4*)p;
+    const unsigned w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  __device__ __forceinline__ static void st(bf16_t* p, const float (&v)[8]) {
+    unsigned w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (unsigned)f32_to_bf16(v[2 * i]) | ((unsigned)f32_to_bf16(v[2 * i + 1]) << 16);
+    *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+};
+template <> struct VC<float> {
+  static constexpr int V = 4;
+  __device__ __forceinline__ static void ld(const float* p, float (&v)[4]) {
+    const float4 q = *(const float4*)p;
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  }
+  __device__ __forceinline__ static void st(float* p, const float (&v)[4]) { *(float4*)p = make_float4(v[0], v[1], v[2], v[3]); }
+};
+
+template <int V> struct IdxVec;
+template <> struct IdxVec<8> {
+  __device__ __forceinline__ static void st(uint8_t* p, const int (&b)[8]) {
+    unsigned lo = 0, hi = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lo |= (unsigned)(b[i] & 255) << (8 * i);
+      hi |= (unsigned)(b[4 + i] & 255) << (8 * i);
+    }
+    *(uint2*)p = make_uint2(lo, hi);
+  }
+  __device__ __forceinline__ static void ld(const uint8_t* p, int (&b)[8]) {
+    const uint2 q = *(const uint2*)p;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      b[i] = (q.x >> (8 * i)) & 255;
+      b[4 + i] = (q.y >> (8 * i)) & 255;
+    }
+  }
+};
+template <> struct IdxVec<4> {
+  __device__ __forceinline__ static void st(uint8_t* p, const int (&b)[4]) {
+    unsigned w = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w |= (unsigned)(b[i] & 255) << (8 * i);
+    *(unsigned*)p = w;
+  }
+  __device__ __forceinline__ static void ld(const uint8_t* p, int (&b)[4]) {
+    const unsigned w = *(const unsigned*)p;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b[i] = (w >> (8 * i)) & 255;
+  }
+};
+
+template <typename T>
+__global__ void maxpool_fwd_vec_kernel(const T* __restrict__ x, T* __restrict__ y, uint8_t* __restrict__ idx, int N,
+                                       int H, int W, int C, int OH, int OW, int k, int s, int p) {
+  constexpr int V = VC<T>::V;
+  const int CV = C / V;
+  const int total = N * OH * OW * CV;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int cv = i % CV;
+    int q = i / CV;
+    const int ow = q % OW;
+    q /= OW;
+    const int oh = q % OH, n = q / OH;
+    float m[V];
+    int best[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      m[e] = -INFINITY;
+      best[e] = -1;
+    }
+    for (int kh = 0; kh < k; ++kh) {
+      const int ih = oh * s - p + kh;
+      if (ih < 0 || ih >= H) continue;
+      for (int kw = 0; kw < k; ++kw) {
+        const int iw = ow * s - p + kw;
+        if (iw < 0 || iw >= W) continue;
+        float v[V];
+        VC<T>::ld(x + ((int64_t)(n * H + ih) * W + iw) * C + cv * V, v);
+        const int tap = kh * k + kw;
+#pragma unroll
+        for (int e = 0; e < V; ++e) {   // PyTorch order: first valid tap, then v > max or NaN
+          if (best[e] < 0) best[e] = tap;
+          if (v[e] > m[e] || v[e] != v[e]) {
+            m[e] = v[e];
+            best[e] = tap;
+          }
+        }
+      }
+    }
+    const int64_t o = (int64_t)i * V;
+    VC<T>::st(y + o, m);
+    IdxVec<V>::st(idx + o, best);
+  }
+}
+
+template <typename T>
+__global__ void maxpool_bwd_vec_kernel(const T* __restrict__ gy, const uint8_t* __restrict__ idx, T* __restrict__ gx,
+                                       int N, int H, int W, int C, int OH, int OW, int k, int s, int p) {
+  constexpr int V = VC<T>::V;
+  const int CV = C / V;
+  const int total = N * H * W * CV;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int cv = i % CV;
+    int q = i / CV;
+    const int iw = q % W;
+    q /= W;
+    const int ih = q % H, n = q / H;
+    const int oh0 = max(0, (ih + p - k + s) / s), oh1 = min(OH - 1, (ih + p) / s);
+    const int ow0 = max(0, (iw + p - k + s) / s), ow1 = min(OW - 1, (iw + p) / s);
+    float acc[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) acc[e] = 0.f;
+    for (int oh = oh0; oh <= oh1; ++oh) {
+      const int kh = ih - (oh * s - p);
+      if (kh < 0 || kh >= k) continue;
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        const int kw = iw - (ow * s - p);
+        if (kw < 0 || kw >= k) continue;
+        const int64_t o = ((int64_t)(n * OH + oh) * OW + ow) * C + cv * V;
+        int b[V];
+        IdxVec<V>::ld(idx + o, b);
+        float g[V];
+        VC<T>::ld(gy + o, g);
+        const int tap = kh * k + kw;
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] += b[e] == tap ? g[e] : 0.f;
+      }
+    }
+    VC<T>::st(gx + (int64_t)i * V, acc);
+  }
+}
+
 template <typename T>
 __global__ void nhwc_copy_kernel(const T* __restrict__ src, T* __restrict__ dst, int N, int H, int W, int C, int sH,
                                  int sW, int64_t sld, int soy, int sox, int dH, int dW, int64_t dld, int doy, int dox) {
@@ -105,6 +250,20 @@ extern "C" int ssseg_maxpool_fwd(const void* x, void* y, uint8_t* idx, int64_t N
   const int64_t total = N * OH * OW * C;
   if (total == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  const int V = dt == SSSEG_BF16 ? 8 : 4;
+  if (C % V == 0 && total / V < 0x7fffffffLL && N * H * W * C < (1LL << 40)) {
+    const dim3 gv(ssseg_grid(total / V, 256, 1 << 20)), bv(256);
+    if (dt == SSSEG_BF16)
+      hipLaunchKernelGGL(maxpool_fwd_vec_kernel<bf16_t>, gv, bv, 0, st, (const bf16_t*)x, (bf16_t*)y, idx, (int)N,
+                         (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
+    else if (dt == SSSEG_F32)
+      hipLaunchKernelGGL(maxpool_fwd_vec_kernel<float>, gv, bv, 0, st, (const float*)x, (float*)y, idx, (int)N, (int)H,
+                         (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
+    else
+      return SSSEG_EUNSUPPORTED;
+    SSSEG_LAUNCH_CHECK();
+    return 0;
+  }
   const dim3 g(ssseg_grid(total, 256, 256 * 16)), b(256);
   if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(maxpool_fwd_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)x, (bf16_t*)y, idx, (int)N, (int)H,
@@ -125,6 +284,20 @@ extern "C" int ssseg_maxpool_bwd(const void* gy, const uint8_t* idx, void* gx, i
   const int64_t total = N * H * W * C;
   if (total == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  const int V = dt == SSSEG_BF16 ? 8 : 4;
+  if (C % V == 0 && total / V < 0x7fffffffLL && N * OH * OW * C < 0x7fffffffLL * V) {
+    const dim3 gv(ssseg_grid(total / V, 256, 1 << 20)), bv(256);
+    if (dt == SSSEG_BF16)
+      hipLaunchKernelGGL(maxpool_bwd_vec_kernel<bf16_t>, gv, bv, 0, st, (const bf16_t*)gy, idx, (bf16_t*)gx, (int)N,
+                         (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
+    else if (dt == SSSEG_F32)
+      hipLaunchKernelGGL(maxpool_bwd_vec_kernel<float>, gv, bv, 0, st, (const float*)gy, idx, (float*)gx, (int)N,
+                         (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
+    else
+      return SSSEG_EUNSUPPORTED;
+    SSSEG_LAUNCH_CHECK();
+    return 0;
+  }
   const dim3 g(ssseg_grid(total, 256, 256 * 16)), b(256);
   if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(maxpool_bwd_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)gy, idx, (bf16_t*)gx, (int)N, (int)H,

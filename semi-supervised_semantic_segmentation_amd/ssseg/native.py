@@ -48,6 +48,7 @@ SIGS = {
     # convolution engine
     'ssseg_conv_igemm': (i32, [vp, vp, vp, vp, i32, i32, vp, i32, vp, sz, vp]),
     'ssseg_conv_igemm_epi': (i32, [vp, vp, vp, vp, i32, i32, vp, vp, sz, vp]),
+    'ssseg_weight_pack_batch': (i32, [vp, i64, i32, vp]),
     'ssseg_conv_igemm_workspace_bytes': (sz, [vp, i32]),
     'ssseg_set_knob': (i32, [i32, i32]),
     'ssseg_conv_wgrad_workspace_bytes': (sz, [vp, i32]),
@@ -59,6 +60,7 @@ SIGS = {
     'ssseg_bn_finalize': (i32, [vp, i64, f64, f32, f32, vp, vp, vp, vp, vp, vp]),
     'ssseg_bn_eval_params': (i32, [vp, vp, f32, i64, vp, vp, vp]),
     'ssseg_bn_fold': (i32, [vp, vp, vp, vp, vp, f32, i64, i64, vp, vp, vp, vp, vp]),
+    'ssseg_bn_fold_batch': (i32, [vp, i64, vp]),
     'ssseg_bn_eval_bwd': (i32, [vp, vp, vp, vp, vp, i64, i64, i64, vp, vp, vp, i32, i32, vp, vp, sz, vp]),
     'ssseg_bn_eval_param_grad': (i32, [vp, i64, vp, vp, vp, vp, vp]),
     'ssseg_bn_apply': (i32, [vp, vp, vp, i64, i64, i64, i64, i64, vp, vp, vp, vp, i32, i32, vp]),

@@ -10,6 +10,8 @@ gradient arena when one is attached, ssseg.arena) and the autograd Functions ret
 a registered reducer (ssseg.ddp) is told when each parameter's gradient is complete so the RCCL
 all-reduce of its bucket can start during the rest of the backward pass.
 """
+import contextlib
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
@@ -214,11 +216,14 @@ class _ConvBase:
     def _ssseg_init(self, head=False):
         self._ssseg_head = head           # writes fp32 logits with the real channel count visible
         self._ssseg_packs = {}
+        self._ssseg_specs = {}
 
     def invalidate_packed(self):
         self._ssseg_packs = {}
+        self._ssseg_specs = {}
 
     def _pack(self, key, Kd, Kr, Cd, Cp, layout, r0, rstep, Rn, s0, sstep, Sn):
+        key = (key, _CFG['dtype'])
         t = self._ssseg_packs.get(key)
         if t is None:
             w = self.weight.detach()
@@ -228,6 +233,7 @@ class _ConvBase:
             N.call('ssseg_weight_pack', N.dev_ptr(w, 'weight'), N.dev_ptr(t), Kd, Kr, Cd, Rs, Ss, Cp, layout, r0,
                    rstep, Rn, s0, sstep, Sn, N.dt_code(t), N.stream())
             self._ssseg_packs[key] = t
+            self._ssseg_specs[key] = (Kd, Kr, Cd, Rs, Ss, Cp, layout, r0, rstep, Rn, s0, sstep, Sn)
         return t
 
     def _igemm(self, x, w, y, desc, out_dt, bias=None, relu=False, fold=None):
@@ -247,9 +253,15 @@ class _ConvBase:
 
     def _fold(self, bn, residual, cout, aux=None):
         """Eval BatchNorm (+ this conv's bias) as the epilogue's per-channel affine.  Returns the epilogue
-        tuple and the (scale, mean_eff, invstd) vectors the backward of a differentiated pass uses."""
+        tuple and the (scale, mean_eff, invstd) vectors the backward of a differentiated pass uses.
+        Inside `folded(model)` the vectors come from that context's single batched launch."""
         if bn.num_features != self.out_channels:
             raise ValueError('conv_bn_act: BatchNorm width != conv out_channels')
+        bn.__dict__['_ssseg_fold_conv'] = self      # remembered for folded(): the pair is fixed by the model
+        pre = bn.__dict__.get('_ssseg_fold_live')
+        if pre is not None and pre[0] is self and pre[1].numel() == 4 * cout:
+            v = pre[1]
+            return (v[:cout], v[cout:2 * cout], residual, aux), (v[:cout], v[2 * cout:3 * cout], v[3 * cout:])
         dev = self.weight.device
         v = torch.empty(4 * cout, dtype=torch.float32, device=dev)
         scale, shift, mean_eff, invstd = v[:cout], v[cout:2 * cout], v[2 * cout:3 * cout], v[3 * cout:]
@@ -761,8 +773,71 @@ def cat_crop(a, b, ca, cb):
     return _CatFn.apply(a, b, ca, cb)
 
 
+@contextlib.contextmanager
+def folded(model):
+    """Fold every eval BatchNorm of `model` that follows a conv (pairs seen by earlier conv_bn_act calls)
+    with ONE ssseg_bn_fold_batch launch, and let conv_bn_act use those vectors inside the block.  Wrap an
+    eval forward in it (teacher forwards, the consistency pass: train.py:69-94); the running statistics and
+    parameters must not change inside the block.  Pairs not seen yet fold per layer as usual."""
+    bns = [m for m in model.modules() if isinstance(m, BatchNorm2d) and '_ssseg_fold_conv' in m.__dict__
+           and not m.training and m.track_running_stats]
+    rows = []
+    for bn in bns:
+        conv = bn.__dict__['_ssseg_fold_conv']
+        cout = conv._dims()[1]
+        buf = bn.__dict__.get('_ssseg_fold_buf')
+        if buf is None or buf.numel() != 4 * cout or buf.device != bn.running_mean.device:
+            buf = torch.empty(4 * cout, dtype=torch.float32, device=bn.running_mean.device)
+            bn.__dict__['_ssseg_fold_buf'] = buf
+        opt = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
+        rows.append((bn, conv, buf, (bn.running_mean.data_ptr(), bn.running_var.data_ptr(), opt(bn.weight),
+                                     opt(bn.bias), opt(conv.bias), buf.data_ptr(), bn.num_features, cout)))
+    if rows:
+        sig = tuple(r[3] + (float(r[0].eps),) for r in rows)
+        cache = model.__dict__.setdefault('_ssseg_fold_table', [None, None])
+        if cache[0] != sig:
+            import struct
+            blob = b''.join(struct.pack('<6q2qd', *r[3], float(r[0].eps)) for r in rows)
+            dev = rows[0][2].device
+            cache[0], cache[1] = sig, torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
+        N.call('ssseg_bn_fold_batch', N.dev_ptr(cache[1]), len(rows), N.stream())
+    try:
+        for bn, conv, buf, _ in rows:
+            bn.__dict__['_ssseg_fold_live'] = (conv, buf)
+        yield
+    finally:
+        for bn, _, _, _ in rows:
+            bn.__dict__.pop('_ssseg_fold_live', None)
+
+
 def invalidate_packed(model):
-    """Drop cached packed weights (call after the master weights change: optimizer step, EMA, load)."""
+    """The master weights changed (optimizer step, EMA, load): refresh every cached packed layout of the
+    model with ONE ssseg_weight_pack_batch launch per dtype (layouts not packed yet stay lazy).  The
+    device descriptor table is cached on the model and rebuilt only when the set of packs changes."""
+    rows = {}
     for m in model.modules():
-        if isinstance(m, _ConvBase):
+        if not isinstance(m, _ConvBase):
+            continue
+        w = m.weight
+        if not m._ssseg_packs:
+            continue
+        if not (w.is_cuda and w.is_contiguous()):
             m.invalidate_packed()
+            continue
+        if w.numel() >= 2 ** 31:
+            m.invalidate_packed()
+            continue
+        for key, t in m._ssseg_packs.items():
+            if t.numel() >= 2 ** 31:
+                raise RuntimeError('ssseg: packed weight too large for the batched repack')
+            rows.setdefault(key[1], []).append((w.data_ptr(), t.data_ptr()) + m._ssseg_specs[key])
+    cache = model.__dict__.setdefault('_ssseg_pack_tables', {})
+    for dt, rr in rows.items():
+        sig = tuple(rr)
+        ent = cache.get(dt)
+        if ent is None or ent[0] != sig:
+            dev = torch.device('cuda', torch.cuda.current_device())
+            ent = (sig, torch.tensor(rr, dtype=torch.int64).to(dev))
+            cache[dt] = ent
+        N.call('ssseg_weight_pack_batch', N.dev_ptr(ent[1]), len(rr), N.dt_code(torch.empty((), dtype=dt)),
+               N.stream())

@@ -47,7 +47,7 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
     unsup_loss = cm_mean = None
     if semi:
         size = unsup_a.shape[2:4]
-        with torch.no_grad():
+        with torch.no_grad(), snn.folded(_inner(ema_model)):   # one batched BN fold for both teacher passes
             ema_pred_a = ops.interpolate_bilinear(ema_model(unsup_a)[-1][-1], size, align_corners=False)
             ema_pred_b = ops.interpolate_bilinear(ema_model(unsup_b)[-1][-1], size, align_corners=False)
             cmask = cowmix.generate_cowmix_masks_like(unsup_a, mask_proportion_range=tc['mask_proportion_range'],
@@ -56,7 +56,8 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
             mixed_images = cowmix.mix_with_mask(unsup_a, unsup_b, cmask)
             del cmask, ema_pred_a, ema_pred_b
         model.eval()
-        student_pred = model(mixed_images)[-1][-1]
+        with snn.folded(_inner(model)):
+            student_pred = model(mixed_images)[-1][-1]
         model.train()
         student_pred = ops.interpolate_bilinear(student_pred, mixed_images.shape[2:4], align_corners=False)
         consistency, cm_mean = ops.consistency_loss(student_pred, mixed_ema_pred, tc['confidence_threshold'])

@@ -319,3 +319,57 @@ def test_no_cpu_fallback_for_layers():
     mod = snn.Conv2d(8, 8, 3, padding=1)
     with pytest.raises(RuntimeError):
         mod(torch.randn(1, 8, 4, 4))
+
+
+def _small_resnet_unet(dev):
+    from models import unet
+    from models.adapters import ListOutput
+    from models.encoders import resnet
+    torch.manual_seed(21)
+    return ListOutput(unet.UNet(2, resnet.resnet50_encoder(), max_width=32, train_upsampling=True)).to(dev)
+
+
+def test_batched_repack_after_weight_update(hip_device):
+    """invalidate_packed() refreshes every cached fwd/dgrad/phase pack with one batched launch: a forward
+    + backward after an in-place weight change equals a model that never packed the old weights."""
+    from ssseg import nn as snn
+    snn.set_compute_dtype(torch.bfloat16)
+    a = _small_resnet_unet(hip_device)
+    b = _small_resnet_unet(hip_device)
+    x = torch.rand(2, 3, 64, 64, device=hip_device)
+    a.train()
+    a(x)[-1][-1].float().sum().backward()          # packs fwd + dgrad layouts of every conv
+    with torch.no_grad():
+        for pa in a.parameters():
+            pa.mul_(0.9)
+    b.load_state_dict(a.state_dict())                 # same weights AND running statistics
+    snn.invalidate_packed(a)
+    a.eval()
+    b.eval()
+    with torch.no_grad():
+        ya = a(x)[-1][-1]
+        yb = b(x)[-1][-1]
+    assert torch.equal(ya, yb)
+
+
+def test_folded_context_bitwise(hip_device):
+    """snn.folded(model): one batched BN fold for the whole eval forward, bit-identical to per-layer folds,
+    with and without autograd (teacher pass / consistency pass)."""
+    from ssseg import nn as snn
+    snn.set_compute_dtype(torch.bfloat16)
+    m = _small_resnet_unet(hip_device)
+    x = torch.rand(2, 3, 64, 64, device=hip_device)
+    m.train()
+    m(x)                       # running stats move away from their init
+    m.eval()
+    with torch.no_grad():
+        y0 = m(x)[-1][-1].clone()          # per-layer folds (records the conv/BN pairs)
+        with snn.folded(m):
+            y1 = m(x)[-1][-1].clone()
+    assert torch.equal(y0, y1)
+    xr = x.clone().requires_grad_(True)
+    g0 = torch.autograd.grad(m(xr)[-1][-1].float().square().sum(), xr)[0]
+    with snn.folded(m):
+        out = m(xr)[-1][-1]
+    g1 = torch.autograd.grad(out.float().square().sum(), xr)[0]
+    assert torch.equal(g0, g1)

@@ -1,25 +1,37 @@
 """Per-kernel summary (pct, total_us, calls, avg_us, name) from a rocprofv3 rocpd database
 (`rocprofv3 --kernel-trace --stats -d DIR -o run -- ...` writes DIR/run_results.db).
 
-    python tools/prof_summary.py gpurun_out/prof3/run_results.db [header comment] > profiles/rN_kernel_stats.tsv
+    python tools/prof_summary.py DB [--tail-ms MS] [--header TEXT] > profiles/rN_kernel_stats.tsv
+
+--tail-ms keeps only dispatches that start in the last MS milliseconds of the trace (the timed steps;
+drops warm-up and one-time autotuning launches).
 """
+import argparse
 import sqlite3
-import sys
 
 
-def summary(db):
+def summary(db, tail_ms=None):
     c = sqlite3.connect(db)
+    t0 = 0
+    if tail_ms:
+        (tmax,) = c.execute('select max(end) from rocpd_kernel_dispatch').fetchone()
+        t0 = tmax - int(tail_ms * 1e6)
     rows = c.execute("""
         select s.kernel_name, count(*), sum(d.end - d.start)
         from rocpd_kernel_dispatch d join rocpd_info_kernel_symbol s on d.kernel_id = s.id
-        group by s.kernel_name order by 3 desc""").fetchall()
+        where d.start >= ? group by s.kernel_name order by 3 desc""", (t0,)).fetchall()
     total = sum(r[2] for r in rows) or 1
     return [(100.0 * ns / total, ns / 1e3, n, ns / 1e3 / n, name) for name, n, ns in rows]
 
 
 if __name__ == '__main__':
-    if len(sys.argv) > 2:
-        print('# ' + sys.argv[2])
+    ap = argparse.ArgumentParser()
+    ap.add_argument('db')
+    ap.add_argument('--tail-ms', type=float, default=None)
+    ap.add_argument('--header', default=None)
+    a = ap.parse_args()
+    if a.header:
+        print('# ' + a.header)
     print('# columns: pct, total_us, calls, avg_us, kernel')
-    for pct, tot, n, avg, name in summary(sys.argv[1]):
+    for pct, tot, n, avg, name in summary(a.db, a.tail_ms):
         print(f'{pct:7.3f}\t{tot:12.1f}\t{n:6d}\t{avg:10.2f}\t{name}')
