@@ -196,7 +196,8 @@ size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* desc_host, int dt
  * knob 2: 64x64 small-M tiles of the register-staged kernel (0 = auto); knob 3: bf16 LDS-DMA kernel
  * (0 = on, -1 = off); knob 4: bf16 variant (0 = auto, 1..10 = an LDS-DMA tile config, 11 = register-staged);
  * knob 5: autotune unseen geometries once on the caller's stream (1 = on, default; 0 = static rule);
- * knob 6 (write 1): clear the per-geometry variant cache.  Variants never change results.  Not thread-safe. */
+ * knob 6 (write 1): clear the per-geometry variant cache; knob 7: LDS-staged coalesced epilogue of the LDS-DMA
+ * kernel (0 = on, default; -1 = off).  Variants never change results.  Not thread-safe. */
 int ssseg_set_knob(int id, int value);
 
 /* dW = sum over output pixels of dY[p][k] * x_col[p][(r,s,c)] (split-K fp32 slabs + deterministic

@@ -165,6 +165,95 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[FN][FM], long long
   }
 }
 
+// LDS-staged epilogue for the LDS-DMA kernel: the raw fp32 accumulators go to LDS (rows padded by 16 B:
+// conflict-free float4 writes), then each thread finishes 8 consecutive channels of one pixel with 16-byte
+// residual loads and 16-byte (bf16) / 2x16-byte (f32) stores, so a pixel row is written in full lines.
+// Same arithmetic as store_tile (fp32 acc*scale + shift + res, then act, then one rounding).
+template <typename TO> struct Out8;
+template <> struct Out8<bf16_t> {
+  __device__ __forceinline__ static void ld(const bf16_t* p, float (&v)[8]) {
+    const uint4 q = *(const uint4*)p;
+    const unsigned w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  __device__ __forceinline__ static void st(bf16_t* p, const float (&v)[8]) {
+    unsigned w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (unsigned)f32_to_bf16(v[2 * i]) | ((unsigned)f32_to_bf16(v[2 * i + 1]) << 16);
+    *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+};
+template <> struct Out8<float> {
+  __device__ __forceinline__ static void ld(const float* p, float (&v)[8]) {
+    const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  __device__ __forceinline__ static void st(float* p, const float (&v)[8]) {
+    *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+    *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+
+template <typename TO, int BM, int BN, int FM, int FN, int NT>
+__device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char* smem, long long m0, int n0, int wmo,
+                                               int wno, int lane, const ConvGeom& g, TO* __restrict__ y,
+                                               const Epi<TO>& ep) {
+  constexpr int LDR = BN * 4 + 16;   // bytes per staged pixel row
+  __syncthreads();                   // every wave is done with the LDS ring
+#pragma unroll
+  for (int j = 0; j < FM; ++j)
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+      *(f32x4*)(smem + (wmo + j * 16 + (lane & 15)) * LDR + (wno + i * 16 + (lane >> 4) * 4) * 4) = acc[i][j];
+  __syncthreads();
+  constexpr int CPR = BN / 8;                 // 8-channel chunks per row
+  const bool vec = (g.ldy & 7) == 0 && (!ep.res || (ep.ldr & 7) == 0);
+  for (int idx = threadIdx.x; idx < BM * CPR; idx += NT) {
+    const int row = idx / CPR, ch = idx - row * CPR;
+    const long long m = m0 + row;
+    const int n = n0 + ch * 8;
+    if (m >= g.M || n >= g.K) continue;
+    const int ox = (int)(m % g.OW);
+    const long long q = m / g.OW;
+    const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
+    const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+    const float* a = (const float*)(smem + row * LDR + ch * 32);
+    float v[8], r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const float4 a0 = *(const float4*)a, a1 = *(const float4*)(a + 4);
+    const float raw[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const bool full = vec && n + 7 < g.K;
+    if (ep.res) {
+      if (full)
+        Out8<TO>::ld(ep.res + op * ep.ldr + n, r);
+      else
+        for (int e = 0; e < 8 && n + e < g.K; ++e) r[e] = io<TO>::ld(ep.res, op * ep.ldr + n + e);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = raw[e];
+      const bool in = n + e < g.K;
+      if (ep.scale && in) t *= ep.scale[n + e];
+      if (ep.shift && in) t += ep.shift[n + e];
+      t += r[e];
+      if (ep.relu) t = fmaxf(t, 0.f);
+      v[e] = t;
+    }
+    if (full) {
+      Out8<TO>::st(y + op * g.ldy + n, v);
+      if (ep.aux) Out8<TO>::st(ep.aux + op * g.ldy + n, raw);
+    } else {
+      for (int e = 0; e < 8 && n + e < g.K; ++e) {
+        io<TO>::st(y, op * g.ldy + n + e, v[e]);
+        if (ep.aux) io<TO>::st(ep.aux, op * g.ldy + n + e, raw[e]);
+      }
+    }
+  }
+}
+
 // XCD-aware remap of a 1-D grid (bijective for any grid size): consecutive tile ids land on one XCD
 __device__ __forceinline__ int xcd_tile(int bid, int ntiles) {
   const int xcd = bid & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
@@ -179,7 +268,8 @@ constexpr int ROWB = 80;   // 64 data bytes + 16 pad per LDS row
 int g_knobs[8] = {0, -1, 0, 0, 0, 1, 0, 0};   // runtime variant switches (ssseg_set_knob)
 // 0: reg-staged pipeline depth; 1: split-K cap (-1 off); 2: 64x64 small-M tiles (reg-staged path);
 // 3: bf16 LDS-DMA path (0 on, -1 off); 4: variant (0 auto, 1..10 LDS-DMA config, 11 register-staged);
-// 5: autotune unseen geometries (1 on, 0 = static heuristic); knob 6 = 1 clears the variant cache
+// 5: autotune unseen geometries (1 on, 0 = static heuristic); knob 6 = 1 clears the variant cache;
+// 7: LDS-staged coalesced epilogue in the LDS-DMA kernel (0 on, -1 off)
 
 template <typename T, typename TO, int BM, int BN, int WM, int WN, bool DEEP>
 __global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __restrict__ x, const T* __restrict__ w,
@@ -365,7 +455,7 @@ template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS>
 __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const bf16_t* __restrict__ x,
                                                                 const bf16_t* __restrict__ w, TO* __restrict__ y,
                                                                 ConvGeom g, Epi<TO> ep, unsigned xbytes,
-                                                                unsigned wbytes) {
+                                                                unsigned wbytes, int g_epi_lds) {
   constexpr int ROW = 128;                       // bytes per LDS row = 64 bf16 of k
   constexpr int STAGE = (BM + BN) * ROW;
   constexpr int AI = BM / 8 / NW;                // A (pixel) wave-instructions per wave per stage
@@ -487,7 +577,14 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const bf16_t* __
     if (kt + D < nk) issue((kt + D) % NS);
     compute(kt % NS);
   }
-  store_tile<TO, FM, FN>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, g, y, ep);
+  if constexpr (BM * (BN * 4 + 16) <= NS * STAGE) {
+    if (g_epi_lds)
+      store_tile_lds<TO, BM, BN, FM, FN, NW * 64>(acc, smem, m0, n0, wm * WTM, wn * WTN, lane, g, y, ep);
+    else
+      store_tile<TO, FM, FN>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, g, y, ep);
+  } else {
+    store_tile<TO, FM, FN>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, g, y, ep);
+  }
 }
 
 // split-K finalize: y[pixel(m)][n] = act(ws[m][n] * scale[n] + shift[n] + res[pixel(m)][n])
@@ -862,7 +959,7 @@ void launch_glds(const void* x, const void* w, void* y, const ConvGeom& g, const
                  hipStream_t s) {
   const long long tiles = ((g.M + BM - 1) / BM) * ((g.K + BN - 1) / BN);
   hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS>), dim3((unsigned)tiles), dim3(NW * 64), 0, s,
-                     (const bf16_t*)x, (const bf16_t*)w, (TO*)y, g, ep, xb, wb);
+                     (const bf16_t*)x, (const bf16_t*)w, (TO*)y, g, ep, xb, wb, (int)(g_knobs[7] == 0));
 }
 
 template <typename TO>
