@@ -170,6 +170,13 @@ typedef struct {
  * When R*S == 0 (an output phase no tap reaches) the phase is zero-filled. */
 int ssseg_conv_igemm(const void* x, const void* w, void* y, const ssseg_conv_desc* desc_host, int dt, int dt_out,
                      const float* bias, int relu, void* ws, size_t ws_bytes, ssseg_stream_t stream);
+/* Activation codes of the fused epilogues, BN kernels and ssseg_act_bwd: ReLU (unet.py:10, encoders),
+ * ReLU6 (MobileNetV2 ConvBNReLU, mobilenetv2.py:39), LeakyReLU(slope) (discriminator.py:16). */
+#define SSSEG_ACT_NONE 0
+#define SSSEG_ACT_RELU 1
+#define SSSEG_ACT_RELU6 2
+#define SSSEG_ACT_LEAKY 3
+
 /* Fused conv epilogue (ssseg_conv_igemm_epi):
  *   y[m][n]   = act(acc[m][n] * scale[n] + shift[n] + residual[pixel(m)][n])
  *   aux[m][n] = acc[m][n]                          (optional; same pixel stride as y)
@@ -183,7 +190,8 @@ typedef struct ssseg_conv_epilogue {
   const void* residual;
   int64_t ldr;
   void* aux;
-  int32_t relu;
+  int32_t relu;    /* activation code SSSEG_ACT_* (1 = ReLU, the historical flag) */
+  float slope;     /* LeakyReLU negative slope (SSSEG_ACT_LEAKY) */
 } ssseg_conv_epilogue;
 int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const ssseg_conv_desc* desc_host, int dt, int dt_out,
                          const ssseg_conv_epilogue* epi, void* ws, size_t ws_bytes, ssseg_stream_t stream);
@@ -225,6 +233,19 @@ typedef struct ssseg_pack_desc {
   int64_t layout, r0, rstep, Rn, s0, sstep, Sn;
 } ssseg_pack_desc;
 int ssseg_weight_pack_batch(const ssseg_pack_desc* descs, int64_t n, int dt, ssseg_stream_t stream);
+
+/* Depthwise convolution (groups == channels; MobileNetV2 ConvBNReLU(groups=hidden), mobilenetv2.py:34-39,58).
+ * The descriptor is the conv engine's with K == C and no output phases; weights packed [R*S][ldw] in the
+ * compute dtype (ssseg_weight_pack layout 1, Kd = Kr = 1).  fwd takes the same fused epilogue as the conv
+ * engine (folded eval BN, residual, activation, raw-accumulator copy).  wgrad writes the PyTorch layout
+ * [C][1][R][S] (c < c_real), += when accumulate; deterministic (fixed-order block partials). */
+int ssseg_dwconv_fwd(const void* x, const void* w, void* y, const ssseg_conv_desc* desc_host, int dt,
+                     const ssseg_conv_epilogue* epi, ssseg_stream_t stream);
+int ssseg_dwconv_dgrad(const void* dy, const void* w, void* dx, const ssseg_conv_desc* desc_host, int dt,
+                       ssseg_stream_t stream);
+size_t ssseg_dwconv_wgrad_workspace_bytes(const ssseg_conv_desc* desc_host, int dt);
+int ssseg_dwconv_wgrad(const void* x, const void* dy, float* dw, const ssseg_conv_desc* desc_host, int dt,
+                       int64_t c_real, int accumulate, void* ws, size_t ws_bytes, ssseg_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * BatchNorm2d / SyncBatchNorm (nn.BatchNorm2d in every ConvBlock, unet.py:9; distributed_trainer.py:36)
@@ -304,6 +325,10 @@ int ssseg_nhwc_copy(const void* src, void* dst, int64_t N, int64_t H, int64_t W,
                     int dt, ssseg_stream_t stream);
 int ssseg_zero(void* p, size_t bytes, ssseg_stream_t stream);
 /* gx = gy * [y > 0]  (ReLU backward from the saved output; ConvTranspose2d+ReLU upsampler unet.py:21-22) */
+/* gx = gy * d act / d z evaluated from the activation output y (SSSEG_ACT_*; the cut gradient is selected
+ * to 0, not multiplied, like PyTorch's threshold_backward) */
+int ssseg_act_bwd(const void* gy, const void* y, void* gx, int64_t n, int act, float slope, int dt,
+                  ssseg_stream_t stream);
 int ssseg_relu_bwd(const void* gy, const void* y, void* gx, int64_t n, int dt, ssseg_stream_t stream);
 
 #ifdef __cplusplus

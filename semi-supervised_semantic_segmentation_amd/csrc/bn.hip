@@ -153,10 +153,7 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x
           } else {
             const float xh = (v[u][e] - mu[e]) * is[e];
             float gr = g[u][e];
-            if (relu) {
-              const float yv = fmaf(ga[e], xh, be[e]) + r[u][e];
-              gr = yv > 0.f ? gr : 0.f;
-            }
+            if (relu) gr = act_bwd(gr, fmaf(ga[e], xh, be[e]) + r[u][e], relu, 0.f);
             s1[e] += (double)gr;
             s2[e] += (double)gr * (double)xh;
           }
@@ -336,7 +333,7 @@ __global__ void __launch_bounds__(256) bn_eval_bwd_kernel(const T* __restrict__ 
         float od[V], oc[V];
 #pragma unroll
         for (int e = 0; e < V; ++e) {
-          float gr = (relu && !(yv[u][e] > 0.f)) ? 0.f : g[u][e];
+          float gr = relu ? act_bwd(g[u][e], yv[u][e], relu, 0.f) : g[u][e];
           gr = live[e] ? gr : 0.f;
           od[e] = gr;
           oc[e] = sc[e] * gr;
@@ -410,7 +407,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
       for (int e = 0; e < V; ++e) {
         const float xh = (v[u][e] - mu[e]) * is[e];
         float a = fmaf(ga[e], xh, be[e]) + r[u][e];
-        if (relu) a = fmaxf(a, 0.f);
+        a = act_fwd(a, relu, 0.f);
         o[e] = live[e] ? a : 0.f;
       }
       Vec<T, V>::st(y + p * ldy + c0, o);
@@ -461,7 +458,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
       for (int e = 0; e < V; ++e) {
         const float xh = (v[u][e] - mu[e]) * is[e];
         float gr = g[u][e];
-        if (relu) gr = (fmaf(ga[e], xh, be[e]) + r[u][e]) > 0.f ? gr : 0.f;
+        if (relu) gr = act_bwd(gr, fmaf(ga[e], xh, be[e]) + r[u][e], relu, 0.f);
         gr = live[e] ? gr : 0.f;
         od[e] = gr;
         const float d = train ? gr - mdy[e] - xh * mdyx[e] : gr;

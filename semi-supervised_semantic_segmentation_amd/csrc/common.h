@@ -75,3 +75,21 @@ static inline int ssseg_grid(int64_t n, int block, int cap = 256 * 16) {
   if (g < 1) g = 1;
   return (int)g;
 }
+
+// activation codes (SSSEG_ACT_*): forward, and the derivative evaluated from the output y (sign and the
+// open interval (0, 6) survive every activation here, so y decides like the pre-activation does) or from
+// the pre-activation z.  PyTorch semantics: ReLU6 = hardtanh(0, 6) passes gradient for 0 < z < 6;
+// LeakyReLU passes 1 for z > 0 and slope otherwise.
+__device__ __forceinline__ float act_fwd(float z, int act, float slope) {
+  if (act == SSSEG_ACT_RELU) return fmaxf(z, 0.f);
+  if (act == SSSEG_ACT_RELU6) return fminf(fmaxf(z, 0.f), 6.f);
+  if (act == SSSEG_ACT_LEAKY) return z > 0.f ? z : z * slope;
+  return z;
+}
+// g * d act / d z with the gradient SELECTED (not multiplied) where it is cut, like threshold_backward
+__device__ __forceinline__ float act_bwd(float g, float yz, int act, float slope) {
+  if (act == SSSEG_ACT_RELU) return yz > 0.f ? g : 0.f;
+  if (act == SSSEG_ACT_RELU6) return (yz > 0.f && yz < 6.f) ? g : 0.f;
+  if (act == SSSEG_ACT_LEAKY) return yz > 0.f ? g : g * slope;
+  return g;
+}

@@ -94,8 +94,9 @@ struct Epi {
   const float* shift;
   const TO* res;
   int ldr;
-  int relu;
-  TO* aux;   // optional copy of the raw accumulator (pre-affine conv output), pixel stride ldy
+  int relu;    // activation code SSSEG_ACT_*
+  TO* aux;     // optional copy of the raw accumulator (pre-affine conv output), pixel stride ldy
+  float slope;
 };
 
 template <typename TO> struct Load4;
@@ -121,9 +122,9 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[FN][FM], long long
   for (int j = 0; j < FM; ++j) {
     const long long m = mb + j * 16 + (lane & 15);
     if (m >= g.M) continue;
-    const int ox = (int)(m % g.OW);
-    const long long q = m / g.OW;
-    const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
+    const int ox = (int)m % g.OW;    // 32-bit decode: geom_ok guarantees M < 2^31
+    const int q = (int)m / g.OW;
+    const int oy = q % g.OH, img = q / g.OH;
     const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
     TO* yp = y + op * g.ldy;
 #pragma unroll
@@ -153,7 +154,7 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[FN][FM], long long
         if (ep.scale && in) a *= ep.scale[n + e];
         if (ep.shift && in) a += ep.shift[n + e];
         a += r[e];
-        if (ep.relu) a = fmaxf(a, 0.f);
+        a = act_fwd(a, ep.relu, ep.slope);
         v[e] = a;
       }
       if (full && (g.ldy & 3) == 0) {
@@ -217,9 +218,9 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
     const long long m = m0 + row;
     const int n = n0 + ch * 8;
     if (m >= g.M || n >= g.K) continue;
-    const int ox = (int)(m % g.OW);
-    const long long q = m / g.OW;
-    const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
+    const int ox = (int)m % g.OW;    // 32-bit decode: geom_ok guarantees M < 2^31
+    const int q = (int)m / g.OW;
+    const int oy = q % g.OH, img = q / g.OH;
     const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
     const float* a = (const float*)(smem + row * LDR + ch * 32);
     float v[8], r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -239,7 +240,7 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
       if (ep.scale && in) t *= ep.scale[n + e];
       if (ep.shift && in) t += ep.shift[n + e];
       t += r[e];
-      if (ep.relu) t = fmaxf(t, 0.f);
+      t = act_fwd(t, ep.relu, ep.slope);
       v[e] = t;
     }
     if (full) {
@@ -306,10 +307,10 @@ __global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __res
     const long long m = m0 + (t >> 2) + 64 * i;
     a_ok[i] = m < g.M;
     const long long mm = a_ok[i] ? m : 0;
-    a_ox[i] = (int)(mm % g.OW);
-    const long long q = mm / g.OW;
-    a_oy[i] = (int)(q % g.OH);
-    a_n[i] = (int)(q / g.OH);
+    a_ox[i] = (int)mm % g.OW;
+    const int q = (int)mm / g.OW;
+    a_oy[i] = q % g.OH;
+    a_n[i] = q / g.OH;
   }
   // k-state of this thread's chunk: k = tap*C + kc, tap = r*S + s (advanced by every load, in order)
   const int k_first = kt0 * BK + chunk * VEC;
@@ -487,9 +488,9 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const bf16_t* __
     const int ch = c_even ^ ((inst & 1) * 4);
     const long long m = m0 + 8 * inst + (lane >> 3);
     if (m < g.M) {
-      const int ox = (int)(m % g.OW);
-      const long long q = m / g.OW;
-      const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
+      const int ox = (int)m % g.OW;
+      const int q = (int)m / g.OW;
+      const int oy = q % g.OH, img = q / g.OH;
       a_iy[ii] = oy * g.sy + g.py;
       a_ix[ii] = ox * g.sx + g.px;
       a_off[ii] = ((img * g.H + a_iy[ii]) * g.W + a_ix[ii]) * g.ldx * 2 + ch * 16;
@@ -594,16 +595,16 @@ __global__ void splitk_finalize_kernel(const float* __restrict__ ws, TO* __restr
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
     const int n = (int)(i % g.K);
     const long long m = i / g.K;
-    const int ox = (int)(m % g.OW);
-    const long long q = m / g.OW;
-    const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
+    const int ox = (int)m % g.OW;    // 32-bit decode: geom_ok guarantees M < 2^31
+    const int q = (int)m / g.OW;
+    const int oy = q % g.OH, img = q / g.OH;
     const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
     float v = ws[i];
     if (ep.aux) io<TO>::st(ep.aux, op * g.ldy + n, v);
     if (ep.scale) v *= ep.scale[n];
     if (ep.shift) v += ep.shift[n];
     if (ep.res) v += io<TO>::ld(ep.res, op * ep.ldr + n);
-    if (ep.relu) v = fmaxf(v, 0.f);
+    v = act_fwd(v, ep.relu, ep.slope);
     io<TO>::st(y, op * g.ldy + n, v);
   }
 }
@@ -615,14 +616,14 @@ __global__ void phase_zero_kernel(TO* y, ConvGeom g, Epi<TO> ep) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
     const int n = (int)(i % g.K);
     const long long m = i / g.K;
-    const int ox = (int)(m % g.OW);
-    const long long q = m / g.OW;
-    const int oy = (int)(q % g.OH), img = (int)(q / g.OH);
+    const int ox = (int)m % g.OW;    // 32-bit decode: geom_ok guarantees M < 2^31
+    const int q = (int)m / g.OW;
+    const int oy = q % g.OH, img = q / g.OH;
     const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
     float v = ep.shift ? ep.shift[n] : 0.f;
     if (ep.aux) io<TO>::st(ep.aux, op * g.ldy + n, 0.f);
     if (ep.res) v += io<TO>::ld(ep.res, op * ep.ldr + n);
-    if (ep.relu) v = fmaxf(v, 0.f);
+    v = act_fwd(v, ep.relu, ep.slope);
     io<TO>::st(y, op * g.ldy + n, v);
   }
 }
@@ -1134,6 +1135,7 @@ bool geom_ok(const ConvGeom& g, int dt) {
   const int vec = dt == SSSEG_BF16 ? 8 : 4;
   if (g.C % vec || g.ldx % vec || g.ldw % vec) return false;
   if (g.N < 1 || g.OH < 1 || g.OW < 1 || g.K < 1 || g.C < 1) return false;
+  if (g.M >= 0x7fffffffLL) return false;   // kernels decode output positions with 32-bit math
   if (g.R < 0 || g.S < 0) return false;
   return true;
 }
@@ -1169,13 +1171,14 @@ extern "C" int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const
   ConvGeom g;
   if (!make_geom(d, g) || !y) return SSSEG_EINVAL;
   if (!geom_ok(g, dt)) return SSSEG_EINVAL;
-  const ssseg_conv_epilogue none = {nullptr, nullptr, nullptr, 0, nullptr, 0};
+  const ssseg_conv_epilogue none = {nullptr, nullptr, nullptr, 0, nullptr, 0, 0.f};
   const ssseg_conv_epilogue& e = epi ? *epi : none;
   if (e.residual && (e.ldr < g.K || e.ldr > 0x7fffffff)) return SSSEG_EINVAL;
   if (g.M == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  const Epi<float> ef{e.scale, e.shift, (const float*)e.residual, (int)e.ldr, e.relu, (float*)e.aux};
-  const Epi<bf16_t> eb{e.scale, e.shift, (const bf16_t*)e.residual, (int)e.ldr, e.relu, (bf16_t*)e.aux};
+  if (e.relu < 0 || e.relu > SSSEG_ACT_LEAKY) return SSSEG_EINVAL;
+  const Epi<float> ef{e.scale, e.shift, (const float*)e.residual, (int)e.ldr, e.relu, (float*)e.aux, e.slope};
+  const Epi<bf16_t> eb{e.scale, e.shift, (const bf16_t*)e.residual, (int)e.ldr, e.relu, (bf16_t*)e.aux, e.slope};
   if (g.KK == 0) {   // no taps reach this output phase: the contraction is zero
     if (dt_out == SSSEG_F32)
       hipLaunchKernelGGL(phase_zero_kernel<float>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, (float*)y, g, ef);
@@ -1202,7 +1205,7 @@ extern "C" int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const
 
 extern "C" int ssseg_conv_igemm(const void* x, const void* w, void* y, const ssseg_conv_desc* d, int dt, int dt_out,
                                 const float* bias, int relu, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
-  const ssseg_conv_epilogue e = {nullptr, bias, nullptr, 0, nullptr, relu};
+  const ssseg_conv_epilogue e = {nullptr, bias, nullptr, 0, nullptr, relu ? SSSEG_ACT_RELU : 0, 0.f};
   return ssseg_conv_igemm_epi(x, w, y, d, dt, dt_out, &e, ws, ws_bytes, stream);
 }
 

@@ -351,23 +351,30 @@ extern "C" int ssseg_zero(void* p, size_t bytes, ssseg_stream_t stream) {
 
 namespace {
 template <typename T>
-__global__ void relu_bwd_kernel(const T* __restrict__ gy, const T* __restrict__ y, T* __restrict__ gx, int64_t n) {
+__global__ void act_bwd_kernel(const T* __restrict__ gy, const T* __restrict__ y, T* __restrict__ gx, int64_t n, int act,
+                               float slope) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    io<T>::st(gx, i, io<T>::ld(y, i) > 0.f ? io<T>::ld(gy, i) : 0.f);
+    io<T>::st(gx, i, act_bwd(io<T>::ld(gy, i), io<T>::ld(y, i), act, slope));
 }
 }  // namespace
 
-extern "C" int ssseg_relu_bwd(const void* gy, const void* y, void* gx, int64_t n, int dt, ssseg_stream_t stream) {
-  if (!gy || !y || !gx || n < 0) return SSSEG_EINVAL;
+extern "C" int ssseg_act_bwd(const void* gy, const void* y, void* gx, int64_t n, int act, float slope, int dt,
+                             ssseg_stream_t stream) {
+  if (!gy || !y || !gx || n < 0 || act < 0 || act > SSSEG_ACT_LEAKY) return SSSEG_EINVAL;
   if (n == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   const dim3 g(ssseg_grid(n, 256, 256 * 16)), b(256);
   if (dt == SSSEG_BF16)
-    hipLaunchKernelGGL(relu_bwd_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)gy, (const bf16_t*)y, (bf16_t*)gx, n);
+    hipLaunchKernelGGL(act_bwd_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)gy, (const bf16_t*)y, (bf16_t*)gx, n, act,
+                       slope);
   else if (dt == SSSEG_F32)
-    hipLaunchKernelGGL(relu_bwd_kernel<float>, g, b, 0, st, (const float*)gy, (const float*)y, (float*)gx, n);
+    hipLaunchKernelGGL(act_bwd_kernel<float>, g, b, 0, st, (const float*)gy, (const float*)y, (float*)gx, n, act, slope);
   else
     return SSSEG_EUNSUPPORTED;
   SSSEG_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int ssseg_relu_bwd(const void* gy, const void* y, void* gx, int64_t n, int dt, ssseg_stream_t stream) {
+  return ssseg_act_bwd(gy, y, gx, n, SSSEG_ACT_RELU, 0.f, dt, stream);
 }

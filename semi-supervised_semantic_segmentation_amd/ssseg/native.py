@@ -49,6 +49,10 @@ SIGS = {
     'ssseg_conv_igemm': (i32, [vp, vp, vp, vp, i32, i32, vp, i32, vp, sz, vp]),
     'ssseg_conv_igemm_epi': (i32, [vp, vp, vp, vp, i32, i32, vp, vp, sz, vp]),
     'ssseg_weight_pack_batch': (i32, [vp, i64, i32, vp]),
+    'ssseg_dwconv_fwd': (i32, [vp, vp, vp, vp, i32, vp, vp]),
+    'ssseg_dwconv_dgrad': (i32, [vp, vp, vp, vp, i32, vp]),
+    'ssseg_dwconv_wgrad_workspace_bytes': (sz, [vp, i32]),
+    'ssseg_dwconv_wgrad': (i32, [vp, vp, vp, vp, i32, i64, i32, vp, sz, vp]),
     'ssseg_conv_igemm_workspace_bytes': (sz, [vp, i32]),
     'ssseg_set_knob': (i32, [i32, i32]),
     'ssseg_conv_wgrad_workspace_bytes': (sz, [vp, i32]),
@@ -73,6 +77,7 @@ SIGS = {
     'ssseg_maxpool_bwd': (i32, [vp, vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, i32, vp]),
     'ssseg_nhwc_copy': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i32, vp]),
     'ssseg_zero': (i32, [vp, sz, vp]),
+    'ssseg_act_bwd': (i32, [vp, vp, vp, i64, i32, f32, i32, vp]),
     'ssseg_relu_bwd': (i32, [vp, vp, vp, i64, i32, vp]),
 }
 
@@ -87,7 +92,7 @@ class ConvDesc(ctypes.Structure):
 class ConvEpilogue(ctypes.Structure):
     """Mirror of ssseg_conv_epilogue (include/ssseg.h)."""
     _fields_ = [('scale', ctypes.c_void_p), ('shift', ctypes.c_void_p), ('residual', ctypes.c_void_p),
-                ('ldr', ctypes.c_int64), ('aux', ctypes.c_void_p), ('relu', ctypes.c_int32)]
+                ('ldr', ctypes.c_int64), ('aux', ctypes.c_void_p), ('relu', ctypes.c_int32), ('slope', ctypes.c_float)]
 
 
 _lib = None

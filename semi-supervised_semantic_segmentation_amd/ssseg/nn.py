@@ -174,12 +174,32 @@ def _phases(stride, pad, R, in_full, dil=1):
     return out
 
 
+ACT_NONE, ACT_RELU, ACT_RELU6, ACT_LEAKY = 0, 1, 2, 3
+
+
+def _act(a):
+    """Activation spec -> (SSSEG_ACT_* code, slope).  Accepts False/None (none), True (ReLU), a code
+    (ACT_RELU6, ...) or ('leaky', slope)."""
+    if a is None or a is False:
+        return ACT_NONE, 0.0
+    if a is True:
+        return ACT_RELU, 0.0
+    if isinstance(a, tuple):
+        if a[0] != 'leaky':
+            raise ValueError(f'unknown activation {a!r}')
+        return ACT_LEAKY, float(a[1])
+    code = int(a)
+    if code not in (ACT_NONE, ACT_RELU, ACT_RELU6):
+        raise ValueError(f'unknown activation {a!r}')
+    return code, 0.0
+
+
 class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, mod, relu):
         y = mod._ssseg_forward(x, relu)
         ctx.mod, ctx.relu = mod, relu
-        ctx.save_for_backward(x, y if relu else None)
+        ctx.save_for_backward(x, y if _act(relu)[0] else None)
         return y
 
     @staticmethod
@@ -187,9 +207,11 @@ class _ConvFn(torch.autograd.Function):
         x, y = ctx.saved_tensors
         mod = ctx.mod
         gy = mod._grad_in(gy)
-        if ctx.relu:
+        code, slope = _act(ctx.relu)
+        if code:
             gm = torch.empty_like(gy)
-            N.call('ssseg_relu_bwd', N.dev_ptr(gy), N.dev_ptr(y), N.dev_ptr(gm), gy.numel(), N.dt_code(gy), N.stream())
+            N.call('ssseg_act_bwd', N.dev_ptr(gy), N.dev_ptr(y), N.dev_ptr(gm), gy.numel(), code, slope, N.dt_code(gy),
+                   N.stream())
             gy = gm
         mod._ssseg_wgrad(x, gy)
         dx = mod._ssseg_dgrad(gy, x.shape) if ctx.needs_input_grad[0] else None
@@ -247,7 +269,7 @@ class _ConvBase:
         ep = N.ConvEpilogue(N.dev_ptr(scale) if scale is not None else None,
                             N.dev_ptr(shift) if shift is not None else None,
                             N.dev_ptr(res) if res is not None else None, res.shape[1] if res is not None else 0,
-                            N.dev_ptr(aux) if aux is not None else None, int(bool(relu)))
+                            N.dev_ptr(aux) if aux is not None else None, *_act(relu))
         N.call('ssseg_conv_igemm_epi', N.dev_ptr(x), N.dev_ptr(w) if w is not None else None, N.dev_ptr(y), dref,
                N.dt_code(x), out_dt, ctypes_ref(ep), N.dev_ptr(ws) if ws is not None else None, nb, N.stream())
 
@@ -282,8 +304,11 @@ class Conv2d(nn.Conv2d, _ConvBase):
 
     def __init__(self, *args, head=False, **kw):
         super().__init__(*args, **kw)
-        if self.groups != 1:
-            raise NotImplementedError('ssseg.nn.Conv2d: grouped/depthwise convolution is not implemented')
+        self._ssseg_dw = self.groups != 1
+        if self._ssseg_dw and not (self.groups == self.in_channels == self.out_channels):
+            raise NotImplementedError('ssseg.nn.Conv2d: grouped convolution other than depthwise is not implemented')
+        if self._ssseg_dw and head:
+            raise NotImplementedError('ssseg.nn.Conv2d: depthwise head')
         if self.padding_mode != 'zeros':
             raise NotImplementedError('ssseg.nn.Conv2d: only zero padding')
         self._ssseg_init(head)
@@ -311,13 +336,55 @@ class Conv2d(nn.Conv2d, _ConvBase):
 
     def forward_relu(self, x):
         """Conv2d followed by ReLU, fused into the GEMM epilogue (unet.py:27-28 with no norm)."""
+        return self.forward_act(x, True)
+
+    def forward_act(self, x, act):
+        """Conv2d followed by an activation (True = ReLU, ACT_RELU6, ('leaky', slope)) in the epilogue
+        (discriminator.py:15-16 Conv + LeakyReLU(0.2))."""
         if not _is_act(x):
             x = to_act(x)
-        return _ConvFn.apply(x, self.weight, self.bias, self, True)
+        return _ConvFn.apply(x, self.weight, self.bias, self, act)
+
+    # ---- depthwise (groups == channels): ssseg_dwconv_* (MobileNetV2, mobilenetv2.py:58) ----
+    def _dw_desc(self, n, H, W):
+        d = self._fwd_desc(n, H, W)
+        d.ldw = d.C
+        return d
+
+    def _dw_pack(self):
+        cin = self._dims()[0]
+        R, S = self.kernel_size
+        return self._pack('dw', 1, 1, self.in_channels, cin, 1, 0, 1, R, 0, 1, S)
+
+    def _dw_forward(self, x, relu, bn, residual, keep_pre):
+        cin, cout = self._dims()
+        n, _, H, W = x.shape
+        d = self._dw_desc(n, H, W)
+        y = new_act(n, cout, d.OH, d.OW, _CFG['dtype'], x.device)
+        aux = bwd = None
+        if bn is not None:
+            _need_res(residual, y)
+            aux = torch.empty_like(y) if keep_pre else None
+            fold, bwd = self._fold(bn, residual, cout, aux)
+        else:
+            fold = (None, self.bias, None, None)
+        scale, shift, res, aux_t = fold
+        code, slope = _act(relu)
+        ep = N.ConvEpilogue(N.dev_ptr(scale) if scale is not None else None,
+                            N.dev_ptr(shift.detach() if shift is not None else None) if shift is not None else None,
+                            N.dev_ptr(res) if res is not None else None, res.shape[1] if res is not None else 0,
+                            N.dev_ptr(aux_t) if aux_t is not None else None, code, slope)
+        R, S = self.kernel_size
+        with _Timed(2.0 * n * d.OH * d.OW * self.in_channels * R * S, 'fwd', _tag(self, n, H, W)):
+            N.call('ssseg_dwconv_fwd', N.dev_ptr(x), N.dev_ptr(self._dw_pack()), N.dev_ptr(y), ctypes_ref(d),
+                   N.dt_code(x), ctypes_ref(ep), N.stream())
+        return (y, aux, bwd) if keep_pre else y
 
     def _ssseg_forward(self, x, relu, bn=None, residual=None, keep_pre=False):
         cin, cout = self._dims()
         _need_act(x, cin, 'Conv2d')
+        if self._ssseg_dw:
+            return self._dw_forward(x, relu, bn, residual, keep_pre)
         n, _, H, W = x.shape
         d = self._fwd_desc(n, H, W)
         R, S = self.kernel_size
@@ -364,6 +431,16 @@ class Conv2d(nn.Conv2d, _ConvBase):
                 _ready(self.bias)
             return
         n, _, H, W = x.shape
+        if self._ssseg_dw:
+            d = self._dw_desc(n, H, W)
+            nb = N.lib().ssseg_dwconv_wgrad_workspace_bytes(ctypes_ref(d), N.dt_code(x))
+            ws = N.workspace(nb, x.device)
+            R, S = self.kernel_size
+            with _Timed(2.0 * n * d.OH * d.OW * self.in_channels * R * S, 'wgrad', _tag(self, n, H, W)):
+                N.call('ssseg_dwconv_wgrad', N.dev_ptr(x), N.dev_ptr(gy), N.dev_ptr(_grad_of(self.weight)),
+                       ctypes_ref(d), N.dt_code(x), self.in_channels, 1, N.dev_ptr(ws), nb, N.stream())
+            _ready(*[p for p in (self.weight, self.bias) if p is not None])
+            return
         d = self._fwd_desc(n, H, W)
         nb = N.lib().ssseg_conv_wgrad_workspace_bytes(ctypes_ref(d), N.dt_code(x))
         ws = N.workspace(nb, x.device)
@@ -382,6 +459,12 @@ class Conv2d(nn.Conv2d, _ConvBase):
         (R, S), (sh, sw), (ph, pw), (dh, dw) = self.kernel_size, self.stride, self.padding, self.dilation
         OH, OW = gy.shape[2], gy.shape[3]
         dx = new_act(n, cin, H, W, _CFG['dtype'], gy.device)
+        if self._ssseg_dw:
+            d = self._dw_desc(n, H, W)
+            with _Timed(2.0 * n * OH * OW * self.in_channels * R * S, 'dgrad', _tag(self, n, H, W)):
+                N.call('ssseg_dwconv_dgrad', N.dev_ptr(gy), N.dev_ptr(self._dw_pack()), N.dev_ptr(dx), ctypes_ref(d),
+                       N.dt_code(gy), N.stream())
+            return dx
         timer = _Timed(_conv_flops(n, OH, OW, self.out_channels, self.in_channels, R, S), 'dgrad', _tag(self, n, H, W))
         if sh == 1 and sw == 1:
             w = self._pack('dgrad', cin, self.in_channels, self.out_channels, cout, 1, R - 1, -1, R, S - 1, -1, S)
@@ -430,7 +513,12 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
 
     def forward_relu(self, x):
         """ConvTranspose2d followed by ReLU, fused into the epilogue (unet.py:20-23)."""
-        return _ConvFn.apply(x, self.weight, self.bias, self, True)
+        return self.forward_act(x, True)
+
+    def forward_act(self, x, act):
+        if not _is_act(x):
+            x = to_act(x)
+        return _ConvFn.apply(x, self.weight, self.bias, self, act)
 
     def _out_hw(self, H, W):
         (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
@@ -550,7 +638,7 @@ class _BNFn(torch.autograd.Function):
         bs = bias.detach() if bias is not None else None
         N.call('ssseg_bn_apply', N.dev_ptr(x), N.dev_ptr(residual) if residual is not None else None, N.dev_ptr(y),
                P, C, cp, cp, cp, N.dev_ptr(mean), N.dev_ptr(invstd), N.dev_ptr(wt) if wt is not None else None,
-               N.dev_ptr(bs) if bs is not None else None, int(bool(relu)), N.dt_code(x), N.stream())
+               N.dev_ptr(bs) if bs is not None else None, _act(relu)[0], N.dt_code(x), N.stream())
         ctx.save_for_backward(x, residual, mean, invstd)
         ctx.mod, ctx.relu, ctx.training, ctx.count = mod, relu, training, count
         return y
@@ -572,7 +660,7 @@ class _BNFn(torch.autograd.Function):
         res_p = N.dev_ptr(residual) if residual is not None else None
         N.call('ssseg_bn_bwd_reduce', N.dev_ptr(gy), N.dev_ptr(x), res_p, P, C, cp, cp, cp, N.dev_ptr(mean),
                N.dev_ptr(invstd), N.dev_ptr(wt) if wt is not None else None,
-               N.dev_ptr(bs) if bs is not None else None, int(bool(ctx.relu)), N.dt_code(x), N.dev_ptr(sums),
+               N.dev_ptr(bs) if bs is not None else None, _act(ctx.relu)[0], N.dt_code(x), N.dev_ptr(sums),
                N.dev_ptr(ws), nb, N.stream())
         if mod.weight is not None and mod.weight.requires_grad:
             N.call('ssseg_bn_param_grad', N.dev_ptr(sums), C, N.dev_ptr(_grad_of(mod.weight)),
@@ -587,7 +675,7 @@ class _BNFn(torch.autograd.Function):
         N.call('ssseg_bn_bwd_apply', N.dev_ptr(gy), N.dev_ptr(x), res_p, N.dev_ptr(dx),
                N.dev_ptr(dres) if dres is not None else None, P, C, cp, cp, cp, cp, N.dev_ptr(mean),
                N.dev_ptr(invstd), N.dev_ptr(wt) if wt is not None else None,
-               N.dev_ptr(bs) if bs is not None else None, int(bool(ctx.relu)), int(bool(ctx.training)),
+               N.dev_ptr(bs) if bs is not None else None, _act(ctx.relu)[0], int(bool(ctx.training)),
                N.dev_ptr(sums), float(count), N.dt_code(x), N.stream())
         return dx, None, None, dres, None, None
 
@@ -638,7 +726,7 @@ class _ConvBNEvalFn(torch.autograd.Function):
         ws = N.workspace(nb, dev)
         N.call('ssseg_bn_eval_bwd', N.dev_ptr(gy), N.dev_ptr(y), N.dev_ptr(aux), N.dev_ptr(dconv),
                N.dev_ptr(dres) if dres is not None else None, n * h * w, C, cp, N.dev_ptr(scale), N.dev_ptr(mean_eff),
-               N.dev_ptr(invstd), int(bool(ctx.relu)), N.dt_code(y), N.dev_ptr(sums), N.dev_ptr(ws), nb, N.stream())
+               N.dev_ptr(invstd), _act(ctx.relu)[0], N.dt_code(y), N.dev_ptr(sums), N.dev_ptr(ws), nb, N.stream())
         want = lambda p: p is not None and p.requires_grad  # noqa: E731
         if want(bn.weight) or want(bn.bias) or want(conv.bias):
             N.call('ssseg_bn_eval_param_grad', N.dev_ptr(sums), C, N.dev_ptr(scale),

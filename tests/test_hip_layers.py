@@ -84,6 +84,34 @@ def test_conv2d_fwd_bwd(hip_device, mode, cin, cout, k, s, p, d, H, W, n):
     _close(xa.grad[:, :cin], xr.grad, mode, 'dx')
 
 
+@pytest.mark.parametrize('C,k,s,p,d,H,W,act', [(24, 3, 1, 1, 1, 9, 11, False), (32, 3, 2, 1, 1, 13, 12, 'relu6'),
+                                                (16, 5, 1, 2, 1, 7, 8, False), (40, 3, 1, 2, 2, 10, 9, 'relu6'),
+                                                (12, 3, 2, 1, 1, 9, 9, False)])
+def test_depthwise_conv_fwd_bwd(hip_device, mode, C, k, s, p, d, H, W, act):
+    """Depthwise conv (MobileNetV2, groups == C) fwd/dgrad/wgrad vs PyTorch fp32, with the fused ReLU6."""
+    from ssseg import nn as snn
+    torch.manual_seed(7)
+    ref = torch.nn.Conv2d(C, C, k, s, p, d, groups=C, bias=False)
+    mod = snn.Conv2d(C, C, k, s, p, d, groups=C, bias=False).to(hip_device)
+    mod.load_state_dict(ref.state_dict())
+    with torch.no_grad():
+        ref.weight.copy_(_q(ref.weight, mode))
+    x = _q(torch.randn(2, C, H, W), mode)
+    xr = x.clone().requires_grad_(True)
+    yr = ref(xr)
+    relu6 = act == 'relu6' and mode == 'f32'   # mask flips at bf16 rounding of 0 / 6 (see the ConvT test)
+    if relu6:
+        yr = torch.clamp(yr, 0, 6)
+    gy = _q(torch.randn_like(yr), mode)
+    yr.backward(gy)
+    xa = _act_in(x, hip_device).detach().requires_grad_(True)
+    y = mod.forward_act(xa, snn.ACT_RELU6) if relu6 else mod(xa)
+    y.backward(_act_in(gy, hip_device))
+    _close(y[:, :C], yr, mode, 'y')
+    _close(mod.weight.grad, ref.weight.grad, mode, 'dW')
+    _close(xa.grad[:, :C], xr.grad, mode, 'dx')
+
+
 @pytest.mark.parametrize('cin,cout,H,W', [(16, 8, 5, 6), (64, 32, 4, 4), (128, 64, 8, 7)])
 def test_conv_transpose_relu(hip_device, mode, cin, cout, H, W):
     from ssseg import nn as snn

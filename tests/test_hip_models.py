@@ -53,6 +53,31 @@ def test_simple_unet_vs_reference_golden(hip_device, f32_mode, tag, up):
             np.testing.assert_allclose(sd[k[6:]].cpu().numpy(), g[k], rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize('tag,up', [('unet_mbv2_t', True), ('unet_mbv2_b', False)])
+def test_unet_mobilenetv2_vs_reference_golden(hip_device, f32_mode, tag, up):
+    """UNet over the MobileNetV2(width 0.35) encoder (depthwise convs, ReLU6, inverted residuals) vs the
+    reference's own outputs (golden G6): eval and train forwards and the BN buffers after train mode."""
+    from models import unet
+    from models.encoders import mobilenetv2
+    g = golden(f'model_{tag}.npz')
+    m = _load(unet.UNet(2, mobilenetv2.mobilenet_v2(width_mult=0.35), 32, train_upsampling=up), g, 'init.', hip_device)
+    x = torch.from_numpy(g['x']).to(hip_device)
+    m.eval()
+    with torch.no_grad():
+        y = m(x)
+    scale = np.abs(g['y_eval']).max()
+    np.testing.assert_allclose(y.cpu().numpy(), g['y_eval'], rtol=0, atol=1e-3 * scale)
+    m.train()
+    with torch.no_grad():
+        y = m(x)
+    scale = np.abs(g['y_train']).max()
+    np.testing.assert_allclose(y.cpu().numpy(), g['y_train'], rtol=0, atol=1e-3 * scale)
+    sd = m.state_dict()
+    for k in g.files:
+        if k.startswith('after.'):
+            np.testing.assert_allclose(sd[k[6:]].cpu().numpy(), g[k], rtol=1e-4, atol=1e-5)
+
+
 def _unet_pair(device, seed=0):
     from models import unet
     from models.encoders import resnet

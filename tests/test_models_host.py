@@ -58,3 +58,18 @@ def test_reference_state_dict_keys_load_into_product():
     ref = models_ref.SimpleUNet(2, 3, 8, 32)
     prod = simple_unet.UNet(2, 3, 8, 32)
     prod.load_state_dict(ref.state_dict(), strict=True)
+
+
+def test_mobilenetv2_encoder_tree_matches_reference_golden():
+    """The drop-in MobileNetV2 encoder has the reference's module tree: the G6 state_dict (made by the
+    reference mobilenetv2.py) loads strictly, endpoint depths match the reference's."""
+    import numpy as np
+    import torch
+    from models import unet
+    from models.encoders import mobilenetv2
+    from conftest import golden
+    g = golden("model_unet_mbv2_t.npz")
+    m = unet.UNet(2, mobilenetv2.mobilenet_v2(width_mult=0.35), 32, train_upsampling=True)
+    sd = {k[5:]: torch.from_numpy(g[k].copy()) for k in g.files if k.startswith('init.')}
+    m.load_state_dict(sd, strict=True)
+    assert m.encoder.endpoint_depths == [8, 8, 16, 32, 112]
