@@ -249,7 +249,7 @@ int ssseg_dwconv_wgrad(const void* x, const void* dy, float* dw, const ssseg_con
 
 /* ---------------------------------------------------------------------------------------------
  * BatchNorm2d / SyncBatchNorm (nn.BatchNorm2d in every ConvBlock, unet.py:9; distributed_trainer.py:36)
- * NHWC [P][ld] activations, C % 4 == 0.  Training: stats -> (all-reduce sums for SyncBN) -> finalize.
+ * NHWC [P][ld] activations, leading dimensions multiples of 4 and >= rup(C, 4) (C itself may be ragged).  Training: stats -> (all-reduce sums for SyncBN) -> finalize.
  * ------------------------------------------------------------------------------------------- */
 size_t ssseg_bn_workspace_bytes(int64_t C);
 /* sums[0:C] = sum_p x, sums[C:2C] = sum_p x^2 (fp64) */
@@ -330,6 +330,45 @@ int ssseg_zero(void* p, size_t bytes, ssseg_stream_t stream);
 int ssseg_act_bwd(const void* gy, const void* y, void* gx, int64_t n, int act, float slope, int dt,
                   ssseg_stream_t stream);
 int ssseg_relu_bwd(const void* gy, const void* y, void* gx, int64_t n, int dt, ssseg_stream_t stream);
+
+
+/* ---------------------------------------------------------------------------------------------
+ * Pooling / elementwise primitives of the C3-C5 model families (csrc/pool.hip)
+ * ------------------------------------------------------------------------------------------- */
+/* nn.AvgPool2d(k, s, p) with PyTorch's defaults (ceil_mode False, count_include_pad True): HarDNet's
+ * AvgPool2d(2, 2) (hardnet.py:157).  NHWC [N][H][W][C], C = physical channels (multiple of 8 bf16 / 4 f32). */
+int ssseg_avgpool_fwd(const void* x, void* y, int64_t N, int64_t H, int64_t W, int64_t C, int64_t OH, int64_t OW,
+                      int64_t k, int64_t s, int64_t p, int dt, ssseg_stream_t stream);
+int ssseg_avgpool_bwd(const void* gy, void* gx, int64_t N, int64_t H, int64_t W, int64_t C, int64_t OH, int64_t OW,
+                      int64_t k, int64_t s, int64_t p, int dt, ssseg_stream_t stream);
+/* nn.AdaptiveAvgPool2d(1) (DeepLabV3 ASPPPooling, torchvision head behind deeplabv3.py:9,43): y[n][c] (pixel
+ * stride ldy) = mean over HW pixels of x[n][p][c] (x pixel stride C).  Deterministic two-pass reduction. */
+size_t ssseg_global_avgpool_workspace_bytes(int64_t N, int64_t HW, int64_t C);
+int ssseg_global_avgpool_fwd(const void* x, void* y, int64_t N, int64_t HW, int64_t C, int64_t ldy, int dt, void* ws,
+                             size_t ws_bytes, ssseg_stream_t stream);
+/* gx[n][p][c] = gy[n][c] / HW (gx pixel stride C, gy row stride ldgy) */
+int ssseg_global_avgpool_bwd(const void* gy, void* gx, int64_t N, int64_t HW, int64_t C, int64_t ldgy, int dt,
+                             ssseg_stream_t stream);
+/* y = act(x_0 + x_1 + ... + x_{n-1}) elementwise over numel (multiple of 8 bf16 / 4 f32, 16-byte aligned
+ * operands), summed left to right in fp32: HRNet TransitionFuse's add chain ending in add_relu
+ * (higher_hrnet.py:473-486).  xs_host: host array of n <= 8 device pointers. */
+int ssseg_add_n(const void* const* xs_host, int n, void* y, int64_t numel, int act, float slope, int dt,
+                ssseg_stream_t stream);
+/* nn.Dropout(p) in training mode (DeepLabV3 ASPP projection): y = u >= p ? x/(1-p) : 0 with u a Philox-4x32-10
+ * uniform of element i (counter offset + i/4, key seed).  The backward is the same call on the output gradient
+ * with the same (seed, offset).  n % 4 == 0. */
+int ssseg_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, uint64_t offset, int dt,
+                  ssseg_stream_t stream);
+/* MultiscaleAttention blend (multiscale_attention.py:52-54), fp32 [N][C][H][W] with arbitrary strides:
+ * out = lo*s + hi*(1-s), s = sigmoid(att[n][0][h][w]); out contiguous NCHW. */
+int ssseg_att_blend_fwd(const float* lo, const int64_t* lo_strides4_host, const float* hi,
+                        const int64_t* hi_strides4_host, const float* att, const int64_t* att_strides4_host, float* out,
+                        int64_t N, int64_t C, int64_t H, int64_t W, ssseg_stream_t stream);
+/* glo = g*s, ghi = g*(1-s), gatt = sum_c g*(lo-hi)*s*(1-s); outputs contiguous NCHW, each may be NULL */
+int ssseg_att_blend_bwd(const float* gout, const int64_t* g_strides4_host, const float* lo,
+                        const int64_t* lo_strides4_host, const float* hi, const int64_t* hi_strides4_host,
+                        const float* att, const int64_t* att_strides4_host, float* glo, float* ghi, float* gatt,
+                        int64_t N, int64_t C, int64_t H, int64_t W, ssseg_stream_t stream);
 
 #ifdef __cplusplus
 }

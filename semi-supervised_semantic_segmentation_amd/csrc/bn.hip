@@ -21,7 +21,10 @@ namespace {
 // registers; it walks pixels with U independent loads in flight.  Channels [C, rup(C, V)) of every
 // output are written as 0 (the NHWC channel padding), so callers need no memset.
 constexpr int U = 4;
-constexpr int CH = 4;   // ABI granularity: C and every leading dimension are multiples of 4
+constexpr int CH = 4;   // ABI granularity: every leading dimension is a multiple of 4 and >= rup(C, 4); C itself
+                        // may be ragged (HarDNet's growth-rate widths 10, 14, 18, ..., hardnet.py:33)
+
+static inline bool ld_bad(int64_t C, int64_t ld) { return ld % CH != 0 || ld < (C + CH - 1) / CH * CH; }
 
 template <typename T, int V> struct Vec;
 template <> struct Vec<float, 4> {
@@ -547,7 +550,7 @@ extern "C" size_t ssseg_bn_workspace_bytes(int64_t C) { return sizeof(double) * 
 
 extern "C" int ssseg_bn_stats(const void* x, int64_t P, int64_t C, int64_t ldx, int dt, double* sums, void* ws,
                               size_t ws_bytes, ssseg_stream_t stream) {
-  if (!x || !sums || P < 1 || C < 1 || C % CH || ldx % CH) return SSSEG_EINVAL;
+  if (!x || !sums || P < 1 || C < 1 || ld_bad(C, ldx)) return SSSEG_EINVAL;
   if (!ws || ws_bytes < ssseg_bn_workspace_bytes(C)) return SSSEG_EWORKSPACE;
   hipStream_t s = (hipStream_t)stream;
   if (dt == SSSEG_BF16)
@@ -620,7 +623,7 @@ extern "C" int ssseg_bn_eval_bwd(const void* dy, const void* y, const void* aux,
                                  int64_t C, int64_t ld, const float* scale, const float* mean_eff, const float* invstd,
                                  int relu, int dt, double* sums, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
   if (!dy || !aux || !dconv || !sums || !scale || !mean_eff || !invstd || (relu && !y) || P < 1 || C < 1 ||
-      C % CH || ld % CH || ld < C)
+      ld_bad(C, ld))
     return SSSEG_EINVAL;
   if (!ws || ws_bytes < ssseg_bn_workspace_bytes(C)) return SSSEG_EWORKSPACE;
   hipStream_t s = (hipStream_t)stream;
@@ -649,7 +652,8 @@ extern "C" int ssseg_bn_eval_param_grad(const double* sums, int64_t C, const flo
 extern "C" int ssseg_bn_apply(const void* x, const void* residual, void* y, int64_t P, int64_t C, int64_t ldx,
                               int64_t ldr, int64_t ldy, const float* mean, const float* invstd, const float* gamma,
                               const float* beta, int relu, int dt, ssseg_stream_t stream) {
-  if (!x || !y || !mean || !invstd || P < 1 || C < 1 || C % CH || ldx % CH || ldy % CH || (residual && ldr % CH))
+  if (!x || !y || !mean || !invstd || P < 1 || C < 1 || ld_bad(C, ldx) || ld_bad(C, ldy) ||
+      (residual && ld_bad(C, ldr)))
     return SSSEG_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const ChanParams prm{mean, invstd, gamma, beta};
@@ -667,7 +671,9 @@ extern "C" int ssseg_bn_bwd_reduce(const void* dy, const void* x, const void* re
                                    int64_t ldx, int64_t ldr, int64_t lddy, const float* mean, const float* invstd,
                                    const float* gamma, const float* beta, int relu, int dt, double* sums, void* ws,
                                    size_t ws_bytes, ssseg_stream_t stream) {
-  if (!dy || !x || !sums || !mean || !invstd || P < 1 || C < 1 || C % CH || ldx % CH || lddy % CH) return SSSEG_EINVAL;
+  if (!dy || !x || !sums || !mean || !invstd || P < 1 || C < 1 || ld_bad(C, ldx) || ld_bad(C, lddy) ||
+      (residual && ld_bad(C, ldr)))
+    return SSSEG_EINVAL;
   if (!ws || ws_bytes < ssseg_bn_workspace_bytes(C)) return SSSEG_EWORKSPACE;
   hipStream_t s = (hipStream_t)stream;
   if (dt == SSSEG_BF16)
@@ -695,7 +701,8 @@ extern "C" int ssseg_bn_bwd_apply(const void* dy, const void* x, const void* res
                                   int64_t C, int64_t ldx, int64_t ldr, int64_t lddy, int64_t lddx, const float* mean,
                                   const float* invstd, const float* gamma, const float* beta, int relu, int train,
                                   const double* sums, double count, int dt, ssseg_stream_t stream) {
-  if (!dy || !x || !dx || !mean || !invstd || P < 1 || C < 1 || C % CH || (train && (!sums || count <= 0)))
+  if (!dy || !x || !dx || !mean || !invstd || P < 1 || C < 1 || ld_bad(C, ldx) || ld_bad(C, lddy) ||
+      ld_bad(C, lddx) || (residual && ld_bad(C, ldr)) || (train && (!sums || count <= 0)))
     return SSSEG_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const ChanParams prm{mean, invstd, gamma, beta};

@@ -79,6 +79,16 @@ SIGS = {
     'ssseg_zero': (i32, [vp, sz, vp]),
     'ssseg_act_bwd': (i32, [vp, vp, vp, i64, i32, f32, i32, vp]),
     'ssseg_relu_bwd': (i32, [vp, vp, vp, i64, i32, vp]),
+    # pooling / elementwise primitives of the C3-C5 model families (csrc/pool.hip)
+    'ssseg_avgpool_fwd': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, i32, vp]),
+    'ssseg_avgpool_bwd': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, i32, vp]),
+    'ssseg_global_avgpool_workspace_bytes': (sz, [i64, i64, i64]),
+    'ssseg_global_avgpool_fwd': (i32, [vp, vp, i64, i64, i64, i64, i32, vp, sz, vp]),
+    'ssseg_global_avgpool_bwd': (i32, [vp, vp, i64, i64, i64, i64, i32, vp]),
+    'ssseg_add_n': (i32, [ctypes.POINTER(ctypes.c_void_p), i32, vp, i64, i32, f32, i32, vp]),
+    'ssseg_dropout': (i32, [vp, vp, i64, f32, u64, u64, i32, vp]),
+    'ssseg_att_blend_fwd': (i32, [vp, I64P, vp, I64P, vp, I64P, vp, i64, i64, i64, i64, vp]),
+    'ssseg_att_blend_bwd': (i32, [vp, I64P, vp, I64P, vp, I64P, vp, I64P, vp, vp, vp, i64, i64, i64, i64, vp]),
 }
 
 

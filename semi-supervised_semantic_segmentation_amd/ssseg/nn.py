@@ -929,3 +929,227 @@ def invalidate_packed(model):
             cache[dt] = ent
         N.call('ssseg_weight_pack_batch', N.dev_ptr(ent[1]), len(rr), N.dt_code(torch.empty((), dtype=dt)),
                N.stream())
+
+
+# ------------------------------------------------------------------------------------------------
+# primitives of the C3-C5 model families: n-way concat, average pooling, activation-layout bilinear
+# resize, n-ary add(+act), dropout (HarDNet, DeepLabV3, HRNet / MultiscaleAttention)
+# ------------------------------------------------------------------------------------------------
+class _CatNFn(torch.autograd.Function):
+    """torch.cat(tensors, 1) of same-size NHWC activations with REAL channel counts `chans` (hardnet.py:67,78,
+    95; higher_hrnet.py:1033; discriminator.py:56): the result packs the real channels densely, padding to the
+    MFMA vector is zero.  Backward slices the gradient back out (zero padding in every slice)."""
+
+    @staticmethod
+    def forward(ctx, chans, *ts):
+        n, _, H, W = ts[0].shape
+        for t in ts:
+            if t.shape[0] != n or t.shape[2] != H or t.shape[3] != W:
+                raise ValueError(f'cat_n: spatial shapes differ: {[tuple(t.shape) for t in ts]}')
+        total = sum(chans)
+        cp = rup(total, vec())
+        y = new_act(n, cp, H, W, ts[0].dtype, ts[0].device, zero=cp != total)
+        c0 = 0
+        for t, c in zip(ts, chans):
+            N.call('ssseg_nhwc_copy', N.dev_ptr(t), N.dev_ptr(y) + c0 * y.element_size(), n, H, W, c, H, W, t.shape[1],
+                   0, 0, H, W, cp, 0, 0, N.dt_code(t), N.stream())
+            c0 += c
+        ctx.meta = (tuple(t.shape[1] for t in ts), tuple(chans), cp)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        phys, chans, cp = ctx.meta
+        n, _, H, W = gy.shape
+        out, c0 = [None], 0
+        for pc, c in zip(phys, chans):
+            g = new_act(n, pc, H, W, gy.dtype, gy.device, zero=pc != c)
+            N.call('ssseg_nhwc_copy', N.dev_ptr(gy) + c0 * gy.element_size(), N.dev_ptr(g), n, H, W, c, H, W, cp, 0, 0,
+                   H, W, pc, 0, 0, N.dt_code(gy), N.stream())
+            out.append(g)
+            c0 += c
+        return tuple(out)
+
+
+def cat_n(tensors, chans):
+    """Concatenate NHWC activations along channels; chans[i] = real channel count of tensors[i]."""
+    for t in tensors:
+        _need_act(t, None, 'cat_n')
+    if len(tensors) == 1:
+        return tensors[0]
+    return _CatNFn.apply(tuple(int(c) for c in chans), *tensors)
+
+
+class _AvgPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        n, c, h, w = x.shape
+        oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+        y = new_act(n, c, oh, ow, x.dtype, x.device)
+        N.call('ssseg_avgpool_fwd', N.dev_ptr(x), N.dev_ptr(y), n, h, w, c, oh, ow, k, s, p, N.dt_code(x), N.stream())
+        ctx.meta = (n, c, h, w, oh, ow, k, s, p, x.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        n, c, h, w, oh, ow, k, s, p, dt = ctx.meta
+        _need_act(gy, c, 'AvgPool2d backward')
+        gx = new_act(n, c, h, w, dt, gy.device)
+        N.call('ssseg_avgpool_bwd', N.dev_ptr(gy), N.dev_ptr(gx), n, h, w, c, oh, ow, k, s, p, N.dt_code(gy),
+               N.stream())
+        return gx, None, None, None
+
+
+def _int1(v):
+    return v if isinstance(v, int) else v[0]
+
+
+class AvgPool2d(nn.AvgPool2d):
+    """nn.AvgPool2d (HarDNet's AvgPool2d(2, 2), hardnet.py:157) on NHWC activations."""
+
+    def forward(self, x):
+        if self.ceil_mode or not self.count_include_pad or self.divisor_override is not None:
+            raise NotImplementedError('ssseg AvgPool2d: ceil_mode / count_include_pad=False / divisor_override')
+        k, s, p = _int1(self.kernel_size), _int1(self.stride if self.stride is not None else self.kernel_size), \
+            _int1(self.padding)
+        _need_act(x, None, 'AvgPool2d')
+        return _AvgPoolFn.apply(x, k, s, p)
+
+
+class _GAPFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        n, c, h, w = x.shape
+        y = new_act(n, c, 1, 1, x.dtype, x.device)
+        nb = N.lib().ssseg_global_avgpool_workspace_bytes(n, h * w, c)
+        ws = N.workspace(nb, x.device)
+        N.call('ssseg_global_avgpool_fwd', N.dev_ptr(x), N.dev_ptr(y), n, h * w, c, c, N.dt_code(x), N.dev_ptr(ws), nb,
+               N.stream())
+        ctx.meta = (n, c, h, w, x.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        n, c, h, w, dt = ctx.meta
+        gx = new_act(n, c, h, w, dt, gy.device)
+        gyc = gy if gy.is_contiguous(memory_format=torch.channels_last) else gy.contiguous(memory_format=torch.channels_last)
+        N.call('ssseg_global_avgpool_bwd', N.dev_ptr(gyc), N.dev_ptr(gx), n, h * w, c, c, N.dt_code(gy), N.stream())
+        return gx
+
+
+def global_avgpool(x):
+    """nn.AdaptiveAvgPool2d(1) on an NHWC activation -> [N, Cp, 1, 1] activation (ASPPPooling)."""
+    _need_act(x, None, 'AdaptiveAvgPool2d(1)')
+    return _GAPFn.apply(x)
+
+
+class AdaptiveAvgPool2d(nn.AdaptiveAvgPool2d):
+    def forward(self, x):
+        if self.output_size not in (1, (1, 1)):
+            raise NotImplementedError('ssseg AdaptiveAvgPool2d: output size 1 only')
+        return global_avgpool(x)
+
+
+class _ActBilinear(torch.autograd.Function):
+    """F.interpolate(mode='bilinear') between NHWC activations (always channels_last in and out, including
+    1x1 maps): HarDNet TransitionUp (hardnet.py:88), HRNet fuse / aggregation (higher_hrnet.py:454,1030),
+    ASPPPooling's broadcast back to the feature size."""
+
+    @staticmethod
+    def forward(ctx, x, size, align_corners):
+        n, c, h, w = x.shape
+        oh, ow = int(size[0]), int(size[1])
+        y = new_act(n, c, oh, ow, x.dtype, x.device)
+        N.call('ssseg_bilinear_fwd', N.dev_ptr(x), N.dev_ptr(y), n, c, h, w, oh, ow, N.strides4(x), N.strides4(y),
+               int(bool(align_corners)), N.dt_code(x), N.stream())
+        ctx.meta = (n, c, h, w, oh, ow, bool(align_corners), x.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        n, c, h, w, oh, ow, ac, dt = ctx.meta
+        gx = new_act(n, c, h, w, dt, gy.device)
+        N.call('ssseg_bilinear_bwd', N.dev_ptr(gy), N.dev_ptr(gx), n, c, h, w, oh, ow, N.strides4(gy), N.strides4(gx),
+               int(ac), N.dt_code(gy), N.stream())
+        return gx, None, None
+
+
+def resize_act(x, size, align_corners=False):
+    """Bilinear resize of an NHWC activation; same-size resizes are the identity (PyTorch's kernel copies)."""
+    _need_act(x, None, 'bilinear resize')
+    if (x.shape[2], x.shape[3]) == (int(size[0]), int(size[1])):
+        return x
+    return _ActBilinear.apply(x, tuple(int(v) for v in size), bool(align_corners))
+
+
+class _AddNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, act, *ts):
+        import ctypes
+        code, slope = _act(act)
+        y = torch.empty_like(ts[0])
+        ptrs = (ctypes.c_void_p * len(ts))(*[N.dev_ptr(t) for t in ts])
+        N.call('ssseg_add_n', ptrs, len(ts), N.dev_ptr(y), y.numel(), code, slope, N.dt_code(y), N.stream())
+        ctx.code, ctx.slope, ctx.n = code, slope, len(ts)
+        ctx.save_for_backward(y if code else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (y,) = ctx.saved_tensors
+        if ctx.code:
+            g = torch.empty_like(gy)
+            N.call('ssseg_act_bwd', N.dev_ptr(gy), N.dev_ptr(y), N.dev_ptr(g), gy.numel(), ctx.code, ctx.slope,
+                   N.dt_code(gy), N.stream())
+        else:
+            g = gy
+        return (None,) + (g,) * ctx.n
+
+
+def add_act(tensors, act=False):
+    """act(t0 + t1 + ... ) over same-shape NHWC activations in one pass (higher_hrnet.py:473-486)."""
+    if len(tensors) > 8:
+        return add_act([add_act(tensors[:8], False)] + list(tensors[8:]), act)
+    for t in tensors:
+        if not _is_act(t) or t.shape != tensors[0].shape:
+            raise ValueError(f'add_act: operands must be matching activations: {[tuple(t.shape) for t in tensors]}')
+    if len(tensors) == 1 and not _act(act)[0]:
+        return tensors[0]
+    return _AddNFn.apply(act, *tensors)
+
+
+_DROP = {'seed': None, 'offset': 0}
+
+
+class _DropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p):
+        if _DROP['seed'] is None:
+            _DROP['seed'] = int(torch.randint(0, 2 ** 62, (1,)).item())
+        seed, off = _DROP['seed'], _DROP['offset']
+        _DROP['offset'] += (x.numel() + 3) // 4 + 1
+        y = torch.empty_like(x)
+        N.call('ssseg_dropout', N.dev_ptr(x), N.dev_ptr(y), x.numel(), float(p), seed, off, N.dt_code(x), N.stream())
+        ctx.meta = (float(p), seed, off)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        p, seed, off = ctx.meta
+        gyc = gy if gy.is_contiguous(memory_format=torch.channels_last) else gy.contiguous(memory_format=torch.channels_last)
+        gx = torch.empty_like(gyc)
+        N.call('ssseg_dropout', N.dev_ptr(gyc), N.dev_ptr(gx), gyc.numel(), p, seed, off, N.dt_code(gy), N.stream())
+        return gx, None
+
+
+class Dropout(nn.Dropout):
+    """nn.Dropout on NHWC activations (DeepLabV3 ASPP projection, torchvision): a counter-based Philox mask
+    regenerated in backward (nothing stored).  Identity in eval mode or with p == 0, like PyTorch."""
+
+    def forward(self, x):
+        if not self.training or self.p == 0:
+            return x
+        _need_act(x, None, 'Dropout')
+        if x.numel() % 4:
+            raise ValueError('ssseg Dropout: element count must be a multiple of 4')
+        return _DropoutFn.apply(x, self.p)

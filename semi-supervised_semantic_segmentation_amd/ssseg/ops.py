@@ -204,3 +204,41 @@ def lovasz_binary(logits, target, valid_weighted=True):
     if not valid_weighted:
         raise NotImplementedError('lovasz_softmax without the valid-sample weighting')
     return _Lovasz.apply(logits, target)
+
+
+# ------------------------------------------------------------------------------------------------
+# Multi-scale attention blend (multiscale_attention.py:52-54)
+# ------------------------------------------------------------------------------------------------
+class _AttBlend(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, lo, hi, att):
+        Nn, C, H, W = hi.shape
+        if tuple(lo.shape) != (Nn, C, H, W) or tuple(att.shape) != (Nn, 1, H, W):
+            raise ValueError(f'att_blend: shapes {tuple(lo.shape)} {tuple(hi.shape)} {tuple(att.shape)}')
+        for t, n in ((lo, 'lo'), (hi, 'hi'), (att, 'att')):
+            if t.dtype != torch.float32:
+                raise RuntimeError(f'att_blend: {n} must be fp32')
+        out = torch.empty((Nn, C, H, W), device=hi.device, dtype=torch.float32)
+        N.call('ssseg_att_blend_fwd', N.dev_ptr(lo, 'lo'), N.strides4(lo), N.dev_ptr(hi, 'hi'), N.strides4(hi),
+               N.dev_ptr(att, 'att'), N.strides4(att), N.dev_ptr(out), Nn, C, H, W, N.stream())
+        ctx.save_for_backward(lo, hi, att)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        lo, hi, att = ctx.saved_tensors
+        Nn, C, H, W = hi.shape
+        g = g.float()
+        glo = torch.empty((Nn, C, H, W), device=g.device, dtype=torch.float32) if ctx.needs_input_grad[0] else None
+        ghi = torch.empty((Nn, C, H, W), device=g.device, dtype=torch.float32) if ctx.needs_input_grad[1] else None
+        gat = torch.empty((Nn, 1, H, W), device=g.device, dtype=torch.float32) if ctx.needs_input_grad[2] else None
+        N.call('ssseg_att_blend_bwd', N.dev_ptr(g), N.strides4(g), N.dev_ptr(lo), N.strides4(lo), N.dev_ptr(hi),
+               N.strides4(hi), N.dev_ptr(att), N.strides4(att), N.dev_ptr(glo), N.dev_ptr(ghi), N.dev_ptr(gat), Nn, C,
+               H, W, N.stream())
+        return glo, ghi, gat
+
+
+def att_blend(lo, hi, att_logits):
+    """lo*sigmoid(a) + hi*(1-sigmoid(a)) (MultiscaleAttention, multiscale_attention.py:52-54); fp32 NCHW
+    tensors of any strides, att [N,1,H,W] pre-sigmoid; returns contiguous NCHW."""
+    return _AttBlend.apply(lo, hi, att_logits)

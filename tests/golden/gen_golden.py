@@ -15,8 +15,11 @@ Fixture index:
   G5  ema.npz           update_ema_variables                              (reference/mean_teacher.py:5-18)
   G6  model_*.npz       SimpleUNet / UNet(MobileNetV2) forwards            (reference/models/*.py)
   G7  trainsteps.npz    3 steps of train.train on a tiny SimpleUNet (DDP, gloo world 1)
+  G6b model2_*.npz      HarDNet / Discriminator / MultiscaleFeatureDiscriminator / MultiscaleAttention(HRNet)
+                        forwards (eval + train), input + selected parameter gradients, BN buffers; weights are
+                        seeded (tests/seeded.py) and pinned by a state_dict SHA-256 instead of stored
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py [all | models2]
 """
 import os
 import sys
@@ -329,7 +332,92 @@ def gen_trainsteps():
          **init, **final_s, **final_t)
 
 
+# ----------------------------------------------------------------------------------------------
+# G6b: the C3-C5 model families (seeded weights + SHA; inputs, outputs, gradients)
+# ----------------------------------------------------------------------------------------------
+def _yacs_shim():
+    """higher_hrnet.py:23 imports yacs (absent here): a dict with attribute access is all it uses."""
+    class CfgNode(dict):
+        def __getattr__(self, k):
+            try:
+                return self[k]
+            except KeyError:
+                raise AttributeError(k)
+
+        def __setattr__(self, k, v):
+            self[k] = v
+    yacs = types.ModuleType('yacs')
+    cfgmod = types.ModuleType('yacs.config')
+    cfgmod.CfgNode = CfgNode
+    yacs.config = cfgmod
+    sys.modules.setdefault('yacs', yacs)
+    sys.modules.setdefault('yacs.config', cfgmod)
+
+
+def gen_models2():
+    sys.path.insert(0, os.path.dirname(OUT))      # tests/ (seeded.py)
+    import seeded
+    _yacs_shim()
+    from functools import partial
+    from models import discriminator, hardnet, higher_hrnet, multiscale_attention
+
+    def msa():
+        return multiscale_attention.MultiscaleAttention(
+            partial(higher_hrnet.get_pose_net, cfg=higher_hrnet.POSE_HIGHER_RESOLUTION_NET), 480, 2)
+
+    specs = [
+        # tag, ctor, seed, input shapes, conv re-init, parameter grads to store
+        ('hardnet', lambda: hardnet.HarDNet(n_classes=2), 61, [(2, 3, 128, 128)], None,
+         ['base.0.conv.weight', 'base.4.layers.1.conv.weight', 'denseBlocksUp.4.layers.3.conv.weight',
+          'finalConv.weight', 'finalConv.bias', 'base.0.norm.weight']),
+        ('disc', lambda: discriminator.Discriminator(5, 2, 64, 512, 1), 62, [(2, 2, 64, 64)], None,
+         ['net.0.0.weight', 'net.0.0.bias', 'net.1.0.weight', 'net.4.0.bias', 'net.5.0.weight']),
+        ('msdisc', lambda: discriminator.MultiscaleFeatureDiscriminator([8, 16, 32, 64], [16, 32, 64, 128, 1]), 63,
+         [(2, 8, 32, 32), (2, 16, 16, 16), (2, 32, 8, 8), (2, 64, 4, 4)], None, 'all'),
+        ('msa_hrnet', msa, 64, [(2, 3, 128, 128)], 'he',
+         ['model.stem.conv1.weight', 'model.stage3.mods.0.fuse_module.fuse_layers.2.0.0.conv.weight',
+          'model.cls_head.2.weight', 'model.cls_head.2.bias', 'attention_head.0.bn.weight',
+          'attention_head.2.weight', 'model.stage4.mods.2.branches.3.1.bn2.weight']),
+    ]
+    for tag, ctor, seed, shapes, conv_std, grad_names in specs:
+        torch.manual_seed(seed)
+        m = ctor()
+        seeded.perturb(m, seed + 1000, conv_std)
+        sha = seeded.state_sha(m)
+        g = torch.Generator().manual_seed(seed + 2000)
+        xs = [torch.rand(*s, generator=g) for s in shapes]
+        arg = xs if len(xs) > 1 else xs[0]
+
+        def logits(out):
+            return out[1][-1] if isinstance(out, tuple) else out
+        m.eval()
+        with torch.no_grad():
+            y_eval = logits(m(arg)).clone()
+        m.train()
+        for x in xs:
+            x.requires_grad_(True)
+        y_train = logits(m(arg))
+        gy = torch.randn(y_train.shape, generator=g)
+        (y_train * gy).sum().backward()
+        params = dict(m.named_parameters())
+        names = list(params) if grad_names == 'all' else grad_names
+        d = dict(seed=seed, sha=np.asarray(sha), y_eval=y_eval, y_train=y_train.detach(), gy=gy,
+                 n_inputs=len(xs))
+        for i, x in enumerate(xs):
+            d[f'x{i}'] = x.detach()
+            d[f'xgrad{i}'] = x.grad
+        for n in names:
+            d['grad.' + n] = params[n].grad
+        for k, v in m.state_dict().items():
+            if 'running' in k or 'num_batches' in k:
+                d['after.' + k] = v
+        save(f'model2_{tag}.npz', **d)
+
+
 if __name__ == '__main__':
+    if len(sys.argv) > 1 and sys.argv[1] == 'models2':
+        gen_models2()
+        sys.exit(0)
     gen_cowmix()
     gen_mix()
     gen_consistency()
@@ -337,3 +425,4 @@ if __name__ == '__main__':
     gen_ema()
     gen_models()
     gen_trainsteps()
+    gen_models2()
