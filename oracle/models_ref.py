@@ -293,3 +293,117 @@ def load_state(module, arrays, prefix):
     sd = {k[len(prefix):]: torch.from_numpy(arrays[k].copy()) for k in arrays.files if k.startswith(prefix)}
     module.load_state_dict(sd, strict=True)
     return module
+
+
+# ---------------------------------------------------------------------------------------------
+# DeepLabV3 / FCN over dilated ResNets (deeplabv3.py:8-108 -> torchvision v0.5.0 layout, restated;
+# torchvision is absent here: parity against the reference unpinned)
+# ---------------------------------------------------------------------------------------------
+class TVBottleneck(nn.Module):
+    def __init__(self, inplanes, planes, stride=1, downsample=None, dilation=1):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride, padding=dilation, dilation=dilation, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+
+    def forward(self, x):
+        idn = x if self.downsample is None else self.downsample(x)
+        y = self.relu(self.bn1(self.conv1(x)))
+        y = self.relu(self.bn2(self.conv2(y)))
+        return self.relu(self.bn3(self.conv3(y)) + idn)
+
+
+class DilatedResNet(nn.Module):
+    def __init__(self, layers, dilate=(False, True, True)):
+        super().__init__()
+        self.inplanes, self.dilation = 64, 1
+        self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(3, 2, 1)
+        self.layer1 = self._layer(64, layers[0])
+        self.layer2 = self._layer(128, layers[1], 2, dilate[0])
+        self.layer3 = self._layer(256, layers[2], 2, dilate[1])
+        self.layer4 = self._layer(512, layers[3], 2, dilate[2])
+
+    def _layer(self, planes, blocks, stride=1, dilate=False):
+        prev = self.dilation
+        if dilate:
+            self.dilation *= stride
+            stride = 1
+        down = None
+        if stride != 1 or self.inplanes != planes * 4:
+            down = nn.Sequential(nn.Conv2d(self.inplanes, planes * 4, 1, stride, bias=False), nn.BatchNorm2d(planes * 4))
+        layers = [TVBottleneck(self.inplanes, planes, stride, down, prev)]
+        self.inplanes = planes * 4
+        layers += [TVBottleneck(self.inplanes, planes, dilation=self.dilation) for _ in range(1, blocks)]
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        return {'out': self.layer4(self.layer3(self.layer2(self.layer1(x))))}
+
+
+class ASPPPooling(nn.Sequential):
+    def __init__(self, cin, cout):
+        super().__init__(nn.AdaptiveAvgPool2d(1), nn.Conv2d(cin, cout, 1, bias=False), nn.BatchNorm2d(cout), nn.ReLU())
+
+    def forward(self, x):
+        size = x.shape[-2:]
+        for m in self:
+            x = m(x)
+        return F.interpolate(x, size=size, mode='bilinear', align_corners=False)
+
+
+class ASPP(nn.Module):
+    def __init__(self, cin, rates, cout=256):
+        super().__init__()
+        mods = [nn.Sequential(nn.Conv2d(cin, cout, 1, bias=False), nn.BatchNorm2d(cout), nn.ReLU())]
+        for r in rates:
+            mods.append(nn.Sequential(nn.Conv2d(cin, cout, 3, padding=r, dilation=r, bias=False), nn.BatchNorm2d(cout),
+                                      nn.ReLU()))
+        mods.append(ASPPPooling(cin, cout))
+        self.convs = nn.ModuleList(mods)
+        self.project = nn.Sequential(nn.Conv2d(len(mods) * cout, cout, 1, bias=False), nn.BatchNorm2d(cout), nn.ReLU(),
+                                     nn.Dropout(0.5))
+
+    def forward(self, x):
+        return self.project(torch.cat([c(x) for c in self.convs], 1))
+
+
+def deeplab_head(cin, num_classes):
+    return nn.Sequential(ASPP(cin, [12, 24, 36]), nn.Conv2d(256, 256, 3, padding=1, bias=False), nn.BatchNorm2d(256),
+                         nn.ReLU(), nn.Conv2d(256, num_classes, 1))
+
+
+def fcn_head(cin, num_classes):
+    return nn.Sequential(nn.Conv2d(cin, cin // 4, 3, padding=1, bias=False), nn.BatchNorm2d(cin // 4), nn.ReLU(),
+                         nn.Dropout(0.1), nn.Conv2d(cin // 4, num_classes, 1))
+
+
+class SegModel(nn.Module):
+    def __init__(self, backbone, classifier):
+        super().__init__()
+        self.backbone = backbone
+        self.classifier = classifier
+
+    def forward(self, x):                                    # deeplabv3.py:28-36
+        y = self.classifier(self.backbone(x)['out'])
+        return F.interpolate(y, size=x.shape[-2:], mode='bilinear', align_corners=False)
+
+
+def deeplabv3_resnet101(num_classes):
+    return SegModel(DilatedResNet([3, 4, 23, 3]), deeplab_head(2048, num_classes))
+
+
+def deeplabv3_resnet50(num_classes):
+    return SegModel(DilatedResNet([3, 4, 6, 3]), deeplab_head(2048, num_classes))
+
+
+def fcn_resnet50(num_classes):
+    return SegModel(DilatedResNet([3, 4, 6, 3]), fcn_head(2048, num_classes))

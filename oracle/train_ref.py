@@ -17,12 +17,38 @@ import torch.nn.functional as F
 from . import cowmix_ref
 
 
-def calculate_loss(pred_list, target, weights=(0.5,)):
-    """CalculateLoss([{'loss_fn': DenseBinaryCrossEntropyLossWithLogits('mean'), 'weight': weights}])."""
+class _Lovasz(torch.autograd.Function):
+    """binary_lovasz_loss_with_logits (losses.py:239-250) on the CPU through the numpy restatement
+    (losses_ref.binary_lovasz, pinned by golden G4)."""
+
+    @staticmethod
+    def forward(ctx, logits, target):
+        from . import losses_ref
+        loss, grad = losses_ref.binary_lovasz(logits.detach().numpy(), target.detach().numpy())
+        ctx.save_for_backward(torch.from_numpy(grad))
+        return torch.tensor(float(loss), dtype=torch.float32)
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        return grad * g, None
+
+
+def lovasz_loss(pred, target):
+    return _Lovasz.apply(pred, target)
+
+
+def bce_loss(pred, target):
+    return F.binary_cross_entropy_with_logits(pred, target, reduction='mean')
+
+
+def calculate_loss(pred_list, target, weights=(0.5,), loss_fn=None):
+    """CalculateLoss([{'loss_fn': f, 'weight': weights}]) (losses.py:15-22); f = BCE-with-logits by default."""
+    loss_fn = loss_fn or bce_loss
     loss = 0
     for i, p in enumerate(pred_list):
         p = F.interpolate(p, size=(target.size(2), target.size(3)), mode='bilinear', align_corners=False)
-        loss = loss + F.binary_cross_entropy_with_logits(p, target, reduction='mean') * weights[i]
+        loss = loss + loss_fn(p, target) * weights[i]
     return loss
 
 
@@ -50,7 +76,7 @@ def ema_update(model, ema_model, alpha):
 
 
 def train_epoch(model, ema_model, optimizer, batches, unsup_iter, epoch, cfg, loss_weights=(0.5,),
-                on_step=None):
+                on_step=None, loss_fn=None):
     """Run len(batches) steps; returns per-step dict(sup_loss, unsup_loss, cm_mean)."""
     tc = cfg
     model.train()
@@ -58,7 +84,7 @@ def train_epoch(model, ema_model, optimizer, batches, unsup_iter, epoch, cfg, lo
     logs = []
     for step, (image, mask) in enumerate(batches):
         _, preds = model(image)
-        sup = calculate_loss(preds, mask, loss_weights)
+        sup = calculate_loss(preds, mask, loss_weights, loss_fn)
         (sup / tc['virtual_batch_size_multiplier']).backward()
         rec = dict(sup_loss=float(sup.detach()))
         if tc['use_semi_supervised']:

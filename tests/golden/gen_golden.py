@@ -354,6 +354,10 @@ def _yacs_shim():
     sys.modules.setdefault('yacs.config', cfgmod)
 
 
+def sha_of(t):
+    return hashlib.sha256(np.ascontiguousarray(t.detach().cpu().numpy()).tobytes()).hexdigest()
+
+
 def gen_models2():
     sys.path.insert(0, os.path.dirname(OUT))      # tests/ (seeded.py)
     import seeded
@@ -367,7 +371,7 @@ def gen_models2():
 
     specs = [
         # tag, ctor, seed, input shapes, conv re-init, parameter grads to store
-        ('hardnet', lambda: hardnet.HarDNet(n_classes=2), 61, [(2, 3, 128, 128)], None,
+        ('hardnet', lambda: hardnet.HarDNet(n_classes=2), 61, [(2, 3, 256, 256)], None,
          ['base.0.conv.weight', 'base.4.layers.1.conv.weight', 'denseBlocksUp.4.layers.3.conv.weight',
           'finalConv.weight', 'finalConv.bias', 'base.0.norm.weight']),
         ('disc', lambda: discriminator.Discriminator(5, 2, 64, 512, 1), 62, [(2, 2, 64, 64)], None,
@@ -390,24 +394,40 @@ def gen_models2():
 
         def logits(out):
             return out[1][-1] if isinstance(out, tuple) else out
-        m.eval()
-        with torch.no_grad():
-            y_eval = logits(m(arg)).clone()
-        m.train()
-        for x in xs:
-            x.requires_grad_(True)
-        y_train = logits(m(arg))
-        gy = torch.randn(y_train.shape, generator=g)
-        (y_train * gy).sum().backward()
-        params = dict(m.named_parameters())
-        names = list(params) if grad_names == 'all' else grad_names
-        d = dict(seed=seed, sha=np.asarray(sha), y_eval=y_eval, y_train=y_train.detach(), gy=gy,
-                 n_inputs=len(xs))
-        for i, x in enumerate(xs):
-            d[f'x{i}'] = x.detach()
-            d[f'xgrad{i}'] = x.grad
-        for n in names:
-            d['grad.' + n] = params[n].grad
+        import copy
+        m64 = copy.deepcopy(m).double()      # the same network in fp64: the yardstick for fp32 rounding
+        d = dict(seed=seed, sha=np.asarray(sha), n_inputs=len(xs))
+        gy = None
+        for net, suf, dt in ((m, '', torch.float32), (m64, '64', torch.float64)):
+            xin = [x.clone().to(dt) for x in xs]
+            a = xin if len(xin) > 1 else xin[0]
+            net.eval()
+            with torch.no_grad():
+                d['y_eval' + suf] = logits(net(a)).clone()
+            net.train()
+            for x in xin:
+                x.requires_grad_(True)
+            y_train = logits(net(a))
+            if gy is None:
+                gy = torch.randn(y_train.shape, generator=g)
+            (y_train * gy.to(dt)).sum().backward()
+            d['y_train' + suf] = y_train.detach()
+            params = dict(net.named_parameters())
+            names = list(params) if grad_names == 'all' else grad_names
+            for i, x in enumerate(xin):     # large inputs are regenerated from the seed in the test (SHA-checked)
+                d[f'shape{i}'] = np.array(xs[i].shape)
+                if xs[i].numel() <= 200_000:
+                    d[f'x{i}'] = xs[i]
+                    d[f'xgrad{i}' + suf] = x.grad
+                else:
+                    d[f'x{i}_sha'] = np.asarray(sha_of(xs[i]))
+            for n in names:
+                d[f'grad{suf}.' + n] = params[n].grad
+        if gy.numel() <= 200_000:
+            d['gy'] = gy
+        else:
+            d['gy_sha'] = np.asarray(sha_of(gy))
+        d = {k: (v.float() if isinstance(v, torch.Tensor) and v.dtype == torch.float64 else v) for k, v in d.items()}
         for k, v in m.state_dict().items():
             if 'running' in k or 'num_batches' in k:
                 d['after.' + k] = v

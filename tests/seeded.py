@@ -32,3 +32,7 @@ def state_sha(model):
         h.update(k.encode())
         h.update(np.ascontiguousarray(v.detach().cpu().numpy()).tobytes())
     return h.hexdigest()
+
+
+def array_sha(t):
+    return hashlib.sha256(np.ascontiguousarray(t.detach().cpu().numpy()).tobytes()).hexdigest()

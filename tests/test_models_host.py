@@ -73,3 +73,47 @@ def test_mobilenetv2_encoder_tree_matches_reference_golden():
     sd = {k[5:]: torch.from_numpy(g[k].copy()) for k in g.files if k.startswith('init.')}
     m.load_state_dict(sd, strict=True)
     assert m.encoder.endpoint_depths == [8, 8, 16, 32, 112]
+
+
+@pytest.mark.parametrize('tag', ['hardnet', 'disc', 'msdisc', 'msa_hrnet'])
+def test_c345_model_trees_reproduce_reference_weights(tag):
+    """HarDNet / discriminators / MultiscaleAttention(HRNet): the same seed gives bit-identical weights to the
+    reference's module tree (state_dict SHA-256 from golden G6b) — names, shapes, construction and init order."""
+    import seeded
+    from conftest import golden
+    from test_hip_models_c345 import _ctor
+    g = golden(f'model2_{tag}.npz')
+    ctor, conv_std = _ctor(tag)
+    torch.manual_seed(int(g['seed']))
+    m = ctor()
+    seeded.perturb(m, int(g['seed']) + 1000, conv_std)
+    assert seeded.state_sha(m) == str(g['sha'])
+
+
+def test_c345_parameter_counts_match_survey():
+    from functools import partial
+    from models import hardnet, higher_hrnet, multiscale_attention
+    msa = multiscale_attention.MultiscaleAttention(
+        partial(higher_hrnet.get_pose_net, cfg=higher_hrnet.POSE_HIGHER_RESOLUTION_NET), 480, 2)
+    assert abs(sum(p.numel() for p in msa.parameters()) / 1e6 - 20.31) < 0.005      # SURVEY §8: 20.31 M
+    assert abs(sum(p.numel() for p in hardnet.HarDNet(n_classes=2).parameters()) / 1e6 - 4.31) < 0.005
+
+
+@pytest.mark.parametrize('fn', ['deeplabv3_resnet101', 'deeplabv3_resnet50', 'fcn_resnet50'])
+def test_deeplab_names_match_oracle(fn):
+    from models import deeplabv3
+    prod, ref = getattr(deeplabv3, fn)(2), getattr(models_ref, fn)(2)
+    assert _sd_shapes(prod) == _sd_shapes(ref)
+    assert list(inspect.signature(getattr(deeplabv3, fn)).parameters)[0] == 'num_classes'
+
+
+def test_deeplabv3_r101_params_and_flops_match_survey():
+    from torch.utils.flop_counter import FlopCounterMode
+    ref = models_ref.deeplabv3_resnet101(2)
+    assert abs(sum(p.numel() for p in ref.parameters()) / 1e6 - 58.63) < 0.005      # SURVEY §8: 58.63 M
+    ref = ref.to('meta').eval()          # eval: ASPP pooling's BN sees one value per channel at batch 1
+    with torch.device('meta'):
+        x = torch.empty(1, 3, 512, 512)
+    with FlopCounterMode(display=False) as fc:
+        ref(x)
+    assert abs(fc.get_total_flops() / 1e9 - 482.3) < 0.1                           # SURVEY §8: 482.3 GFLOP

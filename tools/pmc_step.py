@@ -1,0 +1,113 @@
+"""HBM traffic of the conv engine over ONE C2 training step, from rocprofv3 PMC counters.
+
+Run mode: the bench.py workload (UNet-R50 512x512 bs16 bf16 semi-supervised step), 3 warm-up steps (the
+per-geometry autotune runs there), then one step bracketed by two marker launches (a 256-thread
+ssseg_cast of 8 floats) so the dispatches of exactly that step can be cut out of the counter trace:
+
+    rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_f -o f --output-format csv -- python tools/pmc_step.py
+    rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_w -o w --output-format csv -- python tools/pmc_step.py
+
+Parse mode (CPU):  python tools/pmc_step.py --parse gpurun_out/pmc_f gpurun_out/pmc_w > profiles/<name>.json
+
+FETCH_SIZE / WRITE_SIZE are in KB (rocprofv3 derived counters).  Per MI355X_MICROARCH.md §HBM, gfx950's
+FETCH_SIZE reports half of the bytes of wide (16 B/lane) streaming reads, which is how every conv-engine
+kernel reads (buffer_load ... lds dwordx4 / global_load_dwordx4), so the corrected read traffic is 2x the
+counter; WRITE_SIZE is exact for 16-byte stores.  Both are reported raw and corrected.
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CONV_KERNELS = ('igemm_kernel', 'igemm_glds_kernel', 'wgrad_kernel', 'wgrad_reduce_kernel', 'splitk_finalize_kernel',
+                'slab_finalize_kernel', 'phase_zero_kernel')
+
+
+def run():
+    sys.path[:0] = [ROOT, os.path.join(ROOT, 'semi-supervised_semantic_segmentation_amd')]
+    import torch
+    import bench
+    import train
+    from ssseg import native as N
+    from ssseg import nn as snn
+    dev = torch.device('cuda', 0)
+    snn.set_compute_dtype(torch.bfloat16)
+    model, teacher, opt, cfg = bench.build(16, 512, dev)
+    data = bench.synthetic_batches(2, 16, 512, dev, 0)
+    model.train()
+    opt.zero_grad()
+    for s in range(4):
+        img, mask, ua, ub = data[s % 2]
+        if s == 3:
+            torch.cuda.synchronize()
+            src = torch.zeros(8, device=dev)
+            dst = torch.empty(8, dtype=torch.bfloat16, device=dev)
+            N.call('ssseg_cast', N.dev_ptr(src), N.dev_ptr(dst), 8, N.F32, N.BF16, N.stream())
+        train.train_step(model, teacher, opt, img, mask, ua, ub, 30, s, cfg)
+    N.call('ssseg_cast', N.dev_ptr(src), N.dev_ptr(dst), 8, N.F32, N.BF16, N.stream())
+    torch.cuda.synchronize()
+    print('pmc_step: done')
+
+
+def _rows(d):
+    files = glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True)
+    if not files:
+        raise SystemExit(f'no counter_collection.csv under {d}')
+    rows = []
+    for f in files:
+        with open(f) as fh:
+            rows += list(csv.DictReader(fh))
+    key = 'Dispatch_Id' if 'Dispatch_Id' in rows[0] else 'Correlation_Id'
+    rows.sort(key=lambda r: int(r[key]))
+    return rows
+
+
+def _step_sums(d):
+    rows = _rows(d)
+    marks = [i for i, r in enumerate(rows) if 'cast_kernel' in r['Kernel_Name'] and int(r.get('Grid_Size', 0)) <= 256]
+    if len(marks) < 2:
+        raise SystemExit(f'{d}: markers not found')
+    a, b = marks[-2], marks[-1]
+    per = collections.defaultdict(lambda: [0.0, 0])
+    total, launches = 0.0, 0
+    for r in rows[a + 1:b]:
+        name = r['Kernel_Name']
+        fam = next((k for k in CONV_KERNELS if k in name), None)
+        if fam is None:
+            continue
+        v = float(r['Counter_Value'])
+        per[fam][0] += v
+        per[fam][1] += 1
+        total += v
+        launches += 1
+    return total, launches, {k: v for k, v in per.items()}, rows[0].get('Counter_Name', '?')
+
+
+def parse(fetch_dir, write_dir):
+    f_kb, n_f, f_per, _ = _step_sums(fetch_dir)
+    w_kb, n_w, w_per, _ = _step_sums(write_dir)
+    fetch, write = f_kb * 1024.0, w_kb * 1024.0
+    out = {
+        'what': 'conv-engine HBM traffic of one C2 training step (UNet-R50 512x512 bs16 bf16), rocprofv3 PMC',
+        'kernel_launches': n_f,
+        'fetch_bytes_raw': fetch, 'fetch_bytes_corrected_x2': 2 * fetch, 'write_bytes': write,
+        'traffic_bytes': 2 * fetch + write,
+        'per_kernel_family': {k: {'fetch_kb_raw': f_per.get(k, [0, 0])[0], 'write_kb': w_per.get(k, [0, 0])[0],
+                                  'launches': f_per.get(k, [0, 0])[1]} for k in sorted(set(f_per) | set(w_per))},
+        'correction': 'FETCH_SIZE x2 for 16 B/lane streaming reads on gfx950 (MI355X_MICROARCH.md §HBM)',
+    }
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == '__main__':
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--parse', nargs=2, metavar=('FETCH_DIR', 'WRITE_DIR'))
+    a = ap.parse_args()
+    if a.parse:
+        parse(*a.parse)
+    else:
+        run()
