@@ -115,48 +115,69 @@ template <> struct Load4<bf16_t> {
 };
 
 // Writes one wave's FN x FM fragments: y[pixel(m)][n..n+3] = act(acc*scale + shift + res), NHWC.
+// The per-channel affine of a fragment column is loaded once, and every residual of the column is loaded
+// before the first store (the stores may alias the residual as far as the compiler knows, so it could not
+// batch those loads itself): one HBM round trip per column instead of one per pixel.
 template <typename TO, int FM, int FN>
 __device__ __forceinline__ void store_tile(const f32x4 (&acc)[FN][FM], long long mb, int nb, int lane,
                                            const ConvGeom& g, TO* __restrict__ y, const Epi<TO>& ep) {
+  long long op[FM];   // output pixel of fragment row j (-1: past M)
 #pragma unroll
   for (int j = 0; j < FM; ++j) {
     const long long m = mb + j * 16 + (lane & 15);
-    if (m >= g.M) continue;
-    const int ox = (int)m % g.OW;    // 32-bit decode: geom_ok guarantees M < 2^31
-    const int q = (int)m / g.OW;
-    const int oy = q % g.OH, img = q / g.OH;
-    const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
-    TO* yp = y + op * g.ldy;
+    op[j] = -1;
+    if (m < g.M) {
+      const int ox = (int)m % g.OW;    // 32-bit decode: geom_ok guarantees M < 2^31
+      const int q = (int)m / g.OW;
+      const int oy = q % g.OH, img = q / g.OH;
+      op[j] = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+    }
+  }
 #pragma unroll
-    for (int i = 0; i < FN; ++i) {
-      const int n = nb + i * 16 + (lane >> 4) * 4;
-      if (n >= g.K) continue;
-      const bool full = n + 3 < g.K;
-      float v[4], r[4] = {0.f, 0.f, 0.f, 0.f};
-      if (ep.res) {
-        const TO* rp = ep.res + op * ep.ldr + n;
+  for (int i = 0; i < FN; ++i) {
+    const int n = nb + i * 16 + (lane >> 4) * 4;
+    if (n >= g.K) continue;
+    const bool full = n + 3 < g.K;
+    float sc[4], sh[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bool in = n + e < g.K;
+      sc[e] = (ep.scale && in) ? ep.scale[n + e] : 1.f;
+      sh[e] = (ep.shift && in) ? ep.shift[n + e] : 0.f;
+    }
+    float r[FM][4];
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      r[j][0] = r[j][1] = r[j][2] = r[j][3] = 0.f;
+      if (ep.res && op[j] >= 0) {
+        const TO* rp = ep.res + op[j] * ep.ldr + n;
         if (full && (ep.ldr & 3) == 0)
-          Load4<TO>::ld(rp, r);
+          Load4<TO>::ld(rp, r[j]);
         else
-          for (int e = 0; e < 4 && n + e < g.K; ++e) r[e] = io<TO>::ld(rp, e);
+          for (int e = 0; e < 4 && n + e < g.K; ++e) r[j][e] = io<TO>::ld(rp, e);
       }
+    }
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      if (op[j] < 0) continue;
       if (ep.aux) {
         const float a4[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         if (full && (g.ldy & 3) == 0)
-          Store4<TO>::st(ep.aux + op * g.ldy + n, a4);
+          Store4<TO>::st(ep.aux + op[j] * g.ldy + n, a4);
         else
-          for (int e = 0; e < 4 && n + e < g.K; ++e) io<TO>::st(ep.aux, op * g.ldy + n + e, a4[e]);
+          for (int e = 0; e < 4 && n + e < g.K; ++e) io<TO>::st(ep.aux, op[j] * g.ldy + n + e, a4[e]);
       }
+      float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float a = acc[i][j][e];
-        const bool in = n + e < g.K;
-        if (ep.scale && in) a *= ep.scale[n + e];
-        if (ep.shift && in) a += ep.shift[n + e];
-        a += r[e];
+        if (ep.scale) a *= sc[e];
+        if (ep.shift) a += sh[e];
+        a += r[j][e];
         a = act_fwd(a, ep.relu, ep.slope);
         v[e] = a;
       }
+      TO* yp = y + op[j] * g.ldy;
       if (full && (g.ldy & 3) == 0) {
         Store4<TO>::st(yp + n, v);
       } else {
@@ -212,44 +233,68 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
       *(f32x4*)(smem + (wmo + j * 16 + (lane & 15)) * LDR + (wno + i * 16 + (lane >> 4) * 4) * 4) = acc[i][j];
   __syncthreads();
   constexpr int CPR = BN / 8;                 // 8-channel chunks per row
+  static_assert(NT % CPR == 0, "epilogue: one fixed channel chunk per thread");
+  constexpr int RPP = NT / CPR, NP = (BM + RPP - 1) / RPP;   // rows per pass, passes
+  const int ch = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
+  const int n = n0 + ch * 8;
+  if (n >= g.K) return;
   const bool vec = (g.ldy & 7) == 0 && (!ep.res || (ep.ldr & 7) == 0);
-  for (int idx = threadIdx.x; idx < BM * CPR; idx += NT) {
-    const int row = idx / CPR, ch = idx - row * CPR;
+  const bool full = vec && n + 7 < g.K;
+  // this thread's 8 channels are the same in every pass: the affine is loaded once, and all residual
+  // rows are in flight before the first store
+  float sc[8], sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const bool in = n + e < g.K;
+    sc[e] = (ep.scale && in) ? ep.scale[n + e] : 1.f;
+    sh[e] = (ep.shift && in) ? ep.shift[n + e] : 0.f;
+  }
+  long long op[NP];
+  float r[NP][8];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int row = r0 + p * RPP;
     const long long m = m0 + row;
-    const int n = n0 + ch * 8;
-    if (m >= g.M || n >= g.K) continue;
-    const int ox = (int)m % g.OW;    // 32-bit decode: geom_ok guarantees M < 2^31
-    const int q = (int)m / g.OW;
-    const int oy = q % g.OH, img = q / g.OH;
-    const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
-    const float* a = (const float*)(smem + row * LDR + ch * 32);
-    float v[8], r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    op[p] = -1;
+    if (row < BM && m < g.M) {
+      const int ox = (int)m % g.OW;    // 32-bit decode: geom_ok guarantees M < 2^31
+      const int q = (int)m / g.OW;
+      const int oy = q % g.OH, img = q / g.OH;
+      op[p] = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) r[p][e] = 0.f;
+    if (ep.res && op[p] >= 0) {
+      if (full)
+        Out8<TO>::ld(ep.res + op[p] * ep.ldr + n, r[p]);
+      else
+        for (int e = 0; e < 8 && n + e < g.K; ++e) r[p][e] = io<TO>::ld(ep.res, op[p] * ep.ldr + n + e);
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    if (op[p] < 0) continue;
+    const float* a = (const float*)(smem + (r0 + p * RPP) * LDR + ch * 32);
+    float v[8];
     const float4 a0 = *(const float4*)a, a1 = *(const float4*)(a + 4);
     const float raw[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-    const bool full = vec && n + 7 < g.K;
-    if (ep.res) {
-      if (full)
-        Out8<TO>::ld(ep.res + op * ep.ldr + n, r);
-      else
-        for (int e = 0; e < 8 && n + e < g.K; ++e) r[e] = io<TO>::ld(ep.res, op * ep.ldr + n + e);
-    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float t = raw[e];
-      const bool in = n + e < g.K;
-      if (ep.scale && in) t *= ep.scale[n + e];
-      if (ep.shift && in) t += ep.shift[n + e];
-      t += r[e];
+      if (ep.scale) t *= sc[e];
+      if (ep.shift) t += sh[e];
+      t += r[p][e];
       t = act_fwd(t, ep.relu, ep.slope);
       v[e] = t;
     }
+    const long long o = op[p] * g.ldy + n;
     if (full) {
-      Out8<TO>::st(y + op * g.ldy + n, v);
-      if (ep.aux) Out8<TO>::st(ep.aux + op * g.ldy + n, raw);
+      Out8<TO>::st(y + o, v);
+      if (ep.aux) Out8<TO>::st(ep.aux + o, raw);
     } else {
       for (int e = 0; e < 8 && n + e < g.K; ++e) {
-        io<TO>::st(y, op * g.ldy + n + e, v[e]);
-        if (ep.aux) io<TO>::st(ep.aux, op * g.ldy + n + e, raw[e]);
+        io<TO>::st(y, o + e, v[e]);
+        if (ep.aux) io<TO>::st(ep.aux, o + e, raw[e]);
       }
     }
   }
@@ -266,11 +311,12 @@ constexpr int ROWB = 80;   // 64 data bytes + 16 pad per LDS row
 // ------------------------------------------------------------------------------------------------
 // forward / dgrad / transposed-conv gather GEMM
 // ------------------------------------------------------------------------------------------------
-int g_knobs[8] = {0, -1, 0, 0, 0, 1, 0, 0};   // runtime variant switches (ssseg_set_knob)
+int g_knobs[9] = {0, -1, 0, 0, 0, 1, 0, 0, 0};   // runtime variant switches (ssseg_set_knob)
 // 0: reg-staged pipeline depth; 1: split-K cap (-1 off); 2: 64x64 small-M tiles (reg-staged path);
-// 3: bf16 LDS-DMA path (0 on, -1 off); 4: variant (0 auto, 1..10 LDS-DMA config, 11 register-staged);
+// 3: bf16 LDS-DMA path (0 on, -1 off); 4: variant (0 auto, 1..10 / 12..14 LDS-DMA config, 11 register-staged);
 // 5: autotune unseen geometries (1 on, 0 = static heuristic); knob 6 = 1 clears the variant cache;
-// 7: LDS-staged coalesced epilogue in the LDS-DMA kernel (0 on, -1 off)
+// 7: LDS-staged coalesced epilogue in the LDS-DMA kernel (0 on, -1 off);
+// 8: bf16 weight gradient on the LDS-DMA kernel (0 on, -1 = register-staged wgrad_kernel)
 
 template <typename T, typename TO, int BM, int BN, int WM, int WN, bool DEEP>
 __global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __restrict__ x, const T* __restrict__ w,
@@ -840,6 +886,207 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ x, con
   }
 }
 
+// wgrad output of one wave: lane holds dW for kk .. kk+3 (rows) of channel co (column) per fragment.
+// Single split (dd.dw set): final layout directly (0 = [K][R][S][C], 1 = [k_real][c_real][R][S]),
+// += if accumulate; otherwise the fp32 slab tile slab[split][co][kk] that wgrad_reduce_kernel sums.
+template <int FM, int FN>
+__device__ __forceinline__ void wgrad_store(const f32x4 (&acc)[FM][FN], int kkb0, int cob0, int lane,
+                                            const ConvGeom& g, float* __restrict__ slab, const WDirect& dd) {
+  const int gq = lane >> 4, li = lane & 15;
+  if (dd.dw) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int kkb = kkb0 + i * 16 + 4 * gq;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int co = cob0 + j * 16 + li;
+        if (co >= dd.k_real) continue;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int kk = kkb + e;
+          if (kk >= g.KK) continue;
+          const int c = kk % g.C, tap = kk / g.C;
+          if (c >= dd.c_real) continue;
+          long long o;
+          if (dd.layout == 0) o = ((long long)co * g.R * g.S + tap) * g.C + c;
+          else o = (((long long)co * dd.c_real + c) * g.R + tap / g.S) * g.S + tap % g.S;
+          dd.dw[o] = dd.accumulate ? dd.dw[o] + acc[i][j][e] : acc[i][j][e];
+        }
+      }
+    }
+    return;
+  }
+  float* sl = slab + (long long)blockIdx.z * g.K * g.KK;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int kk = kkb0 + i * 16 + 4 * gq;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int co = cob0 + j * 16 + li;
+      if (co >= g.K || kk >= g.KK) continue;
+      float* p = sl + (long long)co * g.KK + kk;
+      if (kk + 3 < g.KK) {
+        *(float4*)p = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      } else {
+        for (int e = 0; e < 4 && kk + e < g.KK; ++e) p[e] = acc[i][j][e];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// weight gradient on an LDS-DMA pipeline (bf16, gfx950), for C % BMW == 0: a kk-tile never straddles a
+// tap, so the tap (r, s) and the channel block c0 are block-uniform and each x row of a k-tile is one
+// run of BMW channels of one pixel.  The 64-pixel k-tiles of x (gathered rows) and dY are staged by
+// buffer_load ... lds (16 B per lane; padding pixels and rows past the split get an out-of-range offset
+// and read as zeros) into an NS-deep ring, one raw barrier per k-tile with a counted vmcnt, as in
+// igemm_glds_kernel.  LDS rows are unpadded (128 / 256 B); 16-byte chunk ch of row r is stored at
+// ch ^ wswz(r) — applied on the source offset, since the DMA writes lane-linearly — and the
+// ds_read_b64_tr_b16 fragment reads apply the same XOR.  With the k-slot -> pixel-row map wkp (a
+// half-wave's two 4-row blocks 8 rows apart) every transposed read is bank-conflict-free.  Same
+// contraction, split plan and output path as wgrad_kernel.
+// ------------------------------------------------------------------------------------------------
+template <int ROWB>
+__device__ __forceinline__ int wswz(int r) {
+  if constexpr (ROWB == 256) return ((r & 3) << 2) | ((r >> 2) & 3);
+  else return (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 1);
+}
+__device__ __forceinline__ int wkp(int g, int j) { return 16 * (g >> 1) + 8 * (g & 1) + 4 * (j >> 2) + (j & 3); }
+
+template <int BMW, int BNW, int NS>
+__global__ void __launch_bounds__(256) wgrad_glds_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                                                         float* __restrict__ slab, ConvGeom g, long long pix_per_split,
+                                                         WDirect dd, unsigned xbytes, unsigned dbytes) {
+  constexpr int BKP = 64;                                    // pixels per k-tile
+  constexpr int ROWX = BMW * 2, ROWD = BNW * 2;              // LDS row bytes
+  constexpr int XCPR = ROWX / 16, DCPR = ROWD / 16;          // 16-byte chunks per row
+  constexpr int XI = BKP * XCPR / 256, DI = BKP * DCPR / 256;   // wave-instructions per wave per stage
+  constexpr int NL = XI + DI;
+  constexpr int STAGE = BKP * (ROWX + ROWD);
+  constexpr int WTM = BMW / 2, WTN = BNW / 2, FM = WTM / 16, FN = WTN / 16;
+  static_assert(XI >= 1 && DI >= 1 && NS >= 2 && NS <= 3, "wgrad glds tile");
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int kk0 = blockIdx.x * BMW, co0 = blockIdx.y * BNW;
+  const long long p_begin = (long long)blockIdx.z * pix_per_split;
+  const long long p_end = min(p_begin + pix_per_split, g.M);
+  const int tap = kk0 / g.C, c0 = kk0 - tap * g.C;
+  const int tr = tap / g.S, ts = tap - tr * g.S;
+  const int offy = tr * g.dy + g.py, offx = ts * g.dx + g.px;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc((void*)dy, (short)0, (int)dbytes, 0x00020000);
+
+  // x slot ii of this lane: LDS row (wave*XI + ii)*(64/XCPR) + lane/XCPR, logical chunk (lane%XCPR)^swz;
+  // its pixel advances by BKP per k-tile (incremental decode, no per-tile division)
+  long long xp[XI];
+  int xoy[XI], xox[XI], ximg[XI], xcb[XI];
+#pragma unroll
+  for (int ii = 0; ii < XI; ++ii) {
+    const int row = (wave * XI + ii) * (64 / XCPR) + lane / XCPR;
+    xcb[ii] = (c0 + ((lane % XCPR) ^ wswz<ROWX>(row)) * 8) * 2;
+    xp[ii] = p_begin + row;
+    const long long pp = xp[ii] < g.M ? xp[ii] : 0;
+    xox[ii] = (int)(pp % g.OW);
+    const long long q = pp / g.OW;
+    xoy[ii] = (int)(q % g.OH);
+    ximg[ii] = (int)(q / g.OH);
+  }
+  long long dp[DI];
+  int dcb[DI];
+#pragma unroll
+  for (int jj = 0; jj < DI; ++jj) {
+    const int row = (wave * DI + jj) * (64 / DCPR) + lane / DCPR;
+    const int co = co0 + ((lane % DCPR) ^ wswz<ROWD>(row)) * 8;
+    dcb[jj] = co < g.K ? co * 2 : -1;
+    dp[jj] = p_begin + row;
+  }
+  auto issue = [&](int buf) {
+    char* Xs = smem + buf * STAGE;
+    char* Ds = Xs + BKP * ROWX;
+#pragma unroll
+    for (int ii = 0; ii < XI; ++ii) {
+      unsigned off = OOB;
+      if (xp[ii] < p_end) {
+        const int iy = xoy[ii] * g.sy + offy, ix = xox[ii] * g.sx + offx;
+        if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
+          off = (unsigned)(((ximg[ii] * g.H + iy) * g.W + ix) * g.ldx) * 2u + (unsigned)xcb[ii];
+      }
+      bldslds16(xr, Xs + (wave * XI + ii) * 1024, off, 0);
+      xp[ii] += BKP;
+      xox[ii] += BKP;
+      while (xox[ii] >= g.OW) {
+        xox[ii] -= g.OW;
+        if (++xoy[ii] == g.OH) {
+          xoy[ii] = 0;
+          ++ximg[ii];
+        }
+      }
+    }
+#pragma unroll
+    for (int jj = 0; jj < DI; ++jj) {
+      const unsigned off = (dp[jj] < p_end && dcb[jj] >= 0) ? (unsigned)(dp[jj] * g.ldy * 2 + dcb[jj]) : OOB;
+      bldslds16(dr, Ds + (wave * DI + jj) * 1024, off, 0);
+      dp[jj] += BKP;
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int gq = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  auto compute = [&](int buf) {
+    const char* Xs = smem + buf * STAGE;
+    const char* Ds = Xs + BKP * ROWX;
+#pragma unroll
+    for (int ks = 0; ks < BKP / 32; ++ks) {
+      const int r0 = ks * 32 + wkp(gq, q4), r1 = ks * 32 + wkp(gq, 4 + q4);
+      const int sx0 = 16 * wswz<ROWX>(r0), sx1 = 16 * wswz<ROWX>(r1);
+      const int sd0 = 16 * wswz<ROWD>(r0), sd1 = 16 * wswz<ROWD>(r1);
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int col = wm * WTM + i * 16 + 4 * p4;
+        const int cb = 16 * (col >> 3), e8 = 2 * (col & 7);
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Xs + r0 * ROWX + (cb ^ sx0) + e8));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Xs + r1 * ROWX + (cb ^ sx1) + e8));
+        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = wn * WTN + j * 16 + 4 * p4;
+        const int cb = 16 * (col >> 3), e8 = 2 * (col & 7);
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ds + r0 * ROWD + (cb ^ sd0) + e8));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ds + r1 * ROWD + (cb ^ sd1) + e8));
+        bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  const long long npix = p_end > p_begin ? p_end - p_begin : 0;
+  const int nk = (int)((npix + BKP - 1) / BKP);
+  constexpr int D = NS - 1;   // k-tiles in flight ahead of the one being multiplied
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+    if (p < nk) issue(p);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (D >= 2 && kt + 1 < nk) vmcnt_wait<NL>();   // tile kt landed, tile kt+1 may stay in flight
+    else vmcnt_wait<0>();
+    __builtin_amdgcn_s_barrier();                  // every wave's tile kt landed; slot (kt+D)%NS is free
+    if (kt + D < nk) issue((kt + D) % NS);
+    compute(kt % NS);
+  }
+  wgrad_store<FM, FN>(acc, kk0 + wm * WTM, co0 + wn * WTN, lane, g, slab, dd);
+}
+
 // sum the split slabs and write dW in the requested layout: 0 = [K][R][S][C] (packed, C = physical),
 // 1 = [K][C_real][R][S] (PyTorch OIHW).  accumulate: dst += sum.
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int K, int R, int S, int C, int c_real,
@@ -976,6 +1223,11 @@ void launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvG
     case 7: launch_glds<TO, 256, 64, 4, 2, 8, 3>(x, w, y, g, ep, xb, wb, s); break;
     case 8: launch_glds<TO, 128, 128, 2, 2, 4, 4>(x, w, y, g, ep, xb, wb, s); break;
     case 9: launch_glds<TO, 128, 64, 2, 2, 4, 4>(x, w, y, g, ep, xb, wb, s); break;
+    // two-slot rings: 64 / 80 / 48 KB of LDS, so 2-3 workgroups share a CU and hide each other's
+    // pipeline fill and epilogue (the short-k layers: 3x3 over 64-128 channels, nk = 9..18)
+    case 12: launch_glds<TO, 128, 128, 2, 2, 4, 2>(x, w, y, g, ep, xb, wb, s); break;
+    case 13: launch_glds<TO, 256, 64, 4, 1, 4, 2>(x, w, y, g, ep, xb, wb, s); break;
+    case 14: launch_glds<TO, 128, 64, 2, 2, 4, 2>(x, w, y, g, ep, xb, wb, s); break;
     default: launch_glds<TO, 64, 64, 2, 2, 4, 4>(x, w, y, g, ep, xb, wb, s); break;
   }
 }
@@ -1000,7 +1252,7 @@ void dispatch_regstaged(const void* x, const void* w, void* y, const ConvGeom& g
 // speed, never results (tests/test_hip_layers.py::test_conv_variants_bitwise).  Variant 0 is the
 // register-staged kernel, 1..10 the LDS-DMA configs.  With knob 5 on (default) an unseen geometry is
 // timed once over the candidates on the caller's stream (HIP events) and the fastest is cached.
-constexpr int kCandidates[] = {0, 1, 3, 5, 6, 7, 8, 10};
+constexpr int kCandidates[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 14};
 std::unordered_map<unsigned long long, int> g_variant;
 std::mutex g_variant_mu;
 
@@ -1041,6 +1293,11 @@ int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const
   }
   int best = heuristic_variant(g);
   float best_ms = 1e30f;
+  static const bool log = getenv("SSSEG_TUNE_LOG") != nullptr;   // one line per tuned geometry (stderr)
+  char line[512];
+  int len = log ? snprintf(line, sizeof line, "tune N%d %dx%d C%d -> %dx%d K%d %dx%d s%d d%d out%dx%d/%d ep%d%d:",
+                           g.N, g.H, g.W, g.C, g.OH, g.OW, g.K, g.R, g.S, g.sy, g.dy, g.outH, g.outW, g.osy,
+                           ep.scale ? 1 : 0, ep.aux ? 1 : 0) : 0;
   for (int v : kCandidates) {
     run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s);   // warm (code load, caches)
     float ms = 1e30f;
@@ -1051,11 +1308,13 @@ int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const
       float t = 1e30f;
       if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&t, e0, e1) == hipSuccess) ms = std::min(ms, t);
     }
+    if (log && len > 0 && len < (int)sizeof line - 16) len += snprintf(line + len, sizeof line - len, " %d:%.0f", v, ms * 1e3f);
     if (ms < best_ms) {
       best_ms = ms;
       best = v;
     }
   }
+  if (log) fprintf(stderr, "%s -> %d\n", line, best);
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   return best;
@@ -1093,13 +1352,15 @@ void dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, co
 struct WgradPlan {
   int bmw, bnw, mt, nt, splits;
   long long pps;
+  bool glds;
 };
 
 template <typename T>
-WgradPlan plan_wgrad(const ConvGeom& g) {
+WgradPlan plan_wgrad(const ConvGeom& g, int bmw = 0) {
   WgradPlan p;
+  p.glds = false;
   p.bnw = g.K <= 64 ? 64 : 128;
-  p.bmw = g.KK <= 64 ? 64 : 128;   // (a 256x64 tile for Cout <= 64 measured slower: 263 -> 208 TF)
+  p.bmw = bmw ? bmw : (g.KK <= 64 ? 64 : 128);   // (a 256x64 tile for Cout <= 64 measured slower: 263 -> 208 TF)
   p.mt = (g.KK + p.bmw - 1) / p.bmw;
   p.nt = (g.K + p.bnw - 1) / p.bnw;
   const long long tiles = (long long)p.mt * p.nt;
@@ -1131,6 +1392,42 @@ void launch_wgrad(const void* x, const void* dy, float* slab, const ConvGeom& g,
     hipLaunchKernelGGL((wgrad_kernel<T, 128, 128>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, g, p.pps, dd);
 }
 
+// LDS-DMA weight gradient: bf16, C % 64 == 0 (a 64- or 128-channel kk-tile inside one tap), operands < 2 GB
+static bool wgrad_glds_ok(const ConvGeom& g, int dt) {
+  if (dt != SSSEG_BF16 || g_knobs[8] != 0) return false;
+  if (g.C % 64 || g.ldx % 8 || g.ldy % 8 || g.K % 8) return false;
+  const long long xb = (long long)g.N * g.H * g.W * g.ldx * 2, db = g.M * g.ldy * 2;
+  return xb < 0x7fffffffLL && db < 0x7fffffffLL;
+}
+
+static WgradPlan choose_wgrad(const ConvGeom& g, int dt) {
+  WgradPlan p;
+  if (wgrad_glds_ok(g, dt)) {
+    p = plan_wgrad<bf16_t>(g, (g.C % 128 == 0 && g.KK > 64) ? 128 : 64);
+    p.glds = true;
+  } else {
+    p = dt == SSSEG_BF16 ? plan_wgrad<bf16_t>(g) : plan_wgrad<float>(g);
+  }
+  return p;
+}
+
+template <int BMW, int BNW>
+void launch_wgrad_glds_t(const void* x, const void* dy, float* slab, const ConvGeom& g, const WgradPlan& p, WDirect dd,
+                         hipStream_t s) {
+  constexpr int NS = 64 * (BMW + BNW) * 2 <= 24576 ? 3 : 2;   // 48 / 72 / 64 KB of LDS: 2-3 blocks per CU
+  const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.ldx * 2), db = (unsigned)(g.M * g.ldy * 2);
+  hipLaunchKernelGGL((wgrad_glds_kernel<BMW, BNW, NS>), dim3(p.mt, p.nt, p.splits), dim3(256), 0, s, (const bf16_t*)x,
+                     (const bf16_t*)dy, slab, g, p.pps, dd, xb, db);
+}
+
+void launch_wgrad_glds(const void* x, const void* dy, float* slab, const ConvGeom& g, const WgradPlan& p, WDirect dd,
+                       hipStream_t s) {
+  if (p.bmw == 128 && p.bnw == 128) launch_wgrad_glds_t<128, 128>(x, dy, slab, g, p, dd, s);
+  else if (p.bmw == 128) launch_wgrad_glds_t<128, 64>(x, dy, slab, g, p, dd, s);
+  else if (p.bnw == 128) launch_wgrad_glds_t<64, 128>(x, dy, slab, g, p, dd, s);
+  else launch_wgrad_glds_t<64, 64>(x, dy, slab, g, p, dd, s);
+}
+
 bool geom_ok(const ConvGeom& g, int dt) {
   const int vec = dt == SSSEG_BF16 ? 8 : 4;
   if (g.C % vec || g.ldx % vec || g.ldw % vec) return false;
@@ -1143,7 +1440,7 @@ bool geom_ok(const ConvGeom& g, int dt) {
 }  // namespace
 
 extern "C" int ssseg_set_knob(int id, int value) {
-  if (id < 0 || id >= 8) return SSSEG_EINVAL;
+  if (id < 0 || id >= 9) return SSSEG_EINVAL;
   if (id == 6 && value) {
     std::lock_guard<std::mutex> lk(g_variant_mu);
     g_variant.clear();
@@ -1212,7 +1509,7 @@ extern "C" int ssseg_conv_igemm(const void* x, const void* w, void* y, const sss
 extern "C" size_t ssseg_conv_wgrad_workspace_bytes(const ssseg_conv_desc* d, int dt) {
   ConvGeom g;
   if (!make_geom(d, g)) return 0;
-  const WgradPlan p = dt == SSSEG_BF16 ? plan_wgrad<bf16_t>(g) : plan_wgrad<float>(g);
+  const WgradPlan p = choose_wgrad(g, dt);
   return (size_t)p.splits * g.K * g.KK * sizeof(float) + 256;
 }
 
@@ -1228,9 +1525,11 @@ extern "C" int ssseg_conv_wgrad(const void* x, const void* dy, float* dw, const 
   float* slab = (float*)ws;
   WgradPlan p;
   if (dt != SSSEG_BF16 && dt != SSSEG_F32) return SSSEG_EUNSUPPORTED;
-  p = dt == SSSEG_BF16 ? plan_wgrad<bf16_t>(g) : plan_wgrad<float>(g);
+  p = choose_wgrad(g, dt);
   const WDirect dd{p.splits == 1 ? dw : nullptr, (int)c_real, (int)k_real, layout, accumulate};
-  if (dt == SSSEG_BF16)
+  if (p.glds)
+    launch_wgrad_glds(x, dy, slab, g, p, dd, s);
+  else if (dt == SSSEG_BF16)
     launch_wgrad<bf16_t>(x, dy, slab, g, p, dd, s);
   else
     launch_wgrad<float>(x, dy, slab, g, p, dd, s);

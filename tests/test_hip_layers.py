@@ -280,8 +280,8 @@ def test_conv_bn_act_fused_eval_grad(hip_device, mode, monkeypatch, kind, cin, c
 @pytest.mark.parametrize('kind,cin,cout,k,H', [('conv', 64, 128, 3, 19), ('conv', 128, 64, 1, 17), ('conv', 192, 256, 3, 9),
                                                ('convT', 128, 64, 4, 7)])
 def test_conv_variants_bitwise(hip_device, kind, cin, cout, k, H):
-    """Every bf16 engine variant (register-staged, LDS-DMA tile configs 1..10) accumulates the same
-    MFMA k-sequence: forward and input-gradient outputs are bit-identical, so autotuning never
+    """Every bf16 engine variant (register-staged, LDS-DMA tile configs 1..10 and 12..14) accumulates the
+    same MFMA k-sequence: forward and input-gradient outputs are bit-identical, so autotuning never
     changes results."""
     from ssseg import native as N
     from ssseg import nn as snn
@@ -294,7 +294,7 @@ def test_conv_variants_bitwise(hip_device, kind, cin, cout, k, H):
     x = _act_in(torch.randn(2, cin, H, H + 3), hip_device).detach().requires_grad_(True)
     outs = []
     try:
-        for v in [11] + list(range(1, 11)):
+        for v in [11] + list(range(1, 11)) + [12, 13, 14]:
             N.call('ssseg_set_knob', 4, v)
             y = mod(x)
             gy = torch.ones_like(y)
@@ -306,6 +306,55 @@ def test_conv_variants_bitwise(hip_device, kind, cin, cout, k, H):
     for v, y, gx in outs[1:]:
         assert torch.equal(y, outs[0][1]), f'variant {v}: forward differs'
         assert torch.equal(gx, outs[0][2]), f'variant {v}: input gradient differs'
+
+
+WGRAD_CASES = [
+    # cin, cout, k, stride, pad, dil, H, W, N   (C % 64 == 0: the LDS-DMA weight-gradient kernel)
+    (64, 64, 3, 1, 1, 1, 37, 29, 2),      # 64-channel kk-tiles, 64-channel co tile, several pixel splits
+    (128, 192, 3, 1, 1, 1, 21, 19, 2),    # 128-channel kk-tiles, ragged co tile
+    (256, 64, 1, 1, 0, 1, 45, 43, 3),     # 1x1, ragged last split
+    (128, 128, 3, 2, 1, 1, 40, 37, 2),    # stride 2
+    (64, 128, 3, 1, 2, 2, 23, 25, 2),     # dilation 2
+    (512, 256, 1, 2, 0, 1, 18, 18, 2),    # strided 1x1 downsample
+    (128, 64, 1, 1, 0, 1, 9, 11, 2),      # one split: dW written in its final layout directly
+]
+
+
+@pytest.mark.parametrize('cin,cout,k,s,p,d,H,W,n', WGRAD_CASES)
+def test_wgrad_lds_dma(hip_device, cin, cout, k, s, p, d, H, W, n):
+    """bf16 weight gradient on the LDS-DMA kernel (knob 8 = 0, the default) and on the register-staged
+    kernel (knob 8 = -1) vs PyTorch fp32 on the same bf16-rounded operands.  The bf16 products are exact
+    in fp32, so the kernels differ from the reference only by fp32 summation order: 1e-4 of max|dW|."""
+    from ssseg import native as N
+    from ssseg import nn as snn
+    snn.set_compute_dtype(torch.bfloat16)
+    torch.manual_seed(3)
+    ref = torch.nn.Conv2d(cin, cout, k, s, p, d, bias=False)
+    with torch.no_grad():
+        ref.weight.copy_(ref.weight.bfloat16().float())
+    mod = snn.Conv2d(cin, cout, k, s, p, d, bias=False).to(hip_device)
+    mod.load_state_dict(ref.state_dict())
+    x = torch.randn(n, cin, H, W).bfloat16().float()
+    yr = ref(x)
+    gy = torch.randn_like(yr).bfloat16().float()
+    yr.backward(gy)
+    xa = snn.to_act(x.to(hip_device))
+    gya = snn.to_act(gy.to(hip_device))
+    grads = []
+    try:
+        for knob in (0, -1):
+            N.call('ssseg_set_knob', 8, knob)
+            mod.weight.grad = None
+            mod(xa).backward(gya)
+            torch.cuda.synchronize()
+            grads.append(mod.weight.grad.detach().float().cpu())
+    finally:
+        N.call('ssseg_set_knob', 8, 0)
+    gref = ref.weight.grad
+    scale = float(gref.abs().max())
+    for name, g in zip(('lds-dma', 'register-staged'), grads):
+        err = float((g - gref).abs().max()) / scale
+        assert err < 1e-4, f'{name}: max rel err {err}'
 
 
 @pytest.mark.parametrize('k,s,p,ceil', [(3, 2, 1, False), (2, 2, 0, True)])
