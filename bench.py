@@ -28,6 +28,18 @@ import torch.distributed as dist  # noqa: E402
 
 BF16_DENSE_PEAK = 2.5e15        # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, spec)
 FWD_GFLOP_PER_IMAGE = 95.94     # UNet-R50 mw128 ConvT @512 (verified by tests/test_models_host.py)
+# conv-engine HBM bytes of one step from rocprofv3 PMC (tools/pmc_step.py; FETCH_SIZE x2 + WRITE_SIZE, the
+# MI355X_MICROARCH.md gfx950 correction).  PMC cannot run inside the timed process, so the committed
+# measurement of the same workload is reported next to the live flop rate.
+PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r1_v13_pmc_traffic.json')
+
+
+def pmc_traffic():
+    try:
+        with open(PMC_PROFILE) as fh:
+            return int(json.load(fh)['traffic_bytes'])
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def build(batch, size, device):
@@ -183,7 +195,8 @@ def main():
                    'parallelism': f'dp{world}'},
         'roofline': {'bound': 'mfma', 'kernel': 'conv engine (igemm fwd/dgrad/ConvT + wgrad), all launches of one step',
                      'achieved': round(achieved / 1e12, 2), 'peak': BF16_DENSE_PEAK / 1e12, 'unit': 'TFLOP/s',
-                     'frac': round(achieved / BF16_DENSE_PEAK, 4), 'traffic': None,
+                     'frac': round(achieved / BF16_DENSE_PEAK, 4), 'traffic': pmc_traffic(),
+                     'traffic_unit': 'HBM bytes per step, conv engine (rocprofv3 PMC, ' + os.path.relpath(PMC_PROFILE, ROOT) + ')',
                      'conv_ms_per_step': round(conv_ms, 3), 'conv_gflop_per_step': round(conv_flops / 1e9, 1),
                      'launches_per_step': n_launch},
         'step_tflops': round(8 * FWD_GFLOP_PER_IMAGE * args.batch * world / (elapsed / args.steps) / 1e3, 2),

@@ -313,7 +313,7 @@ constexpr int ROWB = 80;   // 64 data bytes + 16 pad per LDS row
 // ------------------------------------------------------------------------------------------------
 int g_knobs[9] = {0, -1, 0, 0, 0, 1, 0, 0, 0};   // runtime variant switches (ssseg_set_knob)
 // 0: reg-staged pipeline depth; 1: split-K cap (-1 off); 2: 64x64 small-M tiles (reg-staged path);
-// 3: bf16 LDS-DMA path (0 on, -1 off); 4: variant (0 auto, 1..10 / 12..14 LDS-DMA config, 11 register-staged);
+// 3: bf16 LDS-DMA path (0 on, -1 off); 4: variant (0 auto, 1..10 / 12..17 LDS-DMA config, 11 register-staged);
 // 5: autotune unseen geometries (1 on, 0 = static heuristic); knob 6 = 1 clears the variant cache;
 // 7: LDS-staged coalesced epilogue in the LDS-DMA kernel (0 on, -1 off);
 // 8: bf16 weight gradient on the LDS-DMA kernel (0 on, -1 = register-staged wgrad_kernel)
@@ -509,8 +509,12 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const bf16_t* __
   constexpr int BI = BN / 8 / NW;                // B (weight) wave-instructions per wave per stage
   constexpr int NL = AI + BI;
   constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
-  static_assert(WM * WN == NW && FM >= 1 && FN >= 1 && AI >= 1 && BI >= 1 && NS >= 2 && NS <= 4, "tile");
-  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
+  static_assert(WM * WN == NW && FM >= 1 && FN >= 1 && AI >= 1 && BI >= 1 && NS >= 1 && NS <= 4, "tile");
+  // NS == 1 (single-slot ring, for nk == 1..2: 1x1 convs over 64-128 channels): the slot is sized to also
+  // hold the staged epilogue, and occupancy (4-9 workgroups per CU) hides the load -> MFMA -> store chain
+  constexpr int EPI = BM * (BN * 4 + 16);
+  constexpr int SMEM = (NS == 1 && EPI > STAGE) ? EPI : NS * STAGE;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -610,21 +614,31 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const bf16_t* __
     }
   };
 
-  constexpr int D = NS - 1;   // tiles in flight ahead of the one being multiplied
+  if constexpr (NS == 1) {
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt) __builtin_amdgcn_s_barrier();   // every wave is done reading the slot
+      issue(0);
+      vmcnt_wait<0>();
+      __builtin_amdgcn_s_barrier();           // every wave's part of tile kt landed
+      compute(0);
+    }
+  } else {
+    constexpr int D = NS - 1;   // tiles in flight ahead of the one being multiplied
 #pragma unroll
-  for (int p = 0; p < D; ++p)
-    if (p < nk) issue(p);
-  for (int kt = 0; kt < nk; ++kt) {
-    // wait for tile kt: the tiles issued after it (at most D-1) may stay in flight
-    const int ahead = min(nk - 1, kt + D - 1) - kt;
-    if (D >= 3 && ahead >= 2) vmcnt_wait<2 * NL>();
-    else if (D >= 2 && ahead >= 1) vmcnt_wait<NL>();
-    else vmcnt_wait<0>();
-    __builtin_amdgcn_s_barrier();   // every wave's tile kt landed; ring slot (kt+D)%NS is free
-    if (kt + D < nk) issue((kt + D) % NS);
-    compute(kt % NS);
+    for (int p = 0; p < D; ++p)
+      if (p < nk) issue(p);
+    for (int kt = 0; kt < nk; ++kt) {
+      // wait for tile kt: the tiles issued after it (at most D-1) may stay in flight
+      const int ahead = min(nk - 1, kt + D - 1) - kt;
+      if (D >= 3 && ahead >= 2) vmcnt_wait<2 * NL>();
+      else if (D >= 2 && ahead >= 1) vmcnt_wait<NL>();
+      else vmcnt_wait<0>();
+      __builtin_amdgcn_s_barrier();   // every wave's tile kt landed; ring slot (kt+D)%NS is free
+      if (kt + D < nk) issue((kt + D) % NS);
+      compute(kt % NS);
+    }
   }
-  if constexpr (BM * (BN * 4 + 16) <= NS * STAGE) {
+  if constexpr (EPI <= SMEM) {
     if (g_epi_lds)
       store_tile_lds<TO, BM, BN, FM, FN, NW * 64>(acc, smem, m0, n0, wm * WTM, wn * WTN, lane, g, y, ep);
     else
@@ -891,7 +905,8 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ x, con
 // += if accumulate; otherwise the fp32 slab tile slab[split][co][kk] that wgrad_reduce_kernel sums.
 template <int FM, int FN>
 __device__ __forceinline__ void wgrad_store(const f32x4 (&acc)[FM][FN], int kkb0, int cob0, int lane,
-                                            const ConvGeom& g, float* __restrict__ slab, const WDirect& dd) {
+                                            const ConvGeom& g, float* __restrict__ slab, const WDirect& dd,
+                                            int split) {
   const int gq = lane >> 4, li = lane & 15;
   if (dd.dw) {
 #pragma unroll
@@ -916,7 +931,7 @@ __device__ __forceinline__ void wgrad_store(const f32x4 (&acc)[FM][FN], int kkb0
     }
     return;
   }
-  float* sl = slab + (long long)blockIdx.z * g.K * g.KK;
+  float* sl = slab + (long long)split * g.K * g.KK;
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int kk = kkb0 + i * 16 + 4 * gq;
@@ -969,8 +984,13 @@ __global__ void __launch_bounds__(256) wgrad_glds_kernel(const bf16_t* __restric
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int kk0 = blockIdx.x * BMW, co0 = blockIdx.y * BNW;
-  const long long p_begin = (long long)blockIdx.z * pix_per_split;
+  // 1-D grid, XCD-aware: consecutive logical ids (the mt x nt tiles of one pixel split, which gather the
+  // same x and dY rows) run on one XCD and share its L2
+  const int mt = (g.KK + BMW - 1) / BMW, nt = (g.K + BNW - 1) / BNW;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int split = tile / (mt * nt), rem = tile - split * (mt * nt);
+  const int kk0 = (rem % mt) * BMW, co0 = (rem / mt) * BNW;
+  const long long p_begin = (long long)split * pix_per_split;
   const long long p_end = min(p_begin + pix_per_split, g.M);
   const int tap = kk0 / g.C, c0 = kk0 - tap * g.C;
   const int tr = tap / g.S, ts = tap - tr * g.S;
@@ -1084,11 +1104,48 @@ __global__ void __launch_bounds__(256) wgrad_glds_kernel(const bf16_t* __restric
     if (kt + D < nk) issue((kt + D) % NS);
     compute(kt % NS);
   }
-  wgrad_store<FM, FN>(acc, kk0 + wm * WTM, co0 + wn * WTN, lane, g, slab, dd);
+  wgrad_store<FM, FN>(acc, kk0 + wm * WTM, co0 + wn * WTN, lane, g, slab, dd, split);
 }
 
 // sum the split slabs and write dW in the requested layout: 0 = [K][R][S][C] (packed, C = physical),
 // 1 = [K][C_real][R][S] (PyTorch OIHW).  accumulate: dst += sum.
+// A block owns 64 consecutive outputs (256-byte slab rows, coalesced) and spreads the splits over its 16
+// waves: wave w sums splits w, w+16, ... in two chains (16 loads in flight per lane with the unroll), then
+// the 16 partials are added in wave order through LDS — a fixed order, so the result is deterministic.
+__global__ void __launch_bounds__(1024) wgrad_reduce_wide_kernel(const float* __restrict__ slab, int splits, int K, int R,
+                                                            int S, int C, int c_real, int k_real,
+                                                            float* __restrict__ dst, int layout, int accumulate) {
+  __shared__ float red[16][64];
+  const long long KK = (long long)R * S * C;
+  const long long total = (long long)K * KK;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long i = (long long)blockIdx.x * 64 + lane;
+  float a0 = 0.f, a1 = 0.f;
+  if (i < total) {
+    int z = w;
+#pragma unroll 8
+    for (; z + 16 < splits; z += 32) {
+      a0 += slab[(long long)z * total + i];
+      a1 += slab[(long long)(z + 16) * total + i];
+    }
+    if (z < splits) a0 += slab[(long long)z * total + i];
+  }
+  red[w][lane] = a0 + a1;
+  __syncthreads();
+  if (w != 0 || i >= total) return;
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) sum += red[k][lane];
+  const int kk = (int)(i % KK), k = (int)(i / KK);
+  const int c = kk % C, tap = kk / C, r = tap / S, s = tap % S;
+  if (c >= c_real || k >= k_real) return;
+  long long o;
+  if (layout == 0) o = ((long long)k * R * S + tap) * C + c;
+  else o = (((long long)k * c_real + c) * R + r) * S + s;
+  dst[o] = accumulate ? dst[o] + sum : sum;
+}
+
+// few splits: one thread per output, 4 independent chains
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int K, int R, int S, int C, int c_real,
                                     int k_real, float* __restrict__ dst, int layout, int accumulate) {
   const long long KK = (long long)R * S * C;
@@ -1097,7 +1154,6 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, 
     const int kk = (int)(i % KK), k = (int)(i / KK);
     const int c = kk % C, tap = kk / C, r = tap / S, s = tap % S;
     if (c >= c_real || k >= k_real) continue;
-    // 4 independent accumulators keep several slab loads in flight (the loop is latency-bound)
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
     int z = 0;
     for (; z + 4 <= splits; z += 4) {
@@ -1228,6 +1284,11 @@ void launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvG
     case 12: launch_glds<TO, 128, 128, 2, 2, 4, 2>(x, w, y, g, ep, xb, wb, s); break;
     case 13: launch_glds<TO, 256, 64, 4, 1, 4, 2>(x, w, y, g, ep, xb, wb, s); break;
     case 14: launch_glds<TO, 128, 64, 2, 2, 4, 2>(x, w, y, g, ep, xb, wb, s); break;
+    // one-slot / small two-slot rings for nk = 1..2 (1x1 expansions 64->256, 128->512): 35 / 17 / 32 KB
+    // of LDS, 4-9 workgroups per CU; output-write bound, so occupancy is what hides the HBM latency
+    case 15: launch_glds<TO, 128, 64, 2, 2, 4, 1>(x, w, y, g, ep, xb, wb, s); break;
+    case 16: launch_glds<TO, 64, 64, 2, 2, 4, 1>(x, w, y, g, ep, xb, wb, s); break;
+    case 17: launch_glds<TO, 64, 64, 2, 2, 4, 2>(x, w, y, g, ep, xb, wb, s); break;
     default: launch_glds<TO, 64, 64, 2, 2, 4, 4>(x, w, y, g, ep, xb, wb, s); break;
   }
 }
@@ -1250,9 +1311,9 @@ void dispatch_regstaged(const void* x, const void* w, void* y, const ConvGeom& g
 // ---- bf16 variant choice: per-geometry autotune cache ----------------------------------------
 // Every variant accumulates the same 32-deep MFMA k-sequence in the same order, so the choice changes
 // speed, never results (tests/test_hip_layers.py::test_conv_variants_bitwise).  Variant 0 is the
-// register-staged kernel, 1..10 the LDS-DMA configs.  With knob 5 on (default) an unseen geometry is
+// register-staged kernel, 1..10 and 12..17 the LDS-DMA configs.  With knob 5 on (default) an unseen geometry is
 // timed once over the candidates on the caller's stream (HIP events) and the fastest is cached.
-constexpr int kCandidates[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 14};
+constexpr int kCandidates[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 14, 15, 16, 17};
 std::unordered_map<unsigned long long, int> g_variant;
 std::mutex g_variant_mu;
 
@@ -1416,7 +1477,7 @@ void launch_wgrad_glds_t(const void* x, const void* dy, float* slab, const ConvG
                          hipStream_t s) {
   constexpr int NS = 64 * (BMW + BNW) * 2 <= 24576 ? 3 : 2;   // 48 / 72 / 64 KB of LDS: 2-3 blocks per CU
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.ldx * 2), db = (unsigned)(g.M * g.ldy * 2);
-  hipLaunchKernelGGL((wgrad_glds_kernel<BMW, BNW, NS>), dim3(p.mt, p.nt, p.splits), dim3(256), 0, s, (const bf16_t*)x,
+  hipLaunchKernelGGL((wgrad_glds_kernel<BMW, BNW, NS>), dim3(p.mt * p.nt * p.splits), dim3(256), 0, s, (const bf16_t*)x,
                      (const bf16_t*)dy, slab, g, p.pps, dd, xb, db);
 }
 
@@ -1538,8 +1599,12 @@ extern "C" int ssseg_conv_wgrad(const void* x, const void* dy, float* dw, const 
     return 0;
   }
   const long long total = (long long)g.K * g.KK;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ssseg_grid(total, 256)), dim3(256), 0, s, slab, p.splits, g.K, g.R, g.S,
-                     g.C, (int)c_real, (int)k_real, dw, layout, accumulate);
+  if (p.splits >= 64)   // many splits: spread them over the 16 waves of a block
+    hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)((total + 63) / 64)), dim3(1024), 0, s, slab, p.splits,
+                       g.K, g.R, g.S, g.C, (int)c_real, (int)k_real, dw, layout, accumulate);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ssseg_grid(total, 256)), dim3(256), 0, s, slab, p.splits, g.K, g.R, g.S,
+                       g.C, (int)c_real, (int)k_real, dw, layout, accumulate);
   SSSEG_LAUNCH_CHECK();
   return 0;
 }

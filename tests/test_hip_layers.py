@@ -278,9 +278,9 @@ def test_conv_bn_act_fused_eval_grad(hip_device, mode, monkeypatch, kind, cin, c
 
 
 @pytest.mark.parametrize('kind,cin,cout,k,H', [('conv', 64, 128, 3, 19), ('conv', 128, 64, 1, 17), ('conv', 192, 256, 3, 9),
-                                               ('convT', 128, 64, 4, 7)])
+                                               ('conv', 64, 256, 1, 21), ('convT', 128, 64, 4, 7)])
 def test_conv_variants_bitwise(hip_device, kind, cin, cout, k, H):
-    """Every bf16 engine variant (register-staged, LDS-DMA tile configs 1..10 and 12..14) accumulates the
+    """Every bf16 engine variant (register-staged, LDS-DMA tile configs 1..10 and 12..17) accumulates the
     same MFMA k-sequence: forward and input-gradient outputs are bit-identical, so autotuning never
     changes results."""
     from ssseg import native as N
@@ -294,7 +294,7 @@ def test_conv_variants_bitwise(hip_device, kind, cin, cout, k, H):
     x = _act_in(torch.randn(2, cin, H, H + 3), hip_device).detach().requires_grad_(True)
     outs = []
     try:
-        for v in [11] + list(range(1, 11)) + [12, 13, 14]:
+        for v in [11] + list(range(1, 11)) + list(range(12, 18)):
             N.call('ssseg_set_knob', 4, v)
             y = mod(x)
             gy = torch.ones_like(y)
