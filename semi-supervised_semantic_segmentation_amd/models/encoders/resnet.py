@@ -31,9 +31,11 @@ class Bottleneck(nn.Module):
             shortcut = snn.conv_bn_act(conv, x, bn, relu=False)
         else:
             shortcut = x
-        y = snn.conv_bn_act(self.conv1, x, self.bn1)
+        # identity shortcut: its gradient is added in conv1's dgrad epilogue (snn.GradHandoff)
+        h = snn.GradHandoff() if self.downsample is None else None
+        y = snn.conv_bn_act(self.conv1, x, self.bn1, grad_in=h)
         y = snn.conv_bn_act(self.conv2, y, self.bn2)
-        return snn.conv_bn_act(self.conv3, y, self.bn3, relu=True, residual=shortcut)
+        return snn.conv_bn_act(self.conv3, y, self.bn3, relu=True, residual=shortcut, grad_out=h)
 
 
 class Stem(nn.Sequential):

@@ -194,11 +194,36 @@ def _act(a):
     return code, 0.0
 
 
+class GradHandoff:
+    """Hands the identity shortcut's gradient of a residual block to the dgrad of the block's first conv,
+    which reads the same input x (Bottleneck, resnet.py): the residual-consuming BN backward (which runs
+    first, it is downstream) parks dres here and returns None for it, and the conv adds it in its dgrad
+    epilogue (y = acc + residual) -- dx = dgrad(conv1) + d(shortcut) in one kernel instead of autograd's
+    separate accumulation add."""
+    __slots__ = ('grad',)
+
+    def __init__(self):
+        self.grad = None
+
+    def put(self, g):
+        if self.grad is not None:
+            raise RuntimeError('GradHandoff: gradient already pending')
+        self.grad = g
+
+    def take(self):
+        g, self.grad = self.grad, None
+        return g
+
+
+def _take(handoff):
+    return handoff.take() if handoff is not None else None
+
+
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, mod, relu):
+    def forward(ctx, x, weight, bias, mod, relu, handoff=None):
         y = mod._ssseg_forward(x, relu)
-        ctx.mod, ctx.relu = mod, relu
+        ctx.mod, ctx.relu, ctx.handoff = mod, relu, handoff
         ctx.save_for_backward(x, y if _act(relu)[0] else None)
         return y
 
@@ -214,8 +239,14 @@ class _ConvFn(torch.autograd.Function):
                    N.stream())
             gy = gm
         mod._ssseg_wgrad(x, gy)
-        dx = mod._ssseg_dgrad(gy, x.shape) if ctx.needs_input_grad[0] else None
-        return dx, None, None, None, None
+        pending = _take(ctx.handoff)
+        if not ctx.needs_input_grad[0]:
+            dx = None
+        elif pending is not None:
+            dx = mod._ssseg_dgrad(gy, x.shape, residual=pending)
+        else:
+            dx = mod._ssseg_dgrad(gy, x.shape)
+        return dx, None, None, None, None, None
 
 
 def _bias_grad(mod, gy):
@@ -329,10 +360,10 @@ class Conv2d(nn.Conv2d, _ConvBase):
         return _desc(N=n, H=H, W=W, C=cin, ldx=cin, OH=OH, OW=OW, K=cout, R=R, S=S, sy=sh, sx=sw, dy=dh, dx=dw,
                      py=-ph, px=-pw, outH=OH, outW=OW, osy=1, osx=1, ooy=0, oox=0, ldy=cout, ldw=R * S * cin)
 
-    def forward(self, x):
+    def forward(self, x, handoff=None):
         if not _is_act(x):
             x = to_act(x)
-        return _ConvFn.apply(x, self.weight, self.bias, self, False)
+        return _ConvFn.apply(x, self.weight, self.bias, self, False, handoff)
 
     def forward_relu(self, x):
         """Conv2d followed by ReLU, fused into the GEMM epilogue (unet.py:27-28 with no norm)."""
@@ -453,12 +484,18 @@ class Conv2d(nn.Conv2d, _ConvBase):
         else:
             _ready(self.weight)
 
-    def _ssseg_dgrad(self, gy, xshape):
+    def _ssseg_dgrad(self, gy, xshape, residual=None):
+        """dx of the conv; `residual` (a pending gradient of x, GradHandoff) is added in the epilogue."""
         cin, cout = self._dims()
         n, _, H, W = xshape
         (R, S), (sh, sw), (ph, pw), (dh, dw) = self.kernel_size, self.stride, self.padding, self.dilation
         OH, OW = gy.shape[2], gy.shape[3]
         dx = new_act(n, cin, H, W, _CFG['dtype'], gy.device)
+        if residual is not None:
+            _need_res(residual, dx)
+            if self._ssseg_dw or sh != 1 or sw != 1:
+                raise NotImplementedError('ssseg.nn.Conv2d: fused input-gradient accumulation needs a stride-1 '
+                                          'dense conv')
         if self._ssseg_dw:
             d = self._dw_desc(n, H, W)
             with _Timed(2.0 * n * OH * OW * self.in_channels * R * S, 'dgrad', _tag(self, n, H, W)):
@@ -472,7 +509,8 @@ class Conv2d(nn.Conv2d, _ConvBase):
                       py=ph - (R - 1) * dh, px=pw - (S - 1) * dw, outH=H, outW=W, osy=1, osx=1, ooy=0, oox=0,
                       ldy=cin, ldw=R * S * cout)
             with timer:
-                self._igemm(gy, w, dx, d, N.dt_code(dx))
+                self._igemm(gy, w, dx, d, N.dt_code(dx),
+                            fold=(None, None, residual, None) if residual is not None else None)
             return dx
         timer.__enter__()
         for (phy, ry0, rny, dly, qy) in _phases(sh, ph, R, H, dh):
@@ -605,7 +643,7 @@ def _pad16(C, dtype):
 
 class _BNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, mod, relu):
+    def forward(ctx, x, weight, bias, residual, mod, relu, handoff=None):
         C = mod.num_features
         n, cp, h, w = x.shape
         P = n * h * w
@@ -640,7 +678,7 @@ class _BNFn(torch.autograd.Function):
                P, C, cp, cp, cp, N.dev_ptr(mean), N.dev_ptr(invstd), N.dev_ptr(wt) if wt is not None else None,
                N.dev_ptr(bs) if bs is not None else None, _act(relu)[0], N.dt_code(x), N.stream())
         ctx.save_for_backward(x, residual, mean, invstd)
-        ctx.mod, ctx.relu, ctx.training, ctx.count = mod, relu, training, count
+        ctx.mod, ctx.relu, ctx.training, ctx.count, ctx.handoff = mod, relu, training, count, handoff
         return y
 
     @staticmethod
@@ -677,7 +715,10 @@ class _BNFn(torch.autograd.Function):
                N.dev_ptr(invstd), N.dev_ptr(wt) if wt is not None else None,
                N.dev_ptr(bs) if bs is not None else None, _act(ctx.relu)[0], int(bool(ctx.training)),
                N.dev_ptr(sums), float(count), N.dt_code(x), N.stream())
-        return dx, None, None, dres, None, None
+        if dres is not None and ctx.handoff is not None:
+            ctx.handoff.put(dres)
+            dres = None
+        return dx, None, None, dres, None, None, None
 
 
 class BatchNorm2d(nn.BatchNorm2d):
@@ -704,10 +745,11 @@ class _ConvBNEvalFn(torch.autograd.Function):
     (and the residual's) plus the BN parameter sums in one pass; then the ordinary conv backward."""
 
     @staticmethod
-    def forward(ctx, x, cweight, cbias, gamma, beta, residual, conv, bn, relu):
+    def forward(ctx, x, cweight, cbias, gamma, beta, residual, conv, bn, relu, grad_in=None, grad_out=None):
         y, aux, (scale, mean_eff, invstd) = conv._ssseg_forward(x, relu, bn=bn, residual=residual, keep_pre=True)
         ctx.save_for_backward(x, y, aux, scale, mean_eff, invstd)
         ctx.conv, ctx.bn, ctx.relu, ctx.has_res = conv, bn, relu, residual is not None
+        ctx.grad_in, ctx.grad_out = grad_in, grad_out
         return y
 
     @staticmethod
@@ -735,17 +777,27 @@ class _ConvBNEvalFn(torch.autograd.Function):
                    N.dev_ptr(_grad_of(conv.bias)) if want(conv.bias) else None, N.stream())
             _ready(*[p for p in (bn.weight, bn.bias) if want(p)])
         conv._ssseg_wgrad(x, dconv, bias_grad=False)
-        dx = conv._ssseg_dgrad(dconv, x.shape) if ctx.needs_input_grad[0] else None
-        return dx, None, None, None, None, dres, None, None, None
+        pending = _take(ctx.grad_in)
+        if not ctx.needs_input_grad[0]:
+            dx = None
+        elif pending is not None:
+            dx = conv._ssseg_dgrad(dconv, x.shape, residual=pending)
+        else:
+            dx = conv._ssseg_dgrad(dconv, x.shape)
+        if dres is not None and ctx.grad_out is not None:
+            ctx.grad_out.put(dres)
+            dres = None
+        return dx, None, None, None, None, dres, None, None, None, None, None
 
 
-def conv_bn_act(conv, x, bn, relu=True, residual=None):
+def conv_bn_act(conv, x, bn, relu=True, residual=None, grad_in=None, grad_out=None):
     """act(bn(conv(x)) [+ residual]).  With an eval-mode BatchNorm the BN, residual add and ReLU run in
     the conv's epilogue (ssseg_bn_fold + ssseg_conv_igemm_epi): one kernel, each activation written once.
     Without gradients (the teacher forwards, reference train.py:69-94) that is all; when the eval pass
     is differentiated (the consistency pass) the epilogue also keeps the raw accumulator and
     _ConvBNEvalFn's backward runs the fused BN backward.  Training-mode BN needs the batch statistics
-    of the conv output first, so it runs as conv, then bn_act."""
+    of the conv output first, so it runs as conv, then bn_act.  grad_in / grad_out (a GradHandoff shared by
+    a block's first conv and its residual join) fuse the shortcut gradient into the first conv's dgrad."""
     fusable = (isinstance(conv, (Conv2d, ConvTranspose2d)) and not conv._ssseg_head and isinstance(bn, BatchNorm2d)
                and not bn.training and bn.track_running_stats)
     if fusable:
@@ -753,16 +805,18 @@ def conv_bn_act(conv, x, bn, relu=True, residual=None):
             x = to_act(x)
         if _no_grad(x, conv.weight, conv.bias, bn.weight, bn.bias, residual):
             return conv._ssseg_forward(x, relu, bn=bn, residual=residual)
-        return _ConvBNEvalFn.apply(x, conv.weight, conv.bias, bn.weight, bn.bias, residual, conv, bn, relu)
-    return bn_act(conv(x), bn, relu=relu, residual=residual)
+        return _ConvBNEvalFn.apply(x, conv.weight, conv.bias, bn.weight, bn.bias, residual, conv, bn, relu, grad_in,
+                                   grad_out)
+    y = conv(x, handoff=grad_in) if (grad_in is not None and type(conv) is Conv2d) else conv(x)
+    return bn_act(y, bn, relu=relu, residual=residual, grad_out=grad_out)
 
 
-def bn_act(x, bn, relu=True, residual=None):
+def bn_act(x, bn, relu=True, residual=None, grad_out=None):
     """act(bn(x) [+ residual]) in one pass: ConvBlock's BN+ReLU (unet.py:9-10), Bottleneck's bn3+add+relu."""
     if not isinstance(bn, BatchNorm2d):
         raise TypeError('ssseg.nn.bn_act needs an ssseg BatchNorm2d')
     _need_act(x, rup(bn.num_features, vec()), 'BatchNorm2d')
-    return _BNFn.apply(x, bn.weight, bn.bias, residual, bn, relu)
+    return _BNFn.apply(x, bn.weight, bn.bias, residual, bn, relu, grad_out)
 
 
 # ------------------------------------------------------------------------------------------------
