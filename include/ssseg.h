@@ -370,6 +370,18 @@ int ssseg_att_blend_bwd(const float* gout, const int64_t* g_strides4_host, const
                         const float* att, const int64_t* att_strides4_host, float* glo, float* ghi, float* gatt,
                         int64_t N, int64_t C, int64_t H, int64_t W, ssseg_stream_t stream);
 
+/* Validation metrics (train.validate, train.py:150-195).  logits [B][2][h][w] f32 and mask [B][2][H][W]
+ * f32, arbitrary strides (host arrays of 4 element strides).  pred = argmax(logits) (first max, NaN is
+ * max), nearest-resized to HxW (ATen nearest_idx); t1 = mask[:,1] > 0.5; label = argmax(mask).
+ * counts [B][8] (u64, overwritten): sum(pred1*t1), sum(pred1), sum(t1), inter0, union0, inter1, union1, pixels.
+ * out4[0] = mean_b (2 I_b + 1)/(card_b + 1)            (metrics.dice_metric metrics.py:1-7 + .mean())
+ * out4[1..2] = 100 * IoU of class 0/1, out4[3] = their mean (lovasz.iou lovasz.py:54-73, per_image=False)
+ * total [8] (nullable): running dataset counts; when given, the batch counts are added and out4[1..3]
+ * are computed from the running totals. */
+int ssseg_seg_metrics(const float* logits, const int64_t* l_strides4_host, int64_t h, int64_t w, const float* mask,
+                      const int64_t* m_strides4_host, int64_t B, int64_t H, int64_t W, unsigned long long* counts,
+                      unsigned long long* total, float* out4, ssseg_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -9,6 +9,8 @@
                                     -> lovasz_softmax(classes=[1], per_image=True)  lovasz.py:155-201
   consistency                    <- inline consistency loss                train.py:97-112
   ema_update                     <- mean_teacher.update_ema_variables      mean_teacher.py:5-18
+  seg_metrics                    <- train.validate Dice (train.py:171-176, metrics.py:1-7) + lovasz.iou
+                                    (lovasz.py:54-73)
 """
 import numpy as np
 
@@ -146,3 +148,48 @@ def ema_update(ema, param, alpha):
     t = (ema * F32(alpha)).astype(F32)
     beta = np.float64(F32(1.0 - alpha))
     return (t.astype(np.float64) + param.astype(np.float64) * beta).astype(F32)
+
+
+def _nearest_src(out_size, in_size):
+    """ATen nearest_idx for scale_factor=None (the `F.interpolate(..., mode='nearest')` of
+    reference/train.py:172): identity, exact 2x, else floor(o * float32(in/out)) clamped."""
+    o = np.arange(out_size)
+    if out_size == in_size:
+        return o
+    if out_size == 2 * in_size:
+        return o >> 1
+    scale = np.float32(in_size) / np.float32(out_size)
+    return np.minimum(np.floor(o.astype(np.float32) * scale).astype(np.int64), in_size - 1)
+
+
+def _argmax2(a0, a1):
+    """torch.argmax over 2 channels: first maximum wins, NaN is the maximum."""
+    return np.where(np.isnan(a0), 0, np.where(np.isnan(a1), 1, (a1 > a0).astype(np.int64)))
+
+
+def seg_metrics(logits, mask):
+    """train.validate's metric (reference/train.py:171-176 + metrics.dice_metric metrics.py:1-7) and
+    lovasz.iou(pred, argmax(mask), C=2) (lovasz.py:54-73, per_image=False) on the same predictions.
+    logits [B,2,h,w], mask [B,2,H,W] -> (dice [B] f32, ious [2] f64 x100, counts [B,8] int64)."""
+    logits = np.asarray(logits, np.float32)
+    mask = np.asarray(mask, np.float32)
+    B, _, h, w = logits.shape
+    H, W = mask.shape[2:]
+    pred_lo = _argmax2(logits[:, 0], logits[:, 1])
+    pred = pred_lo[:, _nearest_src(H, h)][:, :, _nearest_src(W, w)]
+    t1 = (mask[:, 1] > 0.5).astype(np.int64)
+    label = _argmax2(mask[:, 0], mask[:, 1])
+    counts = np.zeros((B, 8), np.int64)
+    counts[:, 0] = (pred * t1).reshape(B, -1).sum(1)
+    counts[:, 1] = pred.reshape(B, -1).sum(1)
+    counts[:, 2] = t1.reshape(B, -1).sum(1)
+    for c in range(2):
+        counts[:, 3 + 2 * c] = ((label == c) & (pred == c)).reshape(B, -1).sum(1)
+        counts[:, 4 + 2 * c] = ((label == c) | (pred == c)).reshape(B, -1).sum(1)
+    counts[:, 7] = H * W
+    inter = counts[:, 0].astype(np.float32)
+    card = counts[:, 1].astype(np.float32) + counts[:, 2].astype(np.float32)
+    dice = (np.float32(2) * inter + np.float32(1)) / (card + np.float32(1))
+    tot = counts.sum(0)
+    ious = np.array([tot[3] / tot[4] if tot[4] else 1., tot[5] / tot[6] if tot[6] else 1.]) * 100
+    return dice.astype(np.float32), ious, counts

@@ -242,3 +242,33 @@ def att_blend(lo, hi, att_logits):
     """lo*sigmoid(a) + hi*(1-sigmoid(a)) (MultiscaleAttention, multiscale_attention.py:52-54); fp32 NCHW
     tensors of any strides, att [N,1,H,W] pre-sigmoid; returns contiguous NCHW."""
     return _AttBlend.apply(lo, hi, att_logits)
+
+
+# ------------------------------------------------------------------------------------------------
+# Validation metrics (train.validate, train.py:150-195)
+# ------------------------------------------------------------------------------------------------
+class SegMetrics:
+    """Dice (metrics.dice_metric on the nearest-resized argmax one-hot, train.py:178-186) and the
+    confusion counts of lovasz.iou (lovasz.py:54-73, C=2, per_image=False) in one pass per batch.
+    `update(logits, mask)` returns a device tensor [dice_mean, iou0, iou1, miou]; the IoUs are over every
+    batch seen so far (running counts on the device)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.total = torch.zeros(8, dtype=torch.int64, device=self.device)
+
+    def update(self, logits, mask):
+        if logits.dim() != 4 or logits.shape[1] != 2 or mask.dim() != 4 or mask.shape[1] != 2:
+            raise ValueError('SegMetrics: binary [B,2,h,w] logits and [B,2,H,W] mask expected')
+        if logits.shape[0] != mask.shape[0]:
+            raise ValueError('SegMetrics: batch size mismatch')
+        logits = logits if logits.dtype == torch.float32 else logits.float()
+        mask = mask if mask.dtype == torch.float32 else mask.float()
+        B, _, h, w = logits.shape
+        H, W = mask.shape[2:]
+        counts = torch.empty(B, 8, dtype=torch.int64, device=logits.device)
+        out = torch.empty(4, dtype=torch.float32, device=logits.device)
+        N.call('ssseg_seg_metrics', N.dev_ptr(logits, 'logits'), N.strides4(logits), h, w, N.dev_ptr(mask, 'mask'),
+               N.strides4(mask), B, H, W, N.dev_ptr(counts), N.dev_ptr(self.total), N.dev_ptr(out), N.stream())
+        self.counts = counts
+        return out

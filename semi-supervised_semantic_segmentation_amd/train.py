@@ -124,27 +124,40 @@ def train(model, ema_model, optimizer, dataloader, unsupervised_dataloader, epoc
 
 
 def validate(model, dataloader, epoch, initial_step, summary_writer, config, device):
-    """train.py:150-195 (Dice on the argmax one-hot; validation is outside the MI355X hot path)."""
+    """train.py:150-195: Dice on the nearest-resized argmax one-hot (the reference metric) plus mIoU over the
+    whole validation set (lovasz.iou, lovasz.py:54-73) from the same device pass (ssseg_seg_metrics)."""
     model.eval()
     avg_loss, avg_metric = utils.AverageMeter(), utils.AverageMeter()
     rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
     world = _world()
+    seg = None
     with torch.no_grad():
         for sample in dataloader:
+            if seg is None:
+                seg = ops.SegMetrics(device)
             image = sample['image'].to(device)
             mask = sample['semantic_mask'].to(device)
             features, pred_maps = model(image)
             loss = config['train']['loss'](pred_maps, mask)
-            logits = pred_maps[-1]
-            one_hot = torch.nn.functional.one_hot(torch.argmax(logits, dim=1), num_classes=2).permute(0, 3, 1, 2)
-            pred_bin = torch.nn.functional.interpolate(one_hot.float(), size=mask.size()[2:4], mode='nearest')
-            metric = metrics.dice_metric(pred_bin[:, 1:], (mask > 0.5).to(mask)[:, 1:]).mean()
+            # argmax -> one-hot -> nearest resize -> dice (train.py:178-186) + lovasz.iou counts: one kernel
+            res = seg.update(pred_maps[-1], mask)
+            metric = res[0:1].clone()[0]
             avg_loss.update(utils.reduce_tensor(loss.clone()) / world)
-            avg_metric.update(utils.reduce_tensor(metric.clone()) / world)
+            avg_metric.update(utils.reduce_tensor(metric) / world)
+    miou = None
+    if seg is not None:
+        total = seg.total.clone()
+        if world > 1:
+            torch.distributed.all_reduce(total)
+        t = total.double()
+        ious = [float(t[3] / t[4]) if t[4] else 1., float(t[5] / t[6]) if t[6] else 1.]
+        miou = 100. * sum(ious) / 2
     if rank == 0:
-        print(f'Eval: Epoch: {epoch} Val loss: {avg_loss.average()} Val metric: {avg_metric.average()}')
+        print(f'Eval: Epoch: {epoch} Val loss: {avg_loss.average()} Val metric: {avg_metric.average()} mIoU: {miou}')
         if summary_writer is not None:
             summary_writer.add_scalar('val_loss_avg', avg_loss.average(), initial_step)
             summary_writer.add_scalar('val_dice', avg_metric.average(), initial_step)
+            if miou is not None:
+                summary_writer.add_scalar('val_miou', miou, initial_step)
     model.train()
     return avg_loss.average(), avg_metric.average()

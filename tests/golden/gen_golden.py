@@ -15,11 +15,14 @@ Fixture index:
   G5  ema.npz           update_ema_variables                              (reference/mean_teacher.py:5-18)
   G6  model_*.npz       SimpleUNet / UNet(MobileNetV2) forwards            (reference/models/*.py)
   G7  trainsteps.npz    3 steps of train.train on a tiny SimpleUNet (DDP, gloo world 1)
+  G9  metrics_*.npz     train.validate's Dice (argmax one-hot -> nearest resize -> metrics.dice_metric) and
+                        lovasz.iou on the same predictions                 (reference/train.py:171-176,
+                        metrics.py:1-7, lovasz.py:54-73)
   G6b model2_*.npz      HarDNet / Discriminator / MultiscaleFeatureDiscriminator / MultiscaleAttention(HRNet)
                         forwards (eval + train), input + selected parameter gradients, BN buffers; weights are
                         seeded (tests/seeded.py) and pinned by a state_dict SHA-256 instead of stored
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py [all | models2]
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py [all | models2 | metrics]
 """
 import os
 import sys
@@ -42,6 +45,7 @@ import cowmix  # noqa: E402  (reference)
 import losses  # noqa: E402
 import lovasz  # noqa: E402
 import mean_teacher  # noqa: E402
+import metrics  # noqa: E402
 import train as ref_train  # noqa: E402
 from models import simple_unet, unet  # noqa: E402
 from models.encoders import mobilenetv2  # noqa: E402
@@ -434,7 +438,36 @@ def gen_models2():
         save(f'model2_{tag}.npz', **d)
 
 
+# ----------------------------------------------------------------------------------------------
+# G9: validation metrics (Dice + IoU)
+# ----------------------------------------------------------------------------------------------
+def gen_metrics():
+    cases = {'a': (3, (33, 47), (64, 80)), 'b': (2, (32, 32), (64, 64)), 'c': (2, (16, 16), (16, 16))}
+    for tag, (B, (h, w), (H, W)) in cases.items():
+        g = torch.Generator().manual_seed(41 + ord(tag))
+        logits = torch.randn(B, 2, h, w, generator=g)
+        logits[:, 1, :3, :] = logits[:, 0, :3, :]            # ties: argmax keeps class 0
+        soft = torch.rand(B, 1, H, W, generator=g)
+        soft[:, :, :2, :] = 0.5                               # mask ties: label 0, t1 = 0
+        soft[0] = soft[0] * 0.4                               # an image with no foreground
+        mask = torch.cat([1 - soft, soft], dim=1)
+        # reference/train.py:171-176
+        one_hot = torch.nn.functional.one_hot(torch.argmax(logits, dim=1), num_classes=2).permute(
+            dims=(0, 3, 1, 2)).to(logits)
+        pred_bin = torch.nn.functional.interpolate(one_hot, size=mask.size()[2:4], mode='nearest')
+        mask_bin = (mask > 0.5).to(mask)
+        dice = metrics.dice_metric(pred_bin[:, 1:], mask_bin[:, 1:])
+        pred = torch.argmax(pred_bin, dim=1)
+        label = torch.argmax(mask, dim=1)
+        ious = lovasz.iou(pred, label, 2)
+        save(f'metrics_{tag}.npz', logits=logits, mask=mask, dice=dice, dice_mean=dice.mean(),
+             ious=np.asarray(ious, dtype=np.float64))
+
+
 if __name__ == '__main__':
+    if len(sys.argv) > 1 and sys.argv[1] == 'metrics':
+        gen_metrics()
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == 'models2':
         gen_models2()
         sys.exit(0)
@@ -446,3 +479,4 @@ if __name__ == '__main__':
     gen_models()
     gen_trainsteps()
     gen_models2()
+    gen_metrics()

@@ -214,3 +214,46 @@ def test_lovasz_ties_loss_invariant(hip_device):
                 np.testing.assert_allclose((-grad[b, 1][m] / sg[b][m]).sum(), (-ref_g[b, 1][m] / sg[b][m]).sum(),
                                            rtol=1e-4, atol=1e-5)
     assert np.all(grad[:, 0] == 0)
+
+
+@pytest.mark.parametrize('tag', ['a', 'b', 'c'])
+def test_seg_metrics_vs_reference_golden(hip_device, tag):
+    """G9 on the device (ssseg_seg_metrics): per-image counts bit-exact with the oracle, Dice bit-exact
+    with the reference's fp32 values, mean Dice within 1e-6 (fp64 vs fp32 mean), IoU within 1e-5; the
+    logits are handed over as a strided 2-channel view of an 8-channel NHWC buffer (the heads' layout)."""
+    g = golden(f'metrics_{tag}.npz')
+    dev = hip_device
+    B, _, h, w = g['logits'].shape
+    phys = torch.zeros(B, h, w, 8, device=dev)
+    phys[..., :2] = torch.from_numpy(g['logits']).to(dev).permute(0, 2, 3, 1)
+    logits = phys.permute(0, 3, 1, 2)[:, :2]
+    seg = ops().SegMetrics(dev)
+    out = seg.update(logits, torch.from_numpy(g['mask']).to(dev)).cpu().numpy()
+    _, _, counts = losses_ref.seg_metrics(g['logits'], g['mask'])
+    np.testing.assert_array_equal(seg.counts.cpu().numpy(), counts)
+    np.testing.assert_allclose(out[0], float(g['dice_mean']), rtol=1e-6)
+    np.testing.assert_allclose(out[1:3], g['ious'], rtol=1e-5)
+    np.testing.assert_allclose(out[3], g['ious'].mean(), rtol=1e-5)
+
+
+def test_seg_metrics_running_totals_and_nan(hip_device):
+    """Running dataset counts across batches (mIoU over the whole validation set), NaN logits follow
+    torch.argmax (NaN is the maximum), 512x512 masks from 256x256 logits (the UNet /2 head)."""
+    dev = hip_device
+    g = torch.Generator().manual_seed(5)
+    seg = ops().SegMetrics(dev)
+    all_counts = []
+    for i in range(3):
+        logits = torch.randn(4, 2, 256, 256, generator=g)
+        logits[0, 0, 0, :7] = float('nan')
+        logits[1, 1, 3, :5] = float('nan')
+        soft = torch.rand(4, 1, 512, 512, generator=g)
+        mask = torch.cat([1 - soft, soft], 1)
+        out = seg.update(logits.to(dev), mask.to(dev)).cpu().numpy()
+        dice, _, counts = losses_ref.seg_metrics(logits.numpy(), mask.numpy())
+        np.testing.assert_array_equal(seg.counts.cpu().numpy(), counts)
+        np.testing.assert_allclose(out[0], dice.astype(np.float64).mean(), rtol=1e-6)
+        all_counts.append(counts)
+    tot = np.concatenate(all_counts).sum(0)
+    np.testing.assert_array_equal(seg.total.cpu().numpy(), tot)
+    np.testing.assert_allclose(out[1:3], [100 * tot[3] / tot[4], 100 * tot[5] / tot[6]], rtol=1e-5)

@@ -136,3 +136,13 @@ def test_trainsteps():
     for k in sd_s:
         np.testing.assert_allclose(sd_s[k].numpy(), g['final_s.' + k], rtol=1e-4, atol=1e-6)
         np.testing.assert_allclose(sd_t[k].numpy(), g['final_t.' + k], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize('tag', ['a', 'b', 'c'])
+def test_seg_metrics_vs_reference_golden(tag):
+    """G9: validation Dice (reference train.py:171-176, metrics.py:1-7) and lovasz.iou, with ties in the
+    logits and the mask, an all-background image, and non-integer / 2x / identity nearest resizes."""
+    g = golden(f'metrics_{tag}.npz')
+    dice, ious, _ = losses_ref.seg_metrics(g['logits'], g['mask'])
+    np.testing.assert_array_equal(dice, g['dice'].reshape(-1))
+    np.testing.assert_allclose(ious, g['ious'], rtol=1e-12)
