@@ -382,6 +382,10 @@ int ssseg_seg_metrics(const float* logits, const int64_t* l_strides4_host, int64
                       const int64_t* m_strides4_host, int64_t B, int64_t H, int64_t W, unsigned long long* counts,
                       unsigned long long* total, float* out4, ssseg_stream_t stream);
 
+/* InferenceWrapper head (models/inference_wrapper.py:17-24): logits contiguous [B][2][HW] f32 ->
+ * prob = sigmoid(logits), onehot = one_hot(argmax_c logits) (first max, NaN is max), both [B][2][HW] f32. */
+int ssseg_prob_onehot(const float* logits, int64_t B, int64_t HW, float* prob, float* onehot, ssseg_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,6 +11,7 @@
   ema_update                     <- mean_teacher.update_ema_variables      mean_teacher.py:5-18
   seg_metrics                    <- train.validate Dice (train.py:171-176, metrics.py:1-7) + lovasz.iou
                                     (lovasz.py:54-73)
+  inference_head                 <- models/inference_wrapper.py:14-24
 """
 import numpy as np
 
@@ -193,3 +194,13 @@ def seg_metrics(logits, mask):
     tot = counts.sum(0)
     ious = np.array([tot[3] / tot[4] if tot[4] else 1., tot[5] / tot[6] if tot[6] else 1.]) * 100
     return dice.astype(np.float32), ious, counts
+
+
+def inference_head(logits, size):
+    """models/inference_wrapper.py:14-24 on the first logit map [1,2,h,w]: bilinear (align_corners=False) to
+    `size`, sigmoid probabilities, one-hot of the argmax -> (binary_mask [2,H,W], probabilities [2,H,W])."""
+    hi = bilinear(logits, size, align_corners=False)
+    prob = sigmoid(hi)
+    cls = _argmax2(hi[:, 0], hi[:, 1])
+    onehot = np.stack([(cls == 0), (cls == 1)], 1).astype(F32)
+    return onehot[0], prob[0].astype(F32)

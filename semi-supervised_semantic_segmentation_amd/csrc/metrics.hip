@@ -112,6 +112,23 @@ __global__ void seg_metrics_final_kernel(const unsigned long long* __restrict__ 
   out[3] = 0.5f * (out[1] + out[2]);
 }
 
+// InferenceWrapper head (models/inference_wrapper.py:17-24): probabilities = sigmoid(logits) and the
+// one-hot of argmax over 2 channels, for contiguous [B][2][HW] fp32 logits; 8 B read + 16 B written / px.
+__global__ void prob_onehot_kernel(const float* __restrict__ logits, int64_t B, int64_t HW, float* __restrict__ prob,
+                                   float* __restrict__ onehot) {
+  const int64_t n = B * HW;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = i / HW, p = i - b * HW;
+    const int64_t o0 = b * 2 * HW + p, o1 = o0 + HW;
+    const float l0 = logits[o0], l1 = logits[o1];
+    prob[o0] = 1.f / (1.f + expf(-l0));
+    prob[o1] = 1.f / (1.f + expf(-l1));
+    const int c = argmax2(l0, l1);
+    onehot[o0] = c == 0 ? 1.f : 0.f;
+    onehot[o1] = c == 1 ? 1.f : 0.f;
+  }
+}
+
 }  // namespace
 
 extern "C" int ssseg_seg_metrics(const float* logits, const int64_t* lstride, int64_t h, int64_t w,
@@ -132,6 +149,18 @@ extern "C" int ssseg_seg_metrics(const float* logits, const int64_t* lstride, in
                      mstride[3], H, W, counts);
   hipLaunchKernelGGL(seg_metrics_final_kernel, dim3(1), dim3(64), 0, s, (const unsigned long long*)counts, B, total,
                      out4);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_prob_onehot(const float* logits, int64_t B, int64_t HW, float* prob, float* onehot,
+                                 ssseg_stream_t stream) {
+  if (!logits || !prob || !onehot || B <= 0 || HW <= 0) return SSSEG_EINVAL;
+  const int64_t n = B * HW;
+  int64_t nb = (n + 255) / 256;
+  if (nb > 8192) nb = 8192;
+  hipLaunchKernelGGL(prob_onehot_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, logits, B, HW, prob,
+                     onehot);
   SSSEG_LAUNCH_CHECK();
   return 0;
 }

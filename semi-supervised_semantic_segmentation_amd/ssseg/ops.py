@@ -272,3 +272,14 @@ class SegMetrics:
                N.strides4(mask), B, H, W, N.dev_ptr(counts), N.dev_ptr(self.total), N.dev_ptr(out), N.stream())
         self.counts = counts
         return out
+
+
+def prob_onehot(logits):
+    """sigmoid probabilities + one-hot argmax mask of binary logits [B,2,H,W] (inference_wrapper.py:17-24)."""
+    if logits.dim() != 4 or logits.shape[1] != 2:
+        raise ValueError('prob_onehot: binary [B,2,H,W] logits expected')
+    x = _c(logits.float())
+    prob, onehot = torch.empty_like(x), torch.empty_like(x)
+    B, _, H, W = x.shape
+    N.call('ssseg_prob_onehot', N.dev_ptr(x, 'logits'), B, H * W, N.dev_ptr(prob), N.dev_ptr(onehot), N.stream())
+    return prob, onehot

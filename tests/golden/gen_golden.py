@@ -18,6 +18,7 @@ Fixture index:
   G9  metrics_*.npz     train.validate's Dice (argmax one-hot -> nearest resize -> metrics.dice_metric) and
                         lovasz.iou on the same predictions                 (reference/train.py:171-176,
                         metrics.py:1-7, lovasz.py:54-73)
+  G10 inference.npz    models.inference_wrapper.InferenceWrapper on a stub model (reference/models/inference_wrapper.py)
   G6b model2_*.npz      HarDNet / Discriminator / MultiscaleFeatureDiscriminator / MultiscaleAttention(HRNet)
                         forwards (eval + train), input + selected parameter gradients, BN buffers; weights are
                         seeded (tests/seeded.py) and pinned by a state_dict SHA-256 instead of stored
@@ -464,9 +465,29 @@ def gen_metrics():
              ious=np.asarray(ious, dtype=np.float64))
 
 
+# ----------------------------------------------------------------------------------------------
+# G10: InferenceWrapper
+# ----------------------------------------------------------------------------------------------
+def gen_inference():
+    from models.inference_wrapper import InferenceWrapper
+
+    g = torch.Generator().manual_seed(51)
+    logits = torch.randn(1, 2, 37, 50, generator=g) * 3
+    logits[0, 1, :2] = logits[0, 0, :2]                       # ties -> class 0
+
+    class Stub(nn.Module):
+        def forward(self, image):
+            return [image], [logits, logits[:, :, ::2, ::2]]
+
+    image = torch.rand(3, 75, 101, generator=g)
+    mask, prob = InferenceWrapper(Stub())(image)
+    save('inference.npz', logits=logits, image_hw=np.asarray([75, 101]), mask=mask, prob=prob)
+
+
 if __name__ == '__main__':
     if len(sys.argv) > 1 and sys.argv[1] == 'metrics':
         gen_metrics()
+        gen_inference()
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == 'models2':
         gen_models2()
@@ -480,3 +501,4 @@ if __name__ == '__main__':
     gen_trainsteps()
     gen_models2()
     gen_metrics()
+    gen_inference()

@@ -257,3 +257,27 @@ def test_seg_metrics_running_totals_and_nan(hip_device):
     tot = np.concatenate(all_counts).sum(0)
     np.testing.assert_array_equal(seg.total.cpu().numpy(), tot)
     np.testing.assert_allclose(out[1:3], [100 * tot[3] / tot[4], 100 * tot[5] / tot[6]], rtol=1e-5)
+
+
+def test_inference_wrapper_vs_reference_golden(hip_device):
+    """G10 through the drop-in models.inference_wrapper.InferenceWrapper (device bilinear + ssseg_prob_onehot):
+    one-hot mask bit-exact with the reference except where the resized logits tie within 1e-5, sigmoid
+    probabilities within 5e-6 (fp32 bilinear + sigmoid rounding on logits of magnitude ~10)."""
+    from models.inference_wrapper import InferenceWrapper
+    g = golden('inference.npz')
+    dev = hip_device
+    logits = torch.from_numpy(g['logits']).to(dev)
+
+    class Stub(torch.nn.Module):
+        def forward(self, image):
+            return [image], [logits, logits[:, :, ::2, ::2]]
+
+    H, W = (int(v) for v in g['image_hw'])
+    mask, prob = InferenceWrapper(Stub())(torch.rand(3, H, W, device=dev))
+    assert mask.shape == (2, H, W) and prob.shape == (2, H, W)
+    prob = prob.cpu().numpy()
+    np.testing.assert_allclose(prob, g["prob"], rtol=0, atol=5e-6)
+    hi = losses_ref.bilinear(g['logits'], (H, W))[0]
+    band = np.abs(hi[1] - hi[0]) < 1e-5
+    diff = (mask.cpu().numpy() != g['mask']).any(0)
+    assert not (diff & ~band).any()

@@ -146,3 +146,12 @@ def test_seg_metrics_vs_reference_golden(tag):
     dice, ious, _ = losses_ref.seg_metrics(g['logits'], g['mask'])
     np.testing.assert_array_equal(dice, g['dice'].reshape(-1))
     np.testing.assert_allclose(ious, g['ious'], rtol=1e-12)
+
+
+def test_inference_head_vs_reference_golden():
+    """G10: reference InferenceWrapper (bilinear to the image size, sigmoid, argmax one-hot) on stub logits;
+    probabilities within 5e-6 (fp32 rounding of the resize)."""
+    g = golden('inference.npz')
+    mask, prob = losses_ref.inference_head(g['logits'], tuple(int(v) for v in g['image_hw']))
+    np.testing.assert_array_equal(mask, g['mask'])
+    np.testing.assert_allclose(prob, g["prob"], rtol=0, atol=5e-6)
