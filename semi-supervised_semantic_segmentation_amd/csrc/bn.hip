@@ -185,20 +185,23 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x
   }
 }
 
-// sums over the per-block partials: block = 8 channels x 32 partial lanes, two accumulator chains per
-// lane, then a fixed-order LDS reduction (deterministic)
+// sums over the per-block partials: block = CH channels x (256/CH) partial lanes, two accumulator chains
+// per lane, then a fixed-order LDS reduction (deterministic).  Narrow channel groups (CH = 2, 4) put more
+// workgroups and shorter load chains on the small-C layers, whose partial count is the largest.
+template <int CH>
 __global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* part, int nparts, int C, double* sums) {
-  __shared__ double red[2][32][8];
-  const int cl = threadIdx.x & 7, pl = threadIdx.x >> 3;
-  const int c = blockIdx.x * 8 + cl;
+  constexpr int LN = 256 / CH;
+  __shared__ double red[2][LN][CH];
+  const int cl = threadIdx.x % CH, pl = threadIdx.x / CH;
+  const int c = blockIdx.x * CH + cl;
   double a0 = 0, a1 = 0, b0 = 0, b1 = 0;
   if (c < C) {
     int i = pl;
-    for (; i + 32 < nparts; i += 64) {
+    for (; i + LN < nparts; i += 2 * LN) {
       a0 += part[(int64_t)(2 * i) * C + c];
       b0 += part[(int64_t)(2 * i + 1) * C + c];
-      a1 += part[(int64_t)(2 * (i + 32)) * C + c];
-      b1 += part[(int64_t)(2 * (i + 32) + 1) * C + c];
+      a1 += part[(int64_t)(2 * (i + LN)) * C + c];
+      b1 += part[(int64_t)(2 * (i + LN) + 1) * C + c];
     }
     if (i < nparts) {
       a0 += part[(int64_t)(2 * i) * C + c];
@@ -210,13 +213,26 @@ __global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* par
   __syncthreads();
   if (pl == 0 && c < C) {
     double a = 0, b = 0;
-    for (int k = 0; k < 32; ++k) {
+    for (int k = 0; k < LN; ++k) {
       a += red[0][k][cl];
       b += red[1][k][cl];
     }
     sums[c] = a;
     sums[C + c] = b;
   }
+}
+
+// one launch of the partial reduction: channel group narrowed until the grid has >= 64 workgroups
+static void launch_partial_final(const double* part, int64_t nparts, int64_t C, double* sums, hipStream_t s) {
+  if (C >= 512 || nparts < 256)
+    hipLaunchKernelGGL(bn_partial_final_kernel<8>, dim3((unsigned)((C + 7) / 8)), dim3(256), 0, s, part, (int)nparts,
+                       (int)C, sums);
+  else if (C >= 128)
+    hipLaunchKernelGGL(bn_partial_final_kernel<4>, dim3((unsigned)((C + 3) / 4)), dim3(256), 0, s, part, (int)nparts,
+                       (int)C, sums);
+  else
+    hipLaunchKernelGGL(bn_partial_final_kernel<2>, dim3((unsigned)((C + 1) / 2)), dim3(256), 0, s, part, (int)nparts,
+                       (int)C, sums);
 }
 
 __global__ void bn_finalize_kernel(const double* sums, int C, double count, float eps, float momentum, float* mean_out,
@@ -497,8 +513,7 @@ void run_partials(const T* x, const T* dy, const T* res, int64_t P, int64_t C, i
   const int64_t gx = pixel_blocks(P, L, MAXG);
   hipLaunchKernelGGL((bn_partial_kernel<T, V, MODE>), dim3((unsigned)gx, L.cblocks), dim3(256), 0, s, x, dy, res, P,
                      (int)C, ldx, lddy, ldr, L, prm, relu, (double*)ws);
-  hipLaunchKernelGGL(bn_partial_final_kernel, dim3((C + 7) / 8), dim3(256), 0, s, (const double*)ws, (int)gx,
-                     (int)C, sums);
+  launch_partial_final((const double*)ws, gx, C, sums, s);
 }
 
 template <typename T, int MODE>
@@ -615,8 +630,7 @@ static void eval_bwd(const T* dy, const T* y, const T* aux, T* dconv, T* dres, i
   else
     hipLaunchKernelGGL((bn_eval_bwd_kernel<T, V16 / 2>), dim3((unsigned)gx, L.cblocks), dim3(256), 0, s, dy, y, aux,
                        dconv, dres, P, (int)C, ld, L, scale, mean_eff, invstd, relu, (double*)ws);
-  hipLaunchKernelGGL(bn_partial_final_kernel, dim3((C + 7) / 8), dim3(256), 0, s, (const double*)ws, (int)gx, (int)C,
-                     sums);
+  launch_partial_final((const double*)ws, gx, C, sums, s);
 }
 
 extern "C" int ssseg_bn_eval_bwd(const void* dy, const void* y, const void* aux, void* dconv, void* dres, int64_t P,
