@@ -260,6 +260,12 @@ int ssseg_bn_stats(const void* x, int64_t P, int64_t C, int64_t ldx, int dt, dou
 int ssseg_bn_finalize(const double* sums, int64_t C, double count, float eps, float momentum, float* mean_out,
                       float* invstd_out, float* running_mean, float* running_var, int64_t* num_batches_tracked,
                       ssseg_stream_t stream);
+/* ssseg_bn_stats + ssseg_bn_finalize in one pass (the finalize runs in the reduction's tail): the
+ * single-process / non-synchronised training BatchNorm (SyncBN all-reduces sums in between instead). */
+int ssseg_bn_stats_finalize(const void* x, int64_t P, int64_t C, int64_t ldx, int dt, double* sums, void* ws,
+                            size_t ws_bytes, double count, float eps, float momentum, float* mean_out, float* invstd_out,
+                            float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                            ssseg_stream_t stream);
 /* eval mode: mean = running_mean, invstd = 1/sqrt(running_var + eps) */
 int ssseg_bn_eval_params(const float* running_mean, const float* running_var, float eps, int64_t C, float* mean_out,
                          float* invstd_out, ssseg_stream_t stream);
@@ -304,6 +310,12 @@ int ssseg_bn_bwd_reduce(const void* dy, const void* x, const void* residual, int
                         ssseg_stream_t stream);
 /* dgamma += sums[C:2C], dbeta += sums[0:C] (local sums, before any SyncBN all-reduce) */
 int ssseg_bn_param_grad(const double* sums, int64_t C, float* dgamma, float* dbeta, ssseg_stream_t stream);
+/* ssseg_bn_bwd_reduce + ssseg_bn_param_grad fused (param grads from the local sums in the reduction's tail;
+ * dgamma / dbeta may be NULL) */
+int ssseg_bn_bwd_reduce_grad(const void* dy, const void* x, const void* residual, int64_t P, int64_t C, int64_t ldx,
+                             int64_t ldr, int64_t lddy, const float* mean, const float* invstd, const float* gamma,
+                             const float* beta, int relu, int dt, double* sums, void* ws, size_t ws_bytes,
+                             float* dgamma, float* dbeta, ssseg_stream_t stream);
 /* backward pass 2: dx = gamma*invstd*(dyr - [train]*(sum_dyr + xhat*sum_dyr_xhat)/count); dres = dyr;
  * padding channels of dx / dres written 0 as in ssseg_bn_apply */
 int ssseg_bn_bwd_apply(const void* dy, const void* x, const void* residual, void* dx, void* dres, int64_t P, int64_t C,

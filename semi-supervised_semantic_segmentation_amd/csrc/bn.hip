@@ -185,12 +185,39 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x
   }
 }
 
+// optional per-channel tail of the partial reduction (saves one tiny launch per BN layer):
+// 1 = training-mode finalize (mean/invstd + running stats, bn_finalize_kernel's math), 2 = param grads
+struct FinalEpi {
+  int mode;
+  double count;
+  float eps, momentum;
+  float *mean_out, *invstd_out, *rmean, *rvar;
+  int64_t* nbt;
+  float *dgamma, *dbeta;
+};
+
+__device__ __forceinline__ void finalize_channel(double s1, double s2, int c, double count, float eps, float momentum,
+                                                 float* mean_out, float* invstd_out, float* rmean, float* rvar) {
+  const double mean = s1 / count;
+  double var = s2 / count - mean * mean;
+  var = var < 0 ? 0 : var;
+  mean_out[c] = (float)mean;
+  invstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (rmean) {
+    const double unb = count > 1 ? var * count / (count - 1) : var;
+    rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+    rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+  }
+}
+
 // sums over the per-block partials: block = CH channels x (256/CH) partial lanes, two accumulator chains
 // per lane, then a fixed-order LDS reduction (deterministic).  Narrow channel groups (CH = 2, 4) put more
 // workgroups and shorter load chains on the small-C layers, whose partial count is the largest.
 template <int CH>
-__global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* part, int nparts, int C, double* sums) {
+__global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* part, int nparts, int C, double* sums,
+                                                               FinalEpi fe) {
   constexpr int LN = 256 / CH;
+  if (fe.mode == 1 && fe.nbt && blockIdx.x == 0 && threadIdx.x == 0) *fe.nbt += 1;
   __shared__ double red[2][LN][CH];
   const int cl = threadIdx.x % CH, pl = threadIdx.x / CH;
   const int c = blockIdx.x * CH + cl;
@@ -219,20 +246,27 @@ __global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* par
     }
     sums[c] = a;
     sums[C + c] = b;
+    if (fe.mode == 1) {
+      finalize_channel(a, b, c, fe.count, fe.eps, fe.momentum, fe.mean_out, fe.invstd_out, fe.rmean, fe.rvar);
+    } else if (fe.mode == 2) {
+      if (fe.dbeta) fe.dbeta[c] += (float)a;
+      if (fe.dgamma) fe.dgamma[c] += (float)b;
+    }
   }
 }
 
 // one launch of the partial reduction: channel group narrowed until the grid has >= 64 workgroups
-static void launch_partial_final(const double* part, int64_t nparts, int64_t C, double* sums, hipStream_t s) {
+static void launch_partial_final(const double* part, int64_t nparts, int64_t C, double* sums, hipStream_t s,
+                                 FinalEpi fe = FinalEpi{}) {
   if (C >= 512 || nparts < 256)
     hipLaunchKernelGGL(bn_partial_final_kernel<8>, dim3((unsigned)((C + 7) / 8)), dim3(256), 0, s, part, (int)nparts,
-                       (int)C, sums);
+                       (int)C, sums, fe);
   else if (C >= 128)
     hipLaunchKernelGGL(bn_partial_final_kernel<4>, dim3((unsigned)((C + 3) / 4)), dim3(256), 0, s, part, (int)nparts,
-                       (int)C, sums);
+                       (int)C, sums, fe);
   else
     hipLaunchKernelGGL(bn_partial_final_kernel<2>, dim3((unsigned)((C + 1) / 2)), dim3(256), 0, s, part, (int)nparts,
-                       (int)C, sums);
+                       (int)C, sums, fe);
 }
 
 __global__ void bn_finalize_kernel(const double* sums, int C, double count, float eps, float momentum, float* mean_out,
@@ -240,16 +274,7 @@ __global__ void bn_finalize_kernel(const double* sums, int C, double count, floa
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c == 0 && nbt) *nbt += 1;
   if (c >= C) return;
-  const double mean = sums[c] / count;
-  double var = sums[C + c] / count - mean * mean;
-  var = var < 0 ? 0 : var;
-  mean_out[c] = (float)mean;
-  invstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
-  if (rmean) {
-    const double unb = count > 1 ? var * count / (count - 1) : var;
-    rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
-    rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
-  }
+  finalize_channel(sums[c], sums[C + c], c, count, eps, momentum, mean_out, invstd_out, rmean, rvar);
 }
 
 __global__ void bn_eval_params_kernel(const float* rmean, const float* rvar, float eps, int C, float* mean_out,
@@ -508,22 +533,22 @@ static bool wide_ok(int64_t C, std::initializer_list<int64_t> lds) {
 
 template <typename T, int V, int MODE>
 void run_partials(const T* x, const T* dy, const T* res, int64_t P, int64_t C, int64_t ldx, int64_t lddy, int64_t ldr,
-                  ChanParams prm, int relu, double* sums, void* ws, hipStream_t s) {
+                  ChanParams prm, int relu, double* sums, void* ws, hipStream_t s, FinalEpi fe) {
   const Layout L = layout_for(C, V);
   const int64_t gx = pixel_blocks(P, L, MAXG);
   hipLaunchKernelGGL((bn_partial_kernel<T, V, MODE>), dim3((unsigned)gx, L.cblocks), dim3(256), 0, s, x, dy, res, P,
                      (int)C, ldx, lddy, ldr, L, prm, relu, (double*)ws);
-  launch_partial_final((const double*)ws, gx, C, sums, s);
+  launch_partial_final((const double*)ws, gx, C, sums, s, fe);
 }
 
 template <typename T, int MODE>
 void partials(const T* x, const T* dy, const T* res, int64_t P, int64_t C, int64_t ldx, int64_t lddy, int64_t ldr,
-              ChanParams prm, int relu, double* sums, void* ws, hipStream_t s) {
+              ChanParams prm, int relu, double* sums, void* ws, hipStream_t s, FinalEpi fe = FinalEpi{}) {
   constexpr int V16 = 16 / sizeof(T);
   if (wide_ok<T>(C, {ldx, MODE ? lddy : ldx, (MODE && res) ? ldr : ldx}))
-    run_partials<T, V16, MODE>(x, dy, res, P, C, ldx, lddy, ldr, prm, relu, sums, ws, s);
+    run_partials<T, V16, MODE>(x, dy, res, P, C, ldx, lddy, ldr, prm, relu, sums, ws, s, fe);
   else
-    run_partials<T, V16 / 2, MODE>(x, dy, res, P, C, ldx, lddy, ldr, prm, relu, sums, ws, s);
+    run_partials<T, V16 / 2, MODE>(x, dy, res, P, C, ldx, lddy, ldr, prm, relu, sums, ws, s, fe);
 }
 
 template <typename T>
@@ -572,6 +597,34 @@ extern "C" int ssseg_bn_stats(const void* x, int64_t P, int64_t C, int64_t ldx, 
     partials<bf16_t, 0>((const bf16_t*)x, nullptr, nullptr, P, C, ldx, 0, 0, ChanParams{}, 0, sums, ws, s);
   else if (dt == SSSEG_F32)
     partials<float, 0>((const float*)x, nullptr, nullptr, P, C, ldx, 0, 0, ChanParams{}, 0, sums, ws, s);
+  else
+    return SSSEG_EUNSUPPORTED;
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_bn_stats_finalize(const void* x, int64_t P, int64_t C, int64_t ldx, int dt, double* sums, void* ws,
+                                       size_t ws_bytes, double count, float eps, float momentum, float* mean_out,
+                                       float* invstd_out, float* running_mean, float* running_var,
+                                       int64_t* num_batches_tracked, ssseg_stream_t stream) {
+  if (!x || !sums || !mean_out || !invstd_out || P < 1 || C < 1 || ld_bad(C, ldx) || count <= 0) return SSSEG_EINVAL;
+  if ((running_mean == nullptr) != (running_var == nullptr)) return SSSEG_EINVAL;
+  if (!ws || ws_bytes < ssseg_bn_workspace_bytes(C)) return SSSEG_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  FinalEpi fe{};
+  fe.mode = 1;
+  fe.count = count;
+  fe.eps = eps;
+  fe.momentum = momentum;
+  fe.mean_out = mean_out;
+  fe.invstd_out = invstd_out;
+  fe.rmean = running_mean;
+  fe.rvar = running_var;
+  fe.nbt = num_batches_tracked;
+  if (dt == SSSEG_BF16)
+    partials<bf16_t, 0>((const bf16_t*)x, nullptr, nullptr, P, C, ldx, 0, 0, ChanParams{}, 0, sums, ws, s, fe);
+  else if (dt == SSSEG_F32)
+    partials<float, 0>((const float*)x, nullptr, nullptr, P, C, ldx, 0, 0, ChanParams{}, 0, sums, ws, s, fe);
   else
     return SSSEG_EUNSUPPORTED;
   SSSEG_LAUNCH_CHECK();
@@ -696,6 +749,32 @@ extern "C" int ssseg_bn_bwd_reduce(const void* dy, const void* x, const void* re
   else if (dt == SSSEG_F32)
     partials<float, 1>((const float*)x, (const float*)dy, (const float*)residual, P, C, ldx, lddy, ldr,
                        ChanParams{mean, invstd, gamma, beta}, relu, sums, ws, s);
+  else
+    return SSSEG_EUNSUPPORTED;
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_bn_bwd_reduce_grad(const void* dy, const void* x, const void* residual, int64_t P, int64_t C,
+                                        int64_t ldx, int64_t ldr, int64_t lddy, const float* mean, const float* invstd,
+                                        const float* gamma, const float* beta, int relu, int dt, double* sums,
+                                        void* ws, size_t ws_bytes, float* dgamma, float* dbeta,
+                                        ssseg_stream_t stream) {
+  if (!dy || !x || !sums || !mean || !invstd || P < 1 || C < 1 || ld_bad(C, ldx) || ld_bad(C, lddy) ||
+      (residual && ld_bad(C, ldr)))
+    return SSSEG_EINVAL;
+  if (!ws || ws_bytes < ssseg_bn_workspace_bytes(C)) return SSSEG_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  FinalEpi fe{};
+  fe.mode = (dgamma || dbeta) ? 2 : 0;
+  fe.dgamma = dgamma;
+  fe.dbeta = dbeta;
+  if (dt == SSSEG_BF16)
+    partials<bf16_t, 1>((const bf16_t*)x, (const bf16_t*)dy, (const bf16_t*)residual, P, C, ldx, lddy, ldr,
+                        ChanParams{mean, invstd, gamma, beta}, relu, sums, ws, s, fe);
+  else if (dt == SSSEG_F32)
+    partials<float, 1>((const float*)x, (const float*)dy, (const float*)residual, P, C, ldx, lddy, ldr,
+                       ChanParams{mean, invstd, gamma, beta}, relu, sums, ws, s, fe);
   else
     return SSSEG_EUNSUPPORTED;
   SSSEG_LAUNCH_CHECK();

@@ -72,6 +72,9 @@ SIGS = {
     'ssseg_bn_apply': (i32, [vp, vp, vp, i64, i64, i64, i64, i64, vp, vp, vp, vp, i32, i32, vp]),
     'ssseg_bn_bwd_reduce': (i32, [vp, vp, vp, i64, i64, i64, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp, sz, vp]),
     'ssseg_bn_param_grad': (i32, [vp, i64, vp, vp, vp]),
+    'ssseg_bn_bwd_reduce_grad': (i32, [vp, vp, vp, i64, i64, i64, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp, sz, vp,
+                                        vp, vp]),
+    'ssseg_bn_stats_finalize': (i32, [vp, i64, i64, i64, i32, vp, vp, sz, f64, f32, f32, vp, vp, vp, vp, vp, vp]),
     'ssseg_bn_bwd_apply': (i32, [vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, vp, vp, vp, vp, i32, i32, vp, f64,
                                  i32, vp]),
     # pooling / copies

@@ -661,18 +661,22 @@ class _BNFn(torch.autograd.Function):
             sums = torch.empty(2 * C, dtype=torch.float64, device=dev)
             nb = N.lib().ssseg_bn_workspace_bytes(C)
             ws = N.workspace(nb, dev)
-            N.call('ssseg_bn_stats', N.dev_ptr(x), P, C, cp, N.dt_code(x), N.dev_ptr(sums), N.dev_ptr(ws), nb,
-                   N.stream())
-            if _sync_group(True):
-                dist.all_reduce(sums)
-                count = float(P * dist.get_world_size())
             track = mod.track_running_stats and mod.training
             if track and mod.momentum is None:
                 raise NotImplementedError('ssseg BatchNorm2d: momentum=None (cumulative average)')
-            N.call('ssseg_bn_finalize', N.dev_ptr(sums), C, count, float(mod.eps),
-                   float(mod.momentum if mod.momentum is not None else 0.0), N.dev_ptr(mean), N.dev_ptr(invstd),
-                   N.dev_ptr(mod.running_mean) if track else None, N.dev_ptr(mod.running_var) if track else None,
-                   N.dev_ptr(mod.num_batches_tracked) if track else None, N.stream())
+            fin = (C, count, float(mod.eps), float(mod.momentum if mod.momentum is not None else 0.0),
+                   N.dev_ptr(mean), N.dev_ptr(invstd), N.dev_ptr(mod.running_mean) if track else None,
+                   N.dev_ptr(mod.running_var) if track else None,
+                   N.dev_ptr(mod.num_batches_tracked) if track else None)
+            if _sync_group(True):
+                N.call('ssseg_bn_stats', N.dev_ptr(x), P, C, cp, N.dt_code(x), N.dev_ptr(sums), N.dev_ptr(ws), nb,
+                       N.stream())
+                dist.all_reduce(sums)
+                count = float(P * dist.get_world_size())
+                N.call('ssseg_bn_finalize', N.dev_ptr(sums), C, count, *fin[2:], N.stream())
+            else:   # one launch: the finalize runs in the reduction's tail
+                N.call('ssseg_bn_stats_finalize', N.dev_ptr(x), P, C, cp, N.dt_code(x), N.dev_ptr(sums),
+                       N.dev_ptr(ws), nb, count, *fin[2:], N.stream())
         else:
             N.call('ssseg_bn_eval_params', N.dev_ptr(mod.running_mean), N.dev_ptr(mod.running_var), float(mod.eps), C,
                    N.dev_ptr(mean), N.dev_ptr(invstd), N.stream())
@@ -701,13 +705,14 @@ class _BNFn(torch.autograd.Function):
         nb = N.lib().ssseg_bn_workspace_bytes(C)
         ws = N.workspace(nb, dev)
         res_p = N.dev_ptr(residual) if residual is not None else None
-        N.call('ssseg_bn_bwd_reduce', N.dev_ptr(gy), N.dev_ptr(x), res_p, P, C, cp, cp, cp, N.dev_ptr(mean),
+        pgrad = mod.weight is not None and mod.weight.requires_grad
+        # reduction + (dgamma, dbeta) from the local sums in one launch (ssseg_bn_bwd_reduce_grad)
+        N.call('ssseg_bn_bwd_reduce_grad', N.dev_ptr(gy), N.dev_ptr(x), res_p, P, C, cp, cp, cp, N.dev_ptr(mean),
                N.dev_ptr(invstd), N.dev_ptr(wt) if wt is not None else None,
                N.dev_ptr(bs) if bs is not None else None, _act(ctx.relu)[0], N.dt_code(x), N.dev_ptr(sums),
-               N.dev_ptr(ws), nb, N.stream())
-        if mod.weight is not None and mod.weight.requires_grad:
-            N.call('ssseg_bn_param_grad', N.dev_ptr(sums), C, N.dev_ptr(_grad_of(mod.weight)),
-                   N.dev_ptr(_grad_of(mod.bias)), N.stream())
+               N.dev_ptr(ws), nb, N.dev_ptr(_grad_of(mod.weight)) if pgrad else None,
+               N.dev_ptr(_grad_of(mod.bias)) if pgrad else None, N.stream())
+        if pgrad:
             _ready(mod.weight, mod.bias)
         count = ctx.count
         if ctx.training and _sync_group(True):
