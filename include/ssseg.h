@@ -299,6 +299,11 @@ int ssseg_bn_eval_bwd(const void* dy, const void* y, const void* aux, void* dcon
  * dconv_bias += scale*sums[0:C] (any pointer may be NULL) */
 int ssseg_bn_eval_param_grad(const double* sums, int64_t C, const float* scale, float* dgamma, float* dbeta,
                              float* dconv_bias, ssseg_stream_t stream);
+/* ssseg_bn_eval_bwd + ssseg_bn_eval_param_grad fused (the param grads run in the reduction's tail) */
+int ssseg_bn_eval_bwd_grad(const void* dy, const void* y, const void* aux, void* dconv, void* dres, int64_t P, int64_t C,
+                           int64_t ld, const float* scale, const float* mean_eff, const float* invstd, int relu, int dt,
+                           double* sums, void* ws, size_t ws_bytes, float* dgamma, float* dbeta, float* dconv_bias,
+                           ssseg_stream_t stream);
 /* y = act(gamma*(x-mean)*invstd + beta [+ residual]); channels [C, rup(C, 16 bytes)) of y are written 0; relu = 1 for ReLU (unet.py:10, Bottleneck add+relu) */
 int ssseg_bn_apply(const void* x, const void* residual, void* y, int64_t P, int64_t C, int64_t ldx, int64_t ldr,
                    int64_t ldy, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu,

@@ -194,6 +194,8 @@ struct FinalEpi {
   float *mean_out, *invstd_out, *rmean, *rvar;
   int64_t* nbt;
   float *dgamma, *dbeta;
+  const float* scale;   // mode 2, folded eval BN: dbias += scale * sums[0:C]
+  float* dbias;
 };
 
 __device__ __forceinline__ void finalize_channel(double s1, double s2, int c, double count, float eps, float momentum,
@@ -251,6 +253,7 @@ __global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* par
     } else if (fe.mode == 2) {
       if (fe.dbeta) fe.dbeta[c] += (float)a;
       if (fe.dgamma) fe.dgamma[c] += (float)b;
+      if (fe.dbias) fe.dbias[c] += fe.scale[c] * (float)a;
     }
   }
 }
@@ -672,7 +675,7 @@ extern "C" int ssseg_bn_fold_batch(const ssseg_fold_desc* descs, int64_t n, ssse
 template <typename T>
 static void eval_bwd(const T* dy, const T* y, const T* aux, T* dconv, T* dres, int64_t P, int64_t C, int64_t ld,
                      const float* scale, const float* mean_eff, const float* invstd, int relu, double* sums, void* ws,
-                     hipStream_t s) {
+                     hipStream_t s, FinalEpi fe) {
   constexpr int V16 = 16 / sizeof(T);
   const bool wide = wide_ok<T>(C, {ld});
   const Layout L = layout_for(C, wide ? V16 : V16 / 2);
@@ -683,12 +686,37 @@ static void eval_bwd(const T* dy, const T* y, const T* aux, T* dconv, T* dres, i
   else
     hipLaunchKernelGGL((bn_eval_bwd_kernel<T, V16 / 2>), dim3((unsigned)gx, L.cblocks), dim3(256), 0, s, dy, y, aux,
                        dconv, dres, P, (int)C, ld, L, scale, mean_eff, invstd, relu, (double*)ws);
-  launch_partial_final((const double*)ws, gx, C, sums, s);
+  launch_partial_final((const double*)ws, gx, C, sums, s, fe);
 }
+
+static int eval_bwd_entry(const void* dy, const void* y, const void* aux, void* dconv, void* dres, int64_t P, int64_t C,
+                          int64_t ld, const float* scale, const float* mean_eff, const float* invstd, int relu, int dt,
+                          double* sums, void* ws, size_t ws_bytes, ssseg_stream_t stream, FinalEpi fe);
 
 extern "C" int ssseg_bn_eval_bwd(const void* dy, const void* y, const void* aux, void* dconv, void* dres, int64_t P,
                                  int64_t C, int64_t ld, const float* scale, const float* mean_eff, const float* invstd,
                                  int relu, int dt, double* sums, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
+  return eval_bwd_entry(dy, y, aux, dconv, dres, P, C, ld, scale, mean_eff, invstd, relu, dt, sums, ws, ws_bytes,
+                        stream, FinalEpi{});
+}
+
+extern "C" int ssseg_bn_eval_bwd_grad(const void* dy, const void* y, const void* aux, void* dconv, void* dres,
+                                      int64_t P, int64_t C, int64_t ld, const float* scale, const float* mean_eff,
+                                      const float* invstd, int relu, int dt, double* sums, void* ws, size_t ws_bytes,
+                                      float* dgamma, float* dbeta, float* dconv_bias, ssseg_stream_t stream) {
+  FinalEpi fe{};
+  fe.mode = (dgamma || dbeta || dconv_bias) ? 2 : 0;
+  fe.dgamma = dgamma;
+  fe.dbeta = dbeta;
+  fe.scale = scale;
+  fe.dbias = dconv_bias;
+  return eval_bwd_entry(dy, y, aux, dconv, dres, P, C, ld, scale, mean_eff, invstd, relu, dt, sums, ws, ws_bytes,
+                        stream, fe);
+}
+
+static int eval_bwd_entry(const void* dy, const void* y, const void* aux, void* dconv, void* dres, int64_t P, int64_t C,
+                          int64_t ld, const float* scale, const float* mean_eff, const float* invstd, int relu, int dt,
+                          double* sums, void* ws, size_t ws_bytes, ssseg_stream_t stream, FinalEpi fe) {
   if (!dy || !aux || !dconv || !sums || !scale || !mean_eff || !invstd || (relu && !y) || P < 1 || C < 1 ||
       ld_bad(C, ld))
     return SSSEG_EINVAL;
@@ -696,10 +724,10 @@ extern "C" int ssseg_bn_eval_bwd(const void* dy, const void* y, const void* aux,
   hipStream_t s = (hipStream_t)stream;
   if (dt == SSSEG_BF16)
     eval_bwd<bf16_t>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)aux, (bf16_t*)dconv, (bf16_t*)dres, P, C, ld,
-                     scale, mean_eff, invstd, relu, sums, ws, s);
+                     scale, mean_eff, invstd, relu, sums, ws, s, fe);
   else if (dt == SSSEG_F32)
     eval_bwd<float>((const float*)dy, (const float*)y, (const float*)aux, (float*)dconv, (float*)dres, P, C, ld, scale,
-                    mean_eff, invstd, relu, sums, ws, s);
+                    mean_eff, invstd, relu, sums, ws, s, fe);
   else
     return SSSEG_EUNSUPPORTED;
   SSSEG_LAUNCH_CHECK();

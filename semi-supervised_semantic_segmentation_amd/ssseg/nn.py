@@ -776,15 +776,15 @@ class _ConvBNEvalFn(torch.autograd.Function):
         sums = torch.empty(2 * C, dtype=torch.float64, device=dev)
         nb = N.lib().ssseg_bn_workspace_bytes(C)
         ws = N.workspace(nb, dev)
-        N.call('ssseg_bn_eval_bwd', N.dev_ptr(gy), N.dev_ptr(y), N.dev_ptr(aux), N.dev_ptr(dconv),
-               N.dev_ptr(dres) if dres is not None else None, n * h * w, C, cp, N.dev_ptr(scale), N.dev_ptr(mean_eff),
-               N.dev_ptr(invstd), _act(ctx.relu)[0], N.dt_code(y), N.dev_ptr(sums), N.dev_ptr(ws), nb, N.stream())
         want = lambda p: p is not None and p.requires_grad  # noqa: E731
-        if want(bn.weight) or want(bn.bias) or want(conv.bias):
-            N.call('ssseg_bn_eval_param_grad', N.dev_ptr(sums), C, N.dev_ptr(scale),
-                   N.dev_ptr(_grad_of(bn.weight)) if want(bn.weight) else None,
-                   N.dev_ptr(_grad_of(bn.bias)) if want(bn.bias) else None,
-                   N.dev_ptr(_grad_of(conv.bias)) if want(conv.bias) else None, N.stream())
+        # dconv/dres + the BN (and conv-bias) parameter grads in one reduction (ssseg_bn_eval_bwd_grad)
+        N.call('ssseg_bn_eval_bwd_grad', N.dev_ptr(gy), N.dev_ptr(y), N.dev_ptr(aux), N.dev_ptr(dconv),
+               N.dev_ptr(dres) if dres is not None else None, n * h * w, C, cp, N.dev_ptr(scale), N.dev_ptr(mean_eff),
+               N.dev_ptr(invstd), _act(ctx.relu)[0], N.dt_code(y), N.dev_ptr(sums), N.dev_ptr(ws), nb,
+               N.dev_ptr(_grad_of(bn.weight)) if want(bn.weight) else None,
+               N.dev_ptr(_grad_of(bn.bias)) if want(bn.bias) else None,
+               N.dev_ptr(_grad_of(conv.bias)) if want(conv.bias) else None, N.stream())
+        if want(bn.weight) or want(bn.bias):
             _ready(*[p for p in (bn.weight, bn.bias) if want(p)])
         conv._ssseg_wgrad(x, dconv, bias_grad=False)
         pending = _take(ctx.grad_in)
