@@ -450,3 +450,50 @@ def test_folded_context_bitwise(hip_device):
         out = m(xr)[-1][-1]
     g1 = torch.autograd.grad(out.float().square().sum(), xr)[0]
     assert torch.equal(g0, g1)
+
+
+@pytest.mark.parametrize('C,P', [(64, 16 * 64 * 64), (200, 3 * 17 * 19), (1024, 16 * 16 * 16)])
+def test_bn_fused_tails_match_unfused(hip_device, C, P):
+    """ssseg_bn_stats_finalize == ssseg_bn_stats + ssseg_bn_finalize (the SyncBN path keeps the split form)
+    and ssseg_bn_bwd_reduce_grad == ssseg_bn_bwd_reduce + ssseg_bn_param_grad, bit for bit (same reduction
+    order; the tail only moves the per-channel math into the reduction kernel)."""
+    from ssseg import native as N
+    dev = hip_device
+    g = torch.Generator().manual_seed(C)
+    cp = (C + 7) // 8 * 8
+    x = torch.zeros(P, cp, dtype=torch.bfloat16)
+    x[:, :C] = (torch.randn(P, C, generator=g) * 2 + 0.5).bfloat16()
+    dy = torch.zeros(P, cp, dtype=torch.bfloat16)
+    dy[:, :C] = torch.randn(P, C, generator=g).bfloat16()
+    x, dy = x.to(dev), dy.to(dev)
+    nb = N.lib().ssseg_bn_workspace_bytes(C)
+    ws = N.workspace(nb, dev)
+    outs = []
+    for fused in (False, True):
+        sums = torch.empty(2 * C, dtype=torch.float64, device=dev)
+        mean = torch.empty(C, device=dev)
+        inv = torch.empty(C, device=dev)
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        nbt = torch.zeros((), dtype=torch.int64, device=dev)
+        tail = (float(P), 1e-5, 0.1, N.dev_ptr(mean), N.dev_ptr(inv), N.dev_ptr(rm), N.dev_ptr(rv), N.dev_ptr(nbt))
+        if fused:
+            N.call('ssseg_bn_stats_finalize', N.dev_ptr(x), P, C, cp, N.BF16, N.dev_ptr(sums), N.dev_ptr(ws), nb,
+                   *tail, N.stream())
+        else:
+            N.call('ssseg_bn_stats', N.dev_ptr(x), P, C, cp, N.BF16, N.dev_ptr(sums), N.dev_ptr(ws), nb, N.stream())
+            N.call('ssseg_bn_finalize', N.dev_ptr(sums), C, *tail, N.stream())
+        gamma = torch.linspace(0.5, 1.5, C, device=dev)
+        beta = torch.linspace(-0.2, 0.2, C, device=dev)
+        bsums = torch.empty(2 * C, dtype=torch.float64, device=dev)
+        dg, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+        args = (N.dev_ptr(dy), N.dev_ptr(x), None, P, C, cp, cp, cp, N.dev_ptr(mean), N.dev_ptr(inv),
+                N.dev_ptr(gamma), N.dev_ptr(beta), 1, N.BF16, N.dev_ptr(bsums), N.dev_ptr(ws), nb)
+        if fused:
+            N.call('ssseg_bn_bwd_reduce_grad', *args, N.dev_ptr(dg), N.dev_ptr(db), N.stream())
+        else:
+            N.call('ssseg_bn_bwd_reduce', *args, N.stream())
+            N.call('ssseg_bn_param_grad', N.dev_ptr(bsums), C, N.dev_ptr(dg), N.dev_ptr(db), N.stream())
+        outs.append([t.cpu() for t in (sums, mean, inv, rm, rv, nbt, bsums, dg, db)])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert int(outs[1][5]) == 1
