@@ -8,8 +8,15 @@ Inputs are synthetic (SURVEY §8d) and pre-generated in HBM (8 batches cycled); 
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--size S] [--no-cpu-baseline]
 
-N>1 is launched by torch.distributed.run (one rank per GPU, RCCL); value = images/sec of the whole job
-(labeled images, N*B*K / max-over-ranks time).  Rank 0 prints ONE JSON line.
+N>1: when WORLD_SIZE is not set, bench.py itself starts torch.distributed.run as a child process
+(before any GPU call) with one rank per GPU on RCCL; under an external launcher it joins as a rank.
+value = images/sec of the whole job (labeled images, N*B*K / max-over-ranks time).  Rank 0 prints
+ONE JSON line.
+
+Liveness: the timed steps run the reference arithmetic with confidence_threshold 0.5 (stated in the
+JSON): at the reference default 0.97 a random-init teacher has no confident pixel, so the consistency
+loss is 0/0 = NaN and the weights turn NaN; the threshold does not change the work a step
+does.  Every timed step's losses are checked finite after the timed region and cm_mean is reported.
 """
 import argparse
 import json
@@ -31,6 +38,7 @@ FWD_GFLOP_PER_IMAGE = 95.94     # UNet-R50 mw128 ConvT @512 (verifie
 # conv-engine HBM bytes of one step from rocprofv3 PMC (tools/pmc_step.py; FETCH_SIZE x2 + WRITE_SIZE, the
 # MI355X_MICROARCH.md gfx950 correction).  PMC cannot run inside the timed process, so the committed
 # measurement of the same workload is reported next to the live flop rate.
+THRESHOLD = 0.5                 # see the module docstring (liveness)
 PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r1_v13_pmc_traffic.json')
 
 
@@ -61,7 +69,7 @@ def build(batch, size, device):
     cfg = {'train': dict(
         loss=losses.CalculateLoss([{'loss_fn': losses.DenseBinaryCrossEntropyLossWithLogits('mean'), 'weight': [0.5]}]),
         virtual_batch_size_multiplier=1, use_semi_supervised=True, mask_proportion_range=(0.45, 0.55),
-        sigma_range=(8, 32), consistency_loss_weight=10, ema_model_alpha=0.99, confidence_threshold=0.97,
+        sigma_range=(8, 32), consistency_loss_weight=10, ema_model_alpha=0.99, confidence_threshold=THRESHOLD,
         gradient_clip_value=5.0, print_freq=10 ** 9)}
     return model, teacher, opt, cfg
 
@@ -113,53 +121,48 @@ def cpu_baseline(size, batch=2, steps=2):
                       f'{steps} timed steps after 1 warm-up ({time.perf_counter() - t0:.1f} s total)'}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
-    ap.add_argument('--warmup', type=int, default=5)
-    ap.add_argument('--batch', type=int, default=16)
-    ap.add_argument('--size', type=int, default=512)
-    ap.add_argument('--no-cpu-baseline', action='store_true')
-    args = ap.parse_args()
+def _spawn_ranks(n):
+    """`bench.py --gpus N` without an external launcher: run torch.distributed.run as a CHILD process (no
+    exec, and nothing has touched the GPU yet) with one rank per GPU, and exit with its code."""
+    import socket
+    import subprocess
+    sock = socket.socket()
+    sock.bind(('127.0.0.1', 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr=127.0.0.1', f'--master-port={port}', os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get('HSA_ENABLE_IPC_MODE_LEGACY', '0'))
+    return subprocess.call(cmd, env=env)
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', rank=rank, world_size=world, device_id=torch.device('cuda', local))
-    device = torch.device('cuda', local)
 
+def timed_run(args, world, rank, device, dtype, probe=True):
+    """Build, warm up, time args.steps steps; returns (elapsed_s, conv probe rows, per-step loss records)."""
     import train
     from ssseg import nn as snn
-    snn.set_compute_dtype(torch.bfloat16)
+    snn.set_compute_dtype(dtype)
     model, teacher, opt, cfg = build(args.batch, args.size, device)
     data = synthetic_batches(8, args.batch, args.size, device, rank)
-
     step_idx = [0]
+    recs = []
 
     def one_step():
         img, mask, ua, ub = data[step_idx[0] % len(data)]
-        train.train_step(model, teacher, opt, img, mask, ua, ub, 30, step_idx[0], cfg)
+        rec = train.train_step(model, teacher, opt, img, mask, ua, ub, 30, step_idx[0], cfg)
         step_idx[0] += 1
+        return rec
 
     model.train()
     opt.zero_grad()
     for _ in range(max(args.warmup, 2)):
         one_step()
     torch.cuda.synchronize()
-
-    # instrumented step: HIP events around every conv-engine launch (dominant kernel family)
-    rows = snn.probe(True)
-    one_step()
-    snn.probe(False)
-    torch.cuda.synchronize()
-    conv_ms = sum(r[0].elapsed_time(r[1]) for r in rows)
-    conv_flops = sum(r[2] for r in rows)
-    n_launch = len(rows)
-
+    rows = []
+    if probe:   # instrumented step: HIP events around every conv-engine launch (dominant kernel family)
+        rows = snn.probe(True)
+        one_step()
+        snn.probe(False)
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -168,19 +171,52 @@ def main():
     e1 = torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(args.steps):
-        one_step()
+        recs.append(one_step())
     e1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    gpu_s = e0.elapsed_time(e1) / 1e3
-    elapsed = max(wall, gpu_s)
+    elapsed = max(wall, e0.elapsed_time(e1) / 1e3)
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
+    live = torch.stack([torch.stack([c.float(), u.float(), m.float()]) for c, u, m in recs]).cpu()
+    snn.set_compute_dtype(torch.bfloat16)
+    return elapsed, rows, live
 
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--batch', type=int, default=16)
+    ap.add_argument('--size', type=int, default=512)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-fp32', action='store_true', help='skip the secondary fp32 (parity-mode) record')
+    args = ap.parse_args()
+
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(_spawn_ranks(args.gpus))
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', rank=rank, world_size=world, device_id=torch.device('cuda', local))
+        print(f'[bench rank {rank}] RCCL process group: world {dist.get_world_size()}, backend '
+              f'{dist.get_backend()}, device cuda:{local}', file=sys.stderr, flush=True)
+    device = torch.device('cuda', local)
+
+    elapsed, rows, live = timed_run(args, world, rank, device, torch.bfloat16)
+    finite = bool(torch.isfinite(live).all())
+    if not finite:
+        raise RuntimeError(f'bench: non-finite loss in the timed steps (rank {rank}): {live.tolist()}')
+    conv_ms = sum(r[0].elapsed_time(r[1]) for r in rows)
+    conv_flops = sum(r[2] for r in rows)
     images = world * args.batch * args.steps
     value = images / elapsed
     achieved = conv_flops / (conv_ms / 1e3)
@@ -192,15 +228,29 @@ def main():
         'config': {'workload': 'C2: UNet(ResNet-50 encoder, max_width=128, ConvT up) 512x512, semi-supervised '
                                'mean-teacher + CowMix step (BCE sup loss w=0.5, consistency w=10, SGD m=0.9)',
                    'global_batch': world * args.batch, 'per_gpu_batch': args.batch, 'image_size': args.size,
-                   'parallelism': f'dp{world}'},
+                   'parallelism': f'dp{world}', 'confidence_threshold': THRESHOLD},
         'roofline': {'bound': 'mfma', 'kernel': 'conv engine (igemm fwd/dgrad/ConvT + wgrad), all launches of one step',
                      'achieved': round(achieved / 1e12, 2), 'peak': BF16_DENSE_PEAK / 1e12, 'unit': 'TFLOP/s',
                      'frac': round(achieved / BF16_DENSE_PEAK, 4), 'traffic': pmc_traffic(),
                      'traffic_unit': 'HBM bytes per step, conv engine (rocprofv3 PMC, ' + os.path.relpath(PMC_PROFILE, ROOT) + ')',
                      'conv_ms_per_step': round(conv_ms, 3), 'conv_gflop_per_step': round(conv_flops / 1e9, 1),
-                     'launches_per_step': n_launch},
+                     'launches_per_step': len(rows)},
         'step_tflops': round(8 * FWD_GFLOP_PER_IMAGE * args.batch * world / (elapsed / args.steps) / 1e3, 2),
+        'liveness': {'losses_finite': finite, 'sup_loss_last': round(float(live[-1, 0]), 6),
+                     'unsup_loss_last': round(float(live[-1, 1]), 6),
+                     'cm_mean_avg': round(float(live[:, 2].mean()), 4)},
     }
+    if rank == 0 and world == 1 and not args.no_fp32:
+        try:
+            f_el, _, f_live = timed_run(argparse.Namespace(**dict(vars(args), steps=min(args.steps, 5), warmup=2)),
+                                        world, rank, device, torch.float32, probe=False)
+            n = min(args.steps, 5)
+            result['fp32_mode'] = {'value': round(args.batch * n / f_el, 3), 'unit': 'images/sec',
+                                   'ms_per_step': round(f_el / n * 1e3, 3), 'steps': n,
+                                   'losses_finite': bool(torch.isfinite(f_live).all()),
+                                   'note': 'same C2 step in the fp32 parity mode (the reference arithmetic)'}
+        except Exception as exc:  # report, never hide
+            result['fp32_mode'] = {'error': repr(exc)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result['cpu_baseline'] = cpu_baseline(args.size)

@@ -135,6 +135,9 @@ int ssseg_lovasz_bwd(const float* logits, const float* target, int64_t B, int64_
  * on the host):  ema = fma(param, (float)(1-alpha), round(ema*alpha))  — bit-exact with torch CPU. */
 int ssseg_ema_update(float* ema, const float* param, int64_t n, double alpha, ssseg_stream_t stream);
 
+/* x[i] *= a (in place): the 1/world average after a SUM all-reduce on backends without AVG (gloo). */
+int ssseg_scale_f32(float* x, int64_t n, float a, ssseg_stream_t stream);
+
 /* sum of squares of x[0,n) accumulated into out[0] (f32, caller zeroes out first: clip_grad_norm_). */
 int ssseg_sqnorm_accum(const float* x, int64_t n, float* out, void* ws, size_t ws_bytes, ssseg_stream_t stream);
 

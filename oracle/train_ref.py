@@ -116,6 +116,74 @@ def train_epoch(model, ema_model, optimizer, batches, unsup_iter, epoch, cfg, lo
     return logs
 
 
+def train_epoch_dp(model, ema_model, optimizer, rank_batches, rank_unsup, epoch, cfg, loss_weights=(0.5,),
+                   on_step=None):
+    """The same steps as train_epoch for a data-parallel job of `world` ranks (distributed_trainer.py:33-44:
+    DDP + SyncBatchNorm, train.py:41-130 on every rank), restated in ONE process on the concatenated batch:
+      - SyncBN training statistics over the global batch == BatchNorm over the concatenation;
+      - every rank's loss is a mean over its own slice; DDP averages the ranks' gradients, i.e. the gradient
+        of mean_r loss_r (SyncBN's backward all-reduce makes each rank's gradient that of sum_r loss_r
+        through the shared statistics, DDP divides by world);
+      - every rank seeds the same generator (distributed_trainer.py:17), so each rank draws the SAME CowMix
+        p, sigma and noise for its own slice: the draw is replayed per rank from one generator state.
+    rank_batches[step] = [(image_r, mask_r) per rank]; rank_unsup[step] = [(ua_r, ub_r) per rank].
+    Returns per-step dicts with per-rank sup/unsup losses."""
+    tc = cfg
+    model.train()
+    optimizer.zero_grad()
+    logs = []
+    for step, ranks in enumerate(rank_batches):
+        world = len(ranks)
+        sizes = [im.shape[0] for im, _ in ranks]
+        image = torch.cat([im for im, _ in ranks])
+        _, preds = model(image)
+        sups = []
+        o = 0
+        for (im, mk), n in zip(ranks, sizes):
+            sups.append(calculate_loss([p[o:o + n] for p in preds], mk, loss_weights))
+            o += n
+        sup = sum(sups) / world
+        (sup / tc['virtual_batch_size_multiplier']).backward()
+        rec = dict(sup_loss=[float(s.detach()) for s in sups])
+        if tc['use_semi_supervised']:
+            uas = [u[0] for u in rank_unsup[step]]
+            ubs = [u[1] for u in rank_unsup[step]]
+            ua, ub = torch.cat(uas), torch.cat(ubs)
+            with torch.no_grad():
+                ta = F.interpolate(ema_model(ua)[-1][-1], ua.shape[2:4], mode='bilinear', align_corners=False)
+                tb = F.interpolate(ema_model(ub)[-1][-1], ua.shape[2:4], mode='bilinear', align_corners=False)
+                state = torch.get_rng_state()
+                ms = []
+                for u in uas:
+                    torch.set_rng_state(state)
+                    ms.append(cowmix_mask_like(u, tc['mask_proportion_range'], tc['sigma_range']))
+                m = torch.cat(ms)
+                t_mix = ta * m + tb * (1. - m)
+                x_mix = ua * m + ub * (1. - m)
+            model.eval()
+            s = model(x_mix)[-1][-1]
+            model.train()
+            s = F.interpolate(s, x_mix.shape[2:4], mode='bilinear', align_corners=False)
+            cons, o = [], 0
+            for n in sizes:
+                c, _ = consistency_loss(s[o:o + n], t_mix[o:o + n], tc['confidence_threshold'])
+                cons.append(c * tc['consistency_loss_weight'] * float(epoch > 25))
+                o += n
+            unsup = sum(cons) / world
+            unsup.backward()
+            rec.update(unsup_loss=[float(c.detach()) for c in cons])
+        if on_step is not None:
+            on_step(step, rec)     # before the optimizer step: grads are the step's averaged gradients
+        if step % tc['virtual_batch_size_multiplier'] == 0 and step != 0:
+            torch.nn.utils.clip_grad_norm_(model.parameters(), tc['gradient_clip_value'])
+            optimizer.step()
+            optimizer.zero_grad()
+        if tc['use_semi_supervised']:
+            ema_update(model, ema_model, tc['ema_model_alpha'])
+        logs.append(rec)
+    return logs
+
+
 def default_cfg(**over):
     cfg = dict(virtual_batch_size_multiplier=1, use_semi_supervised=True, mask_proportion_range=(0.45, 0.55),
                sigma_range=(8, 32), consistency_loss_weight=10, ema_model_alpha=0.99,

@@ -194,7 +194,20 @@ __global__ void sgd_kernel(float* __restrict__ p, float* __restrict__ g, float* 
   }
 }
 
+__global__ void scale_kernel(float* __restrict__ x, int64_t n, float a) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x[i] = __fmul_rn(x[i], a);
+}
+
 }  // namespace
+
+extern "C" int ssseg_scale_f32(float* x, int64_t n, float a, ssseg_stream_t stream) {
+  if (!x || n < 0) return SSSEG_EINVAL;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(scale_kernel, dim3(ssseg_grid(n, 256, 256 * 8)), dim3(256), 0, (hipStream_t)stream, x, n, a);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
 
 extern "C" size_t ssseg_reduce_workspace_bytes(int64_t) { return sizeof(double) * 2 * RED_BLOCKS; }
 

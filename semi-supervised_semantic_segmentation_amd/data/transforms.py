@@ -70,7 +70,9 @@ class PadIfNeeded:
 
 class HorizontalFlip:
     def __init__(self, p=0.5, rng=None):
-        self.p, self.rng = p, rng or random.Random()
+        # default: the module-level `random` (albumentations' convention), which torch reseeds in every
+        # DataLoader worker, so forked workers do not replay one flip sequence
+        self.p, self.rng = p, rng or random
 
     def __call__(self, image, mask=None, **kw):
         flip = self.rng.random() < self.p

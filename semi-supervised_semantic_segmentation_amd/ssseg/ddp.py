@@ -2,10 +2,20 @@
 
 Replaces torch.nn.parallel.DistributedDataParallel (reference distributed_trainer.py:38).  The
 gradients live in the model's flat arena (ssseg.arena), cut into contiguous buckets (~25 MB).  The
-native layers call mark_ready(param) when a parameter's gradient is final; when every parameter of a
-bucket is ready in the *armed* backward pass, the bucket's all-reduce(AVG) is launched on a side HIP
-stream (ordered after the compute stream by an event), so communication overlaps the rest of the
-backward.  finish() joins the side stream.
+native layers call mark_ready(param) every time they have added a gradient contribution to a
+parameter; when every contribution of every parameter of a bucket has landed in the *armed* backward
+pass, the bucket's all-reduce is launched on a side HIP stream (ordered after the compute stream by an
+event), so communication overlaps the rest of the backward.  finish() joins the side stream.
+
+Contribution counting (static graph, like DDP's static_graph=True): a parameter can receive several
+contributions in one backward (MultiscaleAttention runs its base model twice per forward,
+multiscale_attention.py:38-58), so "ready" means "as many mark_ready calls as the parameter receives in
+an armed backward".  The first armed backward learns those counts and launches every bucket in finish()
+(no early launch); later armed backwards launch a bucket as soon as its counts are reached.  A
+contribution arriving after its bucket was launched means the graph changed: that raises instead of
+racing with the in-flight all-reduce.
+
+Reduction op: AVG on RCCL; SUM + a native 1/world scale on the side stream for gloo (which has no AVG).
 
 Reference semantics: DDP all-reduces after EACH of the two backward passes of a step (train.py:61,115).
 Gradients accumulate between them and the all-reduce is linear, so reducing once — armed on the last
@@ -47,8 +57,11 @@ class DistributedDataParallel(nn.Module):
                 self._bucket_of[id(p)] = i
                 if self.world > 1:
                     p._ssseg_reducer = self
+        self._avg = self.world > 1 and dist.get_backend() == 'nccl'
+        self._expected = None         # per-param contributions of an armed backward (learned on the first)
+        self._learning = True
         self._armed = False
-        self._pending = None
+        self.last_early = 0
         self._launched = None
         self._works = []
         self._stream = torch.cuda.Stream() if (self.world > 1 and a.data.is_cuda) else None
@@ -60,33 +73,51 @@ class DistributedDataParallel(nn.Module):
     def arm(self):
         """The next backward pass is the last one of this step: reduce buckets as they complete."""
         self._armed = self.world > 1
-        self._pending = [len(ps) for (_, _, ps) in self.buckets]
         self._launched = [False] * len(self.buckets)
         self._works = []
+        self._seen = {}
+        self.last_early = 0          # buckets launched from inside the backward in the current armed pass
+        if self._expected is not None:
+            self._pending = [sum(self._expected.get(id(p), 0) for p in ps) for (_, _, ps) in self.buckets]
 
     def mark_ready(self, p):
+        """One gradient contribution to `p` has been written (by a kernel on the current stream)."""
         if not self._armed:
             return
         i = self._bucket_of.get(id(p))
-        if i is None or self._launched[i]:
+        if i is None:
             return
+        k = id(p)
+        self._seen[k] = self._seen.get(k, 0) + 1
+        if self._learning:
+            return
+        if self._launched[i]:
+            raise RuntimeError('ssseg DDP: a gradient contribution arrived after its bucket was all-reduced '
+                               '(the backward graph changed between steps; static graph required)')
+        exp = self._expected.get(k, 0)
+        if self._seen[k] > exp:
+            raise RuntimeError('ssseg DDP: more gradient contributions than in the first armed backward '
+                               '(static graph required)')
         self._pending[i] -= 1
-        if self._pending[i] <= 0:
+        if self._pending[i] == 0:
+            self.last_early += 1
             self._launch(i)
 
     def _launch(self, i):
         s, e, _ = self.buckets[i]
         view = self.arena.grad[s:e]
         self._launched[i] = True
+        op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
         if self._stream is not None:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream())
             with torch.cuda.stream(self._stream):
                 self._stream.wait_event(ev)
-                self._works.append(dist.all_reduce(view, op=dist.ReduceOp.AVG, async_op=True))
-        else:   # gloo / CPU: SUM then scale
-            dist.all_reduce(view, op=dist.ReduceOp.SUM)
-            view.div_(self.world)
+                self._works.append((view, dist.all_reduce(view, op=op, async_op=True)))
+        else:   # CPU tensors (gloo): synchronous
+            dist.all_reduce(view, op=op)
+            if not self._avg:
+                view.div_(self.world)
 
     def finish(self):
         """Launch any bucket not yet reduced and make the current stream wait for all of them."""
@@ -95,9 +126,19 @@ class DistributedDataParallel(nn.Module):
         for i in range(len(self.buckets)):
             if not self._launched[i]:
                 self._launch(i)
-        for w in self._works:
-            w.wait()
         if self._stream is not None:
+            from . import native as N
+            with torch.cuda.stream(self._stream):
+                for view, w in self._works:
+                    w.wait()
+                    if not self._avg:
+                        N.call('ssseg_scale_f32', N.dev_ptr(view), view.numel(), 1.0 / self.world, N.stream())
             torch.cuda.current_stream().wait_stream(self._stream)
+        else:
+            for _, w in self._works:
+                w.wait()
+        if self._learning:
+            self._expected = dict(self._seen)
+            self._learning = False
         self._armed = False
         self._works = []

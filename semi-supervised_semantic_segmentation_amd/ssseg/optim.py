@@ -35,6 +35,26 @@ class SGD(torch.optim.Optimizer):
     def zero_grad(self, set_to_none=False):
         self.arena.zero_grad()
 
+    def load_state_dict(self, state_dict):
+        """torch.optim.Optimizer.load_state_dict, then the loaded momentum buffers are copied into the flat
+        momentum arena and the per-parameter state entries point back at its views (resume,
+        distributed_trainer.py:64): the next step continues the momentum like torch.optim.SGD does."""
+        super().load_state_dict(state_dict)
+        loaded = False
+        with torch.no_grad():
+            for p, o in zip(self.arena.params, self.arena.offsets):
+                st = self.state.get(p, {})
+                mb = st.get('momentum_buffer') if isinstance(st, dict) else None
+                if self.buf is None:
+                    continue
+                view = self.buf[o:o + p.numel()].view_as(p)
+                if mb is not None:
+                    view.copy_(mb.to(view.device, view.dtype))
+                    loaded = True
+                self.state[p]['momentum_buffer'] = view
+        if loaded:
+            self._first = False
+
     @torch.no_grad()
     def step(self, closure=None, max_norm=0.0):
         """max_norm > 0 clips the global gradient L2 norm first (clip_grad_norm_, train.py:122)."""

@@ -82,6 +82,22 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
         (cm_mean.detach() if cm_mean is not None else None)
 
 
+def _reduce_meters(meters, keys, world):
+    """Epoch-end average of the loss meters over ranks (the reference logs rank-reduced losses divided by
+    world, train.py:53-59,109-114): one all-reduce of the stacked sums instead of one per step."""
+    if world < 2:
+        return
+    live = [k for k in keys if meters[k].initialized]
+    if not live:
+        return
+    dev = next((meters[k].sum.device for k in live if isinstance(meters[k].sum, torch.Tensor)), None)
+    sums = torch.stack([torch.as_tensor(meters[k].sum, dtype=torch.float32, device=dev).reshape(()) for k in live])
+    torch.distributed.all_reduce(sums)
+    sums = sums / world
+    for i, k in enumerate(live):
+        meters[k].sum = sums[i]
+
+
 def train(model, ema_model, optimizer, dataloader, unsupervised_dataloader, epoch, initial_step, summary_writer,
           config, device):
     model.train()
@@ -114,6 +130,7 @@ def train(model, ema_model, optimizer, dataloader, unsupervised_dataloader, epoc
                 if summary_writer is not None:
                     summary_writer.add_scalar('train_classification_loss', float(red_cls), global_step)
                     summary_writer.add_scalar('train_unsupervised_loss', float(red_uns), global_step)
+    _reduce_meters(meters, ('cls', 'sup', 'unsup', 'cm'), world)
     if rank == 0 and summary_writer is not None and meters['sup'].initialized:
         summary_writer.add_scalar('batch_time', meters['time'].average(), global_step)
         summary_writer.add_scalar('train_loss_avg', meters['sup'].average() + meters['unsup'].average(), global_step)

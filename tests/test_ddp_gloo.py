@@ -66,3 +66,60 @@ def test_ddp_reducer_gloo_world2():
         p.join(120)
     res = dict(q.get(timeout=5) for _ in range(2))
     assert res == {0: True, 1: True}
+
+
+def _worker_reuse(rank, world, port, q):
+    """A parameter used twice per forward (MultiscaleAttention runs its base model twice,
+    multiscale_attention.py:38-58) gets two gradient contributions per backward: its bucket must not be
+    all-reduced before the second one lands."""
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from ssseg.ddp import DistributedDataParallel
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(torch.nn.Linear(64, 300), torch.nn.Linear(300, 70), torch.nn.Linear(70, 5))
+        ddp = DistributedDataParallel(model, bucket_cap_mb=0.05)
+        params = list(model.parameters())
+        ok = True
+        for step in range(3):
+            for i, p in enumerate(params):
+                p.grad.copy_(torch.arange(p.numel(), dtype=torch.float32).view_as(p) * (rank + 1) + i + step)
+            ddp.arm()
+            for p in reversed(params):          # first contribution (hi-res pass)
+                ddp.mark_ready(p)
+            ok = ok and not any(ddp._launched)   # nothing may be reduced yet
+            for p in reversed(params):          # second contribution (lo-res pass)
+                ddp.mark_ready(p)
+            if step > 0:                        # counts learned on step 0: every bucket launched in backward
+                ok = ok and all(ddp._launched) and ddp.last_early == len(ddp.buckets)
+            ddp.finish()
+            ok = ok and all(torch.allclose(p.grad, torch.arange(p.numel(), dtype=torch.float32).view_as(p) * 1.5
+                                           + i + step) for i, p in enumerate(params))
+        # a graph change (a third contribution after the bucket was launched) raises instead of racing
+        ddp.arm()
+        for _ in range(2):
+            for p in reversed(params):
+                ddp.mark_ready(p)
+        try:
+            ddp.mark_ready(params[-1])
+            ok = False
+        except RuntimeError:
+            pass
+        ddp.finish()
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_reducer_gloo_world2_reused_params():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_reuse, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    res = dict(q.get(timeout=5) for _ in range(2))
+    assert res == {0: True, 1: True}

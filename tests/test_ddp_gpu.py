@@ -1,0 +1,176 @@
+"""World-size-2 data-parallel training step of the PRODUCT path on the GPU (reference
+distributed_trainer.py:33-44: DDP + SyncBatchNorm, train.py:41-130 on every rank).
+
+Two processes share the one MI355X of the test box and talk over gloo on HIP tensors (RCCL cannot put
+two ranks on one device; on an 8-GPU node bench.py runs the same code over RCCL).  Each rank runs
+train.train_step on its own half of the batch through ssseg.nn (SyncBN: the fp64 statistic sums are
+all-reduced in forward and backward) and ssseg.ddp (bucketed all-reduce on the side HIP stream, buckets
+launched from inside the backward once their gradient contributions have landed).  The oracle
+(oracle/train_ref.train_epoch_dp) runs the same steps in one process on the concatenated batch.
+Checked: per-rank losses, the averaged gradients after step 0 (no optimizer step there, train.py:121),
+BN running statistics, student and teacher parameters after 3 steps, and that buckets were really
+launched early from the side stream in the steps after the first (learning) one."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+B, H, STEPS, WORLD = 2, 32, 3, 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _data():
+    g = torch.Generator().manual_seed(11)
+    imgs = torch.rand(STEPS, WORLD, B, 3, H, H, generator=g)
+    fg = (torch.rand(STEPS, WORLD, B, 1, H, H, generator=g) > 0.5).float()
+    masks = torch.cat([1 - fg, fg], 3)
+    unl = torch.rand(STEPS, WORLD, 2, B, 3, H, H, generator=g)
+    return imgs, masks, unl
+
+
+def _model():
+    from models import simple_unet
+    from models.adapters import ListOutput
+    torch.manual_seed(0)
+    return ListOutput(simple_unet.UNet(2, num_blocks=3, first_channels=8, max_width=32))
+
+
+def _cfg():
+    import losses
+    return dict(loss=losses.CalculateLoss([{'loss_fn': losses.DenseBinaryCrossEntropyLossWithLogits('mean'),
+                                           'weight': [0.5]}]),
+                virtual_batch_size_multiplier=1, use_semi_supervised=True, mask_proportion_range=(0.45, 0.55),
+                sigma_range=(2, 4), confidence_threshold=0.5, consistency_loss_weight=10, ema_model_alpha=0.99,
+                print_freq=1, gradient_clip_value=5.0)
+
+
+def _worker(rank, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group('gloo', rank=rank, world_size=WORLD)
+    try:
+        import cowmix
+        import train
+        from ssseg import arena, optim
+        from ssseg import nn as snn
+        from ssseg.ddp import DistributedDataParallel
+        dev = torch.device('cuda:0')
+        snn.set_compute_dtype(torch.float32)
+        student = _model().to(dev)
+        teacher = _model().to(dev)
+        for p in teacher.parameters():
+            p.detach_()
+        teacher.eval()
+        model = DistributedDataParallel(student, bucket_cap_mb=0.02)
+        arena.attach(teacher, with_grads=False)
+        opt = optim.SGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
+        imgs, masks, unl = _data()
+        cowmix.NOISE_SOURCE = 'cpu'
+        torch.manual_seed(3)
+        model.train()
+        opt.zero_grad()
+        early, losses, grads0 = [], [], None
+        for step in range(STEPS):
+            c, u, _ = train.train_step(model, teacher, opt, imgs[step, rank].to(dev), masks[step, rank].to(dev),
+                                       unl[step, rank, 0].to(dev), unl[step, rank, 1].to(dev), 30, step,
+                                       {'train': _cfg()})
+            torch.cuda.synchronize()
+            losses.append((float(c), float(u)))
+            early.append(model.last_early)
+            if step == 0:
+                grads0 = {n: p.grad.detach().cpu().numpy().copy() for n, p in student.named_parameters()}
+        # numpy (pickled by value): torch CPU tensors would travel as shared-memory fds that die with this process
+        out = dict(losses=losses, early=early, nbuckets=len(model.buckets), grads0=grads0,
+                   student={k: v.detach().cpu().numpy().copy() for k, v in student.state_dict().items()},
+                   teacher={k: v.detach().cpu().numpy().copy() for k, v in teacher.state_dict().items()})
+        q.put((rank, out))
+    except Exception as exc:   # report to the parent instead of hanging it
+        import traceback
+        q.put((rank, 'ERROR ' + repr(exc) + '\n' + traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _oracle():
+    from oracle import models_ref, train_ref
+    torch.manual_seed(0)
+    s = models_ref.ListOutput(models_ref.SimpleUNet(2, 3, 8, 32))
+    t = models_ref.ListOutput(models_ref.SimpleUNet(2, 3, 8, 32))
+    t.load_state_dict(_model().state_dict())
+    s.load_state_dict(_model().state_dict())
+    for p in t.parameters():
+        p.detach_()
+    t.eval()
+    opt = torch.optim.SGD(s.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
+    imgs, masks, unl = _data()
+    cfg = train_ref.default_cfg(sigma_range=(2, 4), confidence_threshold=0.5)
+    grads = {}
+
+    def on_step(step, rec):
+        if step == 0:
+            for n, p in s.named_parameters():
+                grads[n] = p.grad.detach().clone()
+    torch.manual_seed(3)
+    logs = train_ref.train_epoch_dp(s, t, opt, [[(imgs[k, r], masks[k, r]) for r in range(WORLD)] for k in range(STEPS)],
+                                    [[(unl[k, r, 0], unl[k, r, 1]) for r in range(WORLD)] for k in range(STEPS)], 30,
+                                    cfg, on_step=on_step)
+    return logs, grads, s.state_dict(), t.state_dict()
+
+
+def test_ddp_syncbn_world2_product_path(hip_device):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(WORLD):
+            r, out = q.get(timeout=100)
+            res[r] = out
+    finally:
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    for r in range(WORLD):
+        assert not isinstance(res[r], str), res[r]
+    logs, g_ref, s_ref, t_ref = _oracle()
+    for r in range(WORLD):
+        out = res[r]
+        for k, (c, u) in enumerate(out['losses']):
+            np.testing.assert_allclose(c, logs[k]['sup_loss'][r], rtol=1e-4)
+            np.testing.assert_allclose(u, logs[k]['unsup_loss'][r], rtol=2e-3, atol=1e-6)
+        assert out['nbuckets'] > 2
+        assert out['early'][0] == 0                       # first armed backward learns the counts
+        assert all(e > 0 for e in out['early'][1:]), out['early']   # later ones launch from the backward
+        gmax = max(float(g.abs().max()) for g in g_ref.values())
+        for n, g in g_ref.items():
+            a = out['grads0'][n]
+            b = g.numpy()
+            # floor: gradients that are mathematically zero (a conv bias feeding a BatchNorm) are rounding noise
+            assert np.abs(a - b).max() <= 1e-3 * max(np.abs(b).max(), 1e-3 * gmax), (r, n)
+        for name, got, ref in (('student', out['student'], s_ref), ('teacher', out['teacher'], t_ref)):
+            for k, v in ref.items():
+                a, b = got[k], v.numpy()
+                if not np.issubdtype(b.dtype, np.floating):
+                    assert np.array_equal(a, b), (name, k)
+                    continue
+                assert np.abs(a - b).max() <= 1e-3 * (np.abs(b).max() + 1e-6), (r, name, k)
+    # both ranks hold identical weights (averaged gradients, broadcast init)
+    for k in res[0]['student']:
+        assert np.array_equal(res[0]['student'][k], res[1]['student'][k]), k

@@ -98,8 +98,9 @@ def _grads(model):
     return {n: p.grad.detach().double().cpu() for n, p in model.named_parameters()}
 
 
+@pytest.mark.parametrize('size', [128, 512])
 @pytest.mark.parametrize('dtype', ['f32', 'bf16'])
-def test_unet_r50_fwd_bwd_vs_oracle(hip_device, dtype):
+def test_unet_r50_fwd_bwd_vs_oracle(hip_device, dtype, size):
     """Gradients are compared against an fp64 CPU run of the same network: the HIP error must stay
     within a small multiple of the reference's own fp32 (torch-CPU) error.  Back-propagation through
     ~60 BatchNorm layers amplifies rounding (BN backward subtracts the per-channel means of dy and
@@ -111,7 +112,8 @@ def test_unet_r50_fwd_bwd_vs_oracle(hip_device, dtype):
         prod, ref = _unet_pair(hip_device)
         ref64 = models_ref.UNet(2, models_ref.resnet50_encoder(), 128, train_upsampling=True).double()
         ref64.load_state_dict(ref.state_dict())
-        x = torch.rand(2, 3, 128, 128)
+        # 512x512 is the benchmark geometry (C2): the tile configs autotuned for the bench's layers run here
+        x = torch.rand(2, 3, size, size)
         yr = ref(x)
         gy = torch.randn_like(yr)
         yr.backward(gy)
@@ -225,19 +227,38 @@ def test_train_steps_vs_reference_golden(hip_device, f32_mode):
     finally:
         cowmix.NOISE_SOURCE = old
     np.testing.assert_allclose(sup, g['sup_loss'], rtol=1e-4)
-    np.testing.assert_allclose(uns, g['unsup_loss'], rtol=5e-2, atol=1e-7)
+    # the golden is the reference's own fp32 result, itself ~1e-5 from fp64 (tools/diag_unsup.py steps: HIP is
+    # 2e-6 from an fp64 oracle run, the reference 1.1e-5)
+    np.testing.assert_allclose(uns, g['unsup_loss'], rtol=1e-4, atol=1e-9)
     sd_s, sd_t = student.state_dict(), teacher.state_dict()
     for k in sd_s:
-        np.testing.assert_allclose(sd_s[k].cpu().numpy(), g['final_s.' + k], rtol=1e-3, atol=1e-5, err_msg=k)
-        np.testing.assert_allclose(sd_t[k].cpu().numpy(), g['final_t.' + k], rtol=1e-3, atol=1e-5, err_msg=k)
+        np.testing.assert_allclose(sd_s[k].cpu().numpy(), g['final_s.' + k], rtol=2e-4, atol=2e-6, err_msg=k)
+        np.testing.assert_allclose(sd_t[k].cpu().numpy(), g['final_t.' + k], rtol=2e-4, atol=2e-6, err_msg=k)
 
 
-def test_train_step_vs_oracle_unet_r50(hip_device, f32_mode):
-    """One semi-supervised step of the C2 model family (UNet-R50, 64x64) vs the oracle train step."""
+def _oracle_run(rs, rt, dt, imgs, masks, unl, seed, **cfg):
+    """The oracle train step on CPU in dtype dt (copies of the given reference models)."""
+    import copy
+    s_, t_ = copy.deepcopy(rs).to(dt), copy.deepcopy(rt).to(dt)
+    opt = torch.optim.SGD(s_.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-4)
+    loss_kw = cfg.pop('loss_kw', {})
+    torch.manual_seed(seed)
+    logs = train_ref.train_epoch(s_, t_, opt, list(zip(imgs.to(dt), masks.to(dt))), iter(unl.to(dt)), 30,
+                                 train_ref.default_cfg(**cfg), **loss_kw)
+    return logs, s_
+
+
+@pytest.mark.parametrize('H', [64, 512])
+def test_train_step_vs_oracle_unet_r50(hip_device, f32_mode, H):
+    """Two semi-supervised steps of the C2 model family (UNet-R50, 64x64 and the bench's 512x512) vs the oracle
+    train step, in fp32
+    and fp64 (tests/parity.py: step 0 within 1e-3 of fp64; step 1 within max(1e-3, 2x the reference's own
+    fp32 drift) of fp64)."""
     import cowmix
     import losses
     import train
     from models.adapters import ListOutput
+    from parity import check_losses
     from ssseg import arena, optim
     prod, ref = _unet_pair(hip_device, seed=2)
     prod_t, ref_t = _unet_pair(hip_device, seed=2)
@@ -250,21 +271,20 @@ def test_train_step_vs_oracle_unet_r50(hip_device, f32_mode):
     arena.attach(student)
     arena.attach(teacher, with_grads=False)
     opt = optim.SGD(student.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-4)
-    ropt = torch.optim.SGD(rs.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-4)
     tcfg = dict(loss=losses.CalculateLoss([
         {'loss_fn': losses.DenseBinaryCrossEntropyLossWithLogits(reduction='mean'), 'weight': [0.5]}]),
         virtual_batch_size_multiplier=1, use_semi_supervised=True, mask_proportion_range=(0.45, 0.55),
-        sigma_range=(4, 8), confidence_threshold=0.5, consistency_loss_weight=10, ema_model_alpha=0.99,
-        print_freq=1, gradient_clip_value=5.0)
+        sigma_range=(4, 8) if H == 64 else (8, 32), confidence_threshold=0.5, consistency_loss_weight=10,
+        ema_model_alpha=0.99, print_freq=1, gradient_clip_value=5.0)
     gen = torch.Generator().manual_seed(5)
-    B, H = 2, 64
+    B = 2
     imgs = torch.rand(2, B, 3, H, H, generator=gen)
     fg = (torch.rand(2, B, 1, H, H, generator=gen) > 0.5).float()
     masks = torch.cat([1 - fg, fg], 2)
     unl = torch.rand(4, B, 3, H, H, generator=gen)
-    torch.manual_seed(7)
-    rlogs = train_ref.train_epoch(rs, rt, ropt, list(zip(imgs, masks)), iter(unl), 30,
-                                  train_ref.default_cfg(sigma_range=(4, 8), confidence_threshold=0.5))
+    sr = tcfg['sigma_range']
+    r32, rs32 = _oracle_run(rs, rt, torch.float32, imgs, masks, unl, 7, sigma_range=sr, confidence_threshold=0.5)
+    r64, rs64 = _oracle_run(rs, rt, torch.float64, imgs, masks, unl, 7, sigma_range=sr, confidence_threshold=0.5)
     old = cowmix.NOISE_SOURCE
     cowmix.NOISE_SOURCE = 'cpu'
     try:
@@ -279,11 +299,12 @@ def test_train_step_vs_oracle_unet_r50(hip_device, f32_mode):
             logs.append((float(c), float(u)))
     finally:
         cowmix.NOISE_SOURCE = old
-    for (c, u), r in zip(logs, rlogs):
-        np.testing.assert_allclose(c, r['sup_loss'], rtol=1e-3)
-        np.testing.assert_allclose(u, r['unsup_loss'], rtol=2e-2, atol=1e-6)
-    worst = 0.0
-    for (n, p), (_, q) in zip(student.named_parameters(), rs.named_parameters()):
-        a, b = p.detach().cpu().numpy(), q.detach().numpy()
+    check_losses(logs, [(r['sup_loss'], r['unsup_loss']) for r in r32],
+                 [(r['sup_loss'], r['unsup_loss']) for r in r64])
+    worst = worst32 = 0.0
+    for (n, p), (_, q), (_, q32) in zip(student.named_parameters(), rs64.named_parameters(), rs32.named_parameters()):
+        a, b, c = p.detach().cpu().double().numpy(), q.detach().numpy(), q32.detach().double().numpy()
         worst = max(worst, float(np.abs(a - b).max() / (np.abs(b).max() + 1e-12)))
-    assert worst < 2e-3, worst
+        worst32 = max(worst32, float(np.abs(c - b).max() / (np.abs(b).max() + 1e-12)))
+    print(f'params after 2 steps, worst rel err vs fp64: hip {worst:.2e} ref32 {worst32:.2e}')
+    assert worst < max(1e-3, 2 * worst32), (worst, worst32)
