@@ -195,6 +195,14 @@ typedef struct ssseg_conv_epilogue {
   void* aux;
   int32_t relu;    /* activation code SSSEG_ACT_* (1 = ReLU, the historical flag) */
   float slope;     /* LeakyReLU negative slope (SSSEG_ACT_LEAKY) */
+  /* Fused training-BatchNorm statistics (optional; the BN that consumes y, unet.py:9 / every encoder BN in
+   * train mode): per output tile row r, stats[(2r)*stats_ld + c] = sum of y[.][c] and stats[(2r+1)*stats_ld + c]
+   * = sum of y^2 over the tile's pixels (fp64, of the value as stored), c < stats_ld; *stats_rows_host receives
+   * the number of rows written (<= ceil(M/64)).  Reduce them with ssseg_bn_partials_finalize: the separate
+   * statistics pass over y (ssseg_bn_stats) is not needed.  Not allowed with an empty tap set (R*S == 0). */
+  double* stats;
+  int64_t stats_ld;
+  int64_t* stats_rows_host;
 } ssseg_conv_epilogue;
 int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const ssseg_conv_desc* desc_host, int dt, int dt_out,
                          const ssseg_conv_epilogue* epi, void* ws, size_t ws_bytes, ssseg_stream_t stream);
@@ -269,6 +277,13 @@ int ssseg_bn_stats_finalize(const void* x, int64_t P, int64_t C, int64_t ldx, in
                             size_t ws_bytes, double count, float eps, float momentum, float* mean_out, float* invstd_out,
                             float* running_mean, float* running_var, int64_t* num_batches_tracked,
                             ssseg_stream_t stream);
+/* BatchNorm statistics from the partial rows a conv epilogue wrote (ssseg_conv_epilogue.stats): sums[0:C] /
+ * sums[C:2C] = column sums over nparts rows of part[2*nparts][C] (fixed order, deterministic); when mean_out is
+ * non-NULL the training finalize of ssseg_bn_finalize runs in the same launch (the single-process path; SyncBN
+ * passes mean_out = NULL, all-reduces sums, then calls ssseg_bn_finalize). */
+int ssseg_bn_partials_finalize(const double* part, int64_t nparts, int64_t C, double* sums, double count, float eps,
+                               float momentum, float* mean_out, float* invstd_out, float* running_mean,
+                               float* running_var, int64_t* num_batches_tracked, ssseg_stream_t stream);
 /* eval mode: mean = running_mean, invstd = 1/sqrt(running_var + eps) */
 int ssseg_bn_eval_params(const float* running_mean, const float* running_var, float eps, int64_t C, float* mean_out,
                          float* invstd_out, ssseg_stream_t stream);

@@ -634,6 +634,31 @@ extern "C" int ssseg_bn_stats_finalize(const void* x, int64_t P, int64_t C, int6
   return 0;
 }
 
+extern "C" int ssseg_bn_partials_finalize(const double* part, int64_t nparts, int64_t C, double* sums, double count,
+                                          float eps, float momentum, float* mean_out, float* invstd_out,
+                                          float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                                          ssseg_stream_t stream) {
+  if (!part || !sums || nparts < 1 || C < 1 || nparts > 0x7fffffff) return SSSEG_EINVAL;
+  if ((mean_out == nullptr) != (invstd_out == nullptr) || (running_mean == nullptr) != (running_var == nullptr))
+    return SSSEG_EINVAL;
+  if (mean_out && count <= 0) return SSSEG_EINVAL;
+  FinalEpi fe{};
+  if (mean_out) {
+    fe.mode = 1;
+    fe.count = count;
+    fe.eps = eps;
+    fe.momentum = momentum;
+    fe.mean_out = mean_out;
+    fe.invstd_out = invstd_out;
+    fe.rmean = running_mean;
+    fe.rvar = running_var;
+    fe.nbt = num_batches_tracked;
+  }
+  launch_partial_final(part, nparts, C, sums, (hipStream_t)stream, fe);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int ssseg_bn_finalize(const double* sums, int64_t C, double count, float eps, float momentum, float* mean_out,
                                  float* invstd_out, float* running_mean, float* running_var,
                                  int64_t* num_batches_tracked, ssseg_stream_t stream) {

@@ -1,0 +1,18 @@
+// LDS-DMA implicit-GEMM conv configs, group a (split from conv.hip for parallel compilation).
+#include "conv_kernels.h"
+
+template <typename TO>
+int launch_glds_grp_a(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
+                      unsigned wb, hipStream_t s) {
+  switch (cfg) {
+    case 1: return launch_glds<TO, 256, 128, 2, 2, 4, 3>(x, w, y, g, ep, xb, wb, s);
+    case 2: return launch_glds<TO, 256, 64, 4, 1, 4, 3>(x, w, y, g, ep, xb, wb, s);
+    case 3: return launch_glds<TO, 128, 128, 2, 2, 4, 3>(x, w, y, g, ep, xb, wb, s);
+    default: return -1;
+  }
+}
+
+template int launch_glds_grp_a<bf16_t>(int, const void*, const void*, void*, const ConvGeom&, const Epi<bf16_t>&,
+                                        unsigned, unsigned, hipStream_t);
+template int launch_glds_grp_a<float>(int, const void*, const void*, void*, const ConvGeom&, const Epi<float>&,
+                                       unsigned, unsigned, hipStream_t);

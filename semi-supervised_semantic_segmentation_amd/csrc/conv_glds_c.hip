@@ -1,0 +1,20 @@
+// LDS-DMA implicit-GEMM conv configs, group c (split from conv.hip for parallel compilation).
+#include "conv_kernels.h"
+
+template <typename TO>
+int launch_glds_grp_c(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
+                      unsigned wb, hipStream_t s) {
+  switch (cfg) {
+    case 13: return launch_glds<TO, 256, 64, 4, 1, 4, 2>(x, w, y, g, ep, xb, wb, s);
+    case 14: return launch_glds<TO, 128, 64, 2, 2, 4, 2>(x, w, y, g, ep, xb, wb, s);
+    case 15: return launch_glds<TO, 128, 64, 2, 2, 4, 1>(x, w, y, g, ep, xb, wb, s);
+    case 16: return launch_glds<TO, 64, 64, 2, 2, 4, 1>(x, w, y, g, ep, xb, wb, s);
+    case 17: return launch_glds<TO, 64, 64, 2, 2, 4, 2>(x, w, y, g, ep, xb, wb, s);
+    default: return launch_glds<TO, 64, 64, 2, 2, 4, 4>(x, w, y, g, ep, xb, wb, s);
+  }
+}
+
+template int launch_glds_grp_c<bf16_t>(int, const void*, const void*, void*, const ConvGeom&, const Epi<bf16_t>&,
+                                        unsigned, unsigned, hipStream_t);
+template int launch_glds_grp_c<float>(int, const void*, const void*, void*, const ConvGeom&, const Epi<float>&,
+                                       unsigned, unsigned, hipStream_t);

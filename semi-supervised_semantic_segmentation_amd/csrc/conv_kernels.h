@@ -1,0 +1,864 @@
+// conv_kernels.h: device code of the implicit-GEMM convolution engine (shared by conv*.hip).
+// Implicit-GEMM convolution engine for gfx950 (MFMA 16x16x32 bf16 / 16x16x4 f32), NHWC activations.
+//
+// One gather-GEMM kernel covers every contraction of the conv layers on the hot path
+// (unet.py:8,21-22,27,85; simple_unet.py:64-72,118; encoder convs):
+//   y[m][n] = sum_k A[m][k] * B[n][k]
+//   m = output position (img, oy, ox) of a GEMM grid OHxOW, written to pixel (oy*osy+ooy, ox*osx+oox)
+//   k = (r, s, c):  A = x[img][oy*sy + r*dy + py][ox*sx + s*dx + px][c]  (0 outside),  B = packed weights
+// Forward conv, stride-1 dgrad (flipped taps), strided dgrad and ConvTranspose2d(4,2,1) forward
+// (stride-phase decomposition: one launch per output phase, dilation -1) are all this kernel with
+// different descriptors and weight packings (ssseg_weight_pack).
+// Weight gradients use a second kernel (split-K over pixels, fp32 slabs, deterministic reduce).
+//
+// Tiling: 256 threads = 4 waves; block tile BM pixels x BN channels x 64 bytes of k; LDS double
+// buffer with register-staged global loads (issue next tile's loads before the MFMAs, write them to
+// the other buffer after), one barrier per k-tile.  The MFMA A operand is the weight tile and the B
+// operand the pixel tile, so each lane's accumulator holds 4 consecutive output channels of one
+// pixel: the NHWC epilogue stores them with one 8/16-byte write.
+#pragma once
+#include <algorithm>
+
+#include "common.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+struct ConvGeom {
+  int N, H, W, C, ldx;
+  int OH, OW, K;
+  int R, S, sy, sx, dy, dx, py, px;
+  int outH, outW, osy, osx, ooy, oox, ldy;
+  int ldw;
+  long long M;   // N*OH*OW
+  int KK;        // R*S*C
+};
+
+static inline bool make_geom(const ssseg_conv_desc* d, ConvGeom& g) {
+  if (!d) return false;
+  const int64_t vals[] = {d->N, d->H, d->W, d->C, d->ldx, d->OH, d->OW, d->K, d->R, d->S, d->outH, d->outW, d->ldy,
+                          d->ldw};
+  for (int64_t v : vals)
+    if (v < 0 || v > (int64_t)0x7fffffff) return false;
+  g.N = (int)d->N; g.H = (int)d->H; g.W = (int)d->W; g.C = (int)d->C; g.ldx = (int)d->ldx;
+  g.OH = (int)d->OH; g.OW = (int)d->OW; g.K = (int)d->K;
+  g.R = (int)d->R; g.S = (int)d->S; g.sy = (int)d->sy; g.sx = (int)d->sx; g.dy = (int)d->dy; g.dx = (int)d->dx;
+  g.py = (int)d->py; g.px = (int)d->px;
+  g.outH = (int)d->outH; g.outW = (int)d->outW; g.osy = (int)d->osy; g.osx = (int)d->osx; g.ooy = (int)d->ooy;
+  g.oox = (int)d->oox; g.ldy = (int)d->ldy; g.ldw = (int)d->ldw;
+  g.M = (long long)d->N * d->OH * d->OW;
+  g.KK = (int)(d->R * d->S * d->C);
+  return true;
+}
+
+template <typename T> struct MF;
+template <> struct MF<bf16_t> {
+  static constexpr int VEC = 8;
+  typedef bf16x8 frag;
+  __device__ __forceinline__ static void mma(const frag& a, const frag& b, f32x4& c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct MF<float> {
+  static constexpr int VEC = 4;
+  typedef f32x4 frag;
+  // k inside a 16-element chunk is permuted consistently for A and B: MFMA e consumes element e
+  __device__ __forceinline__ static void mma(const frag& a, const frag& b, f32x4& c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], c, 0, 0, 0);
+  }
+};
+
+template <typename TO> struct Store4;
+template <> struct Store4<float> {
+  __device__ __forceinline__ static void st(float* p, const float (&v)[4]) { *(float4*)p = make_float4(v[0], v[1], v[2], v[3]); }
+};
+template <> struct Store4<bf16_t> {
+  __device__ __forceinline__ static void st(bf16_t* p, const float (&v)[4]) {
+    uint2 u;
+    u.x = (unsigned)f32_to_bf16(v[0]) | ((unsigned)f32_to_bf16(v[1]) << 16);
+    u.y = (unsigned)f32_to_bf16(v[2]) | ((unsigned)f32_to_bf16(v[3]) << 16);
+    *(uint2*)p = u;
+  }
+};
+
+// epilogue: y = act(acc * scale[n] + shift[n] + res[pixel][n]); scale null = 1, shift null = 0
+// (conv bias -> shift; a folded eval BatchNorm -> scale/shift; Bottleneck identity -> res)
+template <typename TO>
+struct Epi {
+  const float* scale;
+  const float* shift;
+  const TO* res;
+  int ldr;
+  int relu;    // activation code SSSEG_ACT_*
+  TO* aux;     // optional copy of the raw accumulator (pre-affine conv output), pixel stride ldy
+  float slope;
+  double* stats;   // optional BatchNorm statistics partials of the stored output: row (2*mtile) = sum y,
+  int sld;         // row (2*mtile+1) = sum y^2, channels [0, sld) (sld = the BN's channel count)
+};
+
+// the value a later pass reads back from the stored output (the BN statistics are those of that value)
+template <typename TO> __device__ __forceinline__ float stored(float v);
+template <> __device__ __forceinline__ float stored<float>(float v) { return v; }
+template <> __device__ __forceinline__ float stored<bf16_t>(float v) { return bf16_to_f32(f32_to_bf16(v)); }
+
+// Per-tile BatchNorm statistics partials from the epilogue (fused training BN statistics, replaces a separate
+// read of the conv output).  Each thread holds fp64 (sum, sumsq) of V consecutive channels starting at
+// channel offset cofs within the tile, over some of the tile's rows; lanes holding the same channels are those
+// whose lane index agrees in the bits below `lstride` (a power of two): xor-shuffle over the higher bits,
+// then the NW waves' partials meet in LDS (fixed order: deterministic) and row mtile of the partial table is
+// written for channels [n0, n0 + BN).  Every thread of the block must call this (two barriers).
+template <int V, int BN, int NW>
+__device__ __forceinline__ void tile_stats(double (&s1)[V], double (&s2)[V], int lstride, bool holder, int cofs,
+                                           char* smem, long long mtile, int n0, double* __restrict__ stats, int sld) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    if (o < lstride) break;
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      s1[e] += __shfl_xor(s1[e], o, 64);
+      s2[e] += __shfl_xor(s2[e], o, 64);
+    }
+  }
+  __syncthreads();   // LDS free (the caller's last LDS reads are done)
+  double* red = (double*)smem;   // [NW][BN][2]
+  const int w = threadIdx.x >> 6;
+  if (holder)
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      red[(w * BN + cofs + e) * 2] = s1[e];
+      red[(w * BN + cofs + e) * 2 + 1] = s2[e];
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < BN; c += NW * 64) {
+    const int n = n0 + c;
+    if (n >= sld) continue;
+    double a = 0.0, b = 0.0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      a += red[(k * BN + c) * 2];
+      b += red[(k * BN + c) * 2 + 1];
+    }
+    stats[(mtile * 2) * sld + n] = a;
+    stats[(mtile * 2 + 1) * sld + n] = b;
+  }
+}
+
+template <typename TO> struct Load4;
+template <> struct Load4<float> {
+  __device__ __forceinline__ static void ld(const float* p, float (&v)[4]) {
+    const float4 q = *(const float4*)p;
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  }
+};
+template <> struct Load4<bf16_t> {
+  __device__ __forceinline__ static void ld(const bf16_t* p, float (&v)[4]) {
+    const uint2 q = *(const uint2*)p;
+    v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
+    v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+  }
+};
+
+// Writes one wave's FN x FM fragments: y[pixel(m)][n..n+3] = act(acc*scale + shift + res), NHWC.
+// The per-channel affine of a fragment column is loaded once, and every residual of the column is loaded
+// before the first store (the stores may alias the residual as far as the compiler knows, so it could not
+// batch those loads itself): one HBM round trip per column instead of one per pixel.
+template <typename TO, int FM, int FN>
+__device__ __forceinline__ void store_tile(const f32x4 (&acc)[FN][FM], long long mb, int nb, int lane,
+                                           const ConvGeom& g, TO* __restrict__ y, const Epi<TO>& ep,
+                                           double (*st1)[4] = nullptr, double (*st2)[4] = nullptr) {
+  long long op[FM];   // output pixel of fragment row j (-1: past M)
+#pragma unroll
+  for (int j = 0; j < FM; ++j) {
+    const long long m = mb + j * 16 + (lane & 15);
+    op[j] = -1;
+    if (m < g.M) {
+      const int ox = (int)m % g.OW;    // 32-bit decode: geom_ok guarantees M < 2^31
+      const int q = (int)m / g.OW;
+      const int oy = q % g.OH, img = q / g.OH;
+      op[j] = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < FN; ++i) {
+    const int n = nb + i * 16 + (lane >> 4) * 4;
+    if (n >= g.K) continue;
+    const bool full = n + 3 < g.K;
+    float sc[4], sh[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bool in = n + e < g.K;
+      sc[e] = (ep.scale && in) ? ep.scale[n + e] : 1.f;
+      sh[e] = (ep.shift && in) ? ep.shift[n + e] : 0.f;
+    }
+    float r[FM][4];
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      r[j][0] = r[j][1] = r[j][2] = r[j][3] = 0.f;
+      if (ep.res && op[j] >= 0) {
+        const TO* rp = ep.res + op[j] * ep.ldr + n;
+        if (full && (ep.ldr & 3) == 0)
+          Load4<TO>::ld(rp, r[j]);
+        else
+          for (int e = 0; e < 4 && n + e < g.K; ++e) r[j][e] = io<TO>::ld(rp, e);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      if (op[j] < 0) continue;
+      if (ep.aux) {
+        const float a4[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (full && (g.ldy & 3) == 0)
+          Store4<TO>::st(ep.aux + op[j] * g.ldy + n, a4);
+        else
+          for (int e = 0; e < 4 && n + e < g.K; ++e) io<TO>::st(ep.aux, op[j] * g.ldy + n + e, a4[e]);
+      }
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float a = acc[i][j][e];
+        if (ep.scale) a *= sc[e];
+        if (ep.shift) a += sh[e];
+        a += r[j][e];
+        a = act_fwd(a, ep.relu, ep.slope);
+        v[e] = a;
+        if (st1 && n + e < g.K) {
+          const double q = (double)stored<TO>(a);
+          st1[i][e] += q;
+          st2[i][e] += q * q;
+        }
+      }
+      TO* yp = y + op[j] * g.ldy;
+      if (full && (g.ldy & 3) == 0) {
+        Store4<TO>::st(yp + n, v);
+      } else {
+        for (int e = 0; e < 4 && n + e < g.K; ++e) io<TO>::st(yp, n + e, v[e]);
+      }
+    }
+  }
+}
+
+// LDS-staged epilogue for the LDS-DMA kernel: the raw fp32 accumulators go to LDS (rows padded by 16 B:
+// conflict-free float4 writes), then each thread finishes 8 consecutive channels of one pixel with 16-byte
+// residual loads and 16-byte (bf16) / 2x16-byte (f32) stores, so a pixel row is written in full lines.
+// Same arithmetic as store_tile (fp32 acc*scale + shift + res, then act, then one rounding).
+template <typename TO> struct Out8;
+template <> struct Out8<bf16_t> {
+  __device__ __forceinline__ static void ld(const bf16_t* p, float (&v)[8]) {
+    const uint4 q = *(const uint4*)p;
+    const unsigned w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  __device__ __forceinline__ static void st(bf16_t* p, const float (&v)[8]) {
+    unsigned w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (unsigned)f32_to_bf16(v[2 * i]) | ((unsigned)f32_to_bf16(v[2 * i + 1]) << 16);
+    *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+};
+template <> struct Out8<float> {
+  __device__ __forceinline__ static void ld(const float* p, float (&v)[8]) {
+    const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  __device__ __forceinline__ static void st(float* p, const float (&v)[8]) {
+    *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+    *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+
+template <typename TO, int BM, int BN, int FM, int FN, int NT>
+__device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char* smem, long long m0, int n0, int wmo,
+                                               int wno, int lane, const ConvGeom& g, TO* __restrict__ y,
+                                               const Epi<TO>& ep) {
+  constexpr int LDR = BN * 4 + 16;   // bytes per staged pixel row
+  __syncthreads();                   // every wave is done with the LDS ring
+#pragma unroll
+  for (int j = 0; j < FM; ++j)
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+      *(f32x4*)(smem + (wmo + j * 16 + (lane & 15)) * LDR + (wno + i * 16 + (lane >> 4) * 4) * 4) = acc[i][j];
+  __syncthreads();
+  constexpr int CPR = BN / 8;                 // 8-channel chunks per row
+  static_assert(NT % CPR == 0 && 64 % CPR == 0, "epilogue: one fixed channel chunk per thread");
+  constexpr int RPP = NT / CPR, NP = (BM + RPP - 1) / RPP;   // rows per pass, passes
+  const int ch = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
+  const int n = n0 + ch * 8;
+  double s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.0;
+  if (n < g.K) {
+    const bool vec = (g.ldy & 7) == 0 && (!ep.res || (ep.ldr & 7) == 0);
+    const bool full = vec && n + 7 < g.K;
+    // this thread's 8 channels are the same in every pass: the affine is loaded once, and all residual
+    // rows are in flight before the first store
+    float sc[8], sh[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bool in = n + e < g.K;
+      sc[e] = (ep.scale && in) ? ep.scale[n + e] : 1.f;
+      sh[e] = (ep.shift && in) ? ep.shift[n + e] : 0.f;
+    }
+    long long op[NP];
+    float r[NP][8];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int row = r0 + p * RPP;
+      const long long m = m0 + row;
+      op[p] = -1;
+      if (row < BM && m < g.M) {
+        const int ox = (int)m % g.OW;    // 32-bit decode: geom_ok guarantees M < 2^31
+        const int q = (int)m / g.OW;
+        const int oy = q % g.OH, img = q / g.OH;
+        op[p] = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) r[p][e] = 0.f;
+      if (ep.res && op[p] >= 0) {
+        if (full)
+          Out8<TO>::ld(ep.res + op[p] * ep.ldr + n, r[p]);
+        else
+          for (int e = 0; e < 8 && n + e < g.K; ++e) r[p][e] = io<TO>::ld(ep.res, op[p] * ep.ldr + n + e);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      if (op[p] < 0) continue;
+      const float* a = (const float*)(smem + (r0 + p * RPP) * LDR + ch * 32);
+      float v[8];
+      const float4 a0 = *(const float4*)a, a1 = *(const float4*)(a + 4);
+      const float raw[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float t = raw[e];
+        if (ep.scale) t *= sc[e];
+        if (ep.shift) t += sh[e];
+        t += r[p][e];
+        t = act_fwd(t, ep.relu, ep.slope);
+        v[e] = t;
+      }
+      if (ep.stats)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const double q = n + e < g.K ? (double)stored<TO>(v[e]) : 0.0;
+          s1[e] += q;
+          s2[e] += q * q;
+        }
+      const long long o = op[p] * g.ldy + n;
+      if (full) {
+        Out8<TO>::st(y + o, v);
+        if (ep.aux) Out8<TO>::st(ep.aux + o, raw);
+      } else {
+        for (int e = 0; e < 8 && n + e < g.K; ++e) {
+          io<TO>::st(y, o + e, v[e]);
+          if (ep.aux) io<TO>::st(ep.aux, o + e, raw[e]);
+        }
+      }
+    }
+  }
+  if (ep.stats)
+    tile_stats<8, BN, NT / 64>(s1, s2, CPR, (threadIdx.x & 63) < CPR, ch * 8, smem, m0 / BM, n0, ep.stats, ep.sld);
+}
+
+// fused statistics after store_tile (register epilogue): lane holds fp64 sums of fragment column i's 4
+// channels over its FM rows; lanes 16 apart hold other channel groups, lanes differing in bits 0-3 other rows
+template <int FN, int BN, int NW>
+__device__ __forceinline__ void frag_stats(double (&st1)[FN][4], double (&st2)[FN][4], int wno, char* smem,
+                                           long long mtile, int n0, double* stats, int sld) {
+  const int lane = threadIdx.x & 63;
+  // reduce over the 16 row lanes of each channel group first (xor 8, 4, 2, 1)
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        st1[i][e] += __shfl_xor(st1[i][e], o, 64);
+        st2[i][e] += __shfl_xor(st2[i][e], o, 64);
+      }
+  __syncthreads();
+  double* red = (double*)smem;   // [NW][BN][2], zero where a wave holds no channel
+  for (int k = threadIdx.x; k < NW * BN * 2; k += NW * 64) red[k] = 0.0;
+  __syncthreads();
+  const int w = threadIdx.x >> 6;
+  if ((lane & 15) == 0)
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = wno + i * 16 + (lane >> 4) * 4 + e;
+        red[(w * BN + c) * 2] = st1[i][e];
+        red[(w * BN + c) * 2 + 1] = st2[i][e];
+      }
+  __syncthreads();
+  for (int c = threadIdx.x; c < BN; c += NW * 64) {
+    const int n = n0 + c;
+    if (n >= sld) continue;
+    double a = 0.0, b = 0.0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      a += red[(k * BN + c) * 2];
+      b += red[(k * BN + c) * 2 + 1];
+    }
+    stats[(mtile * 2) * sld + n] = a;
+    stats[(mtile * 2 + 1) * sld + n] = b;
+  }
+}
+
+// XCD-aware remap of a 1-D grid (bijective for any grid size): consecutive tile ids land on one XCD
+__device__ __forceinline__ int xcd_tile(int bid, int ntiles) {
+  const int xcd = bid & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+}
+
+constexpr int ROWB = 80;   // 64 data bytes + 16 pad per LDS row
+
+// ------------------------------------------------------------------------------------------------
+// forward / dgrad / transposed-conv gather GEMM
+// ------------------------------------------------------------------------------------------------
+extern int g_knobs[9];   // runtime variant switches (ssseg_set_knob), defined in conv.hip
+// 0: reg-staged pipeline depth; 1: split-K cap (-1 off); 2: 64x64 small-M tiles (reg-staged path);
+// 3: bf16 LDS-DMA path (0 on, -1 off); 4: variant (0 auto, 1..10 / 12..17 LDS-DMA config, 11 register-staged);
+// 5: autotune unseen geometries (1 on, 0 = static heuristic); knob 6 = 1 clears the variant cache;
+// 7: LDS-staged coalesced epilogue in the LDS-DMA kernel (0 on, -1 off);
+// 8: bf16 weight gradient on the LDS-DMA kernel (0 on, -1 = register-staged wgrad_kernel)
+
+template <typename T, typename TO, int BM, int BN, int WM, int WN, bool DEEP>
+__global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __restrict__ x, const T* __restrict__ w,
+                                                                  TO* __restrict__ y, ConvGeom g, Epi<TO> ep,
+                                                                  int splits, float* __restrict__ ws) {
+  constexpr int VEC = MF<T>::VEC;
+  constexpr int BK = 64 / (int)sizeof(T);
+  constexpr int A_PER = BM / 64;                 // pixel rows per thread (4 chunks per row)
+  constexpr int B_IT = (BN * 4 + 255) / 256;
+  constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
+  static_assert(WM * WN == 4 && FM >= 1 && FN >= 1, "tile");
+  __shared__ __attribute__((aligned(16))) char smem[2 * (BM + BN) * ROWB];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  // XCD-aware remap of the 1-D grid: consecutive tile ids (the N tiles of one M tile, then the next
+  // M tile) go to the same XCD so the gathered input rows are re-read from that XCD's L2.
+  const int nnt = (g.K + BN - 1) / BN;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const long long m0 = (long long)(tile / nnt) * BM;
+  const int n0 = (tile % nnt) * BN;
+  const int chunk = t & 3;
+  const int RS = g.R * g.S;
+  // split-K: this block reduces k-tiles [kt0, kt1) of the contraction (blockIdx.y = split index)
+  const int nk_all = (g.KK + BK - 1) / BK;
+  const int kper = (nk_all + splits - 1) / splits;
+  const int kt0 = blockIdx.y * kper;
+  const int kt1 = min(nk_all, kt0 + kper);
+
+  int a_n[A_PER], a_oy[A_PER], a_ox[A_PER];
+  bool a_ok[A_PER];
+#pragma unroll
+  for (int i = 0; i < A_PER; ++i) {
+    const long long m = m0 + (t >> 2) + 64 * i;
+    a_ok[i] = m < g.M;
+    const long long mm = a_ok[i] ? m : 0;
+    a_ox[i] = (int)mm % g.OW;
+    const int q = (int)mm / g.OW;
+    a_oy[i] = q % g.OH;
+    a_n[i] = q / g.OH;
+  }
+  // k-state of this thread's chunk: k = tap*C + kc, tap = r*S + s (advanced by every load, in order)
+  const int k_first = kt0 * BK + chunk * VEC;
+  int tap = min(k_first / g.C, RS), kc = k_first - tap * g.C, r = tap / max(g.S, 1), s = tap - r * g.S;
+  const int nk = max(kt1 - kt0, 0);
+
+  auto load = [&](uint4 (&ra)[A_PER], uint4 (&rb)[B_IT], int kt) {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int iy = a_oy[i] * g.sy + r * g.dy + g.py;
+      const int ix = a_ox[i] * g.sx + s * g.dx + g.px;
+      const bool ok = a_ok[i] && tap < RS && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+      ra[i] = ok ? *(const uint4*)(x + ((long long)(a_n[i] * g.H + iy) * g.W + ix) * g.ldx + kc) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < B_IT; ++j) {
+      const int id = t + 256 * j;
+      rb[j] = make_uint4(0, 0, 0, 0);
+      if (id < BN * 4) {
+        const int n = n0 + (id >> 2);
+        const int k = (kt0 + kt) * BK + (id & 3) * VEC;
+        if (n < g.K && k < g.KK) rb[j] = *(const uint4*)(w + (long long)n * g.ldw + k);
+      }
+    }
+    kc += BK;
+    while (kc >= g.C && tap < RS) {
+      kc -= g.C; ++tap;
+      if (++s == g.S) { s = 0; ++r; }
+    }
+  };
+  auto store = [&](const uint4 (&ra)[A_PER], const uint4 (&rb)[B_IT], int buf) {
+    char* As = smem + buf * (BM + BN) * ROWB;
+    char* Bs = As + BM * ROWB;
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) *(uint4*)(As + ((t >> 2) + 64 * i) * ROWB + chunk * 16) = ra[i];
+#pragma unroll
+    for (int j = 0; j < B_IT; ++j) {
+      const int id = t + 256 * j;
+      if (id < BN * 4) *(uint4*)(Bs + (id >> 2) * ROWB + (id & 3) * 16) = rb[j];
+    }
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * (BM + BN) * ROWB;
+    const char* Bs = As + BM * ROWB;
+    typename MF<T>::frag af[FN], bfr[FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+      af[i] = *(const typename MF<T>::frag*)(Bs + (wn * WTN + i * 16 + (lane & 15)) * ROWB + (lane >> 4) * 16);
+#pragma unroll
+    for (int j = 0; j < FM; ++j)
+      bfr[j] = *(const typename MF<T>::frag*)(As + (wm * WTM + j * 16 + (lane & 15)) * ROWB + (lane >> 4) * 16);
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) MF<T>::mma(af[i], bfr[j], acc[i][j]);
+  };
+
+  if constexpr (DEEP) {
+    // two register sets: tile kt+2 is in flight while tile kt is multiplied and tile kt+1 is staged
+    uint4 ra0[A_PER], rb0[B_IT], ra1[A_PER], rb1[B_IT];
+    if (nk > 0) load(ra0, rb0, 0);
+    if (nk > 1) load(ra1, rb1, 1);
+    if (nk > 0) store(ra0, rb0, 0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt += 2) {
+      if (kt + 2 < nk) load(ra0, rb0, kt + 2);
+      compute(0);
+      if (kt + 1 < nk) store(ra1, rb1, 1);
+      __syncthreads();
+      if (kt + 1 >= nk) break;
+      if (kt + 3 < nk) load(ra1, rb1, kt + 3);
+      compute(1);
+      if (kt + 2 < nk) store(ra0, rb0, 0);
+      __syncthreads();
+    }
+  } else {
+    // one register set: tile kt+1 is in flight while tile kt is multiplied
+    uint4 ra0[A_PER], rb0[B_IT];
+    if (nk > 0) {
+      load(ra0, rb0, 0);
+      store(ra0, rb0, 0);
+    }
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) load(ra0, rb0, kt + 1);
+      compute(kt & 1);
+      if (kt + 1 < nk) store(ra0, rb0, (kt + 1) & 1);
+      __syncthreads();
+    }
+  }
+
+  // epilogue: lane holds channels n..n+3 (n = 4*(lane>>4) within a 16-wide fragment) of pixel lane&15
+  if (splits > 1) {   // fp32 partials into ws[m][K]; finalize applies the epilogue and writes y
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      const long long m = m0 + wm * WTM + j * 16 + (lane & 15);
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        const int n = n0 + wn * WTN + i * 16 + (lane >> 4) * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (n + e < g.K) atomicAdd(ws + m * g.K + n + e, acc[i][j][e]);
+      }
+    }
+    return;
+  }
+  if (ep.stats) {
+    double st1[FN][4], st2[FN][4];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) st1[i][e] = st2[i][e] = 0.0;
+    store_tile<TO, FM, FN>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, g, y, ep, st1, st2);
+    frag_stats<FN, BN, 4>(st1, st2, wn * WTN, smem, m0 / BM, n0, ep.stats, ep.sld);
+    return;
+  }
+  store_tile<TO, FM, FN>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, g, y, ep);
+}
+
+// ------------------------------------------------------------------------------------------------
+// bf16 gather GEMM, LDS-DMA pipeline (gfx950), for C % 64 == 0.  Same contraction and epilogue as
+// igemm_kernel.  k runs tap-major (k = tap*C + c) and a k-tile (BK = 64) never straddles a tap, so the
+// tap (r, s) and channel block c0 are wave-uniform scalars.  Tiles are staged by buffer_load ... lds
+// (16 B per lane straight into LDS, no VGPR round trip) into an NS-deep LDS ring: NS-1 tiles are in
+// flight while one is multiplied, one raw barrier per k-tile, counted vmcnt.  Per-lane byte offsets are
+// rebuilt only when the tap changes (padding pixels get an out-of-range offset: the buffer unit
+// returns zeros); inside a tap only the scalar soffset moves.  The LDS image is lane-linear (one
+// wave-instruction = 8 rows x 128 B); the bank swizzle (16-byte chunk c of row r stored at
+// c ^ ((r >> 1) & 7)) is applied on the per-lane source offset, and fragment reads apply the same XOR.
+// ------------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ void bldslds16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_base, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)lds_wave_base, 16, voff, soff, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void vmcnt_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+constexpr unsigned OOB = 0x80000000u;   // > any num_records we build: the load returns zeros
+
+template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS>
+__global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const bf16_t* __restrict__ x,
+                                                                const bf16_t* __restrict__ w, TO* __restrict__ y,
+                                                                ConvGeom g, Epi<TO> ep, unsigned xbytes,
+                                                                unsigned wbytes, int g_epi_lds) {
+  constexpr int ROW = 128;                       // bytes per LDS row = 64 bf16 of k
+  constexpr int STAGE = (BM + BN) * ROW;
+  constexpr int AI = BM / 8 / NW;                // A (pixel) wave-instructions per wave per stage
+  constexpr int BI = BN / 8 / NW;                // B (weight) wave-instructions per wave per stage
+  constexpr int NL = AI + BI;
+  constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
+  static_assert(WM * WN == NW && FM >= 1 && FN >= 1 && AI >= 1 && BI >= 1 && NS >= 1 && NS <= 4, "tile");
+  // NS == 1 (single-slot ring, for nk == 1..2: 1x1 convs over 64-128 channels): the slot is sized to also
+  // hold the staged epilogue, and occupancy (4-9 workgroups per CU) hides the load -> MFMA -> store chain
+  constexpr int EPI = BM * (BN * 4 + 16);
+  constexpr int SMEM = (NS == 1 && EPI > STAGE) ? EPI : NS * STAGE;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int nnt = (g.K + BN - 1) / BN;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const long long m0 = (long long)(tile / nnt) * BM;
+  const int n0 = (tile % nnt) * BN;
+  const int RS = g.R * g.S;
+  const int cpt = g.C >> 6;                      // k-tiles per tap
+  const int nk = RS * cpt;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, (int)wbytes, 0x00020000);
+
+  // lane rows: A row 8*(wave*AI + ii) + (lane>>3), B row 8*(wave*BI + jj) + (lane>>3); the lane loads
+  // logical chunk (lane & 7) ^ swz(row) = (lane & 7) ^ (lane >> 4) ^ 4*(instruction parity)
+  const int c_even = (lane & 7) ^ (lane >> 4);
+  int a_off[AI], a_iy[AI], a_ix[AI];
+#pragma unroll
+  for (int ii = 0; ii < AI; ++ii) {
+    const int inst = wave * AI + ii;
+    const int ch = c_even ^ ((inst & 1) * 4);
+    const long long m = m0 + 8 * inst + (lane >> 3);
+    if (m < g.M) {
+      const int ox = (int)m % g.OW;
+      const int q = (int)m / g.OW;
+      const int oy = q % g.OH, img = q / g.OH;
+      a_iy[ii] = oy * g.sy + g.py;
+      a_ix[ii] = ox * g.sx + g.px;
+      a_off[ii] = ((img * g.H + a_iy[ii]) * g.W + a_ix[ii]) * g.ldx * 2 + ch * 16;
+    } else {
+      a_iy[ii] = -0x40000000;   // never in bounds
+      a_ix[ii] = 0;
+      a_off[ii] = 0;
+    }
+  }
+  unsigned b_off[BI];
+#pragma unroll
+  for (int jj = 0; jj < BI; ++jj) {
+    const int inst = wave * BI + jj;
+    const int ch = c_even ^ ((inst & 1) * 4);
+    const int n = n0 + 8 * inst + (lane >> 3);
+    b_off[jj] = n < g.K ? (unsigned)(n * g.ldw * 2 + ch * 16) : OOB;
+  }
+
+  unsigned a_cur[AI];   // byte offsets of this lane's A rows for the current tap (OOB = padding)
+  auto set_tap = [&](int tap) {
+    const int r = tap / g.S, s_ = tap - (tap / g.S) * g.S;
+    const int dyy = r * g.dy, dxx = s_ * g.dx;
+    const int toff = (dyy * g.W + dxx) * g.ldx * 2;
+#pragma unroll
+    for (int ii = 0; ii < AI; ++ii) {
+      const int iy = a_iy[ii] + dyy, ix = a_ix[ii] + dxx;
+      const bool ok = (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+      a_cur[ii] = ok ? (unsigned)(a_off[ii] + toff) : OOB;
+    }
+  };
+
+  int ld_tap = 0, ld_c = 0, ld_kt = 0;   // k-tile being staged next: tap, channel block, index
+  set_tap(0);
+  auto issue = [&](int buf) {
+    char* As = smem + buf * STAGE;
+    char* Bs = As + BM * ROW;
+    const unsigned sa = (unsigned)ld_c * 128u, sb = (unsigned)ld_kt * 128u;
+#pragma unroll
+    for (int ii = 0; ii < AI; ++ii) bldslds16(xr, As + (wave * AI + ii) * 1024, a_cur[ii], sa);
+#pragma unroll
+    for (int jj = 0; jj < BI; ++jj) bldslds16(wr, Bs + (wave * BI + jj) * 1024, b_off[jj], sb);
+    ++ld_kt;
+    if (++ld_c == cpt) {
+      ld_c = 0;
+      if (++ld_tap < RS) set_tap(ld_tap);
+    }
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int rsw = ((lane & 15) >> 1) & 7;   // read-side swizzle of this lane's fragment row
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + BM * ROW;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int pc = ((ks * 4 + (lane >> 4)) ^ rsw) * 16;
+      bf16x8 af[FN], bfr[FM];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) af[i] = *(const bf16x8*)(Bs + (wn * WTN + i * 16 + (lane & 15)) * ROW + pc);
+#pragma unroll
+      for (int j = 0; j < FM; ++j) bfr[j] = *(const bf16x8*)(As + (wm * WTM + j * 16 + (lane & 15)) * ROW + pc);
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if constexpr (NS == 1) {
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt) __builtin_amdgcn_s_barrier();   // every wave is done reading the slot
+      issue(0);
+      vmcnt_wait<0>();
+      __builtin_amdgcn_s_barrier();           // every wave's part of tile kt landed
+      compute(0);
+    }
+  } else {
+    constexpr int D = NS - 1;   // tiles in flight ahead of the one being multiplied
+#pragma unroll
+    for (int p = 0; p < D; ++p)
+      if (p < nk) issue(p);
+    for (int kt = 0; kt < nk; ++kt) {
+      // wait for tile kt: the tiles issued after it (at most D-1) may stay in flight
+      const int ahead = min(nk - 1, kt + D - 1) - kt;
+      if (D >= 3 && ahead >= 2) vmcnt_wait<2 * NL>();
+      else if (D >= 2 && ahead >= 1) vmcnt_wait<NL>();
+      else vmcnt_wait<0>();
+      __builtin_amdgcn_s_barrier();   // every wave's tile kt landed; ring slot (kt+D)%NS is free
+      if (kt + D < nk) issue((kt + D) % NS);
+      compute(kt % NS);
+    }
+  }
+  if constexpr (EPI <= SMEM) {
+    if (g_epi_lds) {
+      store_tile_lds<TO, BM, BN, FM, FN, NW * 64>(acc, smem, m0, n0, wm * WTM, wn * WTN, lane, g, y, ep);
+      return;
+    }
+  }
+  if (ep.stats) {
+    double st1[FN][4], st2[FN][4];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) st1[i][e] = st2[i][e] = 0.0;
+    store_tile<TO, FM, FN>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, g, y, ep, st1, st2);
+    frag_stats<FN, BN, NW>(st1, st2, wn * WTN, smem, m0 / BM, n0, ep.stats, ep.sld);
+    return;
+  }
+  store_tile<TO, FM, FN>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, g, y, ep);
+}
+
+// split-K finalize: y[pixel(m)][n] = act(ws[m][n] * scale[n] + shift[n] + res[pixel(m)][n])
+template <typename TO>
+__global__ void splitk_finalize_kernel(const float* __restrict__ ws, TO* __restrict__ y, ConvGeom g, Epi<TO> ep) {
+  const long long total = g.M * g.K;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int n = (int)(i % g.K);
+    const long long m = i / g.K;
+    const int ox = (int)m % g.OW;    // 32-bit decode: geom_ok guarantees M < 2^31
+    const int q = (int)m / g.OW;
+    const int oy = q % g.OH, img = q / g.OH;
+    const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+    float v = ws[i];
+    if (ep.aux) io<TO>::st(ep.aux, op * g.ldy + n, v);
+    if (ep.scale) v *= ep.scale[n];
+    if (ep.shift) v += ep.shift[n];
+    if (ep.res) v += io<TO>::ld(ep.res, op * ep.ldr + n);
+    v = act_fwd(v, ep.relu, ep.slope);
+    io<TO>::st(y, op * g.ldy + n, v);
+  }
+}
+
+// output pixels of a phase whose tap set is empty (e.g. odd rows of a 1x1/s2 dgrad): epilogue of 0
+template <typename TO>
+__global__ void phase_zero_kernel(TO* y, ConvGeom g, Epi<TO> ep) {
+  const long long total = g.M * g.K;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int n = (int)(i % g.K);
+    const long long m = i / g.K;
+    const int ox = (int)m % g.OW;    // 32-bit decode: geom_ok guarantees M < 2^31
+    const int q = (int)m / g.OW;
+    const int oy = q % g.OH, img = q / g.OH;
+    const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+    float v = ep.shift ? ep.shift[n] : 0.f;
+    if (ep.aux) io<TO>::st(ep.aux, op * g.ldy + n, 0.f);
+    if (ep.res) v += io<TO>::ld(ep.res, op * ep.ldr + n);
+    v = act_fwd(v, ep.relu, ep.slope);
+    io<TO>::st(y, op * g.ldy + n, v);
+  }
+}
+
+template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS>
+int launch_glds(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb, unsigned wb,
+                hipStream_t s) {
+  const long long tiles = ((g.M + BM - 1) / BM) * ((g.K + BN - 1) / BN);
+  hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS>), dim3((unsigned)tiles), dim3(NW * 64), 0, s,
+                     (const bf16_t*)x, (const bf16_t*)w, (TO*)y, g, ep, xb, wb, (int)(g_knobs[7] == 0));
+  return BM;
+}
+
+
+// LDS-DMA configs, one translation unit per group (conv_glds_*.hip) so the engine compiles in parallel.
+// Each returns the tile height BM of the launched config (the fused BN statistics write ceil(M/BM) rows).
+template <typename TO>
+int launch_glds_grp_a(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
+                      unsigned wb, hipStream_t s);
+template <typename TO>
+int launch_glds_grp_b(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
+                      unsigned wb, hipStream_t s);
+template <typename TO>
+int launch_glds_grp_d(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
+                      unsigned wb, hipStream_t s);
+template <typename TO>
+int launch_glds_grp_c(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
+                      unsigned wb, hipStream_t s);
+
+
+template <typename T, int BM, int BN>
+inline int plan_splits(const ConvGeom& g) {
+  const long long tiles = ((g.M + BM - 1) / BM) * ((g.K + BN - 1) / BN);
+  const int nk = (g.KK + 64 / (int)sizeof(T) - 1) / (64 / (int)sizeof(T));
+  if (g_knobs[1] < 0 || tiles >= 512 || nk < 32) return 1;
+  long long sp = (1024 + tiles - 1) / tiles;
+  sp = std::min<long long>(sp, nk / 16);
+  if (g_knobs[1] > 0) sp = std::min<long long>(sp, g_knobs[1]);
+  return (int)std::max<long long>(1, std::min<long long>(sp, 64));
+}
+
+
+// register-staged kernel launches (conv_reg_*.hip): returns the tile height BM
+template <typename T, typename TO>
+int dispatch_regstaged(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, float* ws,
+                       hipStream_t s);

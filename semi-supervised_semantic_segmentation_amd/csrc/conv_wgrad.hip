@@ -1,0 +1,622 @@
+// Weight gradients of the implicit-GEMM conv engine (split-K over pixels into fp32 slabs + deterministic
+// reduce, or direct when one split suffices).  Split from conv.hip for parallel compilation.
+#include "conv_kernels.h"
+
+// ------------------------------------------------------------------------------------------------
+// weight gradient: dW[co][kk] = sum_p dY[p][co] * x_col[p][kk], kk = (r, s, c)
+// MFMA A = x_col^T (rows kk), B = dY (cols co).  LDS tiles are stored pixel-major as loaded and the
+// k-contiguous fragments come from ds_read_b64_tr_b16 (bf16) / strided ds_read_b32 (f32).
+// Split-K over pixels; every split writes an fp32 slab tile, a reduce kernel sums the slabs.
+// ------------------------------------------------------------------------------------------------
+template <typename T> struct WG;
+template <> struct WG<bf16_t> {
+  static constexpr int BKP = 64;                   // pixels per k-tile (two 32-deep MFMA steps)
+  static constexpr int PADB = 32;                  // row pad bytes (row stride == 8 dwords mod 64)
+};
+template <> struct WG<float> {
+  static constexpr int BKP = 16;
+  static constexpr int PADB = 64;                  // row stride == 16 dwords mod 32
+};
+
+// MFMA k index (8g + j) -> LDS row, conflict-free for the transpose reads
+__device__ __forceinline__ int kperm(int g, int j) { return 16 * (g >> 1) + 8 * (j >> 2) + 4 * (g & 1) + (j & 3); }
+
+struct WDirect {   // splits == 1: write dW in its final layout (no slab, no reduce launch)
+  float* dw;
+  int c_real, k_real, layout, accumulate;
+};
+
+template <typename T, int BMW, int BNW>
+__global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                    float* __restrict__ slab, ConvGeom g, long long pix_per_split,
+                                                    WDirect dd) {
+  constexpr int VEC = MF<T>::VEC;
+  constexpr int BKP = WG<T>::BKP;
+  constexpr int ROWX = BMW * (int)sizeof(T) + WG<T>::PADB;
+  constexpr int ROWD = BNW * (int)sizeof(T) + WG<T>::PADB;
+  constexpr int XCH = BMW / VEC, DCH = BNW / VEC;          // 16-byte chunks per row
+  constexpr int X_IT = BKP * XCH / 256, D_IT = BKP * DCH / 256;
+  static_assert(X_IT >= 1 && D_IT >= 1 && (256 % XCH) == 0 && (256 % DCH) == 0, "wgrad tile");
+  constexpr int WTM = BMW / 2, WTN = BNW / 2, FM = WTM / 16, FN = WTN / 16;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BKP * (ROWX + ROWD)];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int kk0 = blockIdx.x * BMW, co0 = blockIdx.y * BNW;
+  const long long p_begin = (long long)blockIdx.z * pix_per_split;
+  const long long p_end = min(p_begin + pix_per_split, g.M);
+
+  // x_col chunk of this thread: fixed (r, s, c)
+  const int xc = t % XCH;
+  const int kkx = kk0 + xc * VEC;
+  const bool kk_ok = kkx < g.KK;
+  const int tapx = kk_ok ? kkx / g.C : 0, cx = kk_ok ? kkx % g.C : 0;
+  const int rx = tapx / g.S, sx_ = tapx % g.S;
+  const int dc = t % DCH;
+  const int cod = co0 + dc * VEC;
+  const bool co_ok = cod < g.K;
+
+  // pixel state per loaded x row, advanced incrementally (no per-tile division): row pixel
+  // p = p_begin + t/XCH + i*(256/XCH) + kt*BKP, decoded once into (img, oy, ox)
+  long long xp[X_IT];
+  int ximg[X_IT], xoy[X_IT], xox[X_IT];
+  long long dp[D_IT];
+#pragma unroll
+  for (int i = 0; i < X_IT; ++i) {
+    xp[i] = p_begin + t / XCH + i * (256 / XCH);
+    const long long pp = xp[i] < g.M ? xp[i] : 0;
+    xox[i] = (int)(pp % g.OW);
+    const long long q = pp / g.OW;
+    xoy[i] = (int)(q % g.OH);
+    ximg[i] = (int)(q / g.OH);
+  }
+#pragma unroll
+  for (int i = 0; i < D_IT; ++i) dp[i] = p_begin + t / DCH + i * (256 / DCH);
+
+  uint4 rx_[X_IT], rd_[D_IT];
+  auto load = [&]() {
+#pragma unroll
+    for (int i = 0; i < X_IT; ++i) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (xp[i] < p_end && kk_ok) {
+        const int iy = xoy[i] * g.sy + rx * g.dy + g.py, ix = xox[i] * g.sx + sx_ * g.dx + g.px;
+        if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
+          v = *(const uint4*)(x + ((long long)(ximg[i] * g.H + iy) * g.W + ix) * g.ldx + cx);
+      }
+      rx_[i] = v;
+      xp[i] += BKP;
+      xox[i] += BKP;
+      while (xox[i] >= g.OW) {
+        xox[i] -= g.OW;
+        if (++xoy[i] == g.OH) {
+          xoy[i] = 0;
+          ++ximg[i];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < D_IT; ++i) {
+      const long long p = dp[i];
+      rd_[i] = (p < p_end && co_ok) ? *(const uint4*)(dy + p * g.ldy + cod) : make_uint4(0, 0, 0, 0);
+      dp[i] += BKP;
+    }
+  };
+  auto store = [&](int buf) {
+    char* Xs = smem + buf * BKP * (ROWX + ROWD);
+    char* Ds = Xs + BKP * ROWX;
+#pragma unroll
+    for (int i = 0; i < X_IT; ++i) *(uint4*)(Xs + (t / XCH + i * (256 / XCH)) * ROWX + xc * 16) = rx_[i];
+#pragma unroll
+    for (int i = 0; i < D_IT; ++i) *(uint4*)(Ds + (t / DCH + i * (256 / DCH)) * ROWD + dc * 16) = rd_[i];
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const long long npix = p_end > p_begin ? p_end - p_begin : 0;
+  const int nk = (int)((npix + BKP - 1) / BKP);
+  if (nk > 0) {
+    load();
+    store(0);
+    __syncthreads();
+  }
+  const int gq = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) load();
+    const char* Xs = smem + buf * BKP * (ROWX + ROWD);
+    const char* Ds = Xs + BKP * ROWX;
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int ks = 0; ks < BKP / 32; ++ks) {
+      bf16x8 af[FM], bfr[FN];
+      const int r0 = ks * 32 + kperm(gq, q4), r1 = ks * 32 + kperm(gq, 4 + q4);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int col = wm * WTM + i * 16 + 4 * p4;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Xs + r0 * ROWX + col * 2));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Xs + r1 * ROWX + col * 2));
+        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = wn * WTN + j * 16 + 4 * p4;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ds + r0 * ROWD + col * 2));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ds + r1 * ROWD + col * 2));
+        bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < BKP / 4; ++ks) {
+        const int row = ks * 4 + gq;
+        float af[FM], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = *(const float*)(Xs + row * ROWX + (wm * WTM + i * 16 + li) * 4);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfr[j] = *(const float*)(Ds + row * ROWD + (wn * WTN + j * 16 + li) * 4);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  // slab[split][co][kk]: lane holds kk .. kk+3 (rows) of channel co (column)
+  if (dd.dw) {   // single split: final layout directly (0 = [K][R][S][C], 1 = [k_real][c_real][R][S]), += if accumulate
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int kkb = kk0 + wm * WTM + i * 16 + 4 * gq;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int co = co0 + wn * WTN + j * 16 + li;
+        if (co >= dd.k_real) continue;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int kk = kkb + e;
+          if (kk >= g.KK) continue;
+          const int c = kk % g.C, tap = kk / g.C;
+          if (c >= dd.c_real) continue;
+          long long o;
+          if (dd.layout == 0) o = ((long long)co * g.R * g.S + tap) * g.C + c;
+          else o = (((long long)co * dd.c_real + c) * g.R + tap / g.S) * g.S + tap % g.S;
+          dd.dw[o] = dd.accumulate ? dd.dw[o] + acc[i][j][e] : acc[i][j][e];
+        }
+      }
+    }
+    return;
+  }
+  float* sl = slab + (long long)blockIdx.z * g.K * g.KK;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int kk = kk0 + wm * WTM + i * 16 + 4 * gq;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int co = co0 + wn * WTN + j * 16 + li;
+      if (co >= g.K || kk >= g.KK) continue;
+      float* p = sl + (long long)co * g.KK + kk;
+      if (kk + 3 < g.KK) {
+        *(float4*)p = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      } else {
+        for (int e = 0; e < 4 && kk + e < g.KK; ++e) p[e] = acc[i][j][e];
+      }
+    }
+  }
+}
+
+// wgrad output of one wave: lane holds dW for kk .. kk+3 (rows) of channel co (column) per fragment.
+// Single split (dd.dw set): final layout directly (0 = [K][R][S][C], 1 = [k_real][c_real][R][S]),
+// += if accumulate; otherwise the fp32 slab tile slab[split][co][kk] that wgrad_reduce_kernel sums.
+template <int FM, int FN>
+__device__ __forceinline__ void wgrad_store(const f32x4 (&acc)[FM][FN], int kkb0, int cob0, int lane,
+                                            const ConvGeom& g, float* __restrict__ slab, const WDirect& dd,
+                                            int split) {
+  const int gq = lane >> 4, li = lane & 15;
+  if (dd.dw) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int kkb = kkb0 + i * 16 + 4 * gq;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int co = cob0 + j * 16 + li;
+        if (co >= dd.k_real) continue;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int kk = kkb + e;
+          if (kk >= g.KK) continue;
+          const int c = kk % g.C, tap = kk / g.C;
+          if (c >= dd.c_real) continue;
+          long long o;
+          if (dd.layout == 0) o = ((long long)co * g.R * g.S + tap) * g.C + c;
+          else o = (((long long)co * dd.c_real + c) * g.R + tap / g.S) * g.S + tap % g.S;
+          dd.dw[o] = dd.accumulate ? dd.dw[o] + acc[i][j][e] : acc[i][j][e];
+        }
+      }
+    }
+    return;
+  }
+  float* sl = slab + (long long)split * g.K * g.KK;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int kk = kkb0 + i * 16 + 4 * gq;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int co = cob0 + j * 16 + li;
+      if (co >= g.K || kk >= g.KK) continue;
+      float* p = sl + (long long)co * g.KK + kk;
+      if (kk + 3 < g.KK) {
+        *(float4*)p = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      } else {
+        for (int e = 0; e < 4 && kk + e < g.KK; ++e) p[e] = acc[i][j][e];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// weight gradient on an LDS-DMA pipeline (bf16, gfx950), for C % BMW == 0: a kk-tile never straddles a
+// tap, so the tap (r, s) and the channel block c0 are block-uniform and each x row of a k-tile is one
+// run of BMW channels of one pixel.  The 64-pixel k-tiles of x (gathered rows) and dY are staged by
+// buffer_load ... lds (16 B per lane; padding pixels and rows past the split get an out-of-range offset
+// and read as zeros) into an NS-deep ring, one raw barrier per k-tile with a counted vmcnt, as in
+// igemm_glds_kernel.  LDS rows are unpadded (128 / 256 B); 16-byte chunk ch of row r is stored at
+// ch ^ wswz(r) — applied on the source offset, since the DMA writes lane-linearly — and the
+// ds_read_b64_tr_b16 fragment reads apply the same XOR.  With the k-slot -> pixel-row map wkp (a
+// half-wave's two 4-row blocks 8 rows apart) every transposed read is bank-conflict-free.  Same
+// contraction, split plan and output path as wgrad_kernel.
+// ------------------------------------------------------------------------------------------------
+template <int ROWB>
+__device__ __forceinline__ int wswz(int r) {
+  if constexpr (ROWB == 256) return ((r & 3) << 2) | ((r >> 2) & 3);
+  else return (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 1);
+}
+__device__ __forceinline__ int wkp(int g, int j) { return 16 * (g >> 1) + 8 * (g & 1) + 4 * (j >> 2) + (j & 3); }
+
+template <int BMW, int BNW, int NS>
+__global__ void __launch_bounds__(256) wgrad_glds_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                                                         float* __restrict__ slab, ConvGeom g, long long pix_per_split,
+                                                         WDirect dd, unsigned xbytes, unsigned dbytes) {
+  constexpr int BKP = 64;                                    // pixels per k-tile
+  constexpr int ROWX = BMW * 2, ROWD = BNW * 2;              // LDS row bytes
+  constexpr int XCPR = ROWX / 16, DCPR = ROWD / 16;          // 16-byte chunks per row
+  constexpr int XI = BKP * XCPR / 256, DI = BKP * DCPR / 256;   // wave-instructions per wave per stage
+  constexpr int NL = XI + DI;
+  constexpr int STAGE = BKP * (ROWX + ROWD);
+  constexpr int WTM = BMW / 2, WTN = BNW / 2, FM = WTM / 16, FN = WTN / 16;
+  static_assert(XI >= 1 && DI >= 1 && NS >= 2 && NS <= 3, "wgrad glds tile");
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  // 1-D grid, XCD-aware: consecutive logical ids (the mt x nt tiles of one pixel split, which gather the
+  // same x and dY rows) run on one XCD and share its L2
+  const int mt = (g.KK + BMW - 1) / BMW, nt = (g.K + BNW - 1) / BNW;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int split = tile / (mt * nt), rem = tile - split * (mt * nt);
+  const int kk0 = (rem % mt) * BMW, co0 = (rem / mt) * BNW;
+  const long long p_begin = (long long)split * pix_per_split;
+  const long long p_end = min(p_begin + pix_per_split, g.M);
+  const int tap = kk0 / g.C, c0 = kk0 - tap * g.C;
+  const int tr = tap / g.S, ts = tap - tr * g.S;
+  const int offy = tr * g.dy + g.py, offx = ts * g.dx + g.px;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc((void*)dy, (short)0, (int)dbytes, 0x00020000);
+
+  // x slot ii of this lane: LDS row (wave*XI + ii)*(64/XCPR) + lane/XCPR, logical chunk (lane%XCPR)^swz;
+  // its pixel advances by BKP per k-tile (incremental decode, no per-tile division)
+  long long xp[XI];
+  int xoy[XI], xox[XI], ximg[XI], xcb[XI];
+#pragma unroll
+  for (int ii = 0; ii < XI; ++ii) {
+    const int row = (wave * XI + ii) * (64 / XCPR) + lane / XCPR;
+    xcb[ii] = (c0 + ((lane % XCPR) ^ wswz<ROWX>(row)) * 8) * 2;
+    xp[ii] = p_begin + row;
+    const long long pp = xp[ii] < g.M ? xp[ii] : 0;
+    xox[ii] = (int)(pp % g.OW);
+    const long long q = pp / g.OW;
+    xoy[ii] = (int)(q % g.OH);
+    ximg[ii] = (int)(q / g.OH);
+  }
+  long long dp[DI];
+  int dcb[DI];
+#pragma unroll
+  for (int jj = 0; jj < DI; ++jj) {
+    const int row = (wave * DI + jj) * (64 / DCPR) + lane / DCPR;
+    const int co = co0 + ((lane % DCPR) ^ wswz<ROWD>(row)) * 8;
+    dcb[jj] = co < g.K ? co * 2 : -1;
+    dp[jj] = p_begin + row;
+  }
+  auto issue = [&](int buf) {
+    char* Xs = smem + buf * STAGE;
+    char* Ds = Xs + BKP * ROWX;
+#pragma unroll
+    for (int ii = 0; ii < XI; ++ii) {
+      unsigned off = OOB;
+      if (xp[ii] < p_end) {
+        const int iy = xoy[ii] * g.sy + offy, ix = xox[ii] * g.sx + offx;
+        if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
+          off = (unsigned)(((ximg[ii] * g.H + iy) * g.W + ix) * g.ldx) * 2u + (unsigned)xcb[ii];
+      }
+      bldslds16(xr, Xs + (wave * XI + ii) * 1024, off, 0);
+      xp[ii] += BKP;
+      xox[ii] += BKP;
+      while (xox[ii] >= g.OW) {
+        xox[ii] -= g.OW;
+        if (++xoy[ii] == g.OH) {
+          xoy[ii] = 0;
+          ++ximg[ii];
+        }
+      }
+    }
+#pragma unroll
+    for (int jj = 0; jj < DI; ++jj) {
+      const unsigned off = (dp[jj] < p_end && dcb[jj] >= 0) ? (unsigned)(dp[jj] * g.ldy * 2 + dcb[jj]) : OOB;
+      bldslds16(dr, Ds + (wave * DI + jj) * 1024, off, 0);
+      dp[jj] += BKP;
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int gq = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  auto compute = [&](int buf) {
+    const char* Xs = smem + buf * STAGE;
+    const char* Ds = Xs + BKP * ROWX;
+#pragma unroll
+    for (int ks = 0; ks < BKP / 32; ++ks) {
+      const int r0 = ks * 32 + wkp(gq, q4), r1 = ks * 32 + wkp(gq, 4 + q4);
+      const int sx0 = 16 * wswz<ROWX>(r0), sx1 = 16 * wswz<ROWX>(r1);
+      const int sd0 = 16 * wswz<ROWD>(r0), sd1 = 16 * wswz<ROWD>(r1);
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int col = wm * WTM + i * 16 + 4 * p4;
+        const int cb = 16 * (col >> 3), e8 = 2 * (col & 7);
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Xs + r0 * ROWX + (cb ^ sx0) + e8));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Xs + r1 * ROWX + (cb ^ sx1) + e8));
+        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = wn * WTN + j * 16 + 4 * p4;
+        const int cb = 16 * (col >> 3), e8 = 2 * (col & 7);
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ds + r0 * ROWD + (cb ^ sd0) + e8));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ds + r1 * ROWD + (cb ^ sd1) + e8));
+        bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  const long long npix = p_end > p_begin ? p_end - p_begin : 0;
+  const int nk = (int)((npix + BKP - 1) / BKP);
+  constexpr int D = NS - 1;   // k-tiles in flight ahead of the one being multiplied
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+    if (p < nk) issue(p);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (D >= 2 && kt + 1 < nk) vmcnt_wait<NL>();   // tile kt landed, tile kt+1 may stay in flight
+    else vmcnt_wait<0>();
+    __builtin_amdgcn_s_barrier();                  // every wave's tile kt landed; slot (kt+D)%NS is free
+    if (kt + D < nk) issue((kt + D) % NS);
+    compute(kt % NS);
+  }
+  wgrad_store<FM, FN>(acc, kk0 + wm * WTM, co0 + wn * WTN, lane, g, slab, dd, split);
+}
+
+// sum the split slabs and write dW in the requested layout: 0 = [K][R][S][C] (packed, C = physical),
+// 1 = [K][C_real][R][S] (PyTorch OIHW).  accumulate: dst += sum.
+// A block owns 64 consecutive outputs (256-byte slab rows, coalesced) and spreads the splits over its 16
+// waves: wave w sums splits w, w+16, ... in two chains (16 loads in flight per lane with the unroll), then
+// the 16 partials are added in wave order through LDS — a fixed order, so the result is deterministic.
+__global__ void __launch_bounds__(1024) wgrad_reduce_wide_kernel(const float* __restrict__ slab, int splits, int K, int R,
+                                                            int S, int C, int c_real, int k_real,
+                                                            float* __restrict__ dst, int layout, int accumulate) {
+  __shared__ float red[16][64];
+  const long long KK = (long long)R * S * C;
+  const long long total = (long long)K * KK;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long i = (long long)blockIdx.x * 64 + lane;
+  float a0 = 0.f, a1 = 0.f;
+  if (i < total) {
+    int z = w;
+#pragma unroll 8
+    for (; z + 16 < splits; z += 32) {
+      a0 += slab[(long long)z * total + i];
+      a1 += slab[(long long)(z + 16) * total + i];
+    }
+    if (z < splits) a0 += slab[(long long)z * total + i];
+  }
+  red[w][lane] = a0 + a1;
+  __syncthreads();
+  if (w != 0 || i >= total) return;
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) sum += red[k][lane];
+  const int kk = (int)(i % KK), k = (int)(i / KK);
+  const int c = kk % C, tap = kk / C, r = tap / S, s = tap % S;
+  if (c >= c_real || k >= k_real) return;
+  long long o;
+  if (layout == 0) o = ((long long)k * R * S + tap) * C + c;
+  else o = (((long long)k * c_real + c) * R + r) * S + s;
+  dst[o] = accumulate ? dst[o] + sum : sum;
+}
+
+// few splits: one thread per output, 4 independent chains
+__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int K, int R, int S, int C, int c_real,
+                                    int k_real, float* __restrict__ dst, int layout, int accumulate) {
+  const long long KK = (long long)R * S * C;
+  const long long total = (long long)K * KK;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int kk = (int)(i % KK), k = (int)(i / KK);
+    const int c = kk % C, tap = kk / C, r = tap / S, s = tap % S;
+    if (c >= c_real || k >= k_real) continue;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int z = 0;
+    for (; z + 4 <= splits; z += 4) {
+      s0 += slab[(long long)z * total + i];
+      s1 += slab[(long long)(z + 1) * total + i];
+      s2 += slab[(long long)(z + 2) * total + i];
+      s3 += slab[(long long)(z + 3) * total + i];
+    }
+    for (; z < splits; ++z) s0 += slab[(long long)z * total + i];
+    const float sum = (s0 + s1) + (s2 + s3);
+    long long o;
+    if (layout == 0) o = ((long long)k * R * S + tap) * C + c;
+    else o = (((long long)k * c_real + c) * R + r) * S + s;
+    dst[o] = accumulate ? dst[o] + sum : sum;
+  }
+}
+
+namespace {
+
+struct WgradPlan {
+  int bmw, bnw, mt, nt, splits;
+  long long pps;
+  bool glds;
+};
+
+template <typename T>
+WgradPlan plan_wgrad(const ConvGeom& g, int bmw = 0) {
+  WgradPlan p;
+  p.glds = false;
+  p.bnw = g.K <= 64 ? 64 : 128;
+  p.bmw = bmw ? bmw : (g.KK <= 64 ? 64 : 128);   // (a 256x64 tile for Cout <= 64 measured slower: 263 -> 208 TF)
+  p.mt = (g.KK + p.bmw - 1) / p.bmw;
+  p.nt = (g.K + p.bnw - 1) / p.bnw;
+  const long long tiles = (long long)p.mt * p.nt;
+  const int bkp = WG<T>::BKP;
+  const long long max_splits_by_work = std::max<long long>(1, g.M / (bkp * 8));   // >= 8 k-tiles per split
+  long long want = std::max<long long>(1, (1024 + tiles - 1) / tiles);
+  const long long slab_cap = std::max<long long>(1, (64ll << 20) / (4ll * g.K * g.KK + 1));  // <= 64 MiB of slabs
+  // (capping splits by slab traffic measured slower: layer3/4 wgrads need the parallelism, 58 -> 150 us)
+  long long sp = std::min(std::min(want, max_splits_by_work), slab_cap);
+  sp = std::max<long long>(1, std::min<long long>(sp, 65535));
+  p.pps = (g.M + sp - 1) / sp;
+  p.pps = (p.pps + bkp - 1) / bkp * bkp;
+  p.splits = (int)((g.M + p.pps - 1) / p.pps);
+  if (p.splits < 1) p.splits = 1;
+  return p;
+}
+
+template <typename T>
+void launch_wgrad(const void* x, const void* dy, float* slab, const ConvGeom& g, const WgradPlan& p, WDirect dd,
+                  hipStream_t s) {
+  const dim3 grid(p.mt, p.nt, p.splits);
+  if (p.bmw == 64 && p.bnw == 64)
+    hipLaunchKernelGGL((wgrad_kernel<T, 64, 64>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, g, p.pps, dd);
+  else if (p.bmw == 64)
+    hipLaunchKernelGGL((wgrad_kernel<T, 64, 128>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, g, p.pps, dd);
+  else if (p.bnw == 64)
+    hipLaunchKernelGGL((wgrad_kernel<T, 128, 64>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, g, p.pps, dd);
+  else
+    hipLaunchKernelGGL((wgrad_kernel<T, 128, 128>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, g, p.pps, dd);
+}
+
+// LDS-DMA weight gradient: bf16, C % 64 == 0 (a 64- or 128-channel kk-tile inside one tap), operands < 2 GB
+static bool wgrad_glds_ok(const ConvGeom& g, int dt) {
+  if (dt != SSSEG_BF16 || g_knobs[8] != 0) return false;
+  if (g.C % 64 || g.ldx % 8 || g.ldy % 8 || g.K % 8) return false;
+  const long long xb = (long long)g.N * g.H * g.W * g.ldx * 2, db = g.M * g.ldy * 2;
+  return xb < 0x7fffffffLL && db < 0x7fffffffLL;
+}
+
+static WgradPlan choose_wgrad(const ConvGeom& g, int dt) {
+  WgradPlan p;
+  if (wgrad_glds_ok(g, dt)) {
+    p = plan_wgrad<bf16_t>(g, (g.C % 128 == 0 && g.KK > 64) ? 128 : 64);
+    p.glds = true;
+  } else {
+    p = dt == SSSEG_BF16 ? plan_wgrad<bf16_t>(g) : plan_wgrad<float>(g);
+  }
+  return p;
+}
+
+template <int BMW, int BNW>
+void launch_wgrad_glds_t(const void* x, const void* dy, float* slab, const ConvGeom& g, const WgradPlan& p, WDirect dd,
+                         hipStream_t s) {
+  constexpr int NS = 64 * (BMW + BNW) * 2 <= 24576 ? 3 : 2;   // 48 / 72 / 64 KB of LDS: 2-3 blocks per CU
+  const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.ldx * 2), db = (unsigned)(g.M * g.ldy * 2);
+  hipLaunchKernelGGL((wgrad_glds_kernel<BMW, BNW, NS>), dim3(p.mt * p.nt * p.splits), dim3(256), 0, s, (const bf16_t*)x,
+                     (const bf16_t*)dy, slab, g, p.pps, dd, xb, db);
+}
+
+void launch_wgrad_glds(const void* x, const void* dy, float* slab, const ConvGeom& g, const WgradPlan& p, WDirect dd,
+                       hipStream_t s) {
+  if (p.bmw == 128 && p.bnw == 128) launch_wgrad_glds_t<128, 128>(x, dy, slab, g, p, dd, s);
+  else if (p.bmw == 128) launch_wgrad_glds_t<128, 64>(x, dy, slab, g, p, dd, s);
+  else if (p.bnw == 128) launch_wgrad_glds_t<64, 128>(x, dy, slab, g, p, dd, s);
+  else launch_wgrad_glds_t<64, 64>(x, dy, slab, g, p, dd, s);
+}
+
+
+bool wg_geom_ok(const ConvGeom& g, int dt) {
+  const int vec = dt == SSSEG_BF16 ? 8 : 4;
+  if (g.C % vec || g.ldx % vec || g.ldw % vec) return false;
+  if (g.N < 1 || g.OH < 1 || g.OW < 1 || g.K < 1 || g.C < 1) return false;
+  if (g.M >= 0x7fffffffLL) return false;
+  if (g.R < 0 || g.S < 0) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" size_t ssseg_conv_wgrad_workspace_bytes(const ssseg_conv_desc* d, int dt) {
+  ConvGeom g;
+  if (!make_geom(d, g)) return 0;
+  const WgradPlan p = choose_wgrad(g, dt);
+  return (size_t)p.splits * g.K * g.KK * sizeof(float) + 256;
+}
+
+extern "C" int ssseg_conv_wgrad(const void* x, const void* dy, float* dw, const ssseg_conv_desc* d, int dt,
+                                int64_t c_real, int64_t k_real, int layout, int accumulate, void* ws, size_t ws_bytes,
+                                ssseg_stream_t stream) {
+  ConvGeom g;
+  if (!make_geom(d, g) || !x || !dy || !dw) return SSSEG_EINVAL;
+  if (!wg_geom_ok(g, dt) || g.ldy % (dt == SSSEG_BF16 ? 8 : 4) || g.K % (dt == SSSEG_BF16 ? 8 : 4)) return SSSEG_EINVAL;
+  if (c_real < 1 || c_real > g.C || k_real < 1 || k_real > g.K || (layout != 0 && layout != 1)) return SSSEG_EINVAL;
+  if (!ws || ws_bytes < ssseg_conv_wgrad_workspace_bytes(d, dt)) return SSSEG_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  float* slab = (float*)ws;
+  WgradPlan p;
+  if (dt != SSSEG_BF16 && dt != SSSEG_F32) return SSSEG_EUNSUPPORTED;
+  p = choose_wgrad(g, dt);
+  const WDirect dd{p.splits == 1 ? dw : nullptr, (int)c_real, (int)k_real, layout, accumulate};
+  if (p.glds)
+    launch_wgrad_glds(x, dy, slab, g, p, dd, s);
+  else if (dt == SSSEG_BF16)
+    launch_wgrad<bf16_t>(x, dy, slab, g, p, dd, s);
+  else
+    launch_wgrad<float>(x, dy, slab, g, p, dd, s);
+  if (p.splits == 1) {
+    SSSEG_LAUNCH_CHECK();
+    return 0;
+  }
+  const long long total = (long long)g.K * g.KK;
+  if (p.splits >= 64)   // many splits: spread them over the 16 waves of a block
+    hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)((total + 63) / 64)), dim3(1024), 0, s, slab, p.splits,
+                       g.K, g.R, g.S, g.C, (int)c_real, (int)k_real, dw, layout, accumulate);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ssseg_grid(total, 256)), dim3(256), 0, s, slab, p.splits, g.K, g.R, g.S,
+                       g.C, (int)c_real, (int)k_real, dw, layout, accumulate);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+

@@ -22,6 +22,8 @@ Gradients accumulate between them and the all-reduce is linear, so reducing once
 backward of the step — gives the same averaged gradient (up to fp summation order) with half the
 traffic.  Documented in DESIGN.md; arm() on every backward restores the reference's pattern.
 """
+import os
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
@@ -60,6 +62,7 @@ class DistributedDataParallel(nn.Module):
         self._avg = self.world > 1 and dist.get_backend() == 'nccl'
         self._expected = None         # per-param contributions of an armed backward (learned on the first)
         self._learning = True
+        self._overlap = os.environ.get('SSSEG_DDP_OVERLAP', '1') != '0'   # 0: every bucket in finish() (A/B)
         self._armed = False
         self.last_early = 0
         self._launched = None
@@ -89,7 +92,7 @@ class DistributedDataParallel(nn.Module):
             return
         k = id(p)
         self._seen[k] = self._seen.get(k, 0) + 1
-        if self._learning:
+        if self._learning or not self._overlap:
             return
         if self._launched[i]:
             raise RuntimeError('ssseg DDP: a gradient contribution arrived after its bucket was all-reduced '

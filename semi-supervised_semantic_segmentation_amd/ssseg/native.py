@@ -64,6 +64,7 @@ SIGS = {
     # batch norm
     'ssseg_bn_workspace_bytes': (sz, [i64]),
     'ssseg_bn_stats': (i32, [vp, i64, i64, i64, i32, vp, vp, sz, vp]),
+    'ssseg_bn_partials_finalize': (i32, [vp, i64, i64, vp, f64, f32, f32, vp, vp, vp, vp, vp, vp]),
     'ssseg_bn_finalize': (i32, [vp, i64, f64, f32, f32, vp, vp, vp, vp, vp, vp]),
     'ssseg_bn_eval_params': (i32, [vp, vp, f32, i64, vp, vp, vp]),
     'ssseg_bn_fold': (i32, [vp, vp, vp, vp, vp, f32, i64, i64, vp, vp, vp, vp, vp]),
@@ -110,7 +111,8 @@ class ConvDesc(ctypes.Structure):
 class ConvEpilogue(ctypes.Structure):
     """Mirror of ssseg_conv_epilogue (include/ssseg.h)."""
     _fields_ = [('scale', ctypes.c_void_p), ('shift', ctypes.c_void_p), ('residual', ctypes.c_void_p),
-                ('ldr', ctypes.c_int64), ('aux', ctypes.c_void_p), ('relu', ctypes.c_int32), ('slope', ctypes.c_float)]
+                ('ldr', ctypes.c_int64), ('aux', ctypes.c_void_p), ('relu', ctypes.c_int32), ('slope', ctypes.c_float),
+                ('stats', ctypes.c_void_p), ('stats_ld', ctypes.c_int64), ('stats_rows', ctypes.c_void_p)]
 
 
 _lib = None

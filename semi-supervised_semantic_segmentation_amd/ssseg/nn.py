@@ -18,7 +18,7 @@ import torch.nn as nn
 
 from . import native as N
 
-_CFG = {'dtype': torch.bfloat16, 'sync_bn': True}
+_CFG = {'dtype': torch.bfloat16, 'sync_bn': True, 'fuse_stats': True}
 
 
 def set_compute_dtype(dtype):
@@ -32,6 +32,11 @@ def compute_dtype():
 
 def set_sync_bn(flag):
     _CFG['sync_bn'] = bool(flag)
+
+
+def set_fused_bn_stats(flag):
+    """Training BatchNorm statistics from the producing conv's epilogue (default) or a separate pass."""
+    _CFG['fuse_stats'] = bool(flag)
 
 
 def vec(dtype=None):
@@ -219,10 +224,36 @@ def _take(handoff):
     return handoff.take() if handoff is not None else None
 
 
+class StatRows:
+    """fp64 BatchNorm statistics partials written by a conv's epilogue (ssseg_conv_epilogue.stats): rows of
+    (sum y, sum y^2) per output tile, appended launch by launch (a ConvTranspose2d writes one run per output
+    phase).  The training BatchNorm that consumes y reduces them (ssseg_bn_partials_finalize) instead of
+    reading y again."""
+    __slots__ = ('part', 'C', 'rows', 'cap', '_out')
+
+    def __init__(self, C, max_rows, device):
+        import ctypes
+        self.C, self.cap, self.rows = int(C), int(max_rows), 0
+        self.part = torch.empty(2 * self.cap * self.C, dtype=torch.float64, device=device)
+        self._out = ctypes.c_int64(0)
+
+    def launch_fields(self):
+        """(stats pointer for the next launch, ld, host pointer receiving its row count)"""
+        import ctypes
+        if self.rows >= self.cap:
+            raise RuntimeError('ssseg: BN statistics partial table full')
+        return N.dev_ptr(self.part) + 2 * self.rows * self.C * 8, self.C, ctypes.addressof(self._out)
+
+    def commit(self):
+        self.rows += int(self._out.value)
+        if self.rows > self.cap:
+            raise RuntimeError('ssseg: BN statistics partial table overflow')
+
+
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, mod, relu, handoff=None):
-        y = mod._ssseg_forward(x, relu)
+    def forward(ctx, x, weight, bias, mod, relu, handoff=None, stats=None):
+        y = mod._ssseg_forward(x, relu, stats=stats)
         ctx.mod, ctx.relu, ctx.handoff = mod, relu, handoff
         ctx.save_for_backward(x, y if _act(relu)[0] else None)
         return y
@@ -246,7 +277,7 @@ class _ConvFn(torch.autograd.Function):
             dx = mod._ssseg_dgrad(gy, x.shape, residual=pending)
         else:
             dx = mod._ssseg_dgrad(gy, x.shape)
-        return dx, None, None, None, None, None
+        return dx, None, None, None, None, None, None
 
 
 def _bias_grad(mod, gy):
@@ -294,7 +325,7 @@ class _ConvBase:
             _PACK_EPOCH[0] += 1
         return t
 
-    def _igemm(self, x, w, y, desc, out_dt, bias=None, relu=False, fold=None):
+    def _igemm(self, x, w, y, desc, out_dt, bias=None, relu=False, fold=None, stats=None):
         """One engine launch; epilogue y = act(acc*scale + shift + residual) with shift = bias, or
         fold = (scale, shift, residual, aux) from a folded eval BatchNorm (conv_bn_act); aux, when given,
         receives the raw accumulator (the pre-BN activation the differentiated eval pass needs)."""
@@ -302,12 +333,15 @@ class _ConvBase:
         nb = N.lib().ssseg_conv_igemm_workspace_bytes(dref, N.dt_code(x)) if w is not None else 0
         ws = N.workspace(nb, x.device) if nb else None
         scale, shift, res, aux = fold if fold is not None else (None, bias, None, None)
+        sf = stats.launch_fields() if stats is not None else (None, 0, None)
         ep = N.ConvEpilogue(N.dev_ptr(scale) if scale is not None else None,
                             N.dev_ptr(shift) if shift is not None else None,
                             N.dev_ptr(res) if res is not None else None, res.shape[1] if res is not None else 0,
-                            N.dev_ptr(aux) if aux is not None else None, *_act(relu))
+                            N.dev_ptr(aux) if aux is not None else None, *_act(relu), *sf)
         N.call('ssseg_conv_igemm_epi', N.dev_ptr(x), N.dev_ptr(w) if w is not None else None, N.dev_ptr(y), dref,
                N.dt_code(x), out_dt, ctypes_ref(ep), N.dev_ptr(ws) if ws is not None else None, nb, N.stream())
+        if stats is not None:
+            stats.commit()
 
     def _fold(self, bn, residual, cout, aux=None):
         """Eval BatchNorm (+ this conv's bias) as the epilogue's per-channel affine.  Returns the epilogue
@@ -365,10 +399,17 @@ class Conv2d(nn.Conv2d, _ConvBase):
         return _desc(N=n, H=H, W=W, C=cin, ldx=cin, OH=OH, OW=OW, K=cout, R=R, S=S, sy=sh, sx=sw, dy=dh, dx=dw,
                      py=-ph, px=-pw, outH=OH, outW=OW, osy=1, osx=1, ooy=0, oox=0, ldy=cout, ldw=R * S * cin)
 
-    def forward(self, x, handoff=None):
+    def forward(self, x, handoff=None, stats=None):
         if not _is_act(x):
             x = to_act(x)
-        return _ConvFn.apply(x, self.weight, self.bias, self, False, handoff)
+        return _ConvFn.apply(x, self.weight, self.bias, self, False, handoff, stats)
+
+    def stat_rows_cap(self, n, H, W):
+        """Upper bound of the statistics partial rows one forward writes (None: not fusable here)."""
+        if self._ssseg_dw or self._ssseg_head:
+            return None
+        OH, OW = self._out_hw(H, W)
+        return (n * OH * OW + 63) // 64
 
     def forward_relu(self, x):
         """Conv2d followed by ReLU, fused into the GEMM epilogue (unet.py:27-28 with no norm)."""
@@ -416,10 +457,12 @@ class Conv2d(nn.Conv2d, _ConvBase):
                    N.dt_code(x), ctypes_ref(ep), N.stream())
         return (y, aux, bwd) if keep_pre else y
 
-    def _ssseg_forward(self, x, relu, bn=None, residual=None, keep_pre=False):
+    def _ssseg_forward(self, x, relu, bn=None, residual=None, keep_pre=False, stats=None):
         cin, cout = self._dims()
         _need_act(x, cin, 'Conv2d')
         if self._ssseg_dw:
+            if stats is not None:
+                raise NotImplementedError('ssseg: fused BN statistics on a depthwise conv')
             return self._dw_forward(x, relu, bn, residual, keep_pre)
         n, _, H, W = x.shape
         d = self._fwd_desc(n, H, W)
@@ -443,7 +486,7 @@ class Conv2d(nn.Conv2d, _ConvBase):
             return y[:, :self.out_channels]
         y = new_act(n, cout, d.OH, d.OW, _CFG['dtype'], x.device)
         with _Timed(fl, 'fwd', tg):
-            self._igemm(x, w, y, d, N.dt_code(y), self.bias, relu)
+            self._igemm(x, w, y, d, N.dt_code(y), self.bias, relu, stats=stats)
         return y
 
     def _grad_in(self, gy):
@@ -547,12 +590,25 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
         v = vec()
         return rup(self.in_channels, v), rup(self.out_channels, v)
 
-    def forward(self, x, output_size=None):
+    def forward(self, x, output_size=None, stats=None):
         if output_size is not None:
             raise NotImplementedError('ssseg.nn.ConvTranspose2d: output_size')
         if not _is_act(x):
             x = to_act(x)
-        return _ConvFn.apply(x, self.weight, self.bias, self, self._fuse_relu)
+        return _ConvFn.apply(x, self.weight, self.bias, self, self._fuse_relu, None, stats)
+
+    def stat_rows_cap(self, n, H, W):
+        (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
+        OH, OW = self._out_hw(H, W)
+        rows = 0
+        for (_, _, rny, _, qy) in _phases(sh, ph, R, OH):
+            for (_, _, rnx, _, qx) in _phases(sw, pw, S, OW):
+                if qy == 0 or qx == 0:
+                    continue
+                if rny * rnx == 0:
+                    return None     # an empty tap set is zero-filled by a kernel without the statistics
+                rows += (n * qy * qx + 63) // 64
+        return rows
 
     def forward_relu(self, x):
         """ConvTranspose2d followed by ReLU, fused into the epilogue (unet.py:20-23)."""
@@ -567,7 +623,7 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
         (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
         return (H - 1) * sh - 2 * ph + R, (W - 1) * sw - 2 * pw + S
 
-    def _ssseg_forward(self, x, relu, bn=None, residual=None, keep_pre=False):
+    def _ssseg_forward(self, x, relu, bn=None, residual=None, keep_pre=False, stats=None):
         cin, cout = self._dims()
         _need_act(x, cin, 'ConvTranspose2d')
         n, _, H, W = x.shape
@@ -591,7 +647,7 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
                 d = _desc(N=n, H=H, W=W, C=cin, ldx=cin, OH=qy, OW=qx, K=cout, R=rr, S=ss, sy=1, sx=1, dy=-1, dx=-1,
                           py=dly, px=dlx, outH=OH, outW=OW, osy=sh, osx=sw, ooy=phy, oox=phx, ldy=cout,
                           ldw=max(rr * ss * cin, cin))
-                self._igemm(x, w, y, d, N.dt_code(y), self.bias, relu, fold)
+                self._igemm(x, w, y, d, N.dt_code(y), self.bias, relu, fold, stats=stats)
         timer.__exit__()
         return (y, aux, bwd) if keep_pre else y
 
@@ -648,7 +704,7 @@ def _pad16(C, dtype):
 
 class _BNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, mod, relu, handoff=None):
+    def forward(ctx, x, weight, bias, residual, mod, relu, handoff=None, pre=None):
         C = mod.num_features
         n, cp, h, w = x.shape
         P = n * h * w
@@ -668,7 +724,20 @@ class _BNFn(torch.autograd.Function):
                    N.dev_ptr(mean), N.dev_ptr(invstd), N.dev_ptr(mod.running_mean) if track else None,
                    N.dev_ptr(mod.running_var) if track else None,
                    N.dev_ptr(mod.num_batches_tracked) if track else None)
-            if _sync_group(True):
+            if pre is not None and pre.rows > 0:
+                # statistics partials from the producing conv's epilogue: no pass over x here
+                if pre.C != C:
+                    raise ValueError('ssseg BatchNorm2d: fused statistics width mismatch')
+                if _sync_group(True):
+                    N.call('ssseg_bn_partials_finalize', N.dev_ptr(pre.part), pre.rows, C, N.dev_ptr(sums), 0.0, 0.0,
+                           0.0, None, None, None, None, None, N.stream())
+                    dist.all_reduce(sums)
+                    count = float(P * dist.get_world_size())
+                    N.call('ssseg_bn_finalize', N.dev_ptr(sums), C, count, *fin[2:], N.stream())
+                else:
+                    N.call('ssseg_bn_partials_finalize', N.dev_ptr(pre.part), pre.rows, C, N.dev_ptr(sums), count,
+                           *fin[2:], N.stream())
+            elif _sync_group(True):
                 N.call('ssseg_bn_stats', N.dev_ptr(x), P, C, cp, N.dt_code(x), N.dev_ptr(sums), N.dev_ptr(ws), nb,
                        N.stream())
                 dist.all_reduce(sums)
@@ -728,7 +797,7 @@ class _BNFn(torch.autograd.Function):
         if dres is not None and ctx.handoff is not None:
             ctx.handoff.put(dres)
             dres = None
-        return dx, None, None, dres, None, None, None
+        return dx, None, None, dres, None, None, None, None
 
 
 class BatchNorm2d(nn.BatchNorm2d):
@@ -817,16 +886,26 @@ def conv_bn_act(conv, x, bn, relu=True, residual=None, grad_in=None, grad_out=No
             return conv._ssseg_forward(x, relu, bn=bn, residual=residual)
         return _ConvBNEvalFn.apply(x, conv.weight, conv.bias, bn.weight, bn.bias, residual, conv, bn, relu, grad_in,
                                    grad_out)
-    y = conv(x, handoff=grad_in) if (grad_in is not None and type(conv) is Conv2d) else conv(x)
-    return bn_act(y, bn, relu=relu, residual=residual, grad_out=grad_out)
+    stats = None
+    if (_CFG['fuse_stats'] and isinstance(conv, (Conv2d, ConvTranspose2d)) and isinstance(bn, BatchNorm2d)
+            and (bn.training or not bn.track_running_stats) and bn.num_features == conv.out_channels and x.dim() == 4):
+        cap = conv.stat_rows_cap(x.shape[0], x.shape[2], x.shape[3])
+        if cap:
+            stats = StatRows(bn.num_features, cap, x.device)
+    if type(conv) is Conv2d:
+        y = conv(x, handoff=grad_in, stats=stats)
+    else:
+        y = conv(x, stats=stats) if stats is not None else conv(x)
+    return bn_act(y, bn, relu=relu, residual=residual, grad_out=grad_out, pre=stats)
 
 
-def bn_act(x, bn, relu=True, residual=None, grad_out=None):
-    """act(bn(x) [+ residual]) in one pass: ConvBlock's BN+ReLU (unet.py:9-10), Bottleneck's bn3+add+relu."""
+def bn_act(x, bn, relu=True, residual=None, grad_out=None, pre=None):
+    """act(bn(x) [+ residual]) in one pass: ConvBlock's BN+ReLU (unet.py:9-10), Bottleneck's bn3+add+relu.
+    pre: StatRows the producing conv's epilogue filled (fused training statistics)."""
     if not isinstance(bn, BatchNorm2d):
         raise TypeError('ssseg.nn.bn_act needs an ssseg BatchNorm2d')
     _need_act(x, rup(bn.num_features, vec()), 'BatchNorm2d')
-    return _BNFn.apply(x, bn.weight, bn.bias, residual, bn, relu, grad_out)
+    return _BNFn.apply(x, bn.weight, bn.bias, residual, bn, relu, grad_out, pre)
 
 
 # ------------------------------------------------------------------------------------------------

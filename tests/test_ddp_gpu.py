@@ -103,18 +103,19 @@ def _worker(rank, port, q):
         dist.destroy_process_group()
 
 
-def _oracle():
+def _oracle(dt=torch.float32):
     from oracle import models_ref, train_ref
     torch.manual_seed(0)
     s = models_ref.ListOutput(models_ref.SimpleUNet(2, 3, 8, 32))
     t = models_ref.ListOutput(models_ref.SimpleUNet(2, 3, 8, 32))
     t.load_state_dict(_model().state_dict())
     s.load_state_dict(_model().state_dict())
+    s, t = s.to(dt), t.to(dt)
     for p in t.parameters():
         p.detach_()
     t.eval()
     opt = torch.optim.SGD(s.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
-    imgs, masks, unl = _data()
+    imgs, masks, unl = (v.to(dt) for v in _data())
     cfg = train_ref.default_cfg(sigma_range=(2, 4), confidence_threshold=0.5)
     grads = {}
 
@@ -150,6 +151,7 @@ def test_ddp_syncbn_world2_product_path(hip_device):
     for r in range(WORLD):
         assert not isinstance(res[r], str), res[r]
     logs, g_ref, s_ref, t_ref = _oracle()
+    _, _, s64, t64 = _oracle(torch.float64)
     for r in range(WORLD):
         out = res[r]
         for k, (c, u) in enumerate(out['losses']):
@@ -164,13 +166,22 @@ def test_ddp_syncbn_world2_product_path(hip_device):
             b = g.numpy()
             # floor: gradients that are mathematically zero (a conv bias feeding a BatchNorm) are rounding noise
             assert np.abs(a - b).max() <= 1e-3 * max(np.abs(b).max(), 1e-3 * gmax), (r, n)
-        for name, got, ref in (('student', out['student'], s_ref), ('teacher', out['teacher'], t_ref)):
+        # parameters / buffers after 3 steps vs an fp64 oracle run: within max(1e-3, 2x the fp32 oracle's own
+        # drift) of each tensor's scale (tests/parity.py's rule)
+        bad = []
+        for name, got, ref, ref64 in (('student', out['student'], s_ref, s64), ('teacher', out['teacher'], t_ref, t64)):
             for k, v in ref.items():
-                a, b = got[k], v.numpy()
+                a, b, c = got[k], ref64[k].numpy(), v.numpy()
                 if not np.issubdtype(b.dtype, np.floating):
-                    assert np.array_equal(a, b), (name, k)
+                    assert np.array_equal(a, c), (name, k)
                     continue
-                assert np.abs(a - b).max() <= 1e-3 * (np.abs(b).max() + 1e-6), (r, name, k)
+                scale = np.abs(b).max() + 1e-6
+                e_hip = float(np.abs(a - b).max()) / scale
+                e_32 = float(np.abs(c - b).max()) / scale
+                if e_hip > max(1e-3, 2 * e_32):
+                    bad.append((r, name, k, e_hip, e_32))
+        print('rank', r, 'worst tensors (hip vs fp64, ref32 vs fp64):', sorted(bad, key=lambda x: -x[3])[:5])
+        assert not bad, bad[:5]
     # both ranks hold identical weights (averaged gradients, broadcast init)
     for k in res[0]['student']:
         assert np.array_equal(res[0]['student'][k], res[1]['student'][k]), k

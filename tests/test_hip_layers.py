@@ -497,3 +497,48 @@ def test_bn_fused_tails_match_unfused(hip_device, C, P):
     for a, b in zip(*outs):
         assert torch.equal(a, b)
     assert int(outs[1][5]) == 1
+
+
+@pytest.mark.parametrize('kind,cin,cout,k,s,H', [('conv', 64, 128, 3, 1, 19), ('conv', 128, 64, 1, 1, 17),
+                                                 ('conv', 64, 256, 1, 2, 21), ('conv', 16, 40, 3, 1, 13),
+                                                 ('convT', 128, 64, 4, 2, 7), ('conv', 8, 12, 3, 1, 11)])
+def test_fused_bn_stats_match_separate_pass(hip_device, mode, kind, cin, cout, k, s, H):
+    """Training BatchNorm statistics from the producing conv's epilogue (ssseg_conv_epilogue.stats, fp64 tile
+    partials of the stored output) == the separate statistics pass over that output (ssseg_bn_stats): same
+    normalised output, same running statistics — for every bf16 engine variant (register-staged, each
+    LDS-DMA tile config, with and without the LDS-staged epilogue) and the fp32 path."""
+    from ssseg import native as N
+    from ssseg import nn as snn
+    torch.manual_seed(5)
+    if kind == 'conv':
+        conv = snn.Conv2d(cin, cout, k, s, k // 2, bias=False).to(hip_device)
+    else:
+        conv = snn.ConvTranspose2d(cin, cout, k, s, 1, bias=False).to(hip_device)
+    bn = snn.BatchNorm2d(cout).to(hip_device)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    x = _act_in(torch.randn(2, cin, H, H + 2) + 0.3, hip_device)
+    variants = [(0, 0)] if mode == 'f32' else [(v, e) for v in [11] + list(range(1, 11)) + list(range(12, 18))
+                                                 for e in (0, -1)]
+    try:
+        for v, e in variants:
+            N.call('ssseg_set_knob', 4, v)
+            N.call('ssseg_set_knob', 7, e)
+            outs = []
+            for fused in (False, True):
+                snn.set_fused_bn_stats(fused)
+                bn.reset_running_stats()
+                with torch.no_grad():
+                    y = snn.conv_bn_act(conv, x, bn, relu=True)
+                torch.cuda.synchronize()
+                outs.append((y.float().cpu(), bn.running_mean.cpu().clone(), bn.running_var.cpu().clone()))
+            (y0, m0, v0), (y1, m1, v1) = outs
+            assert torch.allclose(m1, m0, rtol=1e-6, atol=1e-7), (v, e, 'running_mean')
+            assert torch.allclose(v1, v0, rtol=1e-6, atol=1e-7), (v, e, 'running_var')
+            tol = 1e-5 if mode == 'f32' else 1e-2
+            assert float((y1 - y0).abs().max()) <= tol * (float(y0.abs().max()) + 1e-6), (v, e, 'output')
+    finally:
+        N.call('ssseg_set_knob', 4, 0)
+        N.call('ssseg_set_knob', 7, 0)
+        snn.set_fused_bn_stats(True)
