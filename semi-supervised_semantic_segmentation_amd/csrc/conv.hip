@@ -117,8 +117,10 @@ static int heuristic_variant(const ConvGeom& g) {
 template <typename T, typename TO>
 int run_variant(int v, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
                 unsigned wb, hipStream_t s) {
-  if (v == 0) return dispatch_regstaged<T, TO>(x, w, y, g, ep, nullptr, s);
-  return launch_glds_cfg<TO>(v, x, w, y, g, ep, xb, wb, s);
+  if constexpr (sizeof(TO) == 2) {
+    if (v != 0) return launch_glds_cfg<TO>(v, x, w, y, g, ep, xb, wb, s);
+  }
+  return dispatch_regstaged<T, TO>(x, w, y, g, ep, nullptr, s);
 }
 
 template <typename T, typename TO>
@@ -164,9 +166,9 @@ int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const
 template <typename T, typename TO>
 int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, float* ws,
                    hipStream_t s) {
-  if constexpr (sizeof(T) == 2) {
+  if constexpr (sizeof(T) == 2 && sizeof(TO) == 2) {
     const long long xb = (long long)g.N * g.H * g.W * g.ldx * 2, wb = (long long)g.K * g.ldw * 2;
-    if (g_knobs[3] == 0 && !ws && g.C % 64 == 0 && g.ldx % 8 == 0 && g.ldw % 8 == 0 && g.ldw == g.KK &&
+    if (sizeof(TO) == 2 && g_knobs[3] == 0 && !ws && g.C % 64 == 0 && g.ldx % 8 == 0 && g.ldw % 8 == 0 && g.ldw == g.KK &&
         g.K > 16 && xb < 0x7fffffffLL && wb < 0x7fffffffLL) {
       int v = g_knobs[4];
       if (v < 0) v = 0;
@@ -234,6 +236,8 @@ extern "C" int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const
   const ssseg_conv_epilogue& e = epi ? *epi : none;
   if (e.residual && (e.ldr < g.K || e.ldr > 0x7fffffff)) return SSSEG_EINVAL;
   if (e.stats && (!e.stats_rows_host || e.stats_ld < 1 || e.stats_ld > g.K)) return SSSEG_EINVAL;
+  // fused statistics are of acc + shift: the conv feeding a training BatchNorm has no affine / residual / act
+  if (e.stats && (e.scale || e.residual || e.relu || e.aux)) return SSSEG_EINVAL;
   if (e.stats_rows_host) *e.stats_rows_host = 0;
   if (g.M == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
@@ -265,6 +269,7 @@ extern "C" int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const
     bm = dispatch_igemm<float, float>(x, w, y, g, ef, wsf, s);
   else
     return SSSEG_EUNSUPPORTED;
+  if (bm <= 0) return SSSEG_EUNSUPPORTED;
   if (e.stats_rows_host && e.stats) *e.stats_rows_host = (g.M + bm - 1) / bm;
   SSSEG_LAUNCH_CHECK();
   return 0;

@@ -18,6 +18,7 @@
 // pixel: the NHWC epilogue stores them with one 8/16-byte write.
 #pragma once
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 
@@ -112,8 +113,8 @@ template <> __device__ __forceinline__ float stored<bf16_t>(float v) { return bf
 // whose lane index agrees in the bits below `lstride` (a power of two): xor-shuffle over the higher bits,
 // then the NW waves' partials meet in LDS (fixed order: deterministic) and row mtile of the partial table is
 // written for channels [n0, n0 + BN).  Every thread of the block must call this (two barriers).
-template <int V, int BN, int NW>
-__device__ __forceinline__ void tile_stats(double (&s1)[V], double (&s2)[V], int lstride, bool holder, int cofs,
+template <int V, int BN, int NW, typename SA>
+__device__ __forceinline__ void tile_stats(SA (&s1)[V], SA (&s2)[V], int lstride, bool holder, int cofs,
                                            char* smem, long long mtile, int n0, double* __restrict__ stats, int sld) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
@@ -130,8 +131,8 @@ __device__ __forceinline__ void tile_stats(double (&s1)[V], double (&s2)[V], int
   if (holder)
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      red[(w * BN + cofs + e) * 2] = s1[e];
-      red[(w * BN + cofs + e) * 2 + 1] = s2[e];
+      red[(w * BN + cofs + e) * 2] = (double)s1[e];
+      red[(w * BN + cofs + e) * 2 + 1] = (double)s2[e];
     }
   __syncthreads();
   for (int c = threadIdx.x; c < BN; c += NW * 64) {
@@ -275,7 +276,7 @@ template <> struct Out8<float> {
   }
 };
 
-template <typename TO, int BM, int BN, int FM, int FN, int NT>
+template <typename TO, int BM, int BN, int FM, int FN, int NT, bool STATS>
 __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char* smem, long long m0, int n0, int wmo,
                                                int wno, int lane, const ConvGeom& g, TO* __restrict__ y,
                                                const Epi<TO>& ep) {
@@ -292,9 +293,6 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
   constexpr int RPP = NT / CPR, NP = (BM + RPP - 1) / RPP;   // rows per pass, passes
   const int ch = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
   const int n = n0 + ch * 8;
-  double s1[8], s2[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.0;
   if (n < g.K) {
     const bool vec = (g.ldy & 7) == 0 && (!ep.res || (ep.ldr & 7) == 0);
     const bool full = vec && n + 7 < g.K;
@@ -345,13 +343,6 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
         t = act_fwd(t, ep.relu, ep.slope);
         v[e] = t;
       }
-      if (ep.stats)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const double q = n + e < g.K ? (double)stored<TO>(v[e]) : 0.0;
-          s1[e] += q;
-          s2[e] += q * q;
-        }
       const long long o = op[p] * g.ldy + n;
       if (full) {
         Out8<TO>::st(y + o, v);
@@ -364,8 +355,36 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
       }
     }
   }
-  if (ep.stats)
-    tile_stats<8, BN, NT / 64>(s1, s2, CPR, (threadIdx.x & 63) < CPR, ch * 8, smem, m0 / BM, n0, ep.stats, ep.sld);
+  if constexpr (STATS) {
+    // a second pass over the staged tile (registers of the store pass are dead by then): the conv feeding a
+    // training BatchNorm has no scale / residual / activation in its epilogue (host contract), so the stored
+    // value is acc + shift.  Per-thread sums over <= BM / RPP rows in the accumulator type SA (fp32 for bf16
+    // outputs: exact products of 8-bit mantissas, <= 32 terms), fp64 across threads and tiles.
+    using SA = typename std::conditional<sizeof(TO) == 2, float, double>::type;
+    SA s1[8], s2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s1[e] = s2[e] = (SA)0;
+    if (n < g.K) {
+      float sh[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sh[e] = (ep.shift && n + e < g.K) ? ep.shift[n + e] : 0.f;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const int row = r0 + p * RPP;
+        if (row >= BM || m0 + row >= g.M) continue;
+        const float* a = (const float*)(smem + row * LDR + ch * 32);
+        const float4 a0 = *(const float4*)a, a1 = *(const float4*)(a + 4);
+        const float raw[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const SA q = n + e < g.K ? (SA)stored<TO>(raw[e] + sh[e]) : (SA)0;
+          s1[e] += q;
+          s2[e] += q * q;
+        }
+      }
+    }
+    tile_stats<8, BN, NT / 64, SA>(s1, s2, CPR, (threadIdx.x & 63) < CPR, ch * 8, smem, m0 / BM, n0, ep.stats, ep.sld);
+  }
 }
 
 // fused statistics after store_tile (register epilogue): lane holds fp64 sums of fragment column i's 4
@@ -431,7 +450,9 @@ extern int g_knobs[9];   // runtime variant switches (ssseg_set_knob), defined i
 // 7: LDS-staged coalesced epilogue in the LDS-DMA kernel (0 on, -1 off);
 // 8: bf16 weight gradient on the LDS-DMA kernel (0 on, -1 = register-staged wgrad_kernel)
 
-template <typename T, typename TO, int BM, int BN, int WM, int WN, bool DEEP>
+// STATS: the epilogue also writes the fused BatchNorm statistics partials (a separate instantiation: the fp64
+// sums raise the register count, which must not cost the launches that do not need them)
+template <typename T, typename TO, int BM, int BN, int WM, int WN, bool DEEP, bool STATS = false>
 __global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __restrict__ x, const T* __restrict__ w,
                                                                   TO* __restrict__ y, ConvGeom g, Epi<TO> ep,
                                                                   int splits, float* __restrict__ ws) {
@@ -584,7 +605,7 @@ __global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __res
     }
     return;
   }
-  if (ep.stats) {
+  if constexpr (STATS) {
     double st1[FN][4], st2[FN][4];
 #pragma unroll
     for (int i = 0; i < FN; ++i)
@@ -621,7 +642,7 @@ __device__ __forceinline__ void vmcnt_wait() {
 
 constexpr unsigned OOB = 0x80000000u;   // > any num_records we build: the load returns zeros
 
-template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS>
+template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS, bool STATS>
 __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const bf16_t* __restrict__ x,
                                                                 const bf16_t* __restrict__ w, TO* __restrict__ y,
                                                                 ConvGeom g, Epi<TO> ep, unsigned xbytes,
@@ -763,11 +784,11 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const bf16_t* __
   }
   if constexpr (EPI <= SMEM) {
     if (g_epi_lds) {
-      store_tile_lds<TO, BM, BN, FM, FN, NW * 64>(acc, smem, m0, n0, wm * WTM, wn * WTN, lane, g, y, ep);
+      store_tile_lds<TO, BM, BN, FM, FN, NW * 64, STATS>(acc, smem, m0, n0, wm * WTM, wn * WTN, lane, g, y, ep);
       return;
     }
   }
-  if (ep.stats) {
+  if constexpr (STATS) {
     double st1[FN][4], st2[FN][4];
 #pragma unroll
     for (int i = 0; i < FN; ++i)
@@ -823,9 +844,14 @@ __global__ void phase_zero_kernel(TO* y, ConvGeom g, Epi<TO> ep) {
 template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS>
 int launch_glds(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb, unsigned wb,
                 hipStream_t s) {
+  static_assert(sizeof(TO) == 2, "LDS-DMA configs write bf16 activations (fp32-output heads have K <= 16)");
   const long long tiles = ((g.M + BM - 1) / BM) * ((g.K + BN - 1) / BN);
-  hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS>), dim3((unsigned)tiles), dim3(NW * 64), 0, s,
-                     (const bf16_t*)x, (const bf16_t*)w, (TO*)y, g, ep, xb, wb, (int)(g_knobs[7] == 0));
+  if (ep.stats)
+    hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, true>), dim3((unsigned)tiles), dim3(NW * 64), 0,
+                       s, (const bf16_t*)x, (const bf16_t*)w, (TO*)y, g, ep, xb, wb, (int)(g_knobs[7] == 0));
+  else
+    hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, false>), dim3((unsigned)tiles), dim3(NW * 64), 0,
+                       s, (const bf16_t*)x, (const bf16_t*)w, (TO*)y, g, ep, xb, wb, (int)(g_knobs[7] == 0));
   return BM;
 }
 

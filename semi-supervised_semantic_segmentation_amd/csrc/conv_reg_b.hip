@@ -9,7 +9,13 @@ int launch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, const
   const long long tiles = ((g.M + BM - 1) / BM) * ((g.K + BN - 1) / BN);
   const dim3 grid((unsigned)tiles, (unsigned)splits);
   if (splits > 1) (void)hipMemsetAsync(ws, 0, sizeof(float) * g.M * g.K, s);
-  if (g_knobs[0] == 0)
+  if (ep.stats) {
+    if constexpr (sizeof(T) == sizeof(TO))
+      hipLaunchKernelGGL((igemm_kernel<T, TO, BM, BN, WM, WN, false, true>), grid, dim3(256), 0, s, (const T*)x,
+                         (const T*)w, (TO*)y, g, ep, splits, ws);
+    else
+      return -1;   // statistics of a compute-dtype activation only
+  } else if (g_knobs[0] == 0)
     hipLaunchKernelGGL((igemm_kernel<T, TO, BM, BN, WM, WN, false>), grid, dim3(256), 0, s, (const T*)x, (const T*)w,
                        (TO*)y, g, ep, splits, ws);
   else

