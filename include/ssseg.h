@@ -135,6 +135,11 @@ int ssseg_lovasz_bwd(const float* logits, const float* target, int64_t B, int64_
  * on the host):  ema = fma(param, (float)(1-alpha), round(ema*alpha))  — bit-exact with torch CPU. */
 int ssseg_ema_update(float* ema, const float* param, int64_t n, double alpha, ssseg_stream_t stream);
 
+/* torch.sigmoid on contiguous fp32 (the discriminator input of the adversarial branch, configs C5):
+ * y = 1/(1+exp(-x)); backward gx = gy * y * (1 - y) from the saved output. */
+int ssseg_sigmoid_fwd(const float* x, float* y, int64_t n, ssseg_stream_t stream);
+int ssseg_sigmoid_bwd(const float* y, const float* gy, float* gx, int64_t n, ssseg_stream_t stream);
+
 /* x[i] *= a (in place): the 1/world average after a SUM all-reduce on backends without AVG (gloo). */
 int ssseg_scale_f32(float* x, int64_t n, float a, ssseg_stream_t stream);
 

@@ -276,6 +276,21 @@ def resnet50_encoder():
     return ResNet50Encoder()
 
 
+class Discriminator(nn.Module):                                 # discriminator.py:6-28
+    def __init__(self, num_layers, in_channels=2, initial_channels=64, max_depth=512, out_channels=1):
+        super().__init__()
+        layers = []
+        cin, cout = in_channels, initial_channels
+        for _ in range(num_layers):
+            layers.append(nn.Sequential(nn.Conv2d(cin, cout, 4, 2, 1), nn.LeakyReLU(0.2)))
+            cin, cout = cout, min(cout * 2, max_depth)
+        layers.append(nn.Sequential(nn.Conv2d(cin, out_channels, 1, bias=False)))
+        self.net = nn.Sequential(*layers)
+
+    def forward(self, x):
+        return self.net(x)
+
+
 class ListOutput(nn.Module):
     """(features, [logits]) adapter."""
 

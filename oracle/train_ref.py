@@ -75,9 +75,40 @@ def ema_update(model, ema_model, alpha):
         eb.data = b.data
 
 
+def adversarial_terms(preds, mask, adv):
+    """Build-defined adversarial branch of config C5 (train.adversarial_terms): D frozen, student term
+    weight * BCE(D(sigmoid(up(logits))), 1) (Hung et al. 2018; the reference only constructs D,
+    default_config.py:116-120)."""
+    D = adv['D']
+    logits = preds[-1]
+    if tuple(logits.shape[2:]) != tuple(mask.shape[2:]):
+        logits = F.interpolate(logits, size=mask.shape[2:], mode='bilinear', align_corners=False)
+    prob = torch.sigmoid(logits)
+    for p in D.parameters():
+        p.requires_grad_(False)
+    d = D(prob)
+    loss = F.binary_cross_entropy_with_logits(d, torch.ones_like(d)) * adv['weight']
+    for p in D.parameters():
+        p.requires_grad_(True)
+    return loss, prob.detach()
+
+
+def discriminator_step(mask, prob, adv):
+    """D update: BCE(D(mask), 1) + BCE(D(p), 0), SGD step every step (train.discriminator_step)."""
+    D, opt = adv['D'], adv['opt']
+    d_real, d_fake = D(mask), D(prob)
+    loss = F.binary_cross_entropy_with_logits(d_real, torch.ones_like(d_real)) + \
+        F.binary_cross_entropy_with_logits(d_fake, torch.zeros_like(d_fake))
+    loss.backward()
+    opt.step()
+    opt.zero_grad()
+    return float(loss.detach())
+
+
 def train_epoch(model, ema_model, optimizer, batches, unsup_iter, epoch, cfg, loss_weights=(0.5,),
-                on_step=None, loss_fn=None):
-    """Run len(batches) steps; returns per-step dict(sup_loss, unsup_loss, cm_mean)."""
+                on_step=None, loss_fn=None, adv=None):
+    """Run len(batches) steps; returns per-step dict(sup_loss, unsup_loss, cm_mean) (+ adv_loss, d_loss with
+    the adversarial branch adv = dict(D, opt, weight))."""
     tc = cfg
     model.train()
     optimizer.zero_grad()
@@ -85,8 +116,15 @@ def train_epoch(model, ema_model, optimizer, batches, unsup_iter, epoch, cfg, lo
     for step, (image, mask) in enumerate(batches):
         _, preds = model(image)
         sup = calculate_loss(preds, mask, loss_weights, loss_fn)
-        (sup / tc['virtual_batch_size_multiplier']).backward()
         rec = dict(sup_loss=float(sup.detach()))
+        total = sup
+        if adv is not None:
+            adv_loss, prob = adversarial_terms(preds, mask, adv)
+            total = sup + adv_loss
+            rec['adv_loss'] = float(adv_loss.detach())
+        (total / tc['virtual_batch_size_multiplier']).backward()
+        if adv is not None:
+            rec['d_loss'] = discriminator_step(mask, prob, adv)
         if tc['use_semi_supervised']:
             ua = next(unsup_iter)
             ub = next(unsup_iter)

@@ -1,7 +1,9 @@
-"""BASELINE config C5: FC-HarDNet(n_classes=2) 512x512 + Discriminator(5 layers, 64 -> 512 channels), DDP on 8
-GPUs.  BASELINE names fp16; the engine's 16-bit mode is bf16 (same storage and MFMA rate, fp32's exponent range,
-so no loss scaling).  The discriminator is built here exactly as the reference config names it
-(default_config.py:116-120); the reference trainer never calls it."""
+"""BASELINE config C5: FC-HarDNet(n_classes=2) 512x512 + Discriminator(5 layers, 64 -> 512 channels), fp16, DDP on
+8 GPUs.  The discriminator is built exactly as the reference config names it (default_config.py:116-120); the
+reference trainer never calls it, so its adversarial use here is build-defined
+(train.adversarial_terms / discriminator_step, after Hung et al. 2018): weight 0.01 on the student's
+BCE(D(sigmoid(logits)), 1), a discriminator SGD step per training step.  fp16 compute runs with dynamic loss
+scaling (ssseg.amp)."""
 from functools import partial
 
 import torch
@@ -13,7 +15,7 @@ from models.discriminator import Discriminator
 from models.hardnet import HarDNet
 
 common = dict(world_size=8, use_cpu=False, workers=8, output_dir='runs/c5_hardnet_disc', num_classes=2,
-              image_size=512, compute_dtype='bf16')
+              image_size=512, compute_dtype='fp16')
 model = dict(model_fn=lambda: ListOutput(HarDNet(n_classes=2)),
              discriminator=partial(Discriminator, num_layers=5, initial_channels=64, max_depth=512, out_channels=1))
 train = dict(print_freq=10, batch_size_per_worker=16, virtual_batch_size_multiplier=1, num_dataloader_workers=2,
@@ -25,6 +27,8 @@ train['loss'] = losses.CalculateLoss([{'loss_fn': losses.DenseBinaryCrossEntropy
                                        'weight': [0.5]}])
 train['min_lr'] = train['base_lr'] * 0.001
 train['optimizer'] = partial(torch.optim.SGD, lr=train['base_lr'], momentum=0.9, weight_decay=0.0005)
+train['adversarial_loss_weight'] = 0.01
+train['discriminator_optimizer'] = partial(torch.optim.SGD, lr=train['base_lr'], momentum=0.9)
 train['lr_scheduler'] = partial(torch.optim.lr_scheduler.CosineAnnealingWarmRestarts, T_0=300, T_mult=2,
                                 eta_min=train['base_lr'] * 0.01, last_epoch=-1)
 train['dataset'] = partial(SyntheticSegDataset, length=1280, size=512, seed=1)

@@ -194,12 +194,41 @@ __global__ void sgd_kernel(float* __restrict__ p, float* __restrict__ g, float* 
   }
 }
 
+__global__ void sigmoid_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = sigmoidf_ref(x[i]);
+}
+
+__global__ void sigmoid_bwd_kernel(const float* __restrict__ y, const float* __restrict__ gy, float* __restrict__ gx,
+                                   int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = y[i];
+    gx[i] = gy[i] * (v * (1.f - v));
+  }
+}
+
 __global__ void scale_kernel(float* __restrict__ x, int64_t n, float a) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     x[i] = __fmul_rn(x[i], a);
 }
 
 }  // namespace
+
+extern "C" int ssseg_sigmoid_fwd(const float* x, float* y, int64_t n, ssseg_stream_t stream) {
+  if (!x || !y || n < 0) return SSSEG_EINVAL;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(sigmoid_fwd_kernel, dim3(ssseg_grid(n, 256)), dim3(256), 0, (hipStream_t)stream, x, y, n);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_sigmoid_bwd(const float* y, const float* gy, float* gx, int64_t n, ssseg_stream_t stream) {
+  if (!y || !gy || !gx || n < 0) return SSSEG_EINVAL;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(sigmoid_bwd_kernel, dim3(ssseg_grid(n, 256)), dim3(256), 0, (hipStream_t)stream, y, gy, gx, n);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
 
 extern "C" int ssseg_scale_f32(float* x, int64_t n, float a, ssseg_stream_t stream) {
   if (!x || n < 0) return SSSEG_EINVAL;

@@ -38,13 +38,22 @@ def distributed_train(rank, cfg_path):
     dist.init_process_group(backend='nccl', rank=rank, world_size=world)
     device = torch.device('cuda', rank % cfg['common']['workers'])
     torch.cuda.set_device(device)
-    snn.set_compute_dtype(torch.float32 if cfg['common'].get('compute_dtype') == 'fp32' else torch.bfloat16)
+    snn.set_compute_dtype({'fp32': torch.float32, 'fp16': torch.float16}.get(cfg['common'].get('compute_dtype'),
+                                                                             torch.bfloat16))
 
     model = DistributedDataParallel(cfg['model']['model_fn']().to(device))
     ema_model = cfg['model']['model_fn']().to(device)
     mean_teacher.detach_model_parameters(ema_model)
     arena.attach(ema_model, with_grads=False)
     optimizer = soptim.from_config(cfg['train']['optimizer'], utils.get_trainable_params(model))
+    disc = None
+    if cfg['model'].get('discriminator') is not None and cfg['train'].get('adversarial_loss_weight'):
+        # config C5: the discriminator the reference config names (default_config.py:116-120) trained by the
+        # build-defined adversarial branch (train.adversarial_terms / discriminator_step), its own DDP + SGD
+        disc = DistributedDataParallel(cfg['model']['discriminator']().to(device))
+        disc_opt = soptim.from_config(cfg['train']['discriminator_optimizer'], disc.parameters())
+        cfg['train']['adversarial'] = dict(discriminator=disc, optimizer=disc_opt,
+                                           weight=float(cfg['train']['adversarial_loss_weight']))
 
     train_dir = cfg['common']['output_dir']
     pre = cfg['train'].get('pretrained_checkpoint_path') or ''
@@ -62,6 +71,10 @@ def distributed_train(rank, cfg_path):
         model.module.load_state_dict(ck['state_dict'], strict=False)
         ema_model.load_state_dict(ck['ema_state_dict'], strict=False)
         optimizer.load_state_dict(ck['optimizer'])
+        if disc is not None and 'discriminator_state_dict' in ck:
+            disc.module.load_state_dict(ck['discriminator_state_dict'])
+            cfg['train']['adversarial']['optimizer'].load_state_dict(ck['discriminator_optimizer'])
+            snn.invalidate_packed(disc.module)
         best_metric, last_epoch = ck['best_metric'], ck['epoch']
         snn.invalidate_packed(model.module)
         snn.invalidate_packed(ema_model)
@@ -96,8 +109,12 @@ def distributed_train(rank, cfg_path):
             lr_scheduler.step(val_loss)
         if rank == 0:
             os.makedirs(train_dir, exist_ok=True)
-            torch.save({'epoch': epoch + 1, 'best_metric': val_loss, 'state_dict': model.module.state_dict(),
-                        'ema_state_dict': ema_model.state_dict(), 'optimizer': optimizer.state_dict()}, latest)
+            ck = {'epoch': epoch + 1, 'best_metric': val_loss, 'state_dict': model.module.state_dict(),
+                  'ema_state_dict': ema_model.state_dict(), 'optimizer': optimizer.state_dict()}
+            if disc is not None:   # extra keys only; the reference's five keys are unchanged
+                ck['discriminator_state_dict'] = disc.module.state_dict()
+                ck['discriminator_optimizer'] = cfg['train']['adversarial']['optimizer'].state_dict()
+            torch.save(ck, latest)
             if best_metric is None or val_loss < best_metric:
                 best_metric = val_loss
                 shutil.copy2(latest, os.path.join(train_dir, 'best.pth'))

@@ -84,6 +84,29 @@ def interpolate_bilinear(x, size, align_corners=False):
     return _Bilinear.apply(x, tuple(size), align_corners)
 
 
+class _Sigmoid(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = _c(x.float())
+        y = torch.empty_like(x)
+        N.call('ssseg_sigmoid_fwd', N.dev_ptr(x, 'x'), N.dev_ptr(y), x.numel(), N.stream())
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (y,) = ctx.saved_tensors
+        gy = _c(gy.float())
+        gx = torch.empty_like(y)
+        N.call('ssseg_sigmoid_bwd', N.dev_ptr(y), N.dev_ptr(gy), N.dev_ptr(gx), y.numel(), N.stream())
+        return gx
+
+
+def sigmoid(x):
+    """torch.sigmoid (fp32, any layout -> contiguous): the probability map the discriminator sees."""
+    return _Sigmoid.apply(x)
+
+
 # ------------------------------------------------------------------------------------------------
 # Losses
 # ------------------------------------------------------------------------------------------------

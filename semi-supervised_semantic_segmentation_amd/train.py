@@ -32,18 +32,89 @@ def _world():
     return torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
 
 
+_TARGETS = {}
+
+
+def _target(ref, value):
+    """Constant real/fake label maps of the discriminator losses, allocated once per shape."""
+    key = (tuple(ref.shape), ref.device, value)
+    t = _TARGETS.get(key)
+    if t is None:
+        t = torch.full(tuple(ref.shape), float(value), device=ref.device, dtype=torch.float32)
+        _TARGETS[key] = t
+    return t
+
+
+def _set_requires_grad(module, flag):
+    for p in module.parameters():
+        p.requires_grad_(flag)
+
+
+def adversarial_terms(pred_maps, mask, adv):
+    """Adversarial semi-supervised branch of config C5 (build-defined: the reference constructs
+    models/discriminator.py's Discriminator from its config, default_config.py:116-120, but its trainer never
+    calls it; the formulation follows Hung et al. 2018, "Adversarial Learning for Semi-Supervised Semantic
+    Segmentation").  The discriminator sees the student's probability map p = sigmoid(up(logits)) at the mask
+    resolution (the reference's BCE treats each of the 2 channels as an independent sigmoid, losses.py:41-48).
+    Student term: weight * BCE(D(p), 1) with D frozen (its native layers skip their weight gradients).
+    Returns (student adversarial loss, detached p for the discriminator update)."""
+    D = adv['discriminator']
+    logits = pred_maps[-1]
+    if tuple(logits.shape[2:]) != tuple(mask.shape[2:]):
+        logits = ops.interpolate_bilinear(logits, mask.shape[2:4], align_corners=False)
+    prob = ops.sigmoid(logits)
+    _set_requires_grad(D, False)
+    d_fake = D(prob)
+    adv_loss = ops.bce_with_logits_mean(d_fake, _target(d_fake, 1.0)) * adv['weight']
+    _set_requires_grad(D, True)
+    return adv_loss, prob.detach()
+
+
+def discriminator_step(mask, prob, adv):
+    """Discriminator update of the adversarial branch: BCE(D(mask), 1) + BCE(D(p), 0) on the labelled
+    batch, backward into D's own gradient arena (all-reduced by its own DDP reducer at world > 1), SGD step
+    (every step: the student's step-0 skip, train.py:121, is a property of the student's accumulation).
+    Returns the device scalar discriminator loss."""
+    D, opt = adv['discriminator'], adv['optimizer']
+    ddp = D if isinstance(D, _DDP) else None
+    d_real = D(mask)
+    d_fake = D(prob)
+    loss_d = ops.bce_with_logits_mean(d_real, _target(d_real, 1.0)) + \
+        ops.bce_with_logits_mean(d_fake, _target(d_fake, 0.0))
+    if ddp is not None:
+        ddp.arm()
+    loss_d.backward()
+    if ddp is not None:
+        ddp.finish()
+    opt.step()
+    opt.zero_grad()
+    snn.invalidate_packed(_inner(D))
+    return loss_d.detach()
+
+
 def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch, step, config):
-    """One step of train.py:44-130.  Returns device scalars (classification loss, unsup loss, cm mean)."""
+    """One step of train.py:44-130.  Returns device scalars (classification loss, unsup loss, cm mean).
+    With config['train']['adversarial'] = dict(discriminator=D, optimizer=opt_D, weight=w) the student's
+    supervised loss gets the adversarial term and D is updated after the supervised backward (C5)."""
     tc = config['train']
     ddp = model if isinstance(model, _DDP) else None
     semi = tc['use_semi_supervised']
+    adv = tc.get('adversarial')
     features, pred_maps = model(image)
     classification_loss = tc['loss'](pred_maps, mask)
     sup_loss = classification_loss
+    prob = None
+    if adv is not None:
+        adv_loss, prob = adversarial_terms(pred_maps, mask, adv)
+        sup_loss = sup_loss + adv_loss
     if ddp is not None and not semi:
         ddp.arm()
     (sup_loss / tc['virtual_batch_size_multiplier']).backward()
     del pred_maps, features
+    if adv is not None:
+        adv['last_loss_d'] = discriminator_step(mask, prob, adv)
+        adv['last_loss_adv'] = adv_loss.detach()
+        del prob
     unsup_loss = cm_mean = None
     if semi:
         size = unsup_a.shape[2:4]

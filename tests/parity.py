@@ -28,3 +28,24 @@ def check_losses(hip, r32, r64, names=('sup', 'unsup')):
     print('\n'.join(lines))
     assert not bad, bad
     return lines
+
+
+def tensor_outliers(got, ref32, ref64, refp=None, rel=1e-3, floor=None):
+    """Per-tensor parity of parameters / gradients after a few optimizer steps: max |got - ref64| relative to
+    the tensor's scale must stay within max(rel, 2x the fp32 oracle's drift, 2x the drift of an fp64 run on
+    inputs perturbed by ~1e-6 (ReLU / max-pool switches of tiny-batch activations)).  Dicts of numpy
+    arrays; `floor` (a global scale) keeps mathematically-zero tensors (a bias feeding a BatchNorm) from
+    being judged on rounding noise.  Returns the violating (name, err, drift32, drift_pert) rows."""
+    import numpy as np
+    bad = []
+    for k, b in ref64.items():
+        b = np.asarray(b, np.float64)
+        if not np.issubdtype(b.dtype, np.floating):
+            continue
+        scale = max(float(np.abs(b).max()), floor or 0.0) + 1e-12
+        e = float(np.abs(np.asarray(got[k], np.float64) - b).max()) / scale
+        d32 = float(np.abs(np.asarray(ref32[k], np.float64) - b).max()) / scale
+        dp = float(np.abs(np.asarray(refp[k], np.float64) - b).max()) / scale if refp is not None else 0.0
+        if e > max(rel, 2 * d32, 2 * dp):
+            bad.append((k, e, d32, dp))
+    return bad
