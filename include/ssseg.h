@@ -13,7 +13,8 @@
  *     call is capturable into a hipGraph;
  *   - return value: 0 on success, a hipError_t (>0) on a launch failure, or SSSEG_E* (<0) on an
  *     argument error detected on the host;
- *   - dtype codes: SSSEG_F32 = fp32, SSSEG_BF16 = bfloat16 (raw 16-bit, round-to-nearest-even).
+ *   - dtype codes: SSSEG_F32 = fp32, SSSEG_BF16 = bfloat16 (raw 16-bit, round-to-nearest-even),
+ *     SSSEG_F16 = IEEE half (the fp16 compute mode of config C5; same storage and MFMA rate as bf16).
  *   - activations inside the networks are NHWC (PyTorch channels_last); loss/CowMix tensors
  *     are NCHW-contiguous like the reference.
  */
@@ -28,7 +29,7 @@ extern "C" {
 
 typedef struct ihipStream_t* ssseg_stream_t;   /* == hipStream_t */
 
-enum { SSSEG_F32 = 0, SSSEG_BF16 = 1 };
+enum { SSSEG_F32 = 0, SSSEG_BF16 = 1, SSSEG_F16 = 2 };
 enum { SSSEG_OK = 0, SSSEG_EINVAL = -1, SSSEG_EUNSUPPORTED = -2, SSSEG_EWORKSPACE = -3 };
 
 /* library identity: returns a static string "ssseg <version> gfx950" */
@@ -149,10 +150,20 @@ int ssseg_sqnorm_accum(const float* x, int64_t n, float* out, void* ws, size_t w
 /* torch.nn.utils.clip_grad_norm_ (train.py:122) + torch.optim.SGD(momentum, weight_decay) step
  * (default_config.py:151-154), fused:  coef = min(1, max_norm/(sqrt(sqnorm[0])+1e-6)) (skipped when
  * max_norm <= 0); g *= coef; d = g + wd*p; buf = first ? d : momentum*buf + d; p -= lr*buf.
- * bf16_shadow (nullable) receives bf16(p) for the compute path.  grad is left clipped. */
+ * bf16_shadow (nullable) receives bf16(p) for the compute path.  grad is left clipped.
+ * amp_state (nullable; the fp16 mode's dynamic loss scale [scale, tracker, found_inf, 1/scale]): the
+ * gradients are loss-scaled: they are unscaled by 1/scale first, and a non-finite sqnorm (which must then be
+ * given) skips the step entirely (GradScaler semantics, decided on the device: no host sync). */
 int ssseg_sgd_step(float* param, float* grad, float* momentum_buf, uint16_t* bf16_shadow, int64_t n,
                    float lr, float momentum, float weight_decay, float max_norm, const float* sqnorm,
-                   int first_step, ssseg_stream_t stream);
+                   int first_step, const float* amp_state, ssseg_stream_t stream);
+/* Dynamic loss-scale update after a step (torch.cuda.amp.GradScaler.update): non-finite sqnorm[0] ->
+ * scale *= backoff, tracker = 0, found_inf = 1; else tracker += 1 and scale *= growth every `interval`
+ * finite steps.  state = [scale, tracker, found_inf, 1/scale] on the device. */
+int ssseg_amp_update(float* state, const float* sqnorm, float growth, float backoff, int interval,
+                     ssseg_stream_t stream);
+/* y = x * s[0] (s a device scalar): the loss-scaled gradient entering the backward pass (fp16 mode). */
+int ssseg_scale_by(const float* x, const float* s, float* y, int64_t n, ssseg_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Convolution engine (implicit GEMM on MFMA).  Replaces the cuDNN/MIOpen convolutions behind

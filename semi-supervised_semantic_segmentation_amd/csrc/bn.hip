@@ -67,6 +67,15 @@ template <> struct Vec<bf16_t, 4> {
   }
 };
 
+template <> struct Vec<f16_t, 8> {
+  __device__ __forceinline__ static void ld(const f16_t* p, float (&v)[8]) { H16::ld8(p, v); }
+  __device__ __forceinline__ static void st(f16_t* p, const float (&v)[8]) { H16::st8(p, v); }
+};
+template <> struct Vec<f16_t, 4> {
+  __device__ __forceinline__ static void ld(const f16_t* p, float (&v)[4]) { H16::ld4(p, v); }
+  __device__ __forceinline__ static void st(f16_t* p, const float (&v)[4]) { H16::st4(p, v); }
+};
+
 struct Layout {
   int cpb;        // chunks per block row (<= 256)
   int ppb;        // pixel rows per block
@@ -598,6 +607,8 @@ extern "C" int ssseg_bn_stats(const void* x, int64_t P, int64_t C, int64_t ldx, 
   hipStream_t s = (hipStream_t)stream;
   if (dt == SSSEG_BF16)
     partials<bf16_t, 0>((const bf16_t*)x, nullptr, nullptr, P, C, ldx, 0, 0, ChanParams{}, 0, sums, ws, s);
+  else if (dt == SSSEG_F16)
+    partials<f16_t, 0>((const f16_t*)x, nullptr, nullptr, P, C, ldx, 0, 0, ChanParams{}, 0, sums, ws, s);
   else if (dt == SSSEG_F32)
     partials<float, 0>((const float*)x, nullptr, nullptr, P, C, ldx, 0, 0, ChanParams{}, 0, sums, ws, s);
   else
@@ -626,6 +637,8 @@ extern "C" int ssseg_bn_stats_finalize(const void* x, int64_t P, int64_t C, int6
   fe.nbt = num_batches_tracked;
   if (dt == SSSEG_BF16)
     partials<bf16_t, 0>((const bf16_t*)x, nullptr, nullptr, P, C, ldx, 0, 0, ChanParams{}, 0, sums, ws, s, fe);
+  else if (dt == SSSEG_F16)
+    partials<f16_t, 0>((const f16_t*)x, nullptr, nullptr, P, C, ldx, 0, 0, ChanParams{}, 0, sums, ws, s, fe);
   else if (dt == SSSEG_F32)
     partials<float, 0>((const float*)x, nullptr, nullptr, P, C, ldx, 0, 0, ChanParams{}, 0, sums, ws, s, fe);
   else
@@ -750,6 +763,9 @@ static int eval_bwd_entry(const void* dy, const void* y, const void* aux, void* 
   if (dt == SSSEG_BF16)
     eval_bwd<bf16_t>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)aux, (bf16_t*)dconv, (bf16_t*)dres, P, C, ld,
                      scale, mean_eff, invstd, relu, sums, ws, s, fe);
+  else if (dt == SSSEG_F16)
+    eval_bwd<f16_t>((const f16_t*)dy, (const f16_t*)y, (const f16_t*)aux, (f16_t*)dconv, (f16_t*)dres, P, C, ld,
+                     scale, mean_eff, invstd, relu, sums, ws, s, fe);
   else if (dt == SSSEG_F32)
     eval_bwd<float>((const float*)dy, (const float*)y, (const float*)aux, (float*)dconv, (float*)dres, P, C, ld, scale,
                     mean_eff, invstd, relu, sums, ws, s, fe);
@@ -779,6 +795,8 @@ extern "C" int ssseg_bn_apply(const void* x, const void* residual, void* y, int6
   const ChanParams prm{mean, invstd, gamma, beta};
   if (dt == SSSEG_BF16)
     apply<bf16_t>((const bf16_t*)x, (const bf16_t*)residual, (bf16_t*)y, P, C, ldx, ldr, ldy, prm, relu, s);
+  else if (dt == SSSEG_F16)
+    apply<f16_t>((const f16_t*)x, (const f16_t*)residual, (f16_t*)y, P, C, ldx, ldr, ldy, prm, relu, s);
   else if (dt == SSSEG_F32)
     apply<float>((const float*)x, (const float*)residual, (float*)y, P, C, ldx, ldr, ldy, prm, relu, s);
   else
@@ -798,6 +816,9 @@ extern "C" int ssseg_bn_bwd_reduce(const void* dy, const void* x, const void* re
   hipStream_t s = (hipStream_t)stream;
   if (dt == SSSEG_BF16)
     partials<bf16_t, 1>((const bf16_t*)x, (const bf16_t*)dy, (const bf16_t*)residual, P, C, ldx, lddy, ldr,
+                        ChanParams{mean, invstd, gamma, beta}, relu, sums, ws, s);
+  else if (dt == SSSEG_F16)
+    partials<f16_t, 1>((const f16_t*)x, (const f16_t*)dy, (const f16_t*)residual, P, C, ldx, lddy, ldr,
                         ChanParams{mean, invstd, gamma, beta}, relu, sums, ws, s);
   else if (dt == SSSEG_F32)
     partials<float, 1>((const float*)x, (const float*)dy, (const float*)residual, P, C, ldx, lddy, ldr,
@@ -824,6 +845,9 @@ extern "C" int ssseg_bn_bwd_reduce_grad(const void* dy, const void* x, const voi
   fe.dbeta = dbeta;
   if (dt == SSSEG_BF16)
     partials<bf16_t, 1>((const bf16_t*)x, (const bf16_t*)dy, (const bf16_t*)residual, P, C, ldx, lddy, ldr,
+                        ChanParams{mean, invstd, gamma, beta}, relu, sums, ws, s, fe);
+  else if (dt == SSSEG_F16)
+    partials<f16_t, 1>((const f16_t*)x, (const f16_t*)dy, (const f16_t*)residual, P, C, ldx, lddy, ldr,
                         ChanParams{mean, invstd, gamma, beta}, relu, sums, ws, s, fe);
   else if (dt == SSSEG_F32)
     partials<float, 1>((const float*)x, (const float*)dy, (const float*)residual, P, C, ldx, lddy, ldr,
@@ -854,6 +878,9 @@ extern "C" int ssseg_bn_bwd_apply(const void* dy, const void* x, const void* res
   const ChanParams prm{mean, invstd, gamma, beta};
   if (dt == SSSEG_BF16)
     bwd_apply<bf16_t>((const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)residual, (bf16_t*)dx, (bf16_t*)dres, P, C,
+                      ldx, ldr, lddy, lddx, prm, relu, train, sums, count, s);
+  else if (dt == SSSEG_F16)
+    bwd_apply<f16_t>((const f16_t*)dy, (const f16_t*)x, (const f16_t*)residual, (f16_t*)dx, (f16_t*)dres, P, C,
                       ldx, ldr, lddy, lddx, prm, relu, train, sums, count, s);
   else if (dt == SSSEG_F32)
     bwd_apply<float>((const float*)dy, (const float*)x, (const float*)residual, (float*)dx, (float*)dres, P, C, ldx,

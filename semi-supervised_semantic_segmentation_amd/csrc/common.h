@@ -34,6 +34,10 @@ __device__ __forceinline__ bf16_t f32_to_bf16(float f) {
   return (bf16_t)(u >> 16);
 }
 
+// IEEE half (the fp16 compute mode, config C5): hardware round-to-nearest-even conversions
+typedef _Float16 f16_t;
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+
 template <typename T> struct io;
 template <> struct io<float> {
   __device__ __forceinline__ static float ld(const float* p, int64_t i) { return p[i]; }
@@ -42,6 +46,43 @@ template <> struct io<float> {
 template <> struct io<bf16_t> {
   __device__ __forceinline__ static float ld(const bf16_t* p, int64_t i) { return bf16_to_f32(p[i]); }
   __device__ __forceinline__ static void st(bf16_t* p, int64_t i, float v) { p[i] = f32_to_bf16(v); }
+};
+template <> struct io<f16_t> {
+  __device__ __forceinline__ static float ld(const f16_t* p, int64_t i) { return (float)p[i]; }
+  __device__ __forceinline__ static void st(f16_t* p, int64_t i, float v) { p[i] = (f16_t)v; }
+};
+
+// 16-byte (8 x fp16) and 8-byte (4 x fp16) vector loads/stores with fp32 values: the fp16 member of the
+// per-file 16-byte chunk helpers (bf16 and fp32 have their own)
+struct H16 {
+  __device__ __forceinline__ static void ld8(const f16_t* p, float (&v)[8]) {
+    const uint4 q = *(const uint4*)p;
+    const unsigned w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f16x2_t h = __builtin_bit_cast(f16x2_t, w[i]);
+      v[2 * i] = (float)h[0];
+      v[2 * i + 1] = (float)h[1];
+    }
+  }
+  __device__ __forceinline__ static void st8(f16_t* p, const float (&v)[8]) {
+    unsigned w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f16x2_t h = {(f16_t)v[2 * i], (f16_t)v[2 * i + 1]};
+      w[i] = __builtin_bit_cast(unsigned, h);
+    }
+    *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  __device__ __forceinline__ static void ld4(const f16_t* p, float (&v)[4]) {
+    const uint2 q = *(const uint2*)p;
+    const f16x2_t a = __builtin_bit_cast(f16x2_t, q.x), b = __builtin_bit_cast(f16x2_t, q.y);
+    v[0] = (float)a[0]; v[1] = (float)a[1]; v[2] = (float)b[0]; v[3] = (float)b[1];
+  }
+  __device__ __forceinline__ static void st4(f16_t* p, const float (&v)[4]) {
+    const f16x2_t a = {(f16_t)v[0], (f16_t)v[1]}, b = {(f16_t)v[2], (f16_t)v[3]};
+    *(uint2*)p = make_uint2(__builtin_bit_cast(unsigned, a), __builtin_bit_cast(unsigned, b));
+  }
 };
 
 // wave64 reductions

@@ -193,7 +193,7 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
 }
 
 bool geom_ok(const ConvGeom& g, int dt) {
-  const int vec = dt == SSSEG_BF16 ? 8 : 4;
+  const int vec = (dt == SSSEG_F32 ? 4 : 8);
   if (g.C % vec || g.ldx % vec || g.ldw % vec) return false;
   if (g.N < 1 || g.OH < 1 || g.OW < 1 || g.K < 1 || g.C < 1) return false;
   if (g.M >= 0x7fffffffLL) return false;   // kernels decode output positions with 32-bit math
@@ -220,10 +220,10 @@ extern "C" size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* d, int
   int sp;
   const long long t128 = ((g.M + 127) / 128) * ((g.K + 127) / 128);
   const bool small = g_knobs[2] == 0 ? (t128 < 512) : (g_knobs[2] > 0);
-  if (g.K <= 16) sp = dt == SSSEG_BF16 ? plan_splits<bf16_t, 256, 16>(g) : plan_splits<float, 256, 16>(g);
-  else if (g.K <= 64 && !small) sp = dt == SSSEG_BF16 ? plan_splits<bf16_t, 256, 64>(g) : plan_splits<float, 256, 64>(g);
-  else if (small) sp = dt == SSSEG_BF16 ? plan_splits<bf16_t, 64, 64>(g) : plan_splits<float, 64, 64>(g);
-  else sp = dt == SSSEG_BF16 ? plan_splits<bf16_t, 128, 128>(g) : plan_splits<float, 128, 128>(g);
+  if (g.K <= 16) sp = dt != SSSEG_F32 ? plan_splits<bf16_t, 256, 16>(g) : plan_splits<float, 256, 16>(g);
+  else if (g.K <= 64 && !small) sp = dt != SSSEG_F32 ? plan_splits<bf16_t, 256, 64>(g) : plan_splits<float, 256, 64>(g);
+  else if (small) sp = dt != SSSEG_F32 ? plan_splits<bf16_t, 64, 64>(g) : plan_splits<float, 64, 64>(g);
+  else sp = dt != SSSEG_F32 ? plan_splits<bf16_t, 128, 128>(g) : plan_splits<float, 128, 128>(g);
   return sp > 1 ? (size_t)g.M * g.K * sizeof(float) : 0;
 }
 
@@ -246,10 +246,15 @@ extern "C" int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const
                       e.stats, (int)e.stats_ld};
   const Epi<bf16_t> eb{e.scale, e.shift, (const bf16_t*)e.residual, (int)e.ldr, e.relu, (bf16_t*)e.aux, e.slope,
                        e.stats, (int)e.stats_ld};
+  const Epi<f16_t> eh{e.scale, e.shift, (const f16_t*)e.residual, (int)e.ldr, e.relu, (f16_t*)e.aux, e.slope,
+                      e.stats, (int)e.stats_ld};
   if (g.KK == 0) {   // no taps reach this output phase: the contraction is zero
     if (e.stats) return SSSEG_EUNSUPPORTED;
     if (dt_out == SSSEG_F32)
       hipLaunchKernelGGL(phase_zero_kernel<float>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, (float*)y, g, ef);
+    else if (dt_out == SSSEG_F16)
+      hipLaunchKernelGGL(phase_zero_kernel<f16_t>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, (f16_t*)y, g,
+                         eh);
     else
       hipLaunchKernelGGL(phase_zero_kernel<bf16_t>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, (bf16_t*)y, g,
                          eb);
@@ -265,6 +270,10 @@ extern "C" int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const
     bm = dispatch_igemm<bf16_t, bf16_t>(x, w, y, g, eb, wsf, s);
   else if (dt == SSSEG_BF16 && dt_out == SSSEG_F32)
     bm = dispatch_igemm<bf16_t, float>(x, w, y, g, ef, wsf, s);
+  else if (dt == SSSEG_F16 && dt_out == SSSEG_F16)
+    bm = dispatch_igemm<f16_t, f16_t>(x, w, y, g, eh, wsf, s);
+  else if (dt == SSSEG_F16 && dt_out == SSSEG_F32)
+    bm = dispatch_igemm<f16_t, float>(x, w, y, g, ef, wsf, s);
   else if (dt == SSSEG_F32 && dt_out == SSSEG_F32)
     bm = dispatch_igemm<float, float>(x, w, y, g, ef, wsf, s);
   else
@@ -287,6 +296,8 @@ extern "C" int ssseg_weight_pack_batch(const ssseg_pack_desc* descs, int64_t n, 
   const dim3 grid(256, (unsigned)n);
   if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(weight_pack_batch_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, descs);
+  else if (dt == SSSEG_F16)
+    hipLaunchKernelGGL(weight_pack_batch_kernel<f16_t>, grid, dim3(256), 0, (hipStream_t)stream, descs);
   else if (dt == SSSEG_F32)
     hipLaunchKernelGGL(weight_pack_batch_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, descs);
   else
@@ -307,6 +318,10 @@ extern "C" int ssseg_weight_pack(const float* src, void* dst, int64_t Kd, int64_
   hipStream_t s = (hipStream_t)stream;
   if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(weight_pack_kernel<bf16_t>, dim3(ssseg_grid(total, 256)), dim3(256), 0, s, src, (bf16_t*)dst,
+                       (int)Kd, (int)Kr, (int)Cd, (int)Rs, (int)Ss, (int)Cp, layout, (int)r0, (int)rstep, (int)Rn,
+                       (int)s0, (int)sstep, (int)Sn);
+  else if (dt == SSSEG_F16)
+    hipLaunchKernelGGL(weight_pack_kernel<f16_t>, dim3(ssseg_grid(total, 256)), dim3(256), 0, s, src, (f16_t*)dst,
                        (int)Kd, (int)Kr, (int)Cd, (int)Rs, (int)Ss, (int)Cp, layout, (int)r0, (int)rstep, (int)Rn,
                        (int)s0, (int)sstep, (int)Sn);
   else if (dt == SSSEG_F32)

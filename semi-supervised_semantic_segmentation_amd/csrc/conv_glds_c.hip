@@ -16,3 +16,5 @@ int launch_glds_grp_c(int cfg, const void* x, const void* w, void* y, const Conv
 
 template int launch_glds_grp_c<bf16_t>(int, const void*, const void*, void*, const ConvGeom&, const Epi<bf16_t>&,
                                         unsigned, unsigned, hipStream_t);
+template int launch_glds_grp_c<f16_t>(int, const void*, const void*, void*, const ConvGeom&, const Epi<f16_t>&,
+                                       unsigned, unsigned, hipStream_t);

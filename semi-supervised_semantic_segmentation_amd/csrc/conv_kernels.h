@@ -23,8 +23,25 @@
 #include "common.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// 16x16x32 MFMA on 16-bit operands held as 8 x 16-bit lanes (the LDS fragments are read as raw bits):
+// bf16 (v_mfma_f32_16x16x32_bf16) or IEEE half (v_mfma_f32_16x16x32_f16, same rate: the fp16 mode)
+template <typename T16> struct M16;
+template <> struct M16<bf16_t> {
+  __device__ __forceinline__ static f32x4 mma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct M16<f16_t> {
+  __device__ __forceinline__ static f32x4 mma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                  0);
+  }
+};
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 struct ConvGeom {
@@ -62,6 +79,13 @@ template <> struct MF<bf16_t> {
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
   }
 };
+template <> struct MF<f16_t> {
+  static constexpr int VEC = 8;
+  typedef f16x8 frag;
+  __device__ __forceinline__ static void mma(const frag& a, const frag& b, f32x4& c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
 template <> struct MF<float> {
   static constexpr int VEC = 4;
   typedef f32x4 frag;
@@ -77,6 +101,9 @@ template <> struct MF<float> {
 template <typename TO> struct Store4;
 template <> struct Store4<float> {
   __device__ __forceinline__ static void st(float* p, const float (&v)[4]) { *(float4*)p = make_float4(v[0], v[1], v[2], v[3]); }
+};
+template <> struct Store4<f16_t> {
+  __device__ __forceinline__ static void st(f16_t* p, const float (&v)[4]) { H16::st4(p, v); }
 };
 template <> struct Store4<bf16_t> {
   __device__ __forceinline__ static void st(bf16_t* p, const float (&v)[4]) {
@@ -106,6 +133,7 @@ struct Epi {
 template <typename TO> __device__ __forceinline__ float stored(float v);
 template <> __device__ __forceinline__ float stored<float>(float v) { return v; }
 template <> __device__ __forceinline__ float stored<bf16_t>(float v) { return bf16_to_f32(f32_to_bf16(v)); }
+template <> __device__ __forceinline__ float stored<f16_t>(float v) { return (float)(f16_t)v; }
 
 // Per-tile BatchNorm statistics partials from the epilogue (fused training BN statistics, replaces a separate
 // read of the conv output).  Each thread holds fp64 (sum, sumsq) of V consecutive channels starting at
@@ -155,6 +183,9 @@ template <> struct Load4<float> {
     const float4 q = *(const float4*)p;
     v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
   }
+};
+template <> struct Load4<f16_t> {
+  __device__ __forceinline__ static void ld(const f16_t* p, float (&v)[4]) { H16::ld4(p, v); }
 };
 template <> struct Load4<bf16_t> {
   __device__ __forceinline__ static void ld(const bf16_t* p, float (&v)[4]) {
@@ -264,6 +295,10 @@ template <> struct Out8<bf16_t> {
     for (int i = 0; i < 4; ++i) w[i] = (unsigned)f32_to_bf16(v[2 * i]) | ((unsigned)f32_to_bf16(v[2 * i + 1]) << 16);
     *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
   }
+};
+template <> struct Out8<f16_t> {
+  __device__ __forceinline__ static void ld(const f16_t* p, float (&v)[8]) { H16::ld8(p, v); }
+  __device__ __forceinline__ static void st(f16_t* p, const float (&v)[8]) { H16::st8(p, v); }
 };
 template <> struct Out8<float> {
   __device__ __forceinline__ static void ld(const float* p, float (&v)[8]) {
@@ -643,8 +678,8 @@ __device__ __forceinline__ void vmcnt_wait() {
 constexpr unsigned OOB = 0x80000000u;   // > any num_records we build: the load returns zeros
 
 template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS, bool STATS>
-__global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const bf16_t* __restrict__ x,
-                                                                const bf16_t* __restrict__ w, TO* __restrict__ y,
+__global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __restrict__ x,
+                                                                const TO* __restrict__ w, TO* __restrict__ y,
                                                                 ConvGeom g, Epi<TO> ep, unsigned xbytes,
                                                                 unsigned wbytes, int g_epi_lds) {
   constexpr int ROW = 128;                       // bytes per LDS row = 64 bf16 of k
@@ -754,7 +789,7 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const bf16_t* __
 #pragma unroll
       for (int i = 0; i < FN; ++i)
 #pragma unroll
-        for (int j = 0; j < FM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FM; ++j) acc[i][j] = M16<TO>::mma(af[i], bfr[j], acc[i][j]);
     }
   };
 
@@ -844,14 +879,14 @@ __global__ void phase_zero_kernel(TO* y, ConvGeom g, Epi<TO> ep) {
 template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS>
 int launch_glds(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb, unsigned wb,
                 hipStream_t s) {
-  static_assert(sizeof(TO) == 2, "LDS-DMA configs write bf16 activations (fp32-output heads have K <= 16)");
+  static_assert(sizeof(TO) == 2, "LDS-DMA configs: 16-bit activations in and out (fp32-output heads have K <= 16)");
   const long long tiles = ((g.M + BM - 1) / BM) * ((g.K + BN - 1) / BN);
   if (ep.stats)
     hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, true>), dim3((unsigned)tiles), dim3(NW * 64), 0,
-                       s, (const bf16_t*)x, (const bf16_t*)w, (TO*)y, g, ep, xb, wb, (int)(g_knobs[7] == 0));
+                       s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, (int)(g_knobs[7] == 0));
   else
     hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, false>), dim3((unsigned)tiles), dim3(NW * 64), 0,
-                       s, (const bf16_t*)x, (const bf16_t*)w, (TO*)y, g, ep, xb, wb, (int)(g_knobs[7] == 0));
+                       s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, (int)(g_knobs[7] == 0));
   return BM;
 }
 

@@ -13,6 +13,7 @@ template <> struct WG<bf16_t> {
   static constexpr int BKP = 64;                   // pixels per k-tile (two 32-deep MFMA steps)
   static constexpr int PADB = 32;                  // row pad bytes (row stride == 8 dwords mod 64)
 };
+template <> struct WG<f16_t> : WG<bf16_t> {};
 template <> struct WG<float> {
   static constexpr int BKP = 16;
   static constexpr int PADB = 64;                  // row stride == 16 dwords mod 32
@@ -151,7 +152,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ x, con
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j) acc[i][j] = M16<T>::mma(af[i], bfr[j], acc[i][j]);
       }
     } else {
 #pragma unroll
@@ -282,8 +283,8 @@ __device__ __forceinline__ int wswz(int r) {
 }
 __device__ __forceinline__ int wkp(int g, int j) { return 16 * (g >> 1) + 8 * (g & 1) + 4 * (j >> 2) + (j & 3); }
 
-template <int BMW, int BNW, int NS>
-__global__ void __launch_bounds__(256) wgrad_glds_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+template <typename T16, int BMW, int BNW, int NS>
+__global__ void __launch_bounds__(256) wgrad_glds_kernel(const T16* __restrict__ x, const T16* __restrict__ dy,
                                                          float* __restrict__ slab, ConvGeom g, long long pix_per_split,
                                                          WDirect dd, unsigned xbytes, unsigned dbytes) {
   constexpr int BKP = 64;                                    // pixels per k-tile
@@ -401,7 +402,7 @@ __global__ void __launch_bounds__(256) wgrad_glds_kernel(const bf16_t* __restric
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j) acc[i][j] = M16<T16>::mma(af[i], bfr[j], acc[i][j]);
     }
   };
 
@@ -532,7 +533,7 @@ void launch_wgrad(const void* x, const void* dy, float* slab, const ConvGeom& g,
 
 // LDS-DMA weight gradient: bf16, C % 64 == 0 (a 64- or 128-channel kk-tile inside one tap), operands < 2 GB
 static bool wgrad_glds_ok(const ConvGeom& g, int dt) {
-  if (dt != SSSEG_BF16 || g_knobs[8] != 0) return false;
+  if ((dt != SSSEG_BF16 && dt != SSSEG_F16) || g_knobs[8] != 0) return false;
   if (g.C % 64 || g.ldx % 8 || g.ldy % 8 || g.K % 8) return false;
   const long long xb = (long long)g.N * g.H * g.W * g.ldx * 2, db = g.M * g.ldy * 2;
   return xb < 0x7fffffffLL && db < 0x7fffffffLL;
@@ -544,31 +545,32 @@ static WgradPlan choose_wgrad(const ConvGeom& g, int dt) {
     p = plan_wgrad<bf16_t>(g, (g.C % 128 == 0 && g.KK > 64) ? 128 : 64);
     p.glds = true;
   } else {
-    p = dt == SSSEG_BF16 ? plan_wgrad<bf16_t>(g) : plan_wgrad<float>(g);
+    p = dt != SSSEG_F32 ? plan_wgrad<bf16_t>(g) : plan_wgrad<float>(g);
   }
   return p;
 }
 
-template <int BMW, int BNW>
+template <typename T16, int BMW, int BNW>
 void launch_wgrad_glds_t(const void* x, const void* dy, float* slab, const ConvGeom& g, const WgradPlan& p, WDirect dd,
                          hipStream_t s) {
   constexpr int NS = 64 * (BMW + BNW) * 2 <= 24576 ? 3 : 2;   // 48 / 72 / 64 KB of LDS: 2-3 blocks per CU
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.ldx * 2), db = (unsigned)(g.M * g.ldy * 2);
-  hipLaunchKernelGGL((wgrad_glds_kernel<BMW, BNW, NS>), dim3(p.mt * p.nt * p.splits), dim3(256), 0, s, (const bf16_t*)x,
-                     (const bf16_t*)dy, slab, g, p.pps, dd, xb, db);
+  hipLaunchKernelGGL((wgrad_glds_kernel<T16, BMW, BNW, NS>), dim3(p.mt * p.nt * p.splits), dim3(256), 0, s,
+                     (const T16*)x, (const T16*)dy, slab, g, p.pps, dd, xb, db);
 }
 
+template <typename T16>
 void launch_wgrad_glds(const void* x, const void* dy, float* slab, const ConvGeom& g, const WgradPlan& p, WDirect dd,
                        hipStream_t s) {
-  if (p.bmw == 128 && p.bnw == 128) launch_wgrad_glds_t<128, 128>(x, dy, slab, g, p, dd, s);
-  else if (p.bmw == 128) launch_wgrad_glds_t<128, 64>(x, dy, slab, g, p, dd, s);
-  else if (p.bnw == 128) launch_wgrad_glds_t<64, 128>(x, dy, slab, g, p, dd, s);
-  else launch_wgrad_glds_t<64, 64>(x, dy, slab, g, p, dd, s);
+  if (p.bmw == 128 && p.bnw == 128) launch_wgrad_glds_t<T16, 128, 128>(x, dy, slab, g, p, dd, s);
+  else if (p.bmw == 128) launch_wgrad_glds_t<T16, 128, 64>(x, dy, slab, g, p, dd, s);
+  else if (p.bnw == 128) launch_wgrad_glds_t<T16, 64, 128>(x, dy, slab, g, p, dd, s);
+  else launch_wgrad_glds_t<T16, 64, 64>(x, dy, slab, g, p, dd, s);
 }
 
 
 bool wg_geom_ok(const ConvGeom& g, int dt) {
-  const int vec = dt == SSSEG_BF16 ? 8 : 4;
+  const int vec = dt == SSSEG_F32 ? 4 : 8;
   if (g.C % vec || g.ldx % vec || g.ldw % vec) return false;
   if (g.N < 1 || g.OH < 1 || g.OW < 1 || g.K < 1 || g.C < 1) return false;
   if (g.M >= 0x7fffffffLL) return false;
@@ -590,19 +592,24 @@ extern "C" int ssseg_conv_wgrad(const void* x, const void* dy, float* dw, const 
                                 ssseg_stream_t stream) {
   ConvGeom g;
   if (!make_geom(d, g) || !x || !dy || !dw) return SSSEG_EINVAL;
-  if (!wg_geom_ok(g, dt) || g.ldy % (dt == SSSEG_BF16 ? 8 : 4) || g.K % (dt == SSSEG_BF16 ? 8 : 4)) return SSSEG_EINVAL;
+  const int vec = dt == SSSEG_F32 ? 4 : 8;
+  if (!wg_geom_ok(g, dt) || g.ldy % vec || g.K % vec) return SSSEG_EINVAL;
   if (c_real < 1 || c_real > g.C || k_real < 1 || k_real > g.K || (layout != 0 && layout != 1)) return SSSEG_EINVAL;
   if (!ws || ws_bytes < ssseg_conv_wgrad_workspace_bytes(d, dt)) return SSSEG_EWORKSPACE;
   hipStream_t s = (hipStream_t)stream;
   float* slab = (float*)ws;
   WgradPlan p;
-  if (dt != SSSEG_BF16 && dt != SSSEG_F32) return SSSEG_EUNSUPPORTED;
+  if (dt != SSSEG_BF16 && dt != SSSEG_F16 && dt != SSSEG_F32) return SSSEG_EUNSUPPORTED;
   p = choose_wgrad(g, dt);
   const WDirect dd{p.splits == 1 ? dw : nullptr, (int)c_real, (int)k_real, layout, accumulate};
-  if (p.glds)
-    launch_wgrad_glds(x, dy, slab, g, p, dd, s);
+  if (p.glds && dt == SSSEG_F16)
+    launch_wgrad_glds<f16_t>(x, dy, slab, g, p, dd, s);
+  else if (p.glds)
+    launch_wgrad_glds<bf16_t>(x, dy, slab, g, p, dd, s);
   else if (dt == SSSEG_BF16)
     launch_wgrad<bf16_t>(x, dy, slab, g, p, dd, s);
+  else if (dt == SSSEG_F16)
+    launch_wgrad<f16_t>(x, dy, slab, g, p, dd, s);
   else
     launch_wgrad<float>(x, dy, slab, g, p, dd, s);
   if (p.splits == 1) {

@@ -329,6 +329,9 @@ extern "C" int ssseg_mix(const void* a, const void* b, const float* mask, void* 
   else if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(mix_kernel<bf16_t>, dim3(ssseg_grid(total, 256)), dim3(256), 0, s, (const bf16_t*)a,
                        (const bf16_t*)b, mask, (bf16_t*)out, C, HW, total);
+  else if (dt == SSSEG_F16)
+    hipLaunchKernelGGL(mix_kernel<f16_t>, dim3(ssseg_grid(total, 256)), dim3(256), 0, s, (const f16_t*)a,
+                       (const f16_t*)b, mask, (f16_t*)out, C, HW, total);
   else
     return SSSEG_EUNSUPPORTED;
   SSSEG_LAUNCH_CHECK();

@@ -32,6 +32,11 @@ template <> struct DV<bf16_t> {
     *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
   }
 };
+template <> struct DV<f16_t> {
+  static constexpr int V = 8;
+  __device__ __forceinline__ static void ld(const f16_t* p, float (&v)[8]) { H16::ld8(p, v); }
+  __device__ __forceinline__ static void st(f16_t* p, const float (&v)[8]) { H16::st8(p, v); }
+};
 template <> struct DV<float> {
   static constexpr int V = 4;
   __device__ __forceinline__ static void ld(const float* p, float (&v)[4]) {
@@ -203,7 +208,7 @@ bool make_dg(const ssseg_conv_desc* d, DG& g, int dt) {
     if (e < 0 || e > 0x7fffffff) return false;
   if (d->K != d->C || d->outH != d->OH || d->outW != d->OW || d->osy != 1 || d->osx != 1 || d->ooy || d->oox)
     return false;
-  const int vec = dt == SSSEG_BF16 ? 8 : 4;
+  const int vec = (dt == SSSEG_F32 ? 4 : 8);
   if (d->C % vec || d->ldx % vec || d->ldy % vec || d->ldw % vec || d->ldw < d->C) return false;
   if (d->R < 1 || d->S < 1 || d->R * d->S > MAXRS || d->sy < 1 || d->sx < 1) return false;
   if (d->N * d->H * d->W * d->ldx >= 0x7fffffffLL || d->N * d->OH * d->OW * d->ldy >= 0x7fffffffLL) return false;
@@ -227,7 +232,7 @@ extern "C" int ssseg_dwconv_fwd(const void* x, const void* w, void* y, const sss
   const ssseg_conv_epilogue none = {nullptr, nullptr, nullptr, 0, nullptr, 0, 0.f};
   const ssseg_conv_epilogue& e = epi ? *epi : none;
   if (e.relu < 0 || e.relu > SSSEG_ACT_LEAKY || (e.residual && (e.ldr < g.C || e.ldr % 8))) return SSSEG_EINVAL;
-  const int V = dt == SSSEG_BF16 ? 8 : 4;
+  const int V = (dt == SSSEG_F32 ? 4 : 8);
   const int64_t total = (int64_t)g.N * g.OH * g.OW * (g.C / V);
   if (total == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
@@ -235,6 +240,9 @@ extern "C" int ssseg_dwconv_fwd(const void* x, const void* w, void* y, const sss
   if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(dw_fwd_kernel<bf16_t>, grid, blk, 0, s, (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, g, e.scale,
                        e.shift, (const bf16_t*)e.residual, (int)e.ldr, (bf16_t*)e.aux, e.relu, e.slope);
+  else if (dt == SSSEG_F16)
+    hipLaunchKernelGGL(dw_fwd_kernel<f16_t>, grid, blk, 0, s, (const f16_t*)x, (const f16_t*)w, (f16_t*)y, g, e.scale,
+                       e.shift, (const f16_t*)e.residual, (int)e.ldr, (f16_t*)e.aux, e.relu, e.slope);
   else if (dt == SSSEG_F32)
     hipLaunchKernelGGL(dw_fwd_kernel<float>, grid, blk, 0, s, (const float*)x, (const float*)w, (float*)y, g, e.scale,
                        e.shift, (const float*)e.residual, (int)e.ldr, (float*)e.aux, e.relu, e.slope);
@@ -248,13 +256,15 @@ extern "C" int ssseg_dwconv_dgrad(const void* dy, const void* w, void* dx, const
                                   ssseg_stream_t stream) {
   DG g;
   if (!dy || !w || !dx || !make_dg(d, g, dt)) return SSSEG_EINVAL;
-  const int V = dt == SSSEG_BF16 ? 8 : 4;
+  const int V = (dt == SSSEG_F32 ? 4 : 8);
   const int64_t total = (int64_t)g.N * g.H * g.W * (g.C / V);
   if (total == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(ssseg_grid(total, 256, 1 << 20)), blk(256);
   if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(dw_dgrad_kernel<bf16_t>, grid, blk, 0, s, (const bf16_t*)dy, (const bf16_t*)w, (bf16_t*)dx, g);
+  else if (dt == SSSEG_F16)
+    hipLaunchKernelGGL(dw_dgrad_kernel<f16_t>, grid, blk, 0, s, (const f16_t*)dy, (const f16_t*)w, (f16_t*)dx, g);
   else if (dt == SSSEG_F32)
     hipLaunchKernelGGL(dw_dgrad_kernel<float>, grid, blk, 0, s, (const float*)dy, (const float*)w, (float*)dx, g);
   else
@@ -274,7 +284,7 @@ extern "C" int ssseg_dwconv_wgrad(const void* x, const void* dy, float* dw, cons
   DG g;
   if (!x || !dy || !dw || !make_dg(d, g, dt) || c_real < 1 || c_real > g.C) return SSSEG_EINVAL;
   if (!ws || ws_bytes < ssseg_dwconv_wgrad_workspace_bytes(d, dt)) return SSSEG_EWORKSPACE;
-  const int V = dt == SSSEG_BF16 ? 8 : 4;
+  const int V = (dt == SSSEG_F32 ? 4 : 8);
   const int CV = g.C / V;
   const int cpb = CV < 256 ? CV : 256;
   const int nblk = wgrad_blocks(g);
@@ -282,6 +292,9 @@ extern "C" int ssseg_dwconv_wgrad(const void* x, const void* dy, float* dw, cons
   const dim3 grid(nblk, (CV + cpb - 1) / cpb);
   if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(dw_wgrad_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)dy, g, cpb,
+                       (float*)ws);
+  else if (dt == SSSEG_F16)
+    hipLaunchKernelGGL(dw_wgrad_kernel<f16_t>, grid, dim3(256), 0, s, (const f16_t*)x, (const f16_t*)dy, g, cpb,
                        (float*)ws);
   else if (dt == SSSEG_F32)
     hipLaunchKernelGGL(dw_wgrad_kernel<float>, grid, dim3(256), 0, s, (const float*)x, (const float*)dy, g, cpb,

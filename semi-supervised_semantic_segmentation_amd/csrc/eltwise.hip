@@ -170,11 +170,16 @@ __global__ void __launch_bounds__(RED_THREADS) sq_final_kernel(const double* par
 
 // ---- clip + SGD ----
 __global__ void sgd_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ buf, bf16_t* shadow,
-                           int64_t n, float lr, float mom, float wd, float max_norm, const float* sqnorm, int first) {
+                           int64_t n, float lr, float mom, float wd, float max_norm, const float* sqnorm, int first,
+                           const float* amp) {
   float coef = 1.f;
+  if (amp) {   // loss-scaled gradients (fp16 mode): unscale; a non-finite norm skips the whole step
+    if (!isfinite(sqnorm[0])) return;
+    coef = amp[3];
+  }
   if (max_norm > 0.f) {
-    const float total = sqrtf(sqnorm[0]);
-    coef = fminf(max_norm / (total + 1e-6f), 1.f);
+    const float total = sqrtf(sqnorm[0]) * coef;
+    coef *= fminf(max_norm / (total + 1e-6f), 1.f);
   }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const float gi = __fmul_rn(g[i], coef);
@@ -207,6 +212,33 @@ __global__ void sigmoid_bwd_kernel(const float* __restrict__ y, const float* __r
   }
 }
 
+// dynamic loss scale (the fp16 compute mode): state = [scale, growth tracker, found_inf, 1/scale]
+__global__ void amp_update_kernel(float* state, const float* sqnorm, float growth, float backoff, int interval) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  float sc = state[0];
+  if (!isfinite(sqnorm[0])) {
+    sc *= backoff;
+    state[1] = 0.f;
+    state[2] = 1.f;
+  } else {
+    state[2] = 0.f;
+    state[1] += 1.f;
+    if (state[1] >= (float)interval) {
+      sc *= growth;
+      state[1] = 0.f;
+    }
+  }
+  state[0] = sc;
+  state[3] = 1.f / sc;
+}
+
+__global__ void scale_by_kernel(const float* __restrict__ x, const float* __restrict__ s, float* __restrict__ y,
+                                int64_t n) {
+  const float a = s[0];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = x[i] * a;
+}
+
 __global__ void scale_kernel(float* __restrict__ x, int64_t n, float a) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     x[i] = __fmul_rn(x[i], a);
@@ -226,6 +258,23 @@ extern "C" int ssseg_sigmoid_bwd(const float* y, const float* gy, float* gx, int
   if (!y || !gy || !gx || n < 0) return SSSEG_EINVAL;
   if (n == 0) return 0;
   hipLaunchKernelGGL(sigmoid_bwd_kernel, dim3(ssseg_grid(n, 256)), dim3(256), 0, (hipStream_t)stream, y, gy, gx, n);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_amp_update(float* state, const float* sqnorm, float growth, float backoff, int interval,
+                                ssseg_stream_t stream) {
+  if (!state || !sqnorm || interval < 1) return SSSEG_EINVAL;
+  hipLaunchKernelGGL(amp_update_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, state, sqnorm, growth, backoff,
+                     interval);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_scale_by(const float* x, const float* s, float* y, int64_t n, ssseg_stream_t stream) {
+  if (!x || !s || !y || n < 0) return SSSEG_EINVAL;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(scale_by_kernel, dim3(ssseg_grid(n, 256)), dim3(256), 0, (hipStream_t)stream, x, s, y, n);
   SSSEG_LAUNCH_CHECK();
   return 0;
 }
@@ -257,6 +306,12 @@ extern "C" int ssseg_nchw_to_nhwc(const void* x, void* y, int64_t N, int64_t C, 
     hipLaunchKernelGGL((nchw_to_nhwc_kernel<bf16_t, bf16_t>), g, b, 0, s, (const bf16_t*)x, (bf16_t*)y, C, H * W, Cp, total);
   else if (dt_in == SSSEG_BF16 && dt_out == SSSEG_F32)
     hipLaunchKernelGGL((nchw_to_nhwc_kernel<bf16_t, float>), g, b, 0, s, (const bf16_t*)x, (float*)y, C, H * W, Cp, total);
+  else if (dt_in == SSSEG_F32 && dt_out == SSSEG_F16)
+    hipLaunchKernelGGL((nchw_to_nhwc_kernel<float, f16_t>), g, b, 0, s, (const float*)x, (f16_t*)y, C, H * W, Cp, total);
+  else if (dt_in == SSSEG_F16 && dt_out == SSSEG_F16)
+    hipLaunchKernelGGL((nchw_to_nhwc_kernel<f16_t, f16_t>), g, b, 0, s, (const f16_t*)x, (f16_t*)y, C, H * W, Cp, total);
+  else if (dt_in == SSSEG_F16 && dt_out == SSSEG_F32)
+    hipLaunchKernelGGL((nchw_to_nhwc_kernel<f16_t, float>), g, b, 0, s, (const f16_t*)x, (float*)y, C, H * W, Cp, total);
   else
     return SSSEG_EUNSUPPORTED;
   SSSEG_LAUNCH_CHECK();
@@ -278,6 +333,12 @@ extern "C" int ssseg_nhwc_to_nchw(const void* x, void* y, int64_t N, int64_t C, 
     hipLaunchKernelGGL((nhwc_to_nchw_kernel<float, bf16_t>), g, b, 0, s, (const float*)x, (bf16_t*)y, C, H * W, ldc, total);
   else if (dt_in == SSSEG_BF16 && dt_out == SSSEG_BF16)
     hipLaunchKernelGGL((nhwc_to_nchw_kernel<bf16_t, bf16_t>), g, b, 0, s, (const bf16_t*)x, (bf16_t*)y, C, H * W, ldc, total);
+  else if (dt_in == SSSEG_F16 && dt_out == SSSEG_F32)
+    hipLaunchKernelGGL((nhwc_to_nchw_kernel<f16_t, float>), g, b, 0, s, (const f16_t*)x, (float*)y, C, H * W, ldc, total);
+  else if (dt_in == SSSEG_F32 && dt_out == SSSEG_F16)
+    hipLaunchKernelGGL((nhwc_to_nchw_kernel<float, f16_t>), g, b, 0, s, (const float*)x, (f16_t*)y, C, H * W, ldc, total);
+  else if (dt_in == SSSEG_F16 && dt_out == SSSEG_F16)
+    hipLaunchKernelGGL((nhwc_to_nchw_kernel<f16_t, f16_t>), g, b, 0, s, (const f16_t*)x, (f16_t*)y, C, H * W, ldc, total);
   else
     return SSSEG_EUNSUPPORTED;
   SSSEG_LAUNCH_CHECK();
@@ -297,6 +358,10 @@ extern "C" int ssseg_cast(const void* x, void* y, int64_t n, int dt_in, int dt_o
     hipLaunchKernelGGL((cast_kernel<float, float>), g, b, 0, s, (const float*)x, (float*)y, n);
   else if (dt_in == SSSEG_BF16 && dt_out == SSSEG_BF16)
     hipLaunchKernelGGL((cast_kernel<bf16_t, bf16_t>), g, b, 0, s, (const bf16_t*)x, (bf16_t*)y, n);
+  else if (dt_in == SSSEG_F32 && dt_out == SSSEG_F16)
+    hipLaunchKernelGGL((cast_kernel<float, f16_t>), g, b, 0, s, (const float*)x, (f16_t*)y, n);
+  else if (dt_in == SSSEG_F16 && dt_out == SSSEG_F32)
+    hipLaunchKernelGGL((cast_kernel<f16_t, float>), g, b, 0, s, (const f16_t*)x, (float*)y, n);
   else
     return SSSEG_EUNSUPPORTED;
   SSSEG_LAUNCH_CHECK();
@@ -372,13 +437,13 @@ extern "C" int ssseg_sqnorm_accum(const float* x, int64_t n, float* out, void* w
 
 extern "C" int ssseg_sgd_step(float* param, float* grad, float* momentum_buf, uint16_t* bf16_shadow, int64_t n,
                               float lr, float momentum, float weight_decay, float max_norm, const float* sqnorm,
-                              int first_step, ssseg_stream_t stream) {
-  if (!param || !grad || n < 0 || (momentum != 0.f && !momentum_buf) || (max_norm > 0.f && !sqnorm))
+                              int first_step, const float* amp_state, ssseg_stream_t stream) {
+  if (!param || !grad || n < 0 || (momentum != 0.f && !momentum_buf) || ((max_norm > 0.f || amp_state) && !sqnorm))
     return SSSEG_EINVAL;
   if (n == 0) return 0;
   hipLaunchKernelGGL(sgd_kernel, dim3(ssseg_grid(n, 256, 256 * 8)), dim3(256), 0, (hipStream_t)stream, param, grad,
                      momentum_buf, (bf16_t*)bf16_shadow, n, lr, momentum, weight_decay, max_norm, sqnorm,
-                     first_step);
+                     first_step, amp_state);
   SSSEG_LAUNCH_CHECK();
   return 0;
 }

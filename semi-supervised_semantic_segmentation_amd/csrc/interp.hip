@@ -144,6 +144,8 @@ extern "C" int ssseg_bilinear_fwd(const void* x, void* y, int64_t N, int64_t C, 
     hipLaunchKernelGGL(bilinear_fwd_kernel<float>, g, b, 0, s, (const float*)x, (float*)y, N, C, ah, aw, xs, ys, cf);
   else if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(bilinear_fwd_kernel<bf16_t>, g, b, 0, s, (const bf16_t*)x, (bf16_t*)y, N, C, ah, aw, xs, ys, cf);
+  else if (dt == SSSEG_F16)
+    hipLaunchKernelGGL(bilinear_fwd_kernel<f16_t>, g, b, 0, s, (const f16_t*)x, (f16_t*)y, N, C, ah, aw, xs, ys, cf);
   else
     return SSSEG_EUNSUPPORTED;
   SSSEG_LAUNCH_CHECK();
@@ -165,6 +167,9 @@ extern "C" int ssseg_bilinear_bwd(const void* gy, void* gx, int64_t N, int64_t C
     hipLaunchKernelGGL(bilinear_bwd_kernel<float>, g, b, 0, s, (const float*)gy, (float*)gx, N, C, ah, aw, gys, gxs, cf);
   else if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(bilinear_bwd_kernel<bf16_t>, g, b, 0, s, (const bf16_t*)gy, (bf16_t*)gx, N, C, ah, aw, gys, gxs,
+                       cf);
+  else if (dt == SSSEG_F16)
+    hipLaunchKernelGGL(bilinear_bwd_kernel<f16_t>, g, b, 0, s, (const f16_t*)gy, (f16_t*)gx, N, C, ah, aw, gys, gxs,
                        cf);
   else
     return SSSEG_EUNSUPPORTED;

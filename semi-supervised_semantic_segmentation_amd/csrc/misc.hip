@@ -86,6 +86,11 @@ template <> struct VC<bf16_t> {
     *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
   }
 };
+template <> struct VC<f16_t> {
+  static constexpr int V = 8;
+  __device__ __forceinline__ static void ld(const f16_t* p, float (&v)[8]) { H16::ld8(p, v); }
+  __device__ __forceinline__ static void st(f16_t* p, const float (&v)[8]) { H16::st8(p, v); }
+};
 template <> struct VC<float> {
   static constexpr int V = 4;
   __device__ __forceinline__ static void ld(const float* p, float (&v)[4]) {
@@ -250,11 +255,14 @@ extern "C" int ssseg_maxpool_fwd(const void* x, void* y, uint8_t* idx, int64_t N
   const int64_t total = N * OH * OW * C;
   if (total == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  const int V = dt == SSSEG_BF16 ? 8 : 4;
+  const int V = (dt == SSSEG_F32 ? 4 : 8);
   if (C % V == 0 && total / V < 0x7fffffffLL && N * H * W * C < (1LL << 40)) {
     const dim3 gv(ssseg_grid(total / V, 256, 1 << 20)), bv(256);
     if (dt == SSSEG_BF16)
       hipLaunchKernelGGL(maxpool_fwd_vec_kernel<bf16_t>, gv, bv, 0, st, (const bf16_t*)x, (bf16_t*)y, idx, (int)N,
+                         (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
+    else if (dt == SSSEG_F16)
+      hipLaunchKernelGGL(maxpool_fwd_vec_kernel<f16_t>, gv, bv, 0, st, (const f16_t*)x, (f16_t*)y, idx, (int)N,
                          (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
     else if (dt == SSSEG_F32)
       hipLaunchKernelGGL(maxpool_fwd_vec_kernel<float>, gv, bv, 0, st, (const float*)x, (float*)y, idx, (int)N, (int)H,
@@ -267,6 +275,9 @@ extern "C" int ssseg_maxpool_fwd(const void* x, void* y, uint8_t* idx, int64_t N
   const dim3 g(ssseg_grid(total, 256, 256 * 16)), b(256);
   if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(maxpool_fwd_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)x, (bf16_t*)y, idx, (int)N, (int)H,
+                       (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
+  else if (dt == SSSEG_F16)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<f16_t>, g, b, 0, st, (const f16_t*)x, (f16_t*)y, idx, (int)N, (int)H,
                        (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
   else if (dt == SSSEG_F32)
     hipLaunchKernelGGL(maxpool_fwd_kernel<float>, g, b, 0, st, (const float*)x, (float*)y, idx, (int)N, (int)H, (int)W,
@@ -284,11 +295,14 @@ extern "C" int ssseg_maxpool_bwd(const void* gy, const uint8_t* idx, void* gx, i
   const int64_t total = N * H * W * C;
   if (total == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  const int V = dt == SSSEG_BF16 ? 8 : 4;
+  const int V = (dt == SSSEG_F32 ? 4 : 8);
   if (C % V == 0 && total / V < 0x7fffffffLL && N * OH * OW * C < 0x7fffffffLL * V) {
     const dim3 gv(ssseg_grid(total / V, 256, 1 << 20)), bv(256);
     if (dt == SSSEG_BF16)
       hipLaunchKernelGGL(maxpool_bwd_vec_kernel<bf16_t>, gv, bv, 0, st, (const bf16_t*)gy, idx, (bf16_t*)gx, (int)N,
+                         (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
+    else if (dt == SSSEG_F16)
+      hipLaunchKernelGGL(maxpool_bwd_vec_kernel<f16_t>, gv, bv, 0, st, (const f16_t*)gy, idx, (f16_t*)gx, (int)N,
                          (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
     else if (dt == SSSEG_F32)
       hipLaunchKernelGGL(maxpool_bwd_vec_kernel<float>, gv, bv, 0, st, (const float*)gy, idx, (float*)gx, (int)N,
@@ -301,6 +315,9 @@ extern "C" int ssseg_maxpool_bwd(const void* gy, const uint8_t* idx, void* gx, i
   const dim3 g(ssseg_grid(total, 256, 256 * 16)), b(256);
   if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(maxpool_bwd_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)gy, idx, (bf16_t*)gx, (int)N, (int)H,
+                       (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
+  else if (dt == SSSEG_F16)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<f16_t>, g, b, 0, st, (const f16_t*)gy, idx, (f16_t*)gx, (int)N, (int)H,
                        (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
   else if (dt == SSSEG_F32)
     hipLaunchKernelGGL(maxpool_bwd_kernel<float>, g, b, 0, st, (const float*)gy, idx, (float*)gx, (int)N, (int)H,
@@ -320,7 +337,7 @@ extern "C" int ssseg_nhwc_copy(const void* src, void* dst, int64_t N, int64_t H,
   const int64_t total = N * H * W * C;
   if (total == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  const int esz = dt == SSSEG_BF16 ? 2 : 4;
+  const int esz = (dt == SSSEG_F32 ? 4 : 2);
   const int v = 16 / esz;
   if (C % v == 0 && sld % v == 0 && dld % v == 0 && (((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
     const int64_t t4 = total / v;
@@ -330,6 +347,10 @@ extern "C" int ssseg_nhwc_copy(const void* src, void* dst, int64_t N, int64_t H,
   } else if (dt == SSSEG_BF16) {
     hipLaunchKernelGGL(nhwc_copy_kernel<bf16_t>, dim3(ssseg_grid(total, 256, 256 * 16)), dim3(256), 0, st,
                        (const bf16_t*)src, (bf16_t*)dst, (int)N, (int)H, (int)W, (int)C, (int)sH, (int)sW, sld, (int)soy,
+                       (int)sox, (int)dH, (int)dW, dld, (int)doy, (int)dox);
+  } else if (dt == SSSEG_F16) {
+    hipLaunchKernelGGL(nhwc_copy_kernel<f16_t>, dim3(ssseg_grid(total, 256, 256 * 16)), dim3(256), 0, st,
+                       (const f16_t*)src, (f16_t*)dst, (int)N, (int)H, (int)W, (int)C, (int)sH, (int)sW, sld, (int)soy,
                        (int)sox, (int)dH, (int)dW, dld, (int)doy, (int)dox);
   } else if (dt == SSSEG_F32) {
     hipLaunchKernelGGL(nhwc_copy_kernel<float>, dim3(ssseg_grid(total, 256, 256 * 16)), dim3(256), 0, st,
@@ -366,6 +387,9 @@ extern "C" int ssseg_act_bwd(const void* gy, const void* y, void* gx, int64_t n,
   const dim3 g(ssseg_grid(n, 256, 256 * 16)), b(256);
   if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(act_bwd_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)gy, (const bf16_t*)y, (bf16_t*)gx, n, act,
+                       slope);
+  else if (dt == SSSEG_F16)
+    hipLaunchKernelGGL(act_bwd_kernel<f16_t>, g, b, 0, st, (const f16_t*)gy, (const f16_t*)y, (f16_t*)gx, n, act,
                        slope);
   else if (dt == SSSEG_F32)
     hipLaunchKernelGGL(act_bwd_kernel<float>, g, b, 0, st, (const float*)gy, (const float*)y, (float*)gx, n, act, slope);

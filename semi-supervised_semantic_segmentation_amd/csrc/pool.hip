@@ -30,6 +30,11 @@ template <> struct CV16<bf16_t> {
     *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
   }
 };
+template <> struct CV16<f16_t> {
+  static constexpr int V = 8;
+  __device__ __forceinline__ static void ld(const f16_t* p, float (&v)[8]) { H16::ld8(p, v); }
+  __device__ __forceinline__ static void st(f16_t* p, const float (&v)[8]) { H16::st8(p, v); }
+};
 template <> struct CV16<float> {
   static constexpr int V = 4;
   __device__ __forceinline__ static void ld(const float* p, float (&v)[4]) {
@@ -298,7 +303,7 @@ S4 s4(const int64_t* v) { return S4{v[0], v[1], v[2], v[3]}; }
 
 extern "C" int ssseg_avgpool_fwd(const void* x, void* y, int64_t N, int64_t H, int64_t W, int64_t C, int64_t OH,
                                  int64_t OW, int64_t k, int64_t s, int64_t p, int dt, ssseg_stream_t stream) {
-  const int V = dt == SSSEG_BF16 ? 8 : 4;
+  const int V = (dt == SSSEG_F32 ? 4 : 8);
   if (!x || !y || k < 1 || s < 1 || p < 0 || 2 * p > k || C % V || N < 0 || OH < 1 || OW < 1) return SSSEG_EINVAL;
   const int64_t total = N * OH * OW * (C / V);
   if (total == 0) return 0;
@@ -307,6 +312,9 @@ extern "C" int ssseg_avgpool_fwd(const void* x, void* y, int64_t N, int64_t H, i
   const dim3 g(ssseg_grid(total, 256, 1 << 20)), b(256);
   if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(avgpool_fwd_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)x, (bf16_t*)y, (int)N, (int)H, (int)W,
+                       (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
+  else if (dt == SSSEG_F16)
+    hipLaunchKernelGGL(avgpool_fwd_kernel<f16_t>, g, b, 0, st, (const f16_t*)x, (f16_t*)y, (int)N, (int)H, (int)W,
                        (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
   else if (dt == SSSEG_F32)
     hipLaunchKernelGGL(avgpool_fwd_kernel<float>, g, b, 0, st, (const float*)x, (float*)y, (int)N, (int)H, (int)W,
@@ -319,7 +327,7 @@ extern "C" int ssseg_avgpool_fwd(const void* x, void* y, int64_t N, int64_t H, i
 
 extern "C" int ssseg_avgpool_bwd(const void* gy, void* gx, int64_t N, int64_t H, int64_t W, int64_t C, int64_t OH,
                                  int64_t OW, int64_t k, int64_t s, int64_t p, int dt, ssseg_stream_t stream) {
-  const int V = dt == SSSEG_BF16 ? 8 : 4;
+  const int V = (dt == SSSEG_F32 ? 4 : 8);
   if (!gy || !gx || k < 1 || s < 1 || p < 0 || 2 * p > k || C % V || N < 0 || H < 1 || W < 1) return SSSEG_EINVAL;
   const int64_t total = N * H * W * (C / V);
   if (total == 0) return 0;
@@ -328,6 +336,9 @@ extern "C" int ssseg_avgpool_bwd(const void* gy, void* gx, int64_t N, int64_t H,
   const dim3 g(ssseg_grid(total, 256, 1 << 20)), b(256);
   if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(avgpool_bwd_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)gy, (bf16_t*)gx, (int)N, (int)H,
+                       (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
+  else if (dt == SSSEG_F16)
+    hipLaunchKernelGGL(avgpool_bwd_kernel<f16_t>, g, b, 0, st, (const f16_t*)gy, (f16_t*)gx, (int)N, (int)H,
                        (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
   else if (dt == SSSEG_F32)
     hipLaunchKernelGGL(avgpool_bwd_kernel<float>, g, b, 0, st, (const float*)gy, (float*)gx, (int)N, (int)H, (int)W,
@@ -349,7 +360,7 @@ extern "C" size_t ssseg_global_avgpool_workspace_bytes(int64_t N, int64_t HW, in
 
 extern "C" int ssseg_global_avgpool_fwd(const void* x, void* y, int64_t N, int64_t HW, int64_t C, int64_t ldy, int dt,
                                         void* ws, size_t ws_bytes, ssseg_stream_t stream) {
-  const int V = dt == SSSEG_BF16 ? 8 : 4;
+  const int V = (dt == SSSEG_F32 ? 4 : 8);
   if (!x || !y || N < 1 || HW < 1 || C < 1 || C % V || ldy < C) return SSSEG_EINVAL;
   if (N > 65535 || N * HW * C >= (1LL << 40)) return SSSEG_EUNSUPPORTED;
   if (!ws || ws_bytes < ssseg_global_avgpool_workspace_bytes(N, HW, C)) return SSSEG_EWORKSPACE;
@@ -362,6 +373,11 @@ extern "C" int ssseg_global_avgpool_fwd(const void* x, void* y, int64_t N, int64
                        splits);
     hipLaunchKernelGGL(gap_final_kernel<bf16_t>, dim3((unsigned)((N * C + 255) / 256)), dim3(256), 0, st,
                        (const float*)ws, (bf16_t*)y, (int)N, (int)C, splits, inv, ldy);
+  } else if (dt == SSSEG_F16) {
+    hipLaunchKernelGGL(gap_partial_kernel<f16_t>, g, dim3(256), 0, st, (const f16_t*)x, (float*)ws, (int)HW, (int)C,
+                       splits);
+    hipLaunchKernelGGL(gap_final_kernel<f16_t>, dim3((unsigned)((N * C + 255) / 256)), dim3(256), 0, st,
+                       (const float*)ws, (f16_t*)y, (int)N, (int)C, splits, inv, ldy);
   } else if (dt == SSSEG_F32) {
     hipLaunchKernelGGL(gap_partial_kernel<float>, g, dim3(256), 0, st, (const float*)x, (float*)ws, (int)HW, (int)C,
                        splits);
@@ -376,7 +392,7 @@ extern "C" int ssseg_global_avgpool_fwd(const void* x, void* y, int64_t N, int64
 
 extern "C" int ssseg_global_avgpool_bwd(const void* gy, void* gx, int64_t N, int64_t HW, int64_t C, int64_t ldgy,
                                         int dt, ssseg_stream_t stream) {
-  const int V = dt == SSSEG_BF16 ? 8 : 4;
+  const int V = (dt == SSSEG_F32 ? 4 : 8);
   if (!gy || !gx || N < 1 || HW < 1 || C < 1 || C % V || ldgy < C || ldgy % V) return SSSEG_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   const int64_t total = N * HW * (C / V);
@@ -384,6 +400,9 @@ extern "C" int ssseg_global_avgpool_bwd(const void* gy, void* gx, int64_t N, int
   const dim3 g(ssseg_grid(total, 256, 1 << 20)), b(256);
   if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(gap_bwd_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)gy, (bf16_t*)gx, (int)N, (int)HW, (int)C,
+                       ldgy, inv);
+  else if (dt == SSSEG_F16)
+    hipLaunchKernelGGL(gap_bwd_kernel<f16_t>, g, b, 0, st, (const f16_t*)gy, (f16_t*)gx, (int)N, (int)HW, (int)C,
                        ldgy, inv);
   else if (dt == SSSEG_F32)
     hipLaunchKernelGGL(gap_bwd_kernel<float>, g, b, 0, st, (const float*)gy, (float*)gx, (int)N, (int)HW, (int)C, ldgy,
@@ -396,7 +415,7 @@ extern "C" int ssseg_global_avgpool_bwd(const void* gy, void* gx, int64_t N, int
 
 extern "C" int ssseg_add_n(const void* const* xs_host, int n, void* y, int64_t numel, int act, float slope, int dt,
                            ssseg_stream_t stream) {
-  const int V = dt == SSSEG_BF16 ? 8 : 4;
+  const int V = (dt == SSSEG_F32 ? 4 : 8);
   if (!xs_host || !y || n < 1 || n > 8 || numel < 0 || numel % V || act < 0 || act > SSSEG_ACT_LEAKY)
     return SSSEG_EINVAL;
   Ptr8 p{};
@@ -411,6 +430,8 @@ extern "C" int ssseg_add_n(const void* const* xs_host, int n, void* y, int64_t n
   const dim3 g(ssseg_grid(nch, 256, 1 << 20)), b(256);
   if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(add_n_kernel<bf16_t>, g, b, 0, st, p, n, (bf16_t*)y, nch, act, slope);
+  else if (dt == SSSEG_F16)
+    hipLaunchKernelGGL(add_n_kernel<f16_t>, g, b, 0, st, p, n, (f16_t*)y, nch, act, slope);
   else if (dt == SSSEG_F32)
     hipLaunchKernelGGL(add_n_kernel<float>, g, b, 0, st, p, n, (float*)y, nch, act, slope);
   else
@@ -428,6 +449,8 @@ extern "C" int ssseg_dropout(const void* x, void* y, int64_t n, float p, uint64_
   const dim3 g(ssseg_grid(n / 4, 256, 1 << 20)), b(256);
   if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(dropout_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)x, (bf16_t*)y, n / 4, p, scale, seed, offset);
+  else if (dt == SSSEG_F16)
+    hipLaunchKernelGGL(dropout_kernel<f16_t>, g, b, 0, st, (const f16_t*)x, (f16_t*)y, n / 4, p, scale, seed, offset);
   else if (dt == SSSEG_F32)
     hipLaunchKernelGGL(dropout_kernel<float>, g, b, 0, st, (const float*)x, (float*)y, n / 4, p, scale, seed, offset);
   else

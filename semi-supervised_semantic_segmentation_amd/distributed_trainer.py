@@ -15,7 +15,7 @@ import config
 import mean_teacher
 import train
 import utils.utils as utils
-from ssseg import arena
+from ssseg import amp, arena
 from ssseg import nn as snn
 from ssseg import optim as soptim
 from ssseg.ddp import DistributedDataParallel
@@ -46,12 +46,17 @@ def distributed_train(rank, cfg_path):
     mean_teacher.detach_model_parameters(ema_model)
     arena.attach(ema_model, with_grads=False)
     optimizer = soptim.from_config(cfg['train']['optimizer'], utils.get_trainable_params(model))
+    fp16 = snn.compute_dtype() == torch.float16
+    if fp16:   # dynamic loss scaling on the device (ssseg.amp): fp16's exponent range flushes small gradients
+        optimizer.grad_scaler = amp.GradScaler(device)
     disc = None
     if cfg['model'].get('discriminator') is not None and cfg['train'].get('adversarial_loss_weight'):
         # config C5: the discriminator the reference config names (default_config.py:116-120) trained by the
         # build-defined adversarial branch (train.adversarial_terms / discriminator_step), its own DDP + SGD
         disc = DistributedDataParallel(cfg['model']['discriminator']().to(device))
         disc_opt = soptim.from_config(cfg['train']['discriminator_optimizer'], disc.parameters())
+        if fp16:
+            disc_opt.grad_scaler = amp.GradScaler(device)
         cfg['train']['adversarial'] = dict(discriminator=disc, optimizer=disc_opt,
                                            weight=float(cfg['train']['adversarial_loss_weight']))
 

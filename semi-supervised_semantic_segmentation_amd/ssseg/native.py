@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libssseg.so')
 HEADER = os.path.join(_HERE, '..', '..', 'include', 'ssseg.h')
 
-F32, BF16 = 0, 1
+F32, BF16, F16 = 0, 1, 2
 _ERRS = {-1: 'SSSEG_EINVAL', -2: 'SSSEG_EUNSUPPORTED', -3: 'SSSEG_EWORKSPACE'}
 
 vp, i64, i32, f32, f64, sz, u64 = (ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_double,
@@ -49,7 +49,9 @@ SIGS = {
     'ssseg_sigmoid_fwd': (i32, [vp, vp, i64, vp]),
     'ssseg_sigmoid_bwd': (i32, [vp, vp, vp, i64, vp]),
     'ssseg_sqnorm_accum': (i32, [vp, i64, vp, vp, sz, vp]),
-    'ssseg_sgd_step': (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp]),
+    'ssseg_sgd_step': (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, i32, vp, vp]),
+    'ssseg_amp_update': (i32, [vp, vp, f32, f32, i32, vp]),
+    'ssseg_scale_by': (i32, [vp, vp, vp, i64, vp]),
     # convolution engine
     'ssseg_conv_igemm': (i32, [vp, vp, vp, vp, i32, i32, vp, i32, vp, sz, vp]),
     'ssseg_conv_igemm_epi': (i32, [vp, vp, vp, vp, i32, i32, vp, vp, sz, vp]),
@@ -166,6 +168,8 @@ def dt_code(t):
         return F32
     if t.dtype == torch.bfloat16:
         return BF16
+    if t.dtype == torch.float16:
+        return F16
     raise RuntimeError(f'ssseg: unsupported dtype {t.dtype}')
 
 

@@ -22,7 +22,7 @@ _CFG = {'dtype': torch.bfloat16, 'sync_bn': True, 'fuse_stats': True}
 
 
 def set_compute_dtype(dtype):
-    assert dtype in (torch.bfloat16, torch.float32)
+    assert dtype in (torch.bfloat16, torch.float16, torch.float32)
     _CFG['dtype'] = dtype
 
 
@@ -40,7 +40,7 @@ def set_fused_bn_stats(flag):
 
 
 def vec(dtype=None):
-    return 8 if (dtype or _CFG['dtype']) == torch.bfloat16 else 4
+    return 4 if (dtype or _CFG['dtype']) == torch.float32 else 8
 
 
 def rup(c, v):

@@ -184,11 +184,12 @@ def sqnorm_(x_flat, out):
     N.call('ssseg_sqnorm_accum', N.dev_ptr(x_flat, 'x'), x_flat.numel(), N.dev_ptr(out), N.dev_ptr(ws), nb, N.stream())
 
 
-def sgd_step_(param, grad, buf, shadow, lr, momentum, wd, max_norm, sqnorm, first):
+def sgd_step_(param, grad, buf, shadow, lr, momentum, wd, max_norm, sqnorm, first, amp_state=None):
     N.call('ssseg_sgd_step', N.dev_ptr(param, 'param'), N.dev_ptr(grad, 'grad'),
            N.dev_ptr(buf) if buf is not None else None, N.dev_ptr(shadow) if shadow is not None else None,
            param.numel(), float(lr), float(momentum), float(wd), float(max_norm),
-           N.dev_ptr(sqnorm) if sqnorm is not None else None, int(bool(first)), N.stream())
+           N.dev_ptr(sqnorm) if sqnorm is not None else None, int(bool(first)),
+           N.dev_ptr(amp_state) if amp_state is not None else None, N.stream())
 
 
 # ------------------------------------------------------------------------------------------------

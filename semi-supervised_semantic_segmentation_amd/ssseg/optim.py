@@ -28,6 +28,7 @@ class SGD(torch.optim.Optimizer):
         self.buf = torch.zeros_like(a.data) if momentum else None
         self._first = True
         self._sq = torch.zeros(1, dtype=torch.float32, device=a.data.device)
+        self.grad_scaler = None     # ssseg.amp.GradScaler in the fp16 compute mode (loss-scaled gradients)
         if self.buf is not None:
             for p, o in zip(a.params, a.offsets):
                 self.state[p]['momentum_buffer'] = self.buf[o:o + p.numel()].view_as(p)
@@ -59,11 +60,15 @@ class SGD(torch.optim.Optimizer):
     def step(self, closure=None, max_norm=0.0):
         """max_norm > 0 clips the global gradient L2 norm first (clip_grad_norm_, train.py:122)."""
         g = self.param_groups[0]
-        if max_norm and max_norm > 0:
+        sc = self.grad_scaler
+        if (max_norm and max_norm > 0) or sc is not None:
             N.call('ssseg_zero', N.dev_ptr(self._sq), 4, N.stream())
             ops.sqnorm_(self.arena.grad, self._sq)
         ops.sgd_step_(self.arena.data, self.arena.grad, self.buf, None, g['lr'], g['momentum'], g['weight_decay'],
-                      max_norm or 0.0, self._sq if max_norm else None, self._first)
+                      max_norm or 0.0, self._sq if (max_norm or sc is not None) else None, self._first,
+                      sc.state if sc is not None else None)
+        if sc is not None:
+            sc.update(self._sq)
         self._first = False
         return None
 

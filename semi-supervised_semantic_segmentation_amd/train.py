@@ -83,13 +83,20 @@ def discriminator_step(mask, prob, adv):
         ops.bce_with_logits_mean(d_fake, _target(d_fake, 0.0))
     if ddp is not None:
         ddp.arm()
-    loss_d.backward()
+    _scaled(loss_d, opt).backward()
     if ddp is not None:
         ddp.finish()
     opt.step()
     opt.zero_grad()
     snn.invalidate_packed(_inner(D))
     return loss_d.detach()
+
+
+def _scaled(loss, optimizer):
+    """fp16 mode: the loss whose backward starts from S*dL (ssseg.amp.GradScaler attached to the optimizer;
+    the optimizer step unscales and skips overflowed steps on the device).  Identity otherwise."""
+    sc = getattr(optimizer, 'grad_scaler', None)
+    return sc.scale(loss) if sc is not None else loss
 
 
 def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch, step, config):
@@ -109,7 +116,7 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
         sup_loss = sup_loss + adv_loss
     if ddp is not None and not semi:
         ddp.arm()
-    (sup_loss / tc['virtual_batch_size_multiplier']).backward()
+    _scaled(sup_loss / tc['virtual_batch_size_multiplier'], optimizer).backward()
     del pred_maps, features
     if adv is not None:
         adv['last_loss_d'] = discriminator_step(mask, prob, adv)
@@ -135,7 +142,7 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
         unsup_loss = consistency * tc['consistency_loss_weight'] * float(epoch > 25)
         if ddp is not None:
             ddp.arm()
-        unsup_loss.backward()
+        _scaled(unsup_loss, optimizer).backward()
     if ddp is not None:
         ddp.finish()
     if step % tc['virtual_batch_size_multiplier'] == 0 and step != 0:

@@ -1,0 +1,100 @@
+"""Config C5 in the fp16 compute mode: FC-HarDNet(n_classes=2) student + EMA teacher + Discriminator(5, 2, 64,
+512, 1) with the adversarial branch, mean-teacher + CowMix consistency, dynamic loss scaling on the device
+(ssseg.amp).  The fp16 run is checked against the same steps in the fp32 mode (step-0 losses are forward
+arithmetic: fp16 storage bound 1e-2 relative) and for liveness over several steps; the loss scaler is checked
+to skip an overflowed step and back off."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+B, H = 2, 128
+
+
+def _run(dtype, steps, hip_device):
+    import cowmix
+    import losses
+    import train
+    from models.adapters import ListOutput
+    from models.discriminator import Discriminator
+    from models.hardnet import HarDNet
+    from ssseg import amp, arena, optim
+    from ssseg import nn as snn
+    snn.set_compute_dtype(dtype)
+    torch.manual_seed(0)
+    s0 = ListOutput(HarDNet(n_classes=2))
+    d0 = Discriminator(5, 2, 64, 512, 1)
+    student, teacher, D = copy.deepcopy(s0).to(hip_device), copy.deepcopy(s0).to(hip_device), d0.to(hip_device)
+    for p in teacher.parameters():
+        p.detach_()
+    teacher.eval()
+    arena.attach(student)
+    arena.attach(teacher, with_grads=False)
+    arena.attach(D)
+    opt = optim.SGD(student.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-4)
+    optd = optim.SGD(D.parameters(), lr=0.01, momentum=0.9)
+    if dtype == torch.float16:
+        opt.grad_scaler = amp.GradScaler(hip_device)
+        optd.grad_scaler = amp.GradScaler(hip_device)
+    adv = dict(discriminator=D, optimizer=optd, weight=0.01)
+    tcfg = dict(loss=losses.CalculateLoss([{'loss_fn': losses.DenseBinaryCrossEntropyLossWithLogits('mean'),
+                                            'weight': [0.5]}]),
+                virtual_batch_size_multiplier=1, use_semi_supervised=True, mask_proportion_range=(0.45, 0.55),
+                sigma_range=(4, 8), confidence_threshold=0.5, consistency_loss_weight=10, ema_model_alpha=0.99,
+                print_freq=1, gradient_clip_value=5.0, adversarial=adv)
+    g = torch.Generator().manual_seed(4)
+    imgs = torch.rand(steps, B, 3, H, H, generator=g)
+    fg = (torch.rand(steps, B, 1, H, H, generator=g) > 0.5).float()
+    masks = torch.cat([1 - fg, fg], 2)
+    unl = torch.rand(2 * steps, B, 3, H, H, generator=g)
+    old = cowmix.NOISE_SOURCE
+    cowmix.NOISE_SOURCE = 'cpu'
+    logs = []
+    try:
+        torch.manual_seed(3)
+        student.train()
+        opt.zero_grad()
+        for k in range(steps):
+            c, u, _ = train.train_step(student, teacher, opt, imgs[k].to(hip_device), masks[k].to(hip_device),
+                                       unl[2 * k].to(hip_device), unl[2 * k + 1].to(hip_device), 30, k,
+                                       {'train': tcfg})
+            logs.append((float(c), float(adv['last_loss_adv']), float(adv['last_loss_d']), float(u)))
+    finally:
+        cowmix.NOISE_SOURCE = old
+        snn.set_compute_dtype(torch.bfloat16)
+    return logs, opt, optd
+
+
+def test_c5_fp16_vs_fp32_mode(hip_device):
+    h, opt, optd = _run(torch.float16, 4, hip_device)
+    f, _, _ = _run(torch.float32, 1, hip_device)
+    print('fp16 steps (sup, adv, disc, unsup):', h, '\nfp32 step 0:', f)
+    assert np.all(np.isfinite(np.array(h))), h
+    for a, b in zip(h[0][:3], f[0][:3]):       # step 0 forward losses: fp16 storage only
+        assert abs(a - b) <= 1e-2 * abs(b), (h[0], f[0])
+    assert opt.grad_scaler.get_scale() > 1.0 and optd.grad_scaler.get_scale() > 1.0
+
+
+def test_grad_scaler_skips_overflowed_step(hip_device):
+    """An overflowed (non-finite) gradient skips the whole SGD step on the device and halves the scale;
+    a finite one unscales by 1/S before the update."""
+    from ssseg import amp, arena, optim
+    m = torch.nn.Linear(16, 4).to(hip_device)
+    arena.attach(m)
+    opt = optim.SGD(m.parameters(), lr=0.1, momentum=0.9)
+    opt.grad_scaler = amp.GradScaler(hip_device, init_scale=1024.0, growth_interval=1)
+    before = [p.detach().clone() for p in m.parameters()]
+    m.weight.grad.fill_(float('inf'))
+    opt.step()
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, p.detach()) for a, p in zip(before, m.parameters()))
+    assert opt.grad_scaler.get_scale() == 512.0 and opt.grad_scaler.found_inf()
+    opt.zero_grad()
+    m.weight.grad.fill_(512.0)          # = 1.0 unscaled
+    opt.step()
+    torch.cuda.synchronize()
+    np.testing.assert_allclose((before[0] - m.weight.detach()).cpu().numpy(), 0.1, rtol=1e-6)
+    assert opt.grad_scaler.get_scale() == 1024.0 and not opt.grad_scaler.found_inf()   # growth_interval 1
