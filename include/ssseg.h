@@ -95,6 +95,15 @@ int ssseg_bilinear_bwd(const void* gy, void* gx, int64_t N, int64_t C, int64_t H
                        int64_t Wo, const int64_t* gy_strides4_host, const int64_t* gx_strides4_host,
                        int align_corners, int dt, ssseg_stream_t stream);
 
+/* Rotation about the image centre by angle_deg (counter-clockwise, OpenCV / kornia get_rotation_matrix2d),
+ * bilinear with zero padding, NCHW contiguous fp32: reversible_augmentations.Rotate.apply / reverse
+ * (reference reversible_augmentations.py:5-23, kornia.rotate; kornia is unpinned and absent, parity with it is
+ * unpinned).  bwd: gx = (d y / d x)^T gy (gx overwritten). */
+int ssseg_rotate_fwd(const float* x, float* y, int64_t N, int64_t C, int64_t H, int64_t W, double angle_deg,
+                     ssseg_stream_t stream);
+int ssseg_rotate_bwd(const float* gy, float* gx, int64_t N, int64_t C, int64_t H, int64_t W, double angle_deg,
+                     ssseg_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Losses.  Reductions are two-stage and deterministic; scalars live in device memory.
  * ------------------------------------------------------------------------------------------- */

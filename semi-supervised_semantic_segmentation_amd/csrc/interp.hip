@@ -176,3 +176,103 @@ extern "C" int ssseg_bilinear_bwd(const void* gy, void* gx, int64_t N, int64_t C
   SSSEG_LAUNCH_CHECK();
   return 0;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Rotation about the image centre (reversible_augmentations.Rotate, reference reversible_augmentations.py:5-23,
+// kornia.rotate): y(p) = bilinear sample of x at M^-1 p, zeros outside, pixel centres on integer coordinates.
+// M is OpenCV's / kornia's get_rotation_matrix2d(centre, angle, 1) (positive angle = counter-clockwise);
+// the inverse map of a rotation is the rotation by -angle about the same centre.  NCHW fp32.
+// Backward scatters each output gradient to its four taps (float atomics: this path is off the hot loop).
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+struct RotMap {
+  float a, b, cx, cy;   // source = (a*(x-cx) + b*(y-cy) + cx, -b*(x-cx) + a*(y-cy) + cy)
+};
+
+__device__ __forceinline__ void rot_src(const RotMap& m, int x, int y, float& sx, float& sy) {
+  const float dx = (float)x - m.cx, dy = (float)y - m.cy;
+  sx = fmaf(m.a, dx, m.b * dy) + m.cx;
+  sy = fmaf(-m.b, dx, m.a * dy) + m.cy;
+}
+
+__global__ void rotate_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t NC, int H, int W,
+                                  RotMap m) {
+  const int64_t total = NC * H * W;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int px = (int)(i % W), py = (int)((i / W) % H);
+    const int64_t plane = i / ((int64_t)H * W);
+    float sx, sy;
+    rot_src(m, px, py, sx, sy);
+    const float fx = floorf(sx), fy = floorf(sy);
+    const int x0 = (int)fx, y0 = (int)fy;
+    const float wx = sx - fx, wy = sy - fy;
+    const float* p = x + plane * H * W;
+    float v = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int xx = x0 + (t & 1), yy = y0 + (t >> 1);
+      const float w = ((t & 1) ? wx : 1.f - wx) * ((t >> 1) ? wy : 1.f - wy);
+      if ((unsigned)xx < (unsigned)W && (unsigned)yy < (unsigned)H) v = fmaf(w, p[(int64_t)yy * W + xx], v);
+    }
+    y[i] = v;
+  }
+}
+
+__global__ void rotate_bwd_kernel(const float* __restrict__ gy, float* __restrict__ gx, int64_t NC, int H, int W,
+                                  RotMap m) {
+  const int64_t total = NC * H * W;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int px = (int)(i % W), py = (int)((i / W) % H);
+    const int64_t plane = i / ((int64_t)H * W);
+    float sx, sy;
+    rot_src(m, px, py, sx, sy);
+    const float fx = floorf(sx), fy = floorf(sy);
+    const int x0 = (int)fx, y0 = (int)fy;
+    const float wx = sx - fx, wy = sy - fy;
+    const float g = gy[i];
+    float* p = gx + plane * H * W;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int xx = x0 + (t & 1), yy = y0 + (t >> 1);
+      const float w = ((t & 1) ? wx : 1.f - wx) * ((t >> 1) ? wy : 1.f - wy);
+      if ((unsigned)xx < (unsigned)W && (unsigned)yy < (unsigned)H) atomicAdd(p + (int64_t)yy * W + xx, w * g);
+    }
+  }
+}
+
+RotMap rot_map(double angle_deg, int64_t H, int64_t W) {
+  const double th = angle_deg * 3.14159265358979323846 / 180.0;
+  RotMap m;
+  // inverse map of the counter-clockwise rotation by `angle` (y axis pointing down): rotate back by -angle
+  m.a = (float)cos(th);
+  m.b = (float)(-sin(th));
+  m.cx = (float)(W - 1) * 0.5f;
+  m.cy = (float)(H - 1) * 0.5f;
+  return m;
+}
+
+}  // namespace
+
+extern "C" int ssseg_rotate_fwd(const float* x, float* y, int64_t N, int64_t C, int64_t H, int64_t W, double angle_deg,
+                                ssseg_stream_t stream) {
+  if (!x || !y || N < 0 || C < 0 || H < 1 || W < 1 || H > 0x7fffffff || W > 0x7fffffff) return SSSEG_EINVAL;
+  const int64_t total = N * C * H * W;
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(rotate_fwd_kernel, dim3(ssseg_grid(total, 256)), dim3(256), 0, (hipStream_t)stream, x, y, N * C,
+                     (int)H, (int)W, rot_map(angle_deg, H, W));
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_rotate_bwd(const float* gy, float* gx, int64_t N, int64_t C, int64_t H, int64_t W, double angle_deg,
+                                ssseg_stream_t stream) {
+  if (!gy || !gx || N < 0 || C < 0 || H < 1 || W < 1 || H > 0x7fffffff || W > 0x7fffffff) return SSSEG_EINVAL;
+  const int64_t total = N * C * H * W;
+  if (total == 0) return 0;
+  SSSEG_TRY(hipMemsetAsync(gx, 0, sizeof(float) * total, (hipStream_t)stream));
+  hipLaunchKernelGGL(rotate_bwd_kernel, dim3(ssseg_grid(total, 256)), dim3(256), 0, (hipStream_t)stream, gy, gx, N * C,
+                     (int)H, (int)W, rot_map(angle_deg, H, W));
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}

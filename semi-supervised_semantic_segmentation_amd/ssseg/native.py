@@ -34,6 +34,8 @@ SIGS = {
     'ssseg_cast': (i32, [vp, vp, i64, i32, i32, vp]),
     'ssseg_bilinear_fwd': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, I64P, I64P, i32, i32, vp]),
     'ssseg_bilinear_bwd': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, I64P, I64P, i32, i32, vp]),
+    'ssseg_rotate_fwd': (i32, [vp, vp, i64, i64, i64, i64, f64, vp]),
+    'ssseg_rotate_bwd': (i32, [vp, vp, i64, i64, i64, i64, f64, vp]),
     'ssseg_reduce_workspace_bytes': (sz, [i64]),
     'ssseg_bce_logits_fwd': (i32, [vp, vp, i64, vp, vp, sz, vp]),
     'ssseg_bce_logits_bwd': (i32, [vp, vp, i64, vp, vp, vp]),

@@ -84,6 +84,31 @@ def interpolate_bilinear(x, size, align_corners=False):
     return _Bilinear.apply(x, tuple(size), align_corners)
 
 
+class _Rotate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, angle):
+        x = _c(x.float())
+        y = torch.empty_like(x)
+        Nn, C, H, W = x.shape
+        N.call('ssseg_rotate_fwd', N.dev_ptr(x, 'x'), N.dev_ptr(y), Nn, C, H, W, float(angle), N.stream())
+        ctx.meta = (Nn, C, H, W, float(angle))
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        Nn, C, H, W, angle = ctx.meta
+        gy = _c(gy.float())
+        gx = torch.empty_like(gy)
+        N.call('ssseg_rotate_bwd', N.dev_ptr(gy), N.dev_ptr(gx), Nn, C, H, W, angle, N.stream())
+        return gx, None
+
+
+def rotate(x, angle_deg):
+    """kornia.rotate(x, angle) for NCHW fp32 (reversible_augmentations.py:13-23): counter-clockwise degrees
+    about the image centre, bilinear, zero padding; differentiable."""
+    return _Rotate.apply(x, angle_deg)
+
+
 class _Sigmoid(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):

@@ -281,3 +281,50 @@ def test_inference_wrapper_vs_reference_golden(hip_device):
     band = np.abs(hi[1] - hi[0]) < 1e-5
     diff = (mask.cpu().numpy() != g['mask']).any(0)
     assert not (diff & ~band).any()
+
+
+@pytest.mark.parametrize('angle', [0.0, 17.5, -90.0, 33.0])
+def test_reversible_rotate_vs_grid_sample(hip_device, angle):
+    """reversible_augmentations.Rotate's kernel (kornia.rotate semantics: counter-clockwise about the centre,
+    bilinear, zero padding; kornia absent so parity with it is unpinned) vs a torch grid_sample restatement of
+    the same inverse map (align_corners=True pixel grid), forward and input gradient."""
+    import math
+    import torch.nn.functional as F
+    from ssseg import ops
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(2, 3, 19, 24, generator=g, dtype=torch.float64)
+    gy = torch.randn(2, 3, 19, 24, generator=g, dtype=torch.float64)
+    N_, C, H, W = x.shape
+    th = math.radians(angle)
+    ys, xs = torch.meshgrid(torch.arange(H, dtype=torch.float64), torch.arange(W, dtype=torch.float64), indexing='ij')
+    cx, cy = (W - 1) / 2, (H - 1) / 2
+    sx = math.cos(th) * (xs - cx) - math.sin(th) * (ys - cy) + cx
+    sy = math.sin(th) * (xs - cx) + math.cos(th) * (ys - cy) + cy
+    grid = torch.stack([sx / (W - 1) * 2 - 1, sy / (H - 1) * 2 - 1], -1).expand(N_, H, W, 2)
+    xr = x.clone().requires_grad_(True)
+    yr = F.grid_sample(xr, grid, mode='bilinear', padding_mode='zeros', align_corners=True)
+    yr.backward(gy)
+    xd = x.float().to(hip_device).requires_grad_(True)
+    y = ops.rotate(xd, angle)
+    y.backward(gy.float().to(hip_device))
+    assert float((y.detach().cpu().double() - yr.detach()).abs().max()) < 1e-5
+    assert float((xd.grad.cpu().double() - xr.grad).abs().max()) < 1e-5
+    if angle == 0.0:
+        assert torch.equal(y.detach().cpu(), x.float())
+
+
+def test_reversible_augmentations_roundtrip(hip_device):
+    """apply() then reverse() on a smooth image: back to the input away from the rotated-out corners."""
+    import reversible_augmentations as RA
+    torch.manual_seed(0)
+    yy, xx = torch.meshgrid(torch.linspace(-1, 1, 64), torch.linspace(-1, 1, 64), indexing='ij')
+    img = torch.stack([torch.sin(2 * xx) * torch.cos(3 * yy)] * 2)[None].to(hip_device)
+    rot = RA.Rotate(20)
+    out = rot.reverse(rot.apply([img]))[0]
+    c = (slice(None), slice(None), slice(20, 44), slice(20, 44))
+    assert float((out[c] - img[c]).abs().max()) < 2e-2
+    res = RA.Rescale(0.5, 0.75)
+    small = res.apply([img])[0]
+    assert small.shape[2] == int(64 * res.scale)
+    back = res.reverse([small])[0]
+    assert back.shape[2] in (63, 64)
