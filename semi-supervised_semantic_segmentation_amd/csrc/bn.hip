@@ -107,16 +107,26 @@ struct ChanParams {
 template <int V>
 __device__ __forceinline__ void load_params(const ChanParams& cp, int c0, int C, float (&mu)[V], float (&is)[V],
                                             float (&ga)[V], float (&be)[V], bool (&live)[V]) {
+  // clamped channel indices: every load unconditional (none waits for another), dead channels zeroed after
 #pragma unroll
   for (int e = 0; e < V; ++e) {
-    const int c = c0 + e;
-    live[e] = c < C;
-    mu[e] = live[e] ? cp.mean[c] : 0.f;
-    is[e] = live[e] ? cp.invstd[c] : 0.f;
-    ga[e] = live[e] ? (cp.gamma ? cp.gamma[c] : 1.f) : 0.f;
-    be[e] = live[e] ? (cp.beta ? cp.beta[c] : 0.f) : 0.f;
+    const int c = min(c0 + e, C - 1);
+    live[e] = c0 + e < C;
+    mu[e] = cp.mean[c];
+    is[e] = cp.invstd[c];
+    ga[e] = cp.gamma ? cp.gamma[c] : 1.f;
+    be[e] = cp.beta ? cp.beta[c] : 0.f;
+  }
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    mu[e] = live[e] ? mu[e] : 0.f;
+    is[e] = live[e] ? is[e] : 0.f;
+    ga[e] = live[e] ? ga[e] : 0.f;
+    be[e] = live[e] ? be[e] : 0.f;
   }
 }
+
+__device__ __forceinline__ int64_t clampp(int64_t p, int64_t P) { return p < P ? p : P - 1; }
 
 constexpr int MAXG = 1024;   // partial blocks along pixels (several per CU: the partial passes are HBM-bound)
 
@@ -138,25 +148,27 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x
     float mu[V], is[V], ga[V], be[V];
     bool live[V];
     if (MODE == 1) load_params<V>(prm, c0, C, mu, is, ga, be, live);
+    using CK = Chunk<T, V>;
     const int64_t stride = (int64_t)gridDim.x * L.ppb;
     for (int64_t p0 = (int64_t)blockIdx.x * L.ppb + pl; p0 < P; p0 += stride * U) {
-      float v[U][V], g[U][V], r[U][V];
+      typename CK::raw qx[U], qg[U], qr[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t p = p0 + u * stride;
-#pragma unroll
-        for (int e = 0; e < V; ++e) v[u][e] = g[u][e] = r[u][e] = 0.f;
-        if (p < P) {
-          Vec<T, V>::ld(x + p * ldx + c0, v[u]);
-          if (MODE == 1) {
-            Vec<T, V>::ld(dy + p * lddy + c0, g[u]);
-            if (res && relu) Vec<T, V>::ld(res + p * ldr + c0, r[u]);
-          }
-        }
+        const int64_t p = clampp(p0 + u * stride, P);
+        qx[u] = CK::ld(x + p * ldx + c0);
+        qg[u] = MODE == 1 ? CK::ld(dy + p * lddy + c0) : CK::zero();
+        qr[u] = CK::zero();
       }
+      if (MODE == 1 && res && relu)
+#pragma unroll
+        for (int u = 0; u < U; ++u) qr[u] = CK::ld(res + clampp(p0 + u * stride, P) * ldr + c0);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (p0 + u * stride >= P) continue;
+        float v[U][V], g[U][V], r[U][V];
+        CK::cvt(qx[u], v[u]);
+        CK::cvt(qg[u], g[u]);
+        CK::cvt(qr[u], r[u]);
 #pragma unroll
         for (int e = 0; e < V; ++e) {
           if (MODE == 0) {
@@ -232,20 +244,29 @@ __global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* par
   __shared__ double red[2][LN][CH];
   const int cl = threadIdx.x % CH, pl = threadIdx.x / CH;
   const int c = blockIdx.x * CH + cl;
-  double a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+  // four row pairs per iteration, all eight loads issued before the adds (independent chains)
+  double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
   if (c < C) {
     int i = pl;
-    for (; i + LN < nparts; i += 2 * LN) {
-      a0 += part[(int64_t)(2 * i) * C + c];
-      b0 += part[(int64_t)(2 * i + 1) * C + c];
-      a1 += part[(int64_t)(2 * (i + LN)) * C + c];
-      b1 += part[(int64_t)(2 * (i + LN) + 1) * C + c];
+    for (; i + 3 * LN < nparts; i += 4 * LN) {
+      double qa[4], qb[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        qa[k] = part[(int64_t)(2 * (i + k * LN)) * C + c];
+        qb[k] = part[(int64_t)(2 * (i + k * LN) + 1) * C + c];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        a[k] += qa[k];
+        b[k] += qb[k];
+      }
     }
-    if (i < nparts) {
-      a0 += part[(int64_t)(2 * i) * C + c];
-      b0 += part[(int64_t)(2 * i + 1) * C + c];
+    for (; i < nparts; i += LN) {
+      a[0] += part[(int64_t)(2 * i) * C + c];
+      b[0] += part[(int64_t)(2 * i + 1) * C + c];
     }
   }
+  const double a0 = a[0] + a[2], a1 = a[1] + a[3], b0 = b[0] + b[2], b1 = b[1] + b[3];
   red[0][pl][cl] = a0 + a1;
   red[1][pl][cl] = b0 + b1;
   __syncthreads();
@@ -363,29 +384,40 @@ __global__ void __launch_bounds__(256) bn_eval_bwd_kernel(const T* __restrict__ 
     bool live[V];
 #pragma unroll
     for (int e = 0; e < V; ++e) {
+      const int c = min(c0 + e, C - 1);
       live[e] = c0 + e < C;
-      sc[e] = live[e] ? scale[c0 + e] : 0.f;
-      me[e] = live[e] ? mean_eff[c0 + e] : 0.f;
-      is[e] = live[e] ? invstd[c0 + e] : 0.f;
+      sc[e] = scale[c];
+      me[e] = mean_eff[c];
+      is[e] = invstd[c];
     }
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      sc[e] = live[e] ? sc[e] : 0.f;
+      me[e] = live[e] ? me[e] : 0.f;
+      is[e] = live[e] ? is[e] : 0.f;
+    }
+    using CK = Chunk<T, V>;
     const int64_t stride = (int64_t)gridDim.x * L.ppb;
     for (int64_t p0 = (int64_t)blockIdx.x * L.ppb + pl; p0 < P; p0 += stride * U) {
-      float g[U][V], yv[U][V], a[U][V];
+      typename CK::raw qg[U], qy[U], qa[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t p = p0 + u * stride;
-#pragma unroll
-        for (int e = 0; e < V; ++e) g[u][e] = yv[u][e] = a[u][e] = 0.f;
-        if (p < P) {
-          Vec<T, V>::ld(dy + p * ld + c0, g[u]);
-          if (relu) Vec<T, V>::ld(y + p * ld + c0, yv[u]);
-          Vec<T, V>::ld(aux + p * ld + c0, a[u]);
-        }
+        const int64_t p = clampp(p0 + u * stride, P);
+        qg[u] = CK::ld(dy + p * ld + c0);
+        qa[u] = CK::ld(aux + p * ld + c0);
+        qy[u] = CK::zero();
       }
+      if (relu)
+#pragma unroll
+        for (int u = 0; u < U; ++u) qy[u] = CK::ld(y + clampp(p0 + u * stride, P) * ld + c0);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t p = p0 + u * stride;
         if (p >= P) continue;
+        float g[U][V], yv[U][V], a[U][V];
+        CK::cvt(qg[u], g[u]);
+        CK::cvt(qy[u], yv[u]);
+        CK::cvt(qa[u], a[u]);
         float od[V], oc[V];
 #pragma unroll
         for (int e = 0; e < V; ++e) {
@@ -442,22 +474,24 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
   bool live[V];
   load_params<V>(prm, c0, C, mu, is, ga, be, live);
   const int64_t stride = (int64_t)gridDim.x * L.ppb;
+  using CK = Chunk<T, V>;
   for (int64_t p0 = (int64_t)blockIdx.x * L.ppb + pl; p0 < P; p0 += stride * U) {
-    float v[U][V], r[U][V];
+    typename CK::raw qx[U], qr[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t p = p0 + u * stride;
-#pragma unroll
-      for (int e = 0; e < V; ++e) v[u][e] = r[u][e] = 0.f;
-      if (p < P) {
-        Vec<T, V>::ld(x + p * ldx + c0, v[u]);
-        if (res) Vec<T, V>::ld(res + p * ldr + c0, r[u]);
-      }
+      qx[u] = CK::ld(x + clampp(p0 + u * stride, P) * ldx + c0);
+      qr[u] = CK::zero();
     }
+    if (res)
+#pragma unroll
+      for (int u = 0; u < U; ++u) qr[u] = CK::ld(res + clampp(p0 + u * stride, P) * ldr + c0);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t p = p0 + u * stride;
       if (p >= P) continue;
+      float v[U][V], r[U][V];
+      CK::cvt(qx[u], v[u]);
+      CK::cvt(qr[u], r[u]);
       float o[V];
 #pragma unroll
       for (int e = 0; e < V; ++e) {
@@ -488,27 +522,45 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
 #pragma unroll
   for (int e = 0; e < V; ++e) {
     gi[e] = ga[e] * is[e];
-    mdy[e] = (train && live[e]) ? (float)(sums[c0 + e] / count) : 0.f;
-    mdyx[e] = (train && live[e]) ? (float)(sums[C + c0 + e] / count) : 0.f;
+    mdy[e] = mdyx[e] = 0.f;
+  }
+  if (train) {
+    double q1[V], q2[V];   // every load issued before the first division
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const int c = min(c0 + e, C - 1);
+      q1[e] = sums[c];
+      q2[e] = sums[C + c];
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const float a = (float)(q1[e] / count), b = (float)(q2[e] / count);
+      mdy[e] = live[e] ? a : 0.f;
+      mdyx[e] = live[e] ? b : 0.f;
+    }
   }
   const int64_t stride = (int64_t)gridDim.x * L.ppb;
+  using CK = Chunk<T, V>;
   for (int64_t p0 = (int64_t)blockIdx.x * L.ppb + pl; p0 < P; p0 += stride * U) {
-    float v[U][V], g[U][V], r[U][V];
+    typename CK::raw qx[U], qg[U], qr[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t p = p0 + u * stride;
-#pragma unroll
-      for (int e = 0; e < V; ++e) v[u][e] = g[u][e] = r[u][e] = 0.f;
-      if (p < P) {
-        Vec<T, V>::ld(x + p * ldx + c0, v[u]);
-        Vec<T, V>::ld(dy + p * lddy + c0, g[u]);
-        if (res && relu) Vec<T, V>::ld(res + p * ldr + c0, r[u]);
-      }
+      const int64_t p = clampp(p0 + u * stride, P);
+      qx[u] = CK::ld(x + p * ldx + c0);
+      qg[u] = CK::ld(dy + p * lddy + c0);
+      qr[u] = CK::zero();
     }
+    if (res && relu)
+#pragma unroll
+      for (int u = 0; u < U; ++u) qr[u] = CK::ld(res + clampp(p0 + u * stride, P) * ldr + c0);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t p = p0 + u * stride;
       if (p >= P) continue;
+      float v[U][V], g[U][V], r[U][V];
+      CK::cvt(qx[u], v[u]);
+      CK::cvt(qg[u], g[u]);
+      CK::cvt(qr[u], r[u]);
       float o[V], od[V];
 #pragma unroll
       for (int e = 0; e < V; ++e) {

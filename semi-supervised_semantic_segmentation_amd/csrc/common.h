@@ -85,6 +85,73 @@ struct H16 {
   }
 };
 
+// Raw V-element chunks (16 or 8 bytes): ld() moves the bits only, cvt() converts to fp32 later.  Streaming
+// kernels issue every load of a batch first (clamped addresses, no branch around a load) and convert after,
+// so the batch is in flight together: a conversion right behind each conditional load makes the compiler
+// wait for that load (s_waitcnt vmcnt(0)) before issuing the next, serialising the memory round trips.
+template <typename T, int V> struct Chunk;
+template <> struct Chunk<bf16_t, 8> {
+  typedef uint4 raw;
+  __device__ __forceinline__ static raw ld(const bf16_t* p) { return *(const uint4*)p; }
+  __device__ __forceinline__ static raw zero() { return make_uint4(0, 0, 0, 0); }
+  __device__ __forceinline__ static void cvt(const raw& q, float (&v)[8]) {
+    const unsigned w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+};
+template <> struct Chunk<bf16_t, 4> {
+  typedef uint2 raw;
+  __device__ __forceinline__ static raw ld(const bf16_t* p) { return *(const uint2*)p; }
+  __device__ __forceinline__ static raw zero() { return make_uint2(0, 0); }
+  __device__ __forceinline__ static void cvt(const raw& q, float (&v)[4]) {
+    v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
+    v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+  }
+};
+template <> struct Chunk<f16_t, 8> {
+  typedef uint4 raw;
+  __device__ __forceinline__ static raw ld(const f16_t* p) { return *(const uint4*)p; }
+  __device__ __forceinline__ static raw zero() { return make_uint4(0, 0, 0, 0); }
+  __device__ __forceinline__ static void cvt(const raw& q, float (&v)[8]) {
+    const unsigned w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f16x2_t h = __builtin_bit_cast(f16x2_t, w[i]);
+      v[2 * i] = (float)h[0];
+      v[2 * i + 1] = (float)h[1];
+    }
+  }
+};
+template <> struct Chunk<f16_t, 4> {
+  typedef uint2 raw;
+  __device__ __forceinline__ static raw ld(const f16_t* p) { return *(const uint2*)p; }
+  __device__ __forceinline__ static raw zero() { return make_uint2(0, 0); }
+  __device__ __forceinline__ static void cvt(const raw& q, float (&v)[4]) {
+    const f16x2_t a = __builtin_bit_cast(f16x2_t, q.x), b = __builtin_bit_cast(f16x2_t, q.y);
+    v[0] = (float)a[0]; v[1] = (float)a[1]; v[2] = (float)b[0]; v[3] = (float)b[1];
+  }
+};
+template <> struct Chunk<float, 4> {
+  typedef float4 raw;
+  __device__ __forceinline__ static raw ld(const float* p) { return *(const float4*)p; }
+  __device__ __forceinline__ static raw zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ __forceinline__ static void cvt(const raw& q, float (&v)[4]) {
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  }
+};
+template <> struct Chunk<float, 2> {
+  typedef float2 raw;
+  __device__ __forceinline__ static raw ld(const float* p) { return *(const float2*)p; }
+  __device__ __forceinline__ static raw zero() { return make_float2(0.f, 0.f); }
+  __device__ __forceinline__ static void cvt(const raw& q, float (&v)[2]) {
+    v[0] = q.x; v[1] = q.y;
+  }
+};
+
 // wave64 reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

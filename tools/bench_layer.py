@@ -36,7 +36,10 @@ def main():
     ap.add_argument('--stride', type=int, default=1)
     ap.add_argument('--hw', type=int, default=128)
     ap.add_argument('--batch', type=int, default=16)
+    ap.add_argument('--rotate', type=int, default=1, help='keep this many outputs alive (>1: cold-cache writes)')
     a = ap.parse_args()
+    import collections
+    keep = collections.deque(maxlen=a.rotate)
     dev = torch.device('cuda')
     snn.set_compute_dtype(torch.bfloat16)
     conv = snn.Conv2d(a.cin, a.cout, a.k, a.stride, a.k // 2, bias=False).to(dev)
@@ -47,14 +50,25 @@ def main():
     in_bytes = x.numel() * 2
     flops = 2.0 * y.shape[0] * y.shape[2] * y.shape[3] * a.cout * a.cin * a.k * a.k
     fill = torch.empty_like(y)
-    t = timeit(lambda: fill.fill_(1.0))
+    fills = [torch.empty_like(y) for _ in range(a.rotate)]
+    it = iter(range(1 << 30))
+    t = timeit(lambda: fills[next(it) % a.rotate].fill_(1.0))
     print(f'layer {a.cin}->{a.cout} k{a.k} s{a.stride} @{a.batch}x{a.hw}^2: out {out_bytes / 1e6:.1f} MB in '
           f'{in_bytes / 1e6:.1f} MB, {flops / 1e9:.1f} GFLOP; torch fill of the output: {t:.1f} us '
           f'({out_bytes / t / 1e3:.0f} GB/s)')
-    for v in [11] + list(range(1, 11)):
+    src = torch.empty(y.numel() // 2 + x.numel() // 2 * 0, dtype=torch.float32, device=dev)
+    dst = torch.empty_like(src)
+    t = timeit(lambda: dst.copy_(src))
+    print(f'torch copy of {src.numel() * 4 / 1e6:.1f} MB: {t:.1f} us ({2 * src.numel() * 4 / t / 1e3:.0f} GB/s)')
+    if a.k == 1 and a.stride == 1:
+        xm = torch.randn(x.numel() // a.cin, a.cin, device=dev, dtype=torch.bfloat16)
+        wm = torch.randn(a.cin, a.cout, device=dev, dtype=torch.bfloat16)
+        t = timeit(lambda: torch.mm(xm, wm))
+        print(f'torch.mm (hipBLASLt) same GEMM: {t:.1f} us  {(in_bytes + out_bytes) / t / 1e3:6.0f} GB/s')
+    for v in [11] + list(range(1, 11)) + list(range(12, 18)):
         N.call('ssseg_set_knob', 4, v)
         with torch.no_grad():
-            t = timeit(lambda: conv(x))
+            t = timeit(lambda: keep.append(conv(x)))
         print(f'variant {v:2d}: {t:8.1f} us  {(in_bytes + out_bytes) / t / 1e3:6.0f} GB/s  {flops / t / 1e6:6.0f} TF')
     N.call('ssseg_set_knob', 4, 0)
 

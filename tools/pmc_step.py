@@ -7,7 +7,12 @@ ssseg_cast of 8 floats) so the dispatches of exactly that step can be cut out of
     rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_f -o f --output-format csv -- python tools/pmc_step.py
     rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_w -o w --output-format csv -- python tools/pmc_step.py
 
-Parse mode (CPU):  python tools/pmc_step.py --parse gpurun_out/pmc_f gpurun_out/pmc_w > profiles/<name>.json
+    rocprofv3 --kernel-trace -d gpurun_out/pmc_t -o t --output-format csv -- python tools/pmc_step.py
+
+Parse mode (CPU):  python tools/pmc_step.py --parse gpurun_out/pmc_f gpurun_out/pmc_w [--trace gpurun_out/pmc_t]
+                   > profiles/<name>.json
+With --trace, every kernel family of the step (not only the conv engine) is listed with its bytes, device time
+and achieved HBM bandwidth (corrected bytes / time).
 
 FETCH_SIZE / WRITE_SIZE are in KB (rocprofv3 derived counters).  Per MI355X_MICROARCH.md §HBM, gfx950's
 FETCH_SIZE reports half of the bytes of wide (16 B/lane) streaming reads, which is how every conv-engine
@@ -66,6 +71,57 @@ def _rows(d):
     return rows
 
 
+def _rows_named(d, pattern):
+    files = glob.glob(os.path.join(d, '**', pattern), recursive=True)
+    if not files:
+        raise SystemExit(f'no {pattern} under {d}')
+    rows = []
+    for f in files:
+        with open(f) as fh:
+            rows += list(csv.DictReader(fh))
+    key = 'Dispatch_Id' if 'Dispatch_Id' in rows[0] else 'Correlation_Id'
+    rows.sort(key=lambda r: int(r[key]))
+    return rows
+
+
+def _family(name):
+    name = name.replace('(anonymous namespace)::', '').replace('void ', '').strip()
+    if not name.startswith('at::'):
+        name = name.split('(')[0].split('<')[0]
+    else:
+        name = name.split('(')[0]
+    for k in CONV_KERNELS:
+        if k in name:
+            return k
+    return name[:90]
+
+
+def _step_rows(rows):
+    marks = [i for i, r in enumerate(rows) if 'cast_kernel' in r['Kernel_Name']
+             and int(r.get('Grid_Size', r.get('Grid_Size_X', 0)) or 0) <= 256]
+    if len(marks) < 2:
+        raise SystemExit('markers not found')
+    return rows[marks[-2] + 1:marks[-1]]
+
+
+def _all_sums(d):
+    per = collections.defaultdict(lambda: [0.0, 0])
+    for r in _step_rows(_rows(d)):
+        fam = _family(r['Kernel_Name'])
+        per[fam][0] += float(r['Counter_Value'])
+        per[fam][1] += 1
+    return per
+
+
+def _trace_sums(d):
+    per = collections.defaultdict(lambda: [0.0, 0])
+    for r in _step_rows(_rows_named(d, '*kernel_trace.csv')):
+        fam = _family(r['Kernel_Name'])
+        per[fam][0] += (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) * 1e-3   # us
+        per[fam][1] += 1
+    return per
+
+
 def _step_sums(d):
     rows = _rows(d)
     marks = [i for i, r in enumerate(rows) if 'cast_kernel' in r['Kernel_Name'] and int(r.get('Grid_Size', 0)) <= 256]
@@ -87,7 +143,7 @@ def _step_sums(d):
     return total, launches, {k: v for k, v in per.items()}, rows[0].get('Counter_Name', '?')
 
 
-def parse(fetch_dir, write_dir):
+def parse(fetch_dir, write_dir, trace_dir=None):
     f_kb, n_f, f_per, _ = _step_sums(fetch_dir)
     w_kb, n_w, w_per, _ = _step_sums(write_dir)
     fetch, write = f_kb * 1024.0, w_kb * 1024.0
@@ -100,14 +156,27 @@ def parse(fetch_dir, write_dir):
                                   'launches': f_per.get(k, [0, 0])[1]} for k in sorted(set(f_per) | set(w_per))},
         'correction': 'FETCH_SIZE x2 for 16 B/lane streaming reads on gfx950 (MI355X_MICROARCH.md §HBM)',
     }
+    if trace_dir:
+        fa, wa, ta = _all_sums(fetch_dir), _all_sums(write_dir), _trace_sums(trace_dir)
+        fams = []
+        for k in sorted(ta, key=lambda k: -ta[k][0]):
+            us = ta[k][0]
+            byt = 2 * fa.get(k, [0, 0])[0] * 1024 + wa.get(k, [0, 0])[0] * 1024
+            fams.append({'kernel': k, 'launches': ta[k][1], 'time_us': round(us, 1),
+                         'fetch_bytes_corrected_x2': 2 * fa.get(k, [0, 0])[0] * 1024,
+                         'write_bytes': wa.get(k, [0, 0])[0] * 1024,
+                         'achieved_GBps': round(byt / (us * 1e3), 1) if us > 0 else None})
+        out['all_kernels_step_time_us'] = round(sum(v[0] for v in ta.values()), 1)
+        out['all_kernels'] = fams
     print(json.dumps(out, indent=1))
 
 
 if __name__ == '__main__':
     ap = argparse.ArgumentParser()
     ap.add_argument('--parse', nargs=2, metavar=('FETCH_DIR', 'WRITE_DIR'))
+    ap.add_argument('--trace', default=None)
     a = ap.parse_args()
     if a.parse:
-        parse(*a.parse)
+        parse(*a.parse, trace_dir=a.trace)
     else:
         run()
