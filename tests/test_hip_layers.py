@@ -281,24 +281,31 @@ def test_conv_bn_act_fused_eval_grad(hip_device, mode, monkeypatch, kind, cin, c
     _close(mb.bias.grad, rb.bias.grad, mode, 'dbeta')
 
 
+ALL_VARIANTS = [11] + list(range(1, 11)) + list(range(12, 18))
+
+
 @pytest.mark.parametrize('kind,cin,cout,k,H', [('conv', 64, 128, 3, 19), ('conv', 128, 64, 1, 17), ('conv', 192, 256, 3, 9),
-                                               ('conv', 64, 256, 1, 21), ('convT', 128, 64, 4, 7)])
+                                               ('conv', 64, 256, 1, 21), ('convT', 128, 64, 4, 7),
+                                               ('conv', 256, 200, 1, 23), ('conv', 192, 1024, 1, 11),
+                                               ('conv_s2', 128, 256, 1, 18), ('conv', 64, 64, 1, 64)])
 def test_conv_variants_bitwise(hip_device, kind, cin, cout, k, H):
     """Every bf16 engine variant (register-staged, LDS-DMA tile configs 1..10 and 12..17) accumulates the
-    same MFMA k-sequence: forward and input-gradient outputs are bit-identical, so autotuning never
-    changes results."""
+    same MFMA k-sequence: forward and input-gradient outputs are bit-identical, so autotuning never changes
+    results."""
     from ssseg import native as N
     from ssseg import nn as snn
     snn.set_compute_dtype(torch.bfloat16)
     torch.manual_seed(11)
     if kind == 'conv':
         mod = snn.Conv2d(cin, cout, k, 1, k // 2, bias=False).to(hip_device)
+    elif kind == 'conv_s2':
+        mod = snn.Conv2d(cin, cout, k, 2, 0, bias=False).to(hip_device)
     else:
         mod = snn.ConvTranspose2d(cin, cout, k, 2, 1).to(hip_device)
     x = _act_in(torch.randn(2, cin, H, H + 3), hip_device).detach().requires_grad_(True)
     outs = []
     try:
-        for v in [11] + list(range(1, 11)) + list(range(12, 18)):
+        for v in ALL_VARIANTS:
             N.call('ssseg_set_knob', 4, v)
             y = mod(x)
             gy = torch.ones_like(y)
@@ -505,7 +512,8 @@ def test_bn_fused_tails_match_unfused(hip_device, C, P):
 
 @pytest.mark.parametrize('kind,cin,cout,k,s,H', [('conv', 64, 128, 3, 1, 19), ('conv', 128, 64, 1, 1, 17),
                                                  ('conv', 64, 256, 1, 2, 21), ('conv', 16, 40, 3, 1, 13),
-                                                 ('convT', 128, 64, 4, 2, 7), ('conv', 8, 12, 3, 1, 11)])
+                                                 ('convT', 128, 64, 4, 2, 7), ('conv', 8, 12, 3, 1, 11),
+                                                 ('conv', 192, 320, 1, 1, 29)])
 def test_fused_bn_stats_match_separate_pass(hip_device, mode, kind, cin, cout, k, s, H):
     """Training BatchNorm statistics from the producing conv's epilogue (ssseg_conv_epilogue.stats, fp64 tile
     partials of the stored output) == the separate statistics pass over that output (ssseg_bn_stats): same
@@ -523,8 +531,7 @@ def test_fused_bn_stats_match_separate_pass(hip_device, mode, kind, cin, cout, k
         bn.weight.uniform_(0.5, 1.5)
         bn.bias.uniform_(-0.2, 0.2)
     x = _act_in(torch.randn(2, cin, H, H + 2) + 0.3, hip_device)
-    variants = [(0, 0)] if mode == 'f32' else [(v, e) for v in [11] + list(range(1, 11)) + list(range(12, 18))
-                                                 for e in (0, -1)]
+    variants = [(0, 0)] if mode == 'f32' else [(v, e) for v in ALL_VARIANTS for e in (0, -1)]
     try:
         for v, e in variants:
             N.call('ssseg_set_knob', 4, v)
@@ -546,3 +553,4 @@ def test_fused_bn_stats_match_separate_pass(hip_device, mode, kind, cin, cout, k
         N.call('ssseg_set_knob', 4, 0)
         N.call('ssseg_set_knob', 7, 0)
         snn.set_fused_bn_stats(True)
+
