@@ -379,6 +379,12 @@ int ssseg_maxpool_fwd(const void* x, void* y, uint8_t* idx, int64_t N, int64_t H
                       int64_t OW, int64_t k, int64_t s, int64_t p, int dt, ssseg_stream_t stream);
 int ssseg_maxpool_bwd(const void* gy, const uint8_t* idx, void* gx, int64_t N, int64_t H, int64_t W, int64_t C,
                       int64_t OH, int64_t OW, int64_t k, int64_t s, int64_t p, int dt, ssseg_stream_t stream);
+/* as ssseg_maxpool_bwd, plus res (NHWC like gx, or NULL): gx = res + gather(gy) in one pass -- an activation read
+ * by the max-pool and by another op (the UNet skip from the stem, unet.py:36-45) gets both gradients without a
+ * separate add (ssseg.nn.GradJoin). */
+int ssseg_maxpool_bwd_res(const void* gy, const uint8_t* idx, const void* res, void* gx, int64_t N, int64_t H,
+                          int64_t W, int64_t C, int64_t OH, int64_t OW, int64_t k, int64_t s, int64_t p, int dt,
+                          ssseg_stream_t stream);
 /* dst[n][h+doy][w+dox][c] = src[n][h+soy][w+sox][c] for h<H, w<W, c<C (pixel strides sld/dld) */
 int ssseg_nhwc_copy(const void* src, void* dst, int64_t N, int64_t H, int64_t W, int64_t C, int64_t sH, int64_t sW,
                     int64_t sld, int64_t soy, int64_t sox, int64_t dH, int64_t dW, int64_t dld, int64_t doy, int64_t dox,

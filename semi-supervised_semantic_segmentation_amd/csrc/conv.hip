@@ -250,6 +250,19 @@ extern "C" int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const
                       e.stats, (int)e.stats_ld};
   if (g.KK == 0) {   // no taps reach this output phase: the contraction is zero
     if (e.stats) return SSSEG_EUNSUPPORTED;
+    const bool v8 = g.K % 8 == 0 && g.ldy % 8 == 0 && (!e.residual || e.ldr % 8 == 0);
+    if (v8 && dt_out == SSSEG_BF16) {
+      hipLaunchKernelGGL(phase_zero_vec_kernel<bf16_t>, dim3(ssseg_grid(g.M * (g.K / 8), 256)), dim3(256), 0, s,
+                         (bf16_t*)y, g, eb);
+      SSSEG_LAUNCH_CHECK();
+      return 0;
+    }
+    if (v8 && dt_out == SSSEG_F16) {
+      hipLaunchKernelGGL(phase_zero_vec_kernel<f16_t>, dim3(ssseg_grid(g.M * (g.K / 8), 256)), dim3(256), 0, s,
+                         (f16_t*)y, g, eh);
+      SSSEG_LAUNCH_CHECK();
+      return 0;
+    }
     if (dt_out == SSSEG_F32)
       hipLaunchKernelGGL(phase_zero_kernel<float>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, (float*)y, g, ef);
     else if (dt_out == SSSEG_F16)

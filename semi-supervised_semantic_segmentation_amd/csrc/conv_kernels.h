@@ -858,6 +858,34 @@ __global__ void splitk_finalize_kernel(const float* __restrict__ ws, TO* __restr
 }
 
 // output pixels of a phase whose tap set is empty (e.g. odd rows of a 1x1/s2 dgrad): epilogue of 0
+// 8 channels per thread (K % 8 == 0, 16-byte aligned rows): one 16-byte store per chunk
+template <typename TO>
+__global__ void phase_zero_vec_kernel(TO* y, ConvGeom g, Epi<TO> ep) {
+  const int kc = g.K >> 3;
+  const long long total = g.M * kc;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int n = (int)(i % kc) * 8;
+    const long long m = i / kc;
+    const int ox = (int)m % g.OW;    // 32-bit decode: geom_ok guarantees M < 2^31
+    const int q = (int)m / g.OW;
+    const int oy = q % g.OH, img = q / g.OH;
+    const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+    float r[8], v[8];
+    if (ep.res) Out8<TO>::ld(ep.res + op * ep.ldr + n, r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = ep.shift ? ep.shift[n + e] : 0.f;
+      if (ep.res) t += r[e];
+      v[e] = act_fwd(t, ep.relu, ep.slope);
+    }
+    if (ep.aux) {
+      const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      Out8<TO>::st(ep.aux + op * g.ldy + n, z);
+    }
+    Out8<TO>::st(y + op * g.ldy + n, v);
+  }
+}
+
 template <typename TO>
 __global__ void phase_zero_kernel(TO* y, ConvGeom g, Epi<TO> ep) {
   const long long total = g.M * g.K;

@@ -38,8 +38,8 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, u
 }
 
 template <typename T>
-__global__ void maxpool_bwd_kernel(const T* __restrict__ gy, const uint8_t* __restrict__ idx, T* __restrict__ gx, int N,
-                                   int H, int W, int C, int OH, int OW, int k, int s, int p) {
+__global__ void maxpool_bwd_kernel(const T* __restrict__ gy, const uint8_t* __restrict__ idx, const T* __restrict__ res,
+                                   T* __restrict__ gx, int N, int H, int W, int C, int OH, int OW, int k, int s, int p) {
   const int64_t total = (int64_t)N * H * W * C;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int c = (int)(i % C);
@@ -50,7 +50,7 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ gy, const uint8_t* __re
     const int n = (int)(q / H);
     const int oh0 = max(0, (ih + p - k + s) / s), oh1 = min(OH - 1, (ih + p) / s);
     const int ow0 = max(0, (iw + p - k + s) / s), ow1 = min(OW - 1, (iw + p) / s);
-    float acc = 0.f;
+    float acc = res ? io<T>::ld(res, i) : 0.f;
     for (int oh = oh0; oh <= oh1; ++oh) {
       const int kh = ih - (oh * s - p);
       if (kh < 0 || kh >= k) continue;
@@ -179,8 +179,9 @@ __global__ void maxpool_fwd_vec_kernel(const T* __restrict__ x, T* __restrict__ 
 }
 
 template <typename T>
-__global__ void maxpool_bwd_vec_kernel(const T* __restrict__ gy, const uint8_t* __restrict__ idx, T* __restrict__ gx,
-                                       int N, int H, int W, int C, int OH, int OW, int k, int s, int p) {
+__global__ void maxpool_bwd_vec_kernel(const T* __restrict__ gy, const uint8_t* __restrict__ idx,
+                                       const T* __restrict__ res, T* __restrict__ gx, int N, int H, int W, int C,
+                                       int OH, int OW, int k, int s, int p) {
   constexpr int V = VC<T>::V;
   const int CV = C / V;
   const int total = N * H * W * CV;
@@ -193,8 +194,11 @@ __global__ void maxpool_bwd_vec_kernel(const T* __restrict__ gy, const uint8_t* 
     const int oh0 = max(0, (ih + p - k + s) / s), oh1 = min(OH - 1, (ih + p) / s);
     const int ow0 = max(0, (iw + p - k + s) / s), ow1 = min(OW - 1, (iw + p) / s);
     float acc[V];
+    if (res)
+      VC<T>::ld(res + (int64_t)i * V, acc);   // the parked gradient of x (GradJoin), added in the same pass
+    else
 #pragma unroll
-    for (int e = 0; e < V; ++e) acc[e] = 0.f;
+      for (int e = 0; e < V; ++e) acc[e] = 0.f;
     for (int oh = oh0; oh <= oh1; ++oh) {
       const int kh = ih - (oh * s - p);
       if (kh < 0 || kh >= k) continue;
@@ -291,6 +295,12 @@ extern "C" int ssseg_maxpool_fwd(const void* x, void* y, uint8_t* idx, int64_t N
 extern "C" int ssseg_maxpool_bwd(const void* gy, const uint8_t* idx, void* gx, int64_t N, int64_t H, int64_t W,
                                  int64_t C, int64_t OH, int64_t OW, int64_t k, int64_t s, int64_t p, int dt,
                                  ssseg_stream_t stream) {
+  return ssseg_maxpool_bwd_res(gy, idx, nullptr, gx, N, H, W, C, OH, OW, k, s, p, dt, stream);
+}
+
+extern "C" int ssseg_maxpool_bwd_res(const void* gy, const uint8_t* idx, const void* res, void* gx, int64_t N, int64_t H,
+                                     int64_t W, int64_t C, int64_t OH, int64_t OW, int64_t k, int64_t s, int64_t p,
+                                     int dt, ssseg_stream_t stream) {
   if (!gy || !gx || !idx || k < 1 || s < 1 || p < 0) return SSSEG_EINVAL;
   const int64_t total = N * H * W * C;
   if (total == 0) return 0;
@@ -299,13 +309,13 @@ extern "C" int ssseg_maxpool_bwd(const void* gy, const uint8_t* idx, void* gx, i
   if (C % V == 0 && total / V < 0x7fffffffLL && N * OH * OW * C < 0x7fffffffLL * V) {
     const dim3 gv(ssseg_grid(total / V, 256, 1 << 20)), bv(256);
     if (dt == SSSEG_BF16)
-      hipLaunchKernelGGL(maxpool_bwd_vec_kernel<bf16_t>, gv, bv, 0, st, (const bf16_t*)gy, idx, (bf16_t*)gx, (int)N,
+      hipLaunchKernelGGL(maxpool_bwd_vec_kernel<bf16_t>, gv, bv, 0, st, (const bf16_t*)gy, idx, (const bf16_t*)res, (bf16_t*)gx, (int)N,
                          (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
     else if (dt == SSSEG_F16)
-      hipLaunchKernelGGL(maxpool_bwd_vec_kernel<f16_t>, gv, bv, 0, st, (const f16_t*)gy, idx, (f16_t*)gx, (int)N,
+      hipLaunchKernelGGL(maxpool_bwd_vec_kernel<f16_t>, gv, bv, 0, st, (const f16_t*)gy, idx, (const f16_t*)res, (f16_t*)gx, (int)N,
                          (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
     else if (dt == SSSEG_F32)
-      hipLaunchKernelGGL(maxpool_bwd_vec_kernel<float>, gv, bv, 0, st, (const float*)gy, idx, (float*)gx, (int)N,
+      hipLaunchKernelGGL(maxpool_bwd_vec_kernel<float>, gv, bv, 0, st, (const float*)gy, idx, (const float*)res, (float*)gx, (int)N,
                          (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
     else
       return SSSEG_EUNSUPPORTED;
@@ -314,13 +324,13 @@ extern "C" int ssseg_maxpool_bwd(const void* gy, const uint8_t* idx, void* gx, i
   }
   const dim3 g(ssseg_grid(total, 256, 256 * 16)), b(256);
   if (dt == SSSEG_BF16)
-    hipLaunchKernelGGL(maxpool_bwd_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)gy, idx, (bf16_t*)gx, (int)N, (int)H,
+    hipLaunchKernelGGL(maxpool_bwd_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)gy, idx, (const bf16_t*)res, (bf16_t*)gx, (int)N, (int)H,
                        (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
   else if (dt == SSSEG_F16)
-    hipLaunchKernelGGL(maxpool_bwd_kernel<f16_t>, g, b, 0, st, (const f16_t*)gy, idx, (f16_t*)gx, (int)N, (int)H,
+    hipLaunchKernelGGL(maxpool_bwd_kernel<f16_t>, g, b, 0, st, (const f16_t*)gy, idx, (const f16_t*)res, (f16_t*)gx, (int)N, (int)H,
                        (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
   else if (dt == SSSEG_F32)
-    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, g, b, 0, st, (const float*)gy, idx, (float*)gx, (int)N, (int)H,
+    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, g, b, 0, st, (const float*)gy, idx, (const float*)res, (float*)gx, (int)N, (int)H,
                        (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
   else
     return SSSEG_EUNSUPPORTED;

@@ -27,6 +27,8 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         if self.downsample is not None:
+            # x feeds conv1 and the projection shortcut: their input gradients meet in one dgrad epilogue
+            snn.mark_join(x)
             conv, bn = self.downsample
             shortcut = snn.conv_bn_act(conv, x, bn, relu=False)
         else:
@@ -75,8 +77,11 @@ class ResNetEncoder(nn.Module):
 
     def forward(self, x):
         outs = []
-        for ep in self.endpoints:
+        for i, ep in enumerate(self.endpoints):
             x = ep(x)
+            if i + 1 < len(self.endpoints):
+                # an endpoint feeds the next stage and (in the UNet) the decoder concat: one joined gradient
+                snn.mark_join(x)
             outs.append(x)
         return outs
 

@@ -90,6 +90,7 @@ SIGS = {
     # pooling / copies
     'ssseg_maxpool_fwd': (i32, [vp, vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, i32, vp]),
     'ssseg_maxpool_bwd': (i32, [vp, vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, i32, vp]),
+    'ssseg_maxpool_bwd_res': (i32, [vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, i32, vp]),
     'ssseg_nhwc_copy': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i32, vp]),
     'ssseg_zero': (i32, [vp, sz, vp]),
     'ssseg_act_bwd': (i32, [vp, vp, vp, i64, i32, f32, i32, vp]),

@@ -18,7 +18,13 @@ import torch.nn as nn
 
 from . import native as N
 
-_CFG = {'dtype': torch.bfloat16, 'sync_bn': True, 'fuse_stats': True}
+_CFG = {'grad_join': True, 'dtype': torch.bfloat16, 'sync_bn': True, 'fuse_stats': True}
+
+
+def set_grad_join(on):
+    """Fuse the input gradients of mark_join'ed activations into their consumers' kernels (default on); off:
+    autograd sums them (the separate add)."""
+    _CFG['grad_join'] = bool(on)
 
 
 def set_compute_dtype(dtype):
@@ -224,6 +230,67 @@ def _take(handoff):
     return handoff.take() if handoff is not None else None
 
 
+class GradJoin:
+    """One activation read by several native ops whose backwards all run: a UNet skip (the decoder concat and
+    the next encoder stage, unet.py:36-45), the input of a ResNet block with a projection shortcut (conv1 and
+    the downsample conv).  Autograd would sum the consumers' input gradients with one separate add per extra
+    consumer; instead every consumer's backward but the last parks its partial sum here and returns None, and
+    the next one adds the parked gradient inside its own output kernel (the dgrad epilogue's residual, the
+    max-pool backward's residual) -- whatever order autograd runs them in.  Opt-in per tensor (mark_join):
+    only where the model guarantees every registered consumer contributes to the loss."""
+    __slots__ = ('uses', 'left', 'pending')
+
+    def __init__(self):
+        self.uses, self.left, self.pending = 0, None, None
+
+
+def mark_join(x):
+    """Route the input gradients of x's native consumers through one GradJoin (call before the consumers)."""
+    if torch.is_grad_enabled() and isinstance(x, torch.Tensor) and x.requires_grad and _CFG['grad_join']:
+        if x.__dict__.get('_ssseg_join') is None:
+            x._ssseg_join = GradJoin()
+    return x
+
+
+def _join_fwd(x):
+    """forward of a consumer (outside Function.apply, where grad mode is live): one more use of x's join"""
+    j = x.__dict__.get('_ssseg_join') if isinstance(x, torch.Tensor) else None
+    if j is None or not torch.is_grad_enabled():
+        return None
+    j.uses += 1
+    return j
+
+
+def _join_take(j):
+    """backward of a consumer: (parked gradient to add or None, whether this consumer is the last)"""
+    if j is None:
+        return None, True
+    if j.left is None:
+        j.left = j.uses
+    j.left -= 1
+    p, j.pending = j.pending, None
+    last = j.left <= 0
+    if last:
+        j.left = None
+    return p, last
+
+
+def _join_give(j, last, g):
+    if j is None or last:
+        return g
+    j.pending = g
+    return None
+
+
+def _sum_pending(a, b):
+    """two pending input gradients (a GradHandoff's and a GradJoin's) for one fused residual: rare"""
+    if a is None:
+        return b
+    if b is None:
+        return a
+    return a + b
+
+
 class StatRows:
     """fp64 BatchNorm statistics partials written by a conv's epilogue (ssseg_conv_epilogue.stats): rows of
     (sum y, sum y^2) per output tile, appended launch by launch (a ConvTranspose2d writes one run per output
@@ -252,9 +319,9 @@ class StatRows:
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, mod, relu, handoff=None, stats=None):
+    def forward(ctx, x, weight, bias, mod, relu, handoff=None, stats=None, join=None):
         y = mod._ssseg_forward(x, relu, stats=stats)
-        ctx.mod, ctx.relu, ctx.handoff = mod, relu, handoff
+        ctx.mod, ctx.relu, ctx.handoff, ctx.join = mod, relu, handoff, join
         ctx.save_for_backward(x, y if _act(relu)[0] else None)
         return y
 
@@ -270,14 +337,22 @@ class _ConvFn(torch.autograd.Function):
                    N.stream())
             gy = gm
         mod._ssseg_wgrad(x, gy)
-        pending = _take(ctx.handoff)
+        joined, last = _join_take(ctx.join)
+        pending = _sum_pending(_take(ctx.handoff), joined)
         if not ctx.needs_input_grad[0]:
             dx = None
-        elif pending is not None:
-            dx = mod._ssseg_dgrad(gy, x.shape, residual=pending)
         else:
-            dx = mod._ssseg_dgrad(gy, x.shape)
-        return dx, None, None, None, None, None, None
+            dx = _dgrad_acc(mod, gy, x.shape, pending)
+        return _join_give(ctx.join, last, dx), None, None, None, None, None, None, None
+
+
+def _dgrad_acc(mod, gy, xshape, pending):
+    """dx (+ a pending gradient of x): fused as the dgrad epilogue's residual where the engine supports it"""
+    if pending is None:
+        return mod._ssseg_dgrad(gy, xshape)
+    if getattr(mod, '_ssseg_res_dgrad', lambda: False)():
+        return mod._ssseg_dgrad(gy, xshape, residual=pending)
+    return mod._ssseg_dgrad(gy, xshape) + pending
 
 
 def _bias_grad(mod, gy):
@@ -399,10 +474,13 @@ class Conv2d(nn.Conv2d, _ConvBase):
         return _desc(N=n, H=H, W=W, C=cin, ldx=cin, OH=OH, OW=OW, K=cout, R=R, S=S, sy=sh, sx=sw, dy=dh, dx=dw,
                      py=-ph, px=-pw, outH=OH, outW=OW, osy=1, osx=1, ooy=0, oox=0, ldy=cout, ldw=R * S * cin)
 
+    def _ssseg_res_dgrad(self):
+        return not self._ssseg_dw
+
     def forward(self, x, handoff=None, stats=None):
         if not _is_act(x):
             x = to_act(x)
-        return _ConvFn.apply(x, self.weight, self.bias, self, False, handoff, stats)
+        return _ConvFn.apply(x, self.weight, self.bias, self, False, handoff, stats, _join_fwd(x))
 
     def stat_rows_cap(self, n, H, W):
         """Upper bound of the statistics partial rows one forward writes (None: not fusable here)."""
@@ -420,7 +498,7 @@ class Conv2d(nn.Conv2d, _ConvBase):
         (discriminator.py:15-16 Conv + LeakyReLU(0.2))."""
         if not _is_act(x):
             x = to_act(x)
-        return _ConvFn.apply(x, self.weight, self.bias, self, act)
+        return _ConvFn.apply(x, self.weight, self.bias, self, act, None, None, _join_fwd(x))
 
     # ---- depthwise (groups == channels): ssseg_dwconv_* (MobileNetV2, mobilenetv2.py:58) ----
     def _dw_desc(self, n, H, W):
@@ -541,9 +619,8 @@ class Conv2d(nn.Conv2d, _ConvBase):
         dx = new_act(n, cin, H, W, _CFG['dtype'], gy.device)
         if residual is not None:
             _need_res(residual, dx)
-            if self._ssseg_dw or sh != 1 or sw != 1:
-                raise NotImplementedError('ssseg.nn.Conv2d: fused input-gradient accumulation needs a stride-1 '
-                                          'dense conv')
+            if self._ssseg_dw:
+                raise NotImplementedError('ssseg.nn.Conv2d: fused input-gradient accumulation needs a dense conv')
         if self._ssseg_dw:
             d = self._dw_desc(n, H, W)
             with _Timed(2.0 * n * OH * OW * self.in_channels * R * S, 'dgrad', _tag(self, n, H, W)):
@@ -571,7 +648,10 @@ class Conv2d(nn.Conv2d, _ConvBase):
                 d = _desc(N=n, H=OH, W=OW, C=cout, ldx=cout, OH=qy, OW=qx, K=cin, R=rr, S=ss, sy=1, sx=1, dy=-1,
                           dx=-1, py=dly, px=dlx, outH=H, outW=W, osy=sh, osx=sw, ooy=phy, oox=phx, ldy=cin,
                           ldw=max(rr * ss * cout, cout))
-                self._igemm(gy, w, dx, d, N.dt_code(dx))
+                # each phase adds the pending gradient at its own output pixels (the residual is indexed by
+                # the output pixel, so the phases together cover it exactly once)
+                self._igemm(gy, w, dx, d, N.dt_code(dx),
+                            fold=(None, None, residual, None) if residual is not None else None)
         timer.__exit__()
         return dx
 
@@ -595,7 +675,7 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
             raise NotImplementedError('ssseg.nn.ConvTranspose2d: output_size')
         if not _is_act(x):
             x = to_act(x)
-        return _ConvFn.apply(x, self.weight, self.bias, self, self._fuse_relu, None, stats)
+        return _ConvFn.apply(x, self.weight, self.bias, self, self._fuse_relu, None, stats, _join_fwd(x))
 
     def stat_rows_cap(self, n, H, W):
         (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
@@ -617,7 +697,7 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
     def forward_act(self, x, act):
         if not _is_act(x):
             x = to_act(x)
-        return _ConvFn.apply(x, self.weight, self.bias, self, act)
+        return _ConvFn.apply(x, self.weight, self.bias, self, act, None, None, _join_fwd(x))
 
     def _out_hw(self, H, W):
         (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
@@ -824,11 +904,11 @@ class _ConvBNEvalFn(torch.autograd.Function):
     (and the residual's) plus the BN parameter sums in one pass; then the ordinary conv backward."""
 
     @staticmethod
-    def forward(ctx, x, cweight, cbias, gamma, beta, residual, conv, bn, relu, grad_in=None, grad_out=None):
+    def forward(ctx, x, cweight, cbias, gamma, beta, residual, conv, bn, relu, grad_in=None, grad_out=None, join=None):
         y, aux, (scale, mean_eff, invstd) = conv._ssseg_forward(x, relu, bn=bn, residual=residual, keep_pre=True)
         ctx.save_for_backward(x, y, aux, scale, mean_eff, invstd)
         ctx.conv, ctx.bn, ctx.relu, ctx.has_res = conv, bn, relu, residual is not None
-        ctx.grad_in, ctx.grad_out = grad_in, grad_out
+        ctx.grad_in, ctx.grad_out, ctx.join = grad_in, grad_out, join
         return y
 
     @staticmethod
@@ -856,17 +936,16 @@ class _ConvBNEvalFn(torch.autograd.Function):
         if want(bn.weight) or want(bn.bias):
             _ready(*[p for p in (bn.weight, bn.bias) if want(p)])
         conv._ssseg_wgrad(x, dconv, bias_grad=False)
-        pending = _take(ctx.grad_in)
+        joined, last = _join_take(ctx.join)
+        pending = _sum_pending(_take(ctx.grad_in), joined)
         if not ctx.needs_input_grad[0]:
             dx = None
-        elif pending is not None:
-            dx = conv._ssseg_dgrad(dconv, x.shape, residual=pending)
         else:
-            dx = conv._ssseg_dgrad(dconv, x.shape)
+            dx = _dgrad_acc(conv, dconv, x.shape, pending)
         if dres is not None and ctx.grad_out is not None:
             ctx.grad_out.put(dres)
             dres = None
-        return dx, None, None, None, None, dres, None, None, None, None, None
+        return _join_give(ctx.join, last, dx), None, None, None, None, dres, None, None, None, None, None, None
 
 
 def conv_bn_act(conv, x, bn, relu=True, residual=None, grad_in=None, grad_out=None):
@@ -885,7 +964,7 @@ def conv_bn_act(conv, x, bn, relu=True, residual=None, grad_in=None, grad_out=No
         if _no_grad(x, conv.weight, conv.bias, bn.weight, bn.bias, residual):
             return conv._ssseg_forward(x, relu, bn=bn, residual=residual)
         return _ConvBNEvalFn.apply(x, conv.weight, conv.bias, bn.weight, bn.bias, residual, conv, bn, relu, grad_in,
-                                   grad_out)
+                                   grad_out, _join_fwd(x))
     stats = None
     if (_CFG['fuse_stats'] and isinstance(conv, (Conv2d, ConvTranspose2d)) and isinstance(bn, BatchNorm2d)
             and (bn.training or not bn.track_running_stats) and bn.num_features == conv.out_channels and x.dim() == 4):
@@ -913,8 +992,9 @@ def bn_act(x, bn, relu=True, residual=None, grad_out=None, pre=None):
 # ------------------------------------------------------------------------------------------------
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k, s, p, ceil_mode):
+    def forward(ctx, x, k, s, p, ceil_mode, join=None):
         n, c, h, w = x.shape
+        ctx.join = join
 
         def osz(L):
             o = (L + 2 * p - k + (s - 1 if ceil_mode else 0)) // s + 1
@@ -936,9 +1016,13 @@ class _MaxPoolFn(torch.autograd.Function):
         n, c, h, w, oh, ow, k, s, p, dt = ctx.meta
         _need_act(gy, c, 'MaxPool2d backward')
         gx = new_act(n, c, h, w, dt, gy.device)
-        N.call('ssseg_maxpool_bwd', N.dev_ptr(gy), N.dev_ptr(idx), N.dev_ptr(gx), n, h, w, c, oh, ow, k, s, p,
-               N.dt_code(gy), N.stream())
-        return gx, None, None, None, None
+        joined, last = _join_take(ctx.join)
+        if joined is not None:
+            _need_res(joined, gx)
+        # gx = gather of the selected taps' gradients (+ the parked gradient of x, in the same pass)
+        N.call('ssseg_maxpool_bwd_res', N.dev_ptr(gy), N.dev_ptr(idx), N.dev_ptr(joined) if joined is not None else None,
+               N.dev_ptr(gx), n, h, w, c, oh, ow, k, s, p, N.dt_code(gy), N.stream())
+        return _join_give(ctx.join, last, gx), None, None, None, None, None
 
 
 class MaxPool2d(nn.MaxPool2d):
@@ -950,7 +1034,7 @@ class MaxPool2d(nn.MaxPool2d):
         if self.dilation not in (1, (1, 1)) or self.return_indices:
             raise NotImplementedError('ssseg MaxPool2d: dilation / return_indices')
         _need_act(x, None, 'MaxPool2d')
-        return _MaxPoolFn.apply(x, k, s, p, bool(self.ceil_mode))
+        return _MaxPoolFn.apply(x, k, s, p, bool(self.ceil_mode), _join_fwd(x))
 
 
 class Upsample(nn.Upsample):
@@ -969,7 +1053,8 @@ class _CatFn(torch.autograd.Function):
     """torch.cat((a, b), 1) with a center-crop of whichever map is larger (unet.py:40-45)."""
 
     @staticmethod
-    def forward(ctx, a, b, ca, cb):
+    def forward(ctx, a, b, ca, cb, ja=None, jb=None):
+        ctx.joins = (ja, jb)
         n = a.shape[0]
         H, W = min(a.shape[2], b.shape[2]), min(a.shape[3], b.shape[3])
         v = vec()
@@ -989,19 +1074,22 @@ class _CatFn(torch.autograd.Function):
         ash, bsh, ca, cb, offs, H, W, cp = ctx.meta
         n = gy.shape[0]
         grads = []
-        for sh, c, c0, (oy, ox) in ((ash, ca, 0, offs[0]), (bsh, cb, ca, offs[1])):
+        for sh, c, c0, (oy, ox), j in ((ash, ca, 0, offs[0], ctx.joins[0]), (bsh, cb, ca, offs[1], ctx.joins[1])):
             cropped = (sh[2], sh[3]) != (H, W)
             g = new_act(n, sh[1], sh[2], sh[3], gy.dtype, gy.device, zero=cropped or sh[1] != c)
             N.call('ssseg_nhwc_copy', N.dev_ptr(gy) + c0 * gy.element_size(), N.dev_ptr(g), n, H, W, c, H, W, cp, 0,
                    0, sh[2], sh[3], sh[1], oy, ox, N.dt_code(gy), N.stream())
-            grads.append(g)
-        return grads[0], grads[1], None, None
+            joined, last = _join_take(j)
+            if joined is not None:   # the concat usually runs first (it is downstream): rare
+                g = g + joined
+            grads.append(_join_give(j, last, g))
+        return grads[0], grads[1], None, None, None, None
 
 
 def cat_crop(a, b, ca, cb):
     """Concatenate NHWC activations a (ca real channels) and b (cb) along channels; the larger map is
     center-cropped to the smaller (unet.py:40-45 compares dim 2; both dims are cropped to match here)."""
-    return _CatFn.apply(a, b, ca, cb)
+    return _CatFn.apply(a, b, ca, cb, _join_fwd(a), _join_fwd(b))
 
 
 @contextlib.contextmanager
