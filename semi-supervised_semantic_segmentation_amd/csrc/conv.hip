@@ -5,7 +5,7 @@
 
 #include "conv_kernels.h"
 
-int g_knobs[9] = {0, -1, 0, 0, 0, 1, 0, 0, 0};   // runtime variant switches (ssseg_set_knob)
+int g_knobs[9] = {0, -1, 0, 0, 0, 1, 0, 0, 0};   // split-K off: measured a net loss on the C2 step (r2u)   // runtime variant switches (ssseg_set_knob)
 
 // ------------------------------------------------------------------------------------------------
 // weight packing: dst[k][rr][ss][c] (c < Cp; zero for c >= Cd) from an fp32 source
@@ -69,24 +69,24 @@ namespace {
 // returns the tile height BM of the launched config (the fused BN statistics write ceil(M / BM) partial rows)
 template <typename TO>
 int launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep,
-                    unsigned xb, unsigned wb, hipStream_t s) {
+                    unsigned xb, unsigned wb, hipStream_t s, float* ws) {
   switch (cfg) {
-    case 1: return launch_glds_grp_a<TO>(cfg, x, w, y, g, ep, xb, wb, s);
-    case 2: return launch_glds_grp_a<TO>(cfg, x, w, y, g, ep, xb, wb, s);
-    case 3: return launch_glds_grp_a<TO>(cfg, x, w, y, g, ep, xb, wb, s);
-    case 4: return launch_glds_grp_d<TO>(cfg, x, w, y, g, ep, xb, wb, s);
-    case 5: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s);
-    case 6: return launch_glds_grp_d<TO>(cfg, x, w, y, g, ep, xb, wb, s);
-    case 7: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s);
-    case 8: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s);
-    case 9: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s);
-    case 12: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s);
-    case 13: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s);
-    case 14: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s);
-    case 15: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s);
-    case 16: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s);
-    case 17: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s);
-    default: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s);
+    case 1: return launch_glds_grp_a<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
+    case 2: return launch_glds_grp_a<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
+    case 3: return launch_glds_grp_a<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
+    case 4: return launch_glds_grp_d<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
+    case 5: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
+    case 6: return launch_glds_grp_d<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
+    case 7: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
+    case 8: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
+    case 9: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
+    case 12: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
+    case 13: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
+    case 14: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
+    case 15: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
+    case 16: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
+    case 17: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
+    default: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
   }
 }
 
@@ -95,6 +95,7 @@ int launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvGe
 // speed, never results (tests/test_hip_layers.py::test_conv_variants_bitwise).  Variant 0 is the
 // register-staged kernel, 1..10 and 12..17 the LDS-DMA configs.  With knob 5 on (default) an unseen geometry is
 // timed once over the candidates on the caller's stream (HIP events) and the fastest is cached.
+constexpr int kSplitBit = 256;   // cached choice flag: run the variant with its split-K plan
 constexpr int kCandidates[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 14, 15, 16, 17};
 std::unordered_map<unsigned long long, int> g_variant;
 std::mutex g_variant_mu;
@@ -116,16 +117,16 @@ static int heuristic_variant(const ConvGeom& g) {
 
 template <typename T, typename TO>
 int run_variant(int v, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                unsigned wb, hipStream_t s) {
+                unsigned wb, hipStream_t s, float* ws) {
   if constexpr (sizeof(TO) == 2) {
-    if (v != 0) return launch_glds_cfg<TO>(v, x, w, y, g, ep, xb, wb, s);
+    if (v != 0) return launch_glds_cfg<TO>(v, x, w, y, g, ep, xb, wb, s, ws);
   }
-  return dispatch_regstaged<T, TO>(x, w, y, g, ep, nullptr, s);
+  return dispatch_regstaged<T, TO>(x, w, y, g, ep, ws, s);
 }
 
 template <typename T, typename TO>
 int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                 unsigned wb, hipStream_t s) {
+                 unsigned wb, hipStream_t s, float* ws) {
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return heuristic_variant(g);
   hipEvent_t e0, e1;
@@ -141,20 +142,26 @@ int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const
   int len = log ? snprintf(line, sizeof line, "tune N%d %dx%d C%d -> %dx%d K%d %dx%d s%d d%d out%dx%d/%d ep%d%d:",
                            g.N, g.H, g.W, g.C, g.OH, g.OW, g.K, g.R, g.S, g.sy, g.dy, g.outH, g.outW, g.osy,
                            ep.scale ? 1 : 0, ep.aux ? 1 : 0) : 0;
-  for (int v : kCandidates) {
-    run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s);   // warm (code load, caches)
-    float ms = 1e30f;
-    for (int rep = 0; rep < 3; ++rep) {
-      (void)hipEventRecord(e0, s);
-      run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s);
-      (void)hipEventRecord(e1, s);
-      float t = 1e30f;
-      if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&t, e0, e1) == hipSuccess) ms = std::min(ms, t);
-    }
-    if (log && len > 0 && len < (int)sizeof line - 16) len += snprintf(line + len, sizeof line - len, " %d:%.0f", v, ms * 1e3f);
-    if (ms < best_ms) {
-      best_ms = ms;
-      best = v;
+  // every variant without split-K and, when a workspace allows it, with the split-K plan of its tile
+  // (choice encoded as variant | kSplitBit)
+  for (int split = 0; split < (ws ? 2 : 1); ++split) {
+    float* wsv = split ? ws : nullptr;
+    for (int v : kCandidates) {
+      run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, wsv);   // warm (code load, caches)
+      float ms = 1e30f;
+      for (int rep = 0; rep < 3; ++rep) {
+        (void)hipEventRecord(e0, s);
+        run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, wsv);
+        (void)hipEventRecord(e1, s);
+        float t = 1e30f;
+        if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&t, e0, e1) == hipSuccess) ms = std::min(ms, t);
+      }
+      if (log && len > 0 && len < (int)sizeof line - 24)
+        len += snprintf(line + len, sizeof line - len, " %d%s:%.0f", v, split ? "s" : "", ms * 1e3f);
+      if (ms < best_ms) {
+        best_ms = ms;
+        best = v | (split ? kSplitBit : 0);
+      }
     }
   }
   if (log) fprintf(stderr, "%s -> %d\n", line, best);
@@ -168,25 +175,28 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
                    hipStream_t s) {
   if constexpr (sizeof(T) == 2 && sizeof(TO) == 2) {
     const long long xb = (long long)g.N * g.H * g.W * g.ldx * 2, wb = (long long)g.K * g.ldw * 2;
-    if (sizeof(TO) == 2 && g_knobs[3] == 0 && !ws && g.C % 64 == 0 && g.ldx % 8 == 0 && g.ldw % 8 == 0 && g.ldw == g.KK &&
+    if (sizeof(TO) == 2 && g_knobs[3] == 0 && g.C % 64 == 0 && g.ldx % 8 == 0 && g.ldw % 8 == 0 && g.ldw == g.KK &&
         g.K > 16 && xb < 0x7fffffffLL && wb < 0x7fffffffLL) {
       int v = g_knobs[4];
       if (v < 0) v = 0;
       if (v == 0) {
         const unsigned long long key =
-            geom_key(g, (int)sizeof(TO) * 8 + (ep.stats ? 4 : 0) + (ep.res ? 2 : 0) + (ep.scale ? 1 : 0));
+            geom_key(g, (int)sizeof(TO) * 8 + (ws ? 8 : 0) + (ep.stats ? 4 : 0) + (ep.res ? 2 : 0) + (ep.scale ? 1 : 0));
         std::lock_guard<std::mutex> lk(g_variant_mu);
         auto it = g_variant.find(key);
         if (it != g_variant.end()) {
           v = it->second;
         } else {
-          v = g_knobs[5] ? tune_variant<T, TO>(x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s) : heuristic_variant(g);
+          v = g_knobs[5] ? tune_variant<T, TO>(x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, ws) : heuristic_variant(g);
           g_variant[key] = v;
         }
       } else if (g_knobs[4] == 11) {
         v = 0;   // forced register-staged
       }
-      return run_variant<T, TO>(v, x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s);
+      // split-K only where the autotuner measured it faster (its fp32 atomics reorder the sums); a variant
+      // forced by knob 4 runs unsplit, so forced variants stay bit-comparable
+      float* wsv = (g_knobs[4] == 0 && (v & kSplitBit)) ? ws : nullptr;
+      return run_variant<T, TO>(v & ~kSplitBit, x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, wsv);
     }
   }
   return dispatch_regstaged<T, TO>(x, w, y, g, ep, ws, s);

@@ -479,7 +479,8 @@ constexpr int ROWB = 80;   // 64 data bytes + 16 pad per LDS row
 // forward / dgrad / transposed-conv gather GEMM
 // ------------------------------------------------------------------------------------------------
 extern int g_knobs[9];   // runtime variant switches (ssseg_set_knob), defined in conv.hip
-// 0: reg-staged pipeline depth; 1: split-K cap (-1 off); 2: 64x64 small-M tiles (reg-staged path);
+// 0: reg-staged pipeline depth; 1: split-K cap (-1 off = default, 0 auto: the autotuner also times each variant with
+// its split plan, fp32-atomic partials + finalize, and keeps it where faster); 2: 64x64 small-M tiles (reg-staged path);
 // 3: bf16 LDS-DMA path (0 on, -1 off); 4: variant (0 auto, 1..10 / 12..17 LDS-DMA config, 11 register-staged);
 // 5: autotune unseen geometries (1 on, 0 = static heuristic); knob 6 = 1 clears the variant cache;
 // 7: LDS-staged coalesced epilogue in the LDS-DMA kernel (0 on, -1 off);
@@ -681,7 +682,8 @@ template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS, bool STAT
 __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __restrict__ x,
                                                                 const TO* __restrict__ w, TO* __restrict__ y,
                                                                 ConvGeom g, Epi<TO> ep, unsigned xbytes,
-                                                                unsigned wbytes, int g_epi_lds) {
+                                                                unsigned wbytes, int g_epi_lds, int splits,
+                                                                float* __restrict__ ws) {
   constexpr int ROW = 128;                       // bytes per LDS row = 64 bf16 of k
   constexpr int STAGE = (BM + BN) * ROW;
   constexpr int AI = BM / 8 / NW;                // A (pixel) wave-instructions per wave per stage
@@ -703,7 +705,11 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
   const int n0 = (tile % nnt) * BN;
   const int RS = g.R * g.S;
   const int cpt = g.C >> 6;                      // k-tiles per tap
-  const int nk = RS * cpt;
+  // split-K (low-tile layers, blockIdx.y = split): this block reduces k-tiles [kt0, kt1) in order
+  const int nk_all = RS * cpt;
+  const int kper = (nk_all + splits - 1) / splits;
+  const int kt0 = min(nk_all, (int)blockIdx.y * kper);
+  const int nk = min(nk_all, kt0 + kper) - kt0;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, (int)wbytes, 0x00020000);
 
@@ -751,8 +757,8 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
     }
   };
 
-  int ld_tap = 0, ld_c = 0, ld_kt = 0;   // k-tile being staged next: tap, channel block, index
-  set_tap(0);
+  int ld_tap = kt0 / cpt, ld_c = kt0 - (kt0 / cpt) * cpt, ld_kt = kt0;   // k-tile staged next: tap, block, index
+  set_tap(min(ld_tap, RS - 1));
   auto issue = [&](int buf) {
     char* As = smem + buf * STAGE;
     char* Bs = As + BM * ROW;
@@ -816,6 +822,21 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
       if (kt + D < nk) issue((kt + D) % NS);
       compute(kt % NS);
     }
+  }
+  if (splits > 1) {   // fp32 partials into ws[m][K] (zeroed by the host); splitk_finalize applies the epilogue
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      const long long m = m0 + wm * WTM + j * 16 + (lane & 15);
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        const int n = n0 + wn * WTN + i * 16 + (lane >> 4) * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (n + e < g.K) atomicAdd(ws + m * g.K + n + e, acc[i][j][e]);
+      }
+    }
+    return;
   }
   if constexpr (EPI <= SMEM) {
     if (g_epi_lds) {
@@ -904,17 +925,32 @@ __global__ void phase_zero_kernel(TO* y, ConvGeom g, Epi<TO> ep) {
   }
 }
 
+template <typename T, int BM, int BN>
+inline int plan_splits(const ConvGeom& g);
+
+template <typename TO>
+__global__ void splitk_finalize_kernel(const float* __restrict__ ws, TO* __restrict__ y, ConvGeom g, Epi<TO> ep);
+
 template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS>
 int launch_glds(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb, unsigned wb,
-                hipStream_t s) {
+                hipStream_t s, float* ws) {
   static_assert(sizeof(TO) == 2, "LDS-DMA configs: 16-bit activations in and out (fp32-output heads have K <= 16)");
   const long long tiles = ((g.M + BM - 1) / BM) * ((g.K + BN - 1) / BN);
-  if (ep.stats)
+  // split-K only with a workspace (never with fused statistics: the host passes none then)
+  const int sp = (ws && !ep.stats) ? plan_splits<TO, BM, BN>(g) : 1;
+  if (sp > 1) {
+    (void)hipMemsetAsync(ws, 0, sizeof(float) * g.M * g.K, s);
+    hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, false>), dim3((unsigned)tiles, (unsigned)sp),
+                       dim3(NW * 64), 0, s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, 0, sp, ws);
+    hipLaunchKernelGGL(splitk_finalize_kernel<TO>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, ws, (TO*)y, g,
+                       ep);
+  } else if (ep.stats) {
     hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, true>), dim3((unsigned)tiles), dim3(NW * 64), 0,
-                       s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, (int)(g_knobs[7] == 0));
-  else
+                       s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, (int)(g_knobs[7] == 0), 1, nullptr);
+  } else {
     hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, false>), dim3((unsigned)tiles), dim3(NW * 64), 0,
-                       s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, (int)(g_knobs[7] == 0));
+                       s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, (int)(g_knobs[7] == 0), 1, nullptr);
+  }
   return BM;
 }
 
@@ -923,16 +959,16 @@ int launch_glds(const void* x, const void* w, void* y, const ConvGeom& g, const 
 // Each returns the tile height BM of the launched config (the fused BN statistics write ceil(M/BM) rows).
 template <typename TO>
 int launch_glds_grp_a(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                      unsigned wb, hipStream_t s);
+                      unsigned wb, hipStream_t s, float* ws);
 template <typename TO>
 int launch_glds_grp_b(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                      unsigned wb, hipStream_t s);
+                      unsigned wb, hipStream_t s, float* ws);
 template <typename TO>
 int launch_glds_grp_d(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                      unsigned wb, hipStream_t s);
+                      unsigned wb, hipStream_t s, float* ws);
 template <typename TO>
 int launch_glds_grp_c(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                      unsigned wb, hipStream_t s);
+                      unsigned wb, hipStream_t s, float* ws);
 
 
 template <typename T, int BM, int BN>
