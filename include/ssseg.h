@@ -231,6 +231,14 @@ typedef struct ssseg_conv_epilogue {
 } ssseg_conv_epilogue;
 int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const ssseg_conv_desc* desc_host, int dt, int dt_out,
                          const ssseg_conv_epilogue* epi, void* ws, size_t ws_bytes, ssseg_stream_t stream);
+/* First conv of an encoder on a 3-channel image (<= 4 real input channels, S <= 8 taps per filter row, R in {3, 7},
+ * dilation 1, stride x <= 2, OW % 128 == 0; e.g. the ResNet-50 stem 7x7/s2/p3): k = (s, c) of one filter row per
+ * 32-deep MFMA step, operands from the block's image patch (channels 0..3 of each pixel; ldx % 4 == 0).  w4 = ssseg_weight_pack output
+ * with Cp = 4, layout 0, full taps: [K][R][S][4].  K % 16 == 0; dt = SSSEG_BF16 or SSSEG_F16 (output dtype = dt).
+ * Same epilogue contract as ssseg_conv_igemm_epi (fused BN statistics rows: ceil(M / 128)).  Replaces the
+ * engine launch of the stem in Conv2d forward (reference: the encoders' first conv, e.g. SURVEY §0.4 ResNet-50). */
+int ssseg_conv_stem_epi(const void* x, const void* w4, void* y, const ssseg_conv_desc* desc_host, int dt,
+                        const ssseg_conv_epilogue* epi, ssseg_stream_t stream);
 /* Workspace for ssseg_conv_igemm: non-zero when the launch splits K across workgroups (few output tiles,
  * long contraction: fp32 partials [M][K] + a finalize pass).  Passing no workspace disables the split. */
 size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* desc_host, int dt);

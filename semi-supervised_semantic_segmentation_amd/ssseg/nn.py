@@ -18,7 +18,12 @@ import torch.nn as nn
 
 from . import native as N
 
-_CFG = {'grad_join': True, 'dtype': torch.bfloat16, 'sync_bn': True, 'fuse_stats': True}
+_CFG = {'grad_join': True, 'stem': True, 'dtype': torch.bfloat16, 'sync_bn': True, 'fuse_stats': True}
+
+
+def set_stem_kernel(on):
+    """Route image-input convs to ssseg_conv_stem_epi (default on); off: the generic engine."""
+    _CFG['stem'] = bool(on)
 
 
 def set_grad_join(on):
@@ -400,12 +405,13 @@ class _ConvBase:
             _PACK_EPOCH[0] += 1
         return t
 
-    def _igemm(self, x, w, y, desc, out_dt, bias=None, relu=False, fold=None, stats=None):
+    def _igemm(self, x, w, y, desc, out_dt, bias=None, relu=False, fold=None, stats=None, stem=False):
         """One engine launch; epilogue y = act(acc*scale + shift + residual) with shift = bias, or
         fold = (scale, shift, residual, aux) from a folded eval BatchNorm (conv_bn_act); aux, when given,
-        receives the raw accumulator (the pre-BN activation the differentiated eval pass needs)."""
+        receives the raw accumulator (the pre-BN activation the differentiated eval pass needs).
+        stem: the image-input kernel (ssseg_conv_stem_epi, w = the Cp-4 pack)."""
         dref = ctypes_ref(desc)
-        nb = N.lib().ssseg_conv_igemm_workspace_bytes(dref, N.dt_code(x)) if w is not None else 0
+        nb = N.lib().ssseg_conv_igemm_workspace_bytes(dref, N.dt_code(x)) if (w is not None and not stem) else 0
         ws = N.workspace(nb, x.device) if nb else None
         scale, shift, res, aux = fold if fold is not None else (None, bias, None, None)
         sf = stats.launch_fields() if stats is not None else (None, 0, None)
@@ -413,8 +419,12 @@ class _ConvBase:
                             N.dev_ptr(shift) if shift is not None else None,
                             N.dev_ptr(res) if res is not None else None, res.shape[1] if res is not None else 0,
                             N.dev_ptr(aux) if aux is not None else None, *_act(relu), *sf)
-        N.call('ssseg_conv_igemm_epi', N.dev_ptr(x), N.dev_ptr(w) if w is not None else None, N.dev_ptr(y), dref,
-               N.dt_code(x), out_dt, ctypes_ref(ep), N.dev_ptr(ws) if ws is not None else None, nb, N.stream())
+        if stem:
+            N.call('ssseg_conv_stem_epi', N.dev_ptr(x), N.dev_ptr(w), N.dev_ptr(y), dref, N.dt_code(x),
+                   ctypes_ref(ep), N.stream())
+        else:
+            N.call('ssseg_conv_igemm_epi', N.dev_ptr(x), N.dev_ptr(w) if w is not None else None, N.dev_ptr(y), dref,
+                   N.dt_code(x), out_dt, ctypes_ref(ep), N.dev_ptr(ws) if ws is not None else None, nb, N.stream())
         if stats is not None:
             stats.commit()
 
@@ -545,7 +555,11 @@ class Conv2d(nn.Conv2d, _ConvBase):
         n, _, H, W = x.shape
         d = self._fwd_desc(n, H, W)
         R, S = self.kernel_size
-        w = self._pack('fwd', cout, self.out_channels, self.in_channels, cin, 0, 0, 1, R, 0, 1, S)
+        stem = self._stem_ok(cout, d.OW)
+        if stem:   # image-input kernel: weights [K][R][S][4]
+            w = self._pack('stem', cout, self.out_channels, self.in_channels, 4, 0, 0, 1, R, 0, 1, S)
+        else:
+            w = self._pack('fwd', cout, self.out_channels, self.in_channels, cin, 0, 0, 1, R, 0, 1, S)
         fl = _conv_flops(n, d.OH, d.OW, self.out_channels, self.in_channels, R, S)
         tg = _tag(self, n, H, W)
         if bn is not None:
@@ -554,7 +568,7 @@ class Conv2d(nn.Conv2d, _ConvBase):
             aux = torch.empty_like(y) if keep_pre else None
             fold, bwd = self._fold(bn, residual, cout, aux)
             with _Timed(fl, 'fwd', tg):
-                self._igemm(x, w, y, d, N.dt_code(y), relu=relu, fold=fold)
+                self._igemm(x, w, y, d, N.dt_code(y), relu=relu, fold=fold, stem=stem)
             return (y, aux, bwd) if keep_pre else y
         if self._ssseg_head:
             y = torch.empty((n, cout, d.OH, d.OW), dtype=torch.float32, device=x.device,
@@ -564,8 +578,17 @@ class Conv2d(nn.Conv2d, _ConvBase):
             return y[:, :self.out_channels]
         y = new_act(n, cout, d.OH, d.OW, _CFG['dtype'], x.device)
         with _Timed(fl, 'fwd', tg):
-            self._igemm(x, w, y, d, N.dt_code(y), self.bias, relu, stats=stats)
+            self._igemm(x, w, y, d, N.dt_code(y), self.bias, relu, stats=stats, stem=stem)
         return y
+
+    def _stem_ok(self, cout, ow=None):
+        """The image-input conv kernel (ssseg_conv_stem_epi) covers this layer: <= 4 input channels, R in {3, 7},
+        S <= 8, dilation 1, stride <= 2, output width % 128 == 0, 16-bit compute, Cout % 16 == 0 (the ResNet /
+        DeepLab 7x7 stems, 3x3 image convs)."""
+        R, S = self.kernel_size
+        return (_CFG['stem'] and not self._ssseg_head and not self._ssseg_dw and self.in_channels <= 4
+                and R in (3, 7) and S <= 8 and self.dilation == (1, 1) and self.stride[1] <= 2 and cout % 16 == 0
+                and _CFG['dtype'] in (torch.bfloat16, torch.float16) and ow is not None and ow % 128 == 0)
 
     def _grad_in(self, gy):
         """Incoming output gradient -> physical NHWC compute-dtype tensor."""

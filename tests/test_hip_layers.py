@@ -554,3 +554,54 @@ def test_fused_bn_stats_match_separate_pass(hip_device, mode, kind, cin, cout, k
         N.call('ssseg_set_knob', 7, 0)
         snn.set_fused_bn_stats(True)
 
+
+
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("k,s,H,W", [(7, 2, 38, 256), (3, 2, 33, 512), (7, 1, 17, 128)])
+def test_stem_conv_kernel(hip_device, dtype, k, s, H, W):
+    """Image-input conv kernel (ssseg_conv_stem_epi: k = (s, c) of one filter row per MFMA step, operands
+    straight from the image) vs the generic engine on the same layer: plain forward, training BatchNorm with
+    fused statistics, eval BatchNorm folded with the raw accumulator kept (the differentiated consistency
+    pass) and its gradients; both within fp32 rounding of each other (different k grouping), and the forward
+    within the 16-bit tolerance of a PyTorch fp32 reference."""
+    from ssseg import nn as snn
+    snn.set_compute_dtype(dtype)
+    tol = 1e-3
+    try:
+        torch.manual_seed(4)
+        conv = snn.Conv2d(3, 64, k, s, k // 2, bias=False).to(hip_device)
+        bn = snn.BatchNorm2d(64).to(hip_device)
+        with torch.no_grad():
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.2, 0.2)
+        x = torch.rand(2, 3, H, W)
+        xa = _act_in(x, hip_device)
+        outs = {}
+        for stem in (False, True):
+            snn.set_stem_kernel(stem)
+            with torch.no_grad():
+                y0 = conv(xa)
+                bn.train()
+                bn.reset_running_stats()
+                y1 = snn.conv_bn_act(conv, xa, bn, relu=True)
+                rm = bn.running_mean.clone()
+                bn.eval()
+            xg = xa.detach().clone().requires_grad_(False)
+            conv.weight.grad = None
+            y2 = snn.conv_bn_act(conv, xg, bn, relu=True)
+            y2.backward(torch.ones_like(y2))
+            torch.cuda.synchronize()
+            outs[stem] = [t.detach().float().cpu().clone() for t in (y0, y1, rm, y2, conv.weight.grad)]
+        for name, a, b in zip(('conv', 'train-bn', 'running_mean', 'eval-bn', 'dW'), outs[False], outs[True]):
+            err = float((a - b).abs().max()) / (float(a.abs().max()) + 1e-6)
+            # same 16-bit inputs and weights, fp32 accumulation in a different k order: outputs differ by at most
+            # one 16-bit rounding step where a sum falls near a rounding boundary
+            assert err <= (1e-2 if dtype == torch.bfloat16 else 2e-3), (name, err)
+        ref = F.conv2d(_q(x, 'bf16' if dtype == torch.bfloat16 else 'f16'),
+                       _q(conv.weight.detach().cpu(), 'bf16' if dtype == torch.bfloat16 else 'f16'), stride=s,
+                       padding=k // 2)
+        _close(outs[True][0][:, :64], ref, 'bf16' if dtype == torch.bfloat16 else 'f16', 'stem y')
+    finally:
+        snn.set_stem_kernel(True)
+        snn.set_compute_dtype(torch.bfloat16)
+    del tol

@@ -13,7 +13,31 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, 'semi-supervised_semantic_segmentation_amd')]
 
+import re  # noqa: E402
+
 import torch  # noqa: E402
+
+TAG = re.compile(r'(Conv2d|ConvTranspose2d) (\d+)->(\d+) k(\d+) s(\d+) @(\d+)x(\d+)x(\d+)')
+
+
+def algorithmic_bytes(kind, tag):
+    """Bytes a conv launch must move at minimum (bf16 activations and packed weights read once, outputs
+    written once; wgrad writes the fp32 OIHW gradient): fwd x + W -> y; dgrad dy + W -> dx; wgrad x + dy -> dW.
+    None when the tag is not a plain conv (heads etc. are counted by flops only)."""
+    m = TAG.match(tag)
+    if not m:
+        return None
+    typ, cin, cout, k, s, n, h, w = m.group(1), *map(int, m.groups()[1:])
+    if typ == 'ConvTranspose2d':
+        oh, ow = h * s, w * s
+    else:
+        oh, ow = -(-h // s), -(-w // s)
+    x, y, wt = n * h * w * cin * 2, n * oh * ow * cout * 2, cout * cin * k * k * 2
+    if kind == 'fwd':
+        return x + wt + y
+    if kind == 'dgrad':
+        return y + wt + x
+    return x + y + cout * cin * k * k * 4
 
 
 def main():
@@ -40,7 +64,7 @@ def main():
     train.train_step(model, teacher, opt, img, mask, ua, ub, 30, 3, cfg)
     snn.probe(False)
     torch.cuda.synchronize()
-    agg = collections.defaultdict(lambda: [0.0, 0.0, 0])
+    agg = collections.defaultdict(lambda: [0.0, 0.0, 0, 0])
     by_kind = collections.defaultdict(lambda: [0.0, 0.0])
     for e0, e1, fl, kind, tag in rows:
         ms = e0.elapsed_time(e1)
@@ -48,16 +72,20 @@ def main():
         r[0] += ms
         r[1] += fl
         r[2] += 1
+        r[3] += algorithmic_bytes(kind, tag) or 0
         by_kind[kind][0] += ms
         by_kind[kind][1] += fl
     tot_ms = sum(v[0] for v in agg.values())
     tot_fl = sum(v[1] for v in agg.values())
-    print(f'conv engine: {tot_ms:.3f} ms, {tot_fl / 1e9:.1f} GFLOP, {tot_fl / tot_ms / 1e9:.1f} TF/s, {len(rows)} calls')
+    tot_b = sum(v[3] for v in agg.values())
+    print(f'conv engine: {tot_ms:.3f} ms, {tot_fl / 1e9:.1f} GFLOP, {tot_fl / tot_ms / 1e9:.1f} TF/s, {len(rows)} calls, '
+          f'algorithmic bytes {tot_b / 1e9:.2f} GB ({tot_b / tot_ms / 1e9:.2f} TB/s over the conv time)')
     for k, (ms, fl) in sorted(by_kind.items(), key=lambda kv: -kv[1][0]):
         print(f'  {k:6s} {ms:8.3f} ms  {fl / 1e9:8.1f} GFLOP  {fl / ms / 1e9:7.1f} TF/s')
-    print(f'{"ms":>8s} {"pct":>6s} {"calls":>5s} {"GFLOP":>8s} {"TF/s":>7s}  kind   layer')
-    for (kind, tag), (ms, fl, n) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:a.top]:
-        print(f'{ms:8.3f} {100 * ms / tot_ms:6.2f} {n:5d} {fl / 1e9:8.1f} {fl / ms / 1e9:7.1f}  {kind:6s} {tag}')
+    print(f'{"ms":>8s} {"pct":>6s} {"calls":>5s} {"GFLOP":>8s} {"TF/s":>7s} {"alg MB":>8s} {"TB/s":>6s}  kind   layer')
+    for (kind, tag), (ms, fl, n, by) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:a.top]:
+        print(f'{ms:8.3f} {100 * ms / tot_ms:6.2f} {n:5d} {fl / 1e9:8.1f} {fl / ms / 1e9:7.1f} {by / 1e6:8.1f} '
+              f'{by / ms / 1e9:6.2f}  {kind:6s} {tag}')
 
 
 if __name__ == '__main__':
