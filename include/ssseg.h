@@ -231,6 +231,16 @@ typedef struct ssseg_conv_epilogue {
 } ssseg_conv_epilogue;
 int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const ssseg_conv_desc* desc_host, int dt, int dt_out,
                          const ssseg_conv_epilogue* epi, void* ws, size_t ws_bytes, ssseg_stream_t stream);
+/* The output phases of a transposed conv in ONE launch (ConvTranspose2d(4,2,1): four 2x2-tap phases over the same
+ * input; on 16x16..32x32 inputs a single phase has too few tiles to fill 256 CUs).  desc describes a phase's GEMM
+ * (every phase: same K, taps R x S, weight stride ldw, output sub-grid OH x OW); phase_geom[4*p .. 4*p+3] =
+ * (py, px, ooy, oox) of phase p, w[p] its packed weights.  1 <= nphase <= 4; dt = dt_out = SSSEG_BF16 / SSSEG_F16.
+ * Same epilogue contract as ssseg_conv_igemm_epi; fused statistics rows: phase-major, nphase x ceil(M / BM).
+ * Replaces the per-phase loop of nn.ConvTranspose2d forward (unet.py:21, train_upsampling=True). */
+int ssseg_conv_igemm_phases(const void* x, void* y, const ssseg_conv_desc* desc_host, int dt, int dt_out,
+                            const ssseg_conv_epilogue* epi, int64_t nphase, const int64_t* phase_geom,
+                            const void* const* w, ssseg_stream_t stream);
+
 /* First conv of an encoder on a 3-channel image (<= 4 real input channels, S <= 8 taps per filter row, R in {3, 7},
  * dilation 1, stride x <= 2, OW % 128 == 0; e.g. the ResNet-50 stem 7x7/s2/p3): k = (s, c) of one filter row per
  * 32-deep MFMA step, operands from the block's image patch (channels 0..3 of each pixel; ldx % 4 == 0).  w4 = ssseg_weight_pack output

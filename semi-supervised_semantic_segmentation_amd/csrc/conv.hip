@@ -69,24 +69,24 @@ namespace {
 // returns the tile height BM of the launched config (the fused BN statistics write ceil(M / BM) partial rows)
 template <typename TO>
 int launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep,
-                    unsigned xb, unsigned wb, hipStream_t s, float* ws) {
+                    unsigned xb, unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph) {
   switch (cfg) {
-    case 1: return launch_glds_grp_a<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
-    case 2: return launch_glds_grp_a<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
-    case 3: return launch_glds_grp_a<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
-    case 4: return launch_glds_grp_d<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
-    case 5: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
-    case 6: return launch_glds_grp_d<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
-    case 7: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
-    case 8: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
-    case 9: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
-    case 12: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
-    case 13: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
-    case 14: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
-    case 15: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
-    case 16: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
-    case 17: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
-    default: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws);
+    case 1: return launch_glds_grp_a<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 2: return launch_glds_grp_a<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 3: return launch_glds_grp_a<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 4: return launch_glds_grp_d<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 5: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 6: return launch_glds_grp_d<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 7: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 8: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 9: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 12: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 13: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 14: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 15: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 16: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 17: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
+    default: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
   }
 }
 
@@ -117,16 +117,33 @@ static int heuristic_variant(const ConvGeom& g) {
 
 template <typename T, typename TO>
 int run_variant(int v, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                unsigned wb, hipStream_t s, float* ws) {
+                unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph = nullptr) {
   if constexpr (sizeof(TO) == 2) {
-    if (v != 0) return launch_glds_cfg<TO>(v, x, w, y, g, ep, xb, wb, s, ws);
+    if (v != 0) return launch_glds_cfg<TO>(v, x, w, y, g, ep, xb, wb, s, ws, ph);
+  }
+  if (ph && ph->n > 1) {   // register-staged kernel: one launch per phase
+    int bm = 0;
+    long long rows = 0;
+    for (int p = 0; p < ph->n; ++p) {
+      ConvGeom gp = g;
+      gp.py = ph->py[p];
+      gp.px = ph->px[p];
+      gp.ooy = ph->ooy[p];
+      gp.oox = ph->oox[p];
+      Epi<TO> ep2 = ep;
+      if (ep.stats) ep2.stats = ep.stats + rows * 2 * ep.sld;
+      bm = dispatch_regstaged<T, TO>(x, ph->w[p], y, gp, ep2, ws, s);
+      if (bm <= 0) return bm;
+      rows += (g.M + bm - 1) / bm;
+    }
+    return bm;
   }
   return dispatch_regstaged<T, TO>(x, w, y, g, ep, ws, s);
 }
 
 template <typename T, typename TO>
 int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                 unsigned wb, hipStream_t s, float* ws) {
+                 unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph) {
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return heuristic_variant(g);
   hipEvent_t e0, e1;
@@ -147,11 +164,11 @@ int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const
   for (int split = 0; split < (ws ? 2 : 1); ++split) {
     float* wsv = split ? ws : nullptr;
     for (int v : kCandidates) {
-      run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, wsv);   // warm (code load, caches)
+      run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, ph ? nullptr : wsv, ph);   // warm (code load, caches)
       float ms = 1e30f;
       for (int rep = 0; rep < 3; ++rep) {
         (void)hipEventRecord(e0, s);
-        run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, wsv);
+        run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, ph ? nullptr : wsv, ph);
         (void)hipEventRecord(e1, s);
         float t = 1e30f;
         if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&t, e0, e1) == hipSuccess) ms = std::min(ms, t);
@@ -172,7 +189,7 @@ int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const
 
 template <typename T, typename TO>
 int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, float* ws,
-                   hipStream_t s) {
+                   hipStream_t s, const PhaseTab* ph = nullptr) {
   if constexpr (sizeof(T) == 2 && sizeof(TO) == 2) {
     const long long xb = (long long)g.N * g.H * g.W * g.ldx * 2, wb = (long long)g.K * g.ldw * 2;
     if (sizeof(TO) == 2 && g_knobs[3] == 0 && g.C % 64 == 0 && g.ldx % 8 == 0 && g.ldw % 8 == 0 && g.ldw == g.KK &&
@@ -181,13 +198,15 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
       if (v < 0) v = 0;
       if (v == 0) {
         const unsigned long long key =
-            geom_key(g, (int)sizeof(TO) * 8 + (ws ? 8 : 0) + (ep.stats ? 4 : 0) + (ep.res ? 2 : 0) + (ep.scale ? 1 : 0));
+            geom_key(g, (int)sizeof(TO) * 8 + (ws ? 8 : 0) + (ep.stats ? 4 : 0) + (ep.res ? 2 : 0) + (ep.scale ? 1 : 0) +
+                        64 * (ph ? ph->n : 1));
         std::lock_guard<std::mutex> lk(g_variant_mu);
         auto it = g_variant.find(key);
         if (it != g_variant.end()) {
           v = it->second;
         } else {
-          v = g_knobs[5] ? tune_variant<T, TO>(x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, ws) : heuristic_variant(g);
+          v = g_knobs[5] ? tune_variant<T, TO>(x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, ws, ph)
+                         : heuristic_variant(g);
           g_variant[key] = v;
         }
       } else if (g_knobs[4] == 11) {
@@ -196,10 +215,10 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
       // split-K only where the autotuner measured it faster (its fp32 atomics reorder the sums); a variant
       // forced by knob 4 runs unsplit, so forced variants stay bit-comparable
       float* wsv = (g_knobs[4] == 0 && (v & kSplitBit)) ? ws : nullptr;
-      return run_variant<T, TO>(v & ~kSplitBit, x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, wsv);
+      return run_variant<T, TO>(v & ~kSplitBit, x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, ph ? nullptr : wsv, ph);
     }
   }
-  return dispatch_regstaged<T, TO>(x, w, y, g, ep, ws, s);
+  return run_variant<T, TO>(0, x, w, y, g, ep, 0, 0, s, ph ? nullptr : ws, ph);
 }
 
 bool geom_ok(const ConvGeom& g, int dt) {
@@ -353,6 +372,52 @@ extern "C" int ssseg_weight_pack(const float* src, void* dst, int64_t Kd, int64_
                        (int)s0, (int)sstep, (int)Sn);
   else
     return SSSEG_EUNSUPPORTED;
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_conv_igemm_phases(const void* x, void* y, const ssseg_conv_desc* d, int dt, int dt_out,
+                                       const ssseg_conv_epilogue* epi, int64_t nphase, const int64_t* phase_geom,
+                                       const void* const* w, ssseg_stream_t stream) {
+  ConvGeom g;
+  if (!make_geom(d, g) || !x || !y || !w || !phase_geom || nphase < 1 || nphase > 4) return SSSEG_EINVAL;
+  if (!geom_ok(g, dt) || g.KK == 0 || dt != dt_out || (dt != SSSEG_BF16 && dt != SSSEG_F16)) return SSSEG_EINVAL;
+  const ssseg_conv_epilogue none = {nullptr, nullptr, nullptr, 0, nullptr, 0, 0.f, nullptr, 0, nullptr};
+  const ssseg_conv_epilogue& e = epi ? *epi : none;
+  if (e.residual && (e.ldr < g.K || e.ldr > 0x7fffffff)) return SSSEG_EINVAL;
+  if (e.stats && (!e.stats_rows_host || e.stats_ld < 1 || e.stats_ld > g.K)) return SSSEG_EINVAL;
+  if (e.stats && (e.scale || e.residual || e.relu || e.aux)) return SSSEG_EINVAL;
+  if (e.relu < 0 || e.relu > SSSEG_ACT_LEAKY) return SSSEG_EINVAL;
+  if (e.stats_rows_host) *e.stats_rows_host = 0;
+  PhaseTab ph{(int)nphase, {0}, {0}, {0}, {0}, {nullptr}};
+  for (int p = 0; p < (int)nphase; ++p) {
+    const int64_t* q = phase_geom + 4 * p;
+    for (int k = 0; k < 4; ++k)
+      if (q[k] < -0x40000000LL || q[k] > 0x40000000LL) return SSSEG_EINVAL;
+    if (!w[p]) return SSSEG_EINVAL;
+    ph.py[p] = (int)q[0];
+    ph.px[p] = (int)q[1];
+    ph.ooy[p] = (int)q[2];
+    ph.oox[p] = (int)q[3];
+    ph.w[p] = w[p];
+  }
+  g.py = ph.py[0];
+  g.px = ph.px[0];
+  g.ooy = ph.ooy[0];
+  g.oox = ph.oox[0];
+  hipStream_t s = (hipStream_t)stream;
+  int bm;
+  if (dt == SSSEG_BF16) {
+    const Epi<bf16_t> eb{e.scale, e.shift, (const bf16_t*)e.residual, (int)e.ldr, e.relu, (bf16_t*)e.aux, e.slope,
+                         e.stats, (int)e.stats_ld};
+    bm = dispatch_igemm<bf16_t, bf16_t>(x, w[0], y, g, eb, nullptr, s, &ph);
+  } else {
+    const Epi<f16_t> eh{e.scale, e.shift, (const f16_t*)e.residual, (int)e.ldr, e.relu, (f16_t*)e.aux, e.slope,
+                        e.stats, (int)e.stats_ld};
+    bm = dispatch_igemm<f16_t, f16_t>(x, w[0], y, g, eh, nullptr, s, &ph);
+  }
+  if (bm <= 0) return SSSEG_EUNSUPPORTED;
+  if (e.stats_rows_host && e.stats) *e.stats_rows_host = nphase * ((g.M + bm - 1) / bm);
   SSSEG_LAUNCH_CHECK();
   return 0;
 }

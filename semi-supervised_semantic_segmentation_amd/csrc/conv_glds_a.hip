@@ -3,16 +3,16 @@
 
 template <typename TO>
 int launch_glds_grp_a(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                      unsigned wb, hipStream_t s, float* ws) {
+                      unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph) {
   switch (cfg) {
-    case 1: return launch_glds<TO, 256, 128, 2, 2, 4, 3>(x, w, y, g, ep, xb, wb, s, ws);
-    case 2: return launch_glds<TO, 256, 64, 4, 1, 4, 3>(x, w, y, g, ep, xb, wb, s, ws);
-    case 3: return launch_glds<TO, 128, 128, 2, 2, 4, 3>(x, w, y, g, ep, xb, wb, s, ws);
+    case 1: return launch_glds<TO, 256, 128, 2, 2, 4, 3>(x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 2: return launch_glds<TO, 256, 64, 4, 1, 4, 3>(x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 3: return launch_glds<TO, 128, 128, 2, 2, 4, 3>(x, w, y, g, ep, xb, wb, s, ws, ph);
     default: return -1;
   }
 }
 
 template int launch_glds_grp_a<bf16_t>(int, const void*, const void*, void*, const ConvGeom&, const Epi<bf16_t>&,
-                                        unsigned, unsigned, hipStream_t, float*);
+                                        unsigned, unsigned, hipStream_t, float*, const PhaseTab*);
 template int launch_glds_grp_a<f16_t>(int, const void*, const void*, void*, const ConvGeom&, const Epi<f16_t>&,
-                                       unsigned, unsigned, hipStream_t, float*);
+                                       unsigned, unsigned, hipStream_t, float*, const PhaseTab*);

@@ -3,18 +3,18 @@
 
 template <typename TO>
 int launch_glds_grp_c(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                      unsigned wb, hipStream_t s, float* ws) {
+                      unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph) {
   switch (cfg) {
-    case 13: return launch_glds<TO, 256, 64, 4, 1, 4, 2>(x, w, y, g, ep, xb, wb, s, ws);
-    case 14: return launch_glds<TO, 128, 64, 2, 2, 4, 2>(x, w, y, g, ep, xb, wb, s, ws);
-    case 15: return launch_glds<TO, 128, 64, 2, 2, 4, 1>(x, w, y, g, ep, xb, wb, s, ws);
-    case 16: return launch_glds<TO, 64, 64, 2, 2, 4, 1>(x, w, y, g, ep, xb, wb, s, ws);
-    case 17: return launch_glds<TO, 64, 64, 2, 2, 4, 2>(x, w, y, g, ep, xb, wb, s, ws);
-    default: return launch_glds<TO, 64, 64, 2, 2, 4, 4>(x, w, y, g, ep, xb, wb, s, ws);
+    case 13: return launch_glds<TO, 256, 64, 4, 1, 4, 2>(x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 14: return launch_glds<TO, 128, 64, 2, 2, 4, 2>(x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 15: return launch_glds<TO, 128, 64, 2, 2, 4, 1>(x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 16: return launch_glds<TO, 64, 64, 2, 2, 4, 1>(x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 17: return launch_glds<TO, 64, 64, 2, 2, 4, 2>(x, w, y, g, ep, xb, wb, s, ws, ph);
+    default: return launch_glds<TO, 64, 64, 2, 2, 4, 4>(x, w, y, g, ep, xb, wb, s, ws, ph);
   }
 }
 
 template int launch_glds_grp_c<bf16_t>(int, const void*, const void*, void*, const ConvGeom&, const Epi<bf16_t>&,
-                                        unsigned, unsigned, hipStream_t, float*);
+                                        unsigned, unsigned, hipStream_t, float*, const PhaseTab*);
 template int launch_glds_grp_c<f16_t>(int, const void*, const void*, void*, const ConvGeom&, const Epi<f16_t>&,
-                                       unsigned, unsigned, hipStream_t, float*);
+                                       unsigned, unsigned, hipStream_t, float*, const PhaseTab*);

@@ -177,6 +177,15 @@ __device__ __forceinline__ void tile_stats(SA (&s1)[V], SA (&s2)[V], int lstride
   }
 }
 
+// Output phases of one transposed conv (ConvTranspose2d(4,2,1): four 2x2-tap phases) in ONE launch: blockIdx.y =
+// phase, each with its own input offset, output sub-grid and packed weights (same K, taps and weight stride).
+// A 16x16-input layer has only 32-128 tiles per phase: one launch fills the chip where four could not.
+struct PhaseTab {
+  int n;                          // phases (1: a plain launch)
+  int py[4], px[4], ooy[4], oox[4];
+  const void* w[4];
+};
+
 template <typename TO> struct Load4;
 template <> struct Load4<float> {
   __device__ __forceinline__ static void ld(const float* p, float (&v)[4]) {
@@ -683,7 +692,7 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
                                                                 const TO* __restrict__ w, TO* __restrict__ y,
                                                                 ConvGeom g, Epi<TO> ep, unsigned xbytes,
                                                                 unsigned wbytes, int g_epi_lds, int splits,
-                                                                float* __restrict__ ws) {
+                                                                float* __restrict__ ws, PhaseTab ph) {
   constexpr int ROW = 128;                       // bytes per LDS row = 64 bf16 of k
   constexpr int STAGE = (BM + BN) * ROW;
   constexpr int AI = BM / 8 / NW;                // A (pixel) wave-instructions per wave per stage
@@ -703,12 +712,21 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
   const long long m0 = (long long)(tile / nnt) * BM;
   const int n0 = (tile % nnt) * BN;
+  if (ph.n > 1) {   // this block's output phase: offsets, sub-grid, weights, statistics rows
+    const int p = blockIdx.y;
+    g.py = ph.py[p];
+    g.px = ph.px[p];
+    g.ooy = ph.ooy[p];
+    g.oox = ph.oox[p];
+    w = (const TO*)ph.w[p];
+    if (ep.stats) ep.stats += (long long)p * ((g.M + BM - 1) / BM) * 2 * ep.sld;
+  }
   const int RS = g.R * g.S;
   const int cpt = g.C >> 6;                      // k-tiles per tap
   // split-K (low-tile layers, blockIdx.y = split): this block reduces k-tiles [kt0, kt1) in order
   const int nk_all = RS * cpt;
   const int kper = (nk_all + splits - 1) / splits;
-  const int kt0 = min(nk_all, (int)blockIdx.y * kper);
+  const int kt0 = min(nk_all, (ph.n > 1 ? 0 : (int)blockIdx.y) * kper);
   const int nk = min(nk_all, kt0 + kper) - kt0;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, (int)wbytes, 0x00020000);
@@ -933,23 +951,35 @@ __global__ void splitk_finalize_kernel(const float* __restrict__ ws, TO* __restr
 
 template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS>
 int launch_glds(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb, unsigned wb,
-                hipStream_t s, float* ws) {
+                hipStream_t s, float* ws, const PhaseTab* ph) {
   static_assert(sizeof(TO) == 2, "LDS-DMA configs: 16-bit activations in and out (fp32-output heads have K <= 16)");
   const long long tiles = ((g.M + BM - 1) / BM) * ((g.K + BN - 1) / BN);
+  if (ph && ph->n > 1) {   // all phases in one launch (no split-K)
+    if (ep.stats)
+      hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, true>), dim3((unsigned)tiles, (unsigned)ph->n),
+                         dim3(NW * 64), 0, s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb,
+                         (int)(g_knobs[7] == 0), 1, nullptr, *ph);
+    else
+      hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, false>), dim3((unsigned)tiles, (unsigned)ph->n),
+                         dim3(NW * 64), 0, s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb,
+                         (int)(g_knobs[7] == 0), 1, nullptr, *ph);
+    return BM;
+  }
+  const PhaseTab one{1, {0}, {0}, {0}, {0}, {nullptr}};
   // split-K only with a workspace (never with fused statistics: the host passes none then)
   const int sp = (ws && !ep.stats) ? plan_splits<TO, BM, BN>(g) : 1;
   if (sp > 1) {
     (void)hipMemsetAsync(ws, 0, sizeof(float) * g.M * g.K, s);
     hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, false>), dim3((unsigned)tiles, (unsigned)sp),
-                       dim3(NW * 64), 0, s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, 0, sp, ws);
+                       dim3(NW * 64), 0, s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, 0, sp, ws, one);
     hipLaunchKernelGGL(splitk_finalize_kernel<TO>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, ws, (TO*)y, g,
                        ep);
   } else if (ep.stats) {
     hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, true>), dim3((unsigned)tiles), dim3(NW * 64), 0,
-                       s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, (int)(g_knobs[7] == 0), 1, nullptr);
+                       s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, (int)(g_knobs[7] == 0), 1, nullptr, one);
   } else {
     hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, false>), dim3((unsigned)tiles), dim3(NW * 64), 0,
-                       s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, (int)(g_knobs[7] == 0), 1, nullptr);
+                       s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, (int)(g_knobs[7] == 0), 1, nullptr, one);
   }
   return BM;
 }
@@ -959,16 +989,16 @@ int launch_glds(const void* x, const void* w, void* y, const ConvGeom& g, const 
 // Each returns the tile height BM of the launched config (the fused BN statistics write ceil(M/BM) rows).
 template <typename TO>
 int launch_glds_grp_a(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                      unsigned wb, hipStream_t s, float* ws);
+                      unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph);
 template <typename TO>
 int launch_glds_grp_b(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                      unsigned wb, hipStream_t s, float* ws);
+                      unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph);
 template <typename TO>
 int launch_glds_grp_d(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                      unsigned wb, hipStream_t s, float* ws);
+                      unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph);
 template <typename TO>
 int launch_glds_grp_c(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                      unsigned wb, hipStream_t s, float* ws);
+                      unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph);
 
 
 template <typename T, int BM, int BN>

@@ -56,6 +56,7 @@ SIGS = {
     'ssseg_scale_by': (i32, [vp, vp, vp, i64, vp]),
     # convolution engine
     'ssseg_conv_igemm': (i32, [vp, vp, vp, vp, i32, i32, vp, i32, vp, sz, vp]),
+    'ssseg_conv_igemm_phases': (i32, [vp, vp, vp, i32, i32, vp, i64, vp, vp, vp]),
     'ssseg_conv_stem_epi': (i32, [vp, vp, vp, vp, i32, vp, vp]),
     'ssseg_conv_igemm_epi': (i32, [vp, vp, vp, vp, i32, i32, vp, vp, sz, vp]),
     'ssseg_weight_pack_batch': (i32, [vp, i64, i32, vp]),

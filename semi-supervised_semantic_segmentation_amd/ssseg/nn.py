@@ -18,7 +18,12 @@ import torch.nn as nn
 
 from . import native as N
 
-_CFG = {'grad_join': True, 'stem': True, 'dtype': torch.bfloat16, 'sync_bn': True, 'fuse_stats': True}
+_CFG = {'grad_join': True, 'stem': True, 'phases': True, 'dtype': torch.bfloat16, 'sync_bn': True, 'fuse_stats': True}
+
+
+def set_phase_launch(on):
+    """One launch over a transposed conv's output phases (ssseg_conv_igemm_phases; default on)."""
+    _CFG['phases'] = bool(on)
 
 
 def set_stem_kernel(on):
@@ -740,6 +745,7 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
             fold, bwd = self._fold(bn, residual, cout, aux)
         timer = _Timed(_conv_flops(n, H, W, self.out_channels, self.in_channels, R, S), 'fwd', _tag(self, n, H, W))
         timer.__enter__()
+        phases = []
         for (phy, ry0, rny, dly, qy) in _phases(sh, ph, R, OH):
             for (phx, rx0, rnx, dlx, qx) in _phases(sw, pw, S, OW):
                 if qy == 0 or qx == 0:
@@ -750,9 +756,33 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
                 d = _desc(N=n, H=H, W=W, C=cin, ldx=cin, OH=qy, OW=qx, K=cout, R=rr, S=ss, sy=1, sx=1, dy=-1, dx=-1,
                           py=dly, px=dlx, outH=OH, outW=OW, osy=sh, osx=sw, ooy=phy, oox=phx, ldy=cout,
                           ldw=max(rr * ss * cin, cin))
+                phases.append((w, d, (rr, ss, qy, qx), (dly, dlx, phy, phx)))
+        shapes = {p[2] for p in phases}
+        if (_CFG['phases'] and 1 < len(phases) <= 4 and len(shapes) == 1 and phases[0][0] is not None
+                and _CFG['dtype'] in (torch.bfloat16, torch.float16)):
+            # every phase has the same taps and sub-grid: one launch over all of them (ssseg_conv_igemm_phases)
+            self._igemm_phases(x, [p[0] for p in phases], y, phases[0][1], [p[3] for p in phases], self.bias, relu,
+                               fold, stats)
+        else:
+            for w, d, _, _ in phases:
                 self._igemm(x, w, y, d, N.dt_code(y), self.bias, relu, fold, stats=stats)
         timer.__exit__()
         return (y, aux, bwd) if keep_pre else y
+
+    def _igemm_phases(self, x, ws, y, desc, geoms, bias, relu, fold, stats):
+        import ctypes
+        scale, shift, res, aux = fold if fold is not None else (None, bias, None, None)
+        sf = stats.launch_fields() if stats is not None else (None, 0, None)
+        ep = N.ConvEpilogue(N.dev_ptr(scale) if scale is not None else None,
+                            N.dev_ptr(shift) if shift is not None else None,
+                            N.dev_ptr(res) if res is not None else None, res.shape[1] if res is not None else 0,
+                            N.dev_ptr(aux) if aux is not None else None, *_act(relu), *sf)
+        geo = (ctypes.c_int64 * (4 * len(geoms)))(*[v for g4 in geoms for v in g4])
+        wp = (ctypes.c_void_p * len(ws))(*[N.dev_ptr(w) for w in ws])
+        N.call('ssseg_conv_igemm_phases', N.dev_ptr(x), N.dev_ptr(y), ctypes_ref(desc), N.dt_code(x), N.dt_code(y),
+               ctypes_ref(ep), len(ws), ctypes.addressof(geo), ctypes.addressof(wp), N.stream())
+        if stats is not None:
+            stats.commit()
 
     def _grad_in(self, gy):
         _need_act(gy, self._dims()[1], 'ConvTranspose2d backward')
