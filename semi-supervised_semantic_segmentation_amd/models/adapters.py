@@ -9,6 +9,10 @@ class ListOutput(nn.Module):
         super().__init__()
         self.model = model
 
+    @property
+    def ssseg_batched_eval(self):
+        return getattr(self.model, 'ssseg_batched_eval', False)
+
     def forward(self, x):
         y = self.model(x)
         return [y], [y]

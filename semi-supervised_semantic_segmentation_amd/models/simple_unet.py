@@ -45,6 +45,8 @@ class UpBlock(nn.Module):
 
 
 class UNet(nn.Module):
+    ssseg_batched_eval = True   # per-sample eval forward on an NHWC activation batch (batched teacher)
+
     def __init__(self, num_classes, num_blocks, first_channels=32, max_width=256, norm_layer=nn.BatchNorm2d,
                  train_upsampling=True):
         super().__init__()

@@ -40,6 +40,9 @@ class UpBlock(nn.Module):
 
 
 class UNet(nn.Module):
+    # eval forward is per-sample and accepts an NHWC activation batch (train.train_step batches the teacher)
+    ssseg_batched_eval = True
+
     def __init__(self, num_classes, encoder, max_width, norm_layer=nn.BatchNorm2d, train_upsampling=False):
         super().__init__()
         self.encoder = encoder

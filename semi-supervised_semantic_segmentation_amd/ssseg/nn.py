@@ -170,6 +170,24 @@ def to_act(x):
     return _ToAct.apply(x)
 
 
+def to_act_cat(xs):
+    """Several NCHW image batches -> ONE compute-dtype NHWC activation batch, each converted straight into its
+    slice (no concat pass): an eval-mode model's passes over several batches become one forward (no autograd)."""
+    n = sum(int(x.shape[0]) for x in xs)
+    _, c, h, w = xs[0].shape
+    cp = rup(c, vec())
+    y = new_act(n, cp, h, w, _CFG['dtype'], xs[0].device)
+    off = 0
+    for x in xs:
+        if tuple(x.shape[1:]) != (c, h, w):
+            raise ValueError('to_act_cat: batches of different image shapes')
+        xc = x if x.is_contiguous() else x.contiguous()
+        N.call('ssseg_nchw_to_nhwc', N.dev_ptr(xc, 'image'), N.dev_ptr(y) + off * cp * h * w * y.element_size(),
+               int(x.shape[0]), c, h, w, cp, N.dt_code(xc), N.dt_code(y), N.stream())
+        off += int(x.shape[0])
+    return y
+
+
 # ------------------------------------------------------------------------------------------------
 # convolution
 # ------------------------------------------------------------------------------------------------

@@ -28,6 +28,14 @@ def _inner(model):
     return model.module if hasattr(model, 'module') else model
 
 
+def _batched_eval_ok(ema_model, a, b):
+    """The teacher takes an NHWC activation batch and is per-sample in eval mode (models that declare
+    ssseg_batched_eval), and both unlabelled batches have the same image shape."""
+    m = _inner(ema_model)
+    return (getattr(m, 'ssseg_batched_eval', False) and tuple(a.shape[1:]) == tuple(b.shape[1:])
+            and a.dtype == b.dtype)
+
+
 def _world():
     return torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
 
@@ -126,8 +134,19 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
     if semi:
         size = unsup_a.shape[2:4]
         with torch.no_grad(), snn.folded(_inner(ema_model)):   # one batched BN fold for both teacher passes
-            ema_pred_a = ops.interpolate_bilinear(ema_model(unsup_a)[-1][-1], size, align_corners=False)
-            ema_pred_b = ops.interpolate_bilinear(ema_model(unsup_b)[-1][-1], size, align_corners=False)
+            if _batched_eval_ok(ema_model, unsup_a, unsup_b):
+                # train.py:69-75 runs the teacher twice; in eval mode every output depends on its own sample
+                # only, so ONE forward over [unsup_a; unsup_b] gives the same logits (the conv variants
+                # accumulate the same k-sequence at any batch) with half the launches and twice the tiles on
+                # the small-map layers
+                b = unsup_a.shape[0]
+                ema_logits = ema_model(snn.to_act_cat([unsup_a, unsup_b]))[-1][-1]
+                ema_pred_a = ops.interpolate_bilinear(ema_logits[:b], size, align_corners=False)
+                ema_pred_b = ops.interpolate_bilinear(ema_logits[b:], size, align_corners=False)
+                del ema_logits
+            else:
+                ema_pred_a = ops.interpolate_bilinear(ema_model(unsup_a)[-1][-1], size, align_corners=False)
+                ema_pred_b = ops.interpolate_bilinear(ema_model(unsup_b)[-1][-1], size, align_corners=False)
             cmask = cowmix.generate_cowmix_masks_like(unsup_a, mask_proportion_range=tc['mask_proportion_range'],
                                                       sigma_range=tc['sigma_range'])
             mixed_ema_pred = cowmix.mix_with_mask(ema_pred_a, ema_pred_b, cmask)

@@ -84,3 +84,24 @@ def test_grad_join_any_consumer_order(hip_device):
         snn.set_grad_join(True)
         snn.set_compute_dtype(torch.bfloat16)
     assert float((g_sum - g_join).abs().max()) <= 1e-5 * (float(g_sum.abs().max()) + 1e-12)
+
+
+@pytest.mark.parametrize('dtype', ['f32', 'bf16'])
+def test_batched_teacher_forward_bitwise(hip_device, dtype):
+    """train_step runs the teacher's two eval passes (reference train.py:69-75) as ONE forward over both
+    batches (snn.to_act_cat): the logits equal the two separate passes bit for bit."""
+    from models import unet
+    from models.encoders import resnet
+    from ssseg import nn as snn
+    snn.set_compute_dtype(torch.float32 if dtype == 'f32' else torch.bfloat16)
+    try:
+        torch.manual_seed(2)
+        model = unet.UNet(2, resnet.resnet50_encoder(), 64, train_upsampling=True).to(hip_device).eval()
+        a = torch.rand(2, 3, 96, 96, device=hip_device)
+        b = torch.rand(2, 3, 96, 96, device=hip_device)
+        with torch.no_grad(), snn.folded(model):
+            ya, yb = model(a).float().cpu(), model(b).float().cpu()
+            yab = model(snn.to_act_cat([a, b])).float().cpu()
+    finally:
+        snn.set_compute_dtype(torch.bfloat16)
+    assert torch.equal(yab[:2], ya) and torch.equal(yab[2:], yb)
