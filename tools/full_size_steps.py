@@ -1,0 +1,101 @@
+"""Full-size smoke of the BASELINE configs C3-C5 on ONE GPU (world 1): the model, teacher, optimizer and (C5) the
+discriminator built exactly as distributed_trainer.distributed_train builds them, synthetic batches at the config's
+image size and per-worker batch, three train_step calls (epoch 30: the consistency term is live).  Checks memory fit
+and 32-bit offsets at the real geometries (every kernel entry validates its offsets) and prints per config: losses,
+finiteness of losses and parameters, ms/step of the last two steps, peak device memory.
+
+    python tools/full_size_steps.py [--configs c3,c4,c5] > gpurun_out/full_size.log
+The confidence threshold is set to 0.0 (every pixel confident): with random init the teachers' max sigmoid is
+<= 0.5 on whole batches (HRNet-MSA's eval logits are ~1e-14: tools/diag_c4.py), so the reference's 0.97 -- and even
+bench.py's 0.5 -- gives an all-zero mask and the reference's own 0/0 NaN.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, 'semi-supervised_semantic_segmentation_amd')
+sys.path[:0] = [ROOT, PKG]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+CFGS = {'c3': 'configs/c3_deeplabv3_r101.py', 'c4': 'configs/c4_msa_hrnet.py', 'c5': 'configs/c5_hardnet_disc.py'}
+
+
+def run(name, path, dev):
+    import config
+    import mean_teacher
+    import train
+    from ssseg import amp, arena
+    from ssseg import nn as snn
+    from ssseg import optim as soptim
+    from ssseg.ddp import DistributedDataParallel
+    torch.manual_seed(0)
+    cfg = config.fromfile(os.path.join(PKG, path))
+    snn.set_compute_dtype({'fp32': torch.float32, 'fp16': torch.float16}.get(cfg['common'].get('compute_dtype'),
+                                                                             torch.bfloat16))
+    model = DistributedDataParallel(cfg['model']['model_fn']().to(dev))
+    ema = cfg['model']['model_fn']().to(dev)
+    mean_teacher.detach_model_parameters(ema)
+    arena.attach(ema, with_grads=False)
+    ema.eval()
+    opt = soptim.from_config(cfg['train']['optimizer'], [p for p in model.parameters() if p.requires_grad])
+    if snn.compute_dtype() == torch.float16:
+        opt.grad_scaler = amp.GradScaler(dev)
+    tc = cfg['train']
+    tc['confidence_threshold'] = 0.0
+    tc['print_freq'] = 10 ** 9
+    if cfg['model'].get('discriminator') is not None and tc.get('adversarial_loss_weight'):
+        disc = DistributedDataParallel(cfg['model']['discriminator']().to(dev))
+        dopt = soptim.from_config(tc['discriminator_optimizer'], disc.parameters())
+        if snn.compute_dtype() == torch.float16:
+            dopt.grad_scaler = amp.GradScaler(dev)
+        tc['adversarial'] = dict(discriminator=disc, optimizer=dopt, weight=float(tc['adversarial_loss_weight']))
+    b, s = tc['batch_size_per_worker'], cfg['common']['image_size']
+    g = torch.Generator().manual_seed(5)
+    img = torch.rand(b, 3, s, s, generator=g).to(dev)
+    fg = (torch.rand(b, 1, s, s, generator=g) > 0.5).float().to(dev)
+    mask = torch.cat([1 - fg, fg], 1).contiguous()
+    ua = torch.rand(b, 3, s, s, generator=g).to(dev)
+    ub = torch.rand(b, 3, s, s, generator=g).to(dev)
+    torch.cuda.reset_peak_memory_stats(dev)
+    times, out = [], []
+    for step in range(3):
+        torch.cuda.synchronize()
+        t0 = time.time()
+        cls, unsup, cm = train.train_step(model, ema, opt, img, mask, ua, ub, 30, step, cfg)
+        torch.cuda.synchronize()
+        times.append(time.time() - t0)
+        out.append((float(cls), float(unsup) if unsup is not None else None, float(cm) if cm is not None else None))
+    params_finite = all(bool(torch.isfinite(p).all()) for p in model.parameters())
+    losses_finite = all(v is None or v == v and abs(v) != float('inf') for row in out for v in row)
+    rec = {'config': name, 'image_size': s, 'batch': b, 'dtype': str(snn.compute_dtype()).replace('torch.', ''),
+           'losses': out, 'losses_finite': losses_finite, 'params_finite': params_finite,
+           'ms_per_step_last2': round(1e3 * sum(times[1:]) / 2, 1), 'first_step_s': round(times[0], 1),
+           'peak_mem_GB': round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)}
+    if 'adversarial' in tc:
+        rec['loss_d'] = float(tc['adversarial']['last_loss_d'])
+    print(json.dumps(rec), flush=True)
+    return rec['losses_finite'] and rec['params_finite']
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--configs', default='c3,c4,c5')
+    a = ap.parse_args()
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group('nccl', init_method='tcp://127.0.0.1:29533', rank=0, world_size=1)
+    ok = True
+    for name in a.configs.split(','):
+        ok &= run(name, CFGS[name], dev)
+        torch.cuda.empty_cache()
+    dist.destroy_process_group()
+    sys.exit(0 if ok else 1)
+
+
+if __name__ == '__main__':
+    main()
