@@ -123,3 +123,42 @@ def test_ddp_reducer_gloo_world2_reused_params():
         p.join(120)
     res = dict(q.get(timeout=5) for _ in range(2))
     assert res == {0: True, 1: True}
+
+
+def _meters_worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        import train
+        from utils import utils
+        # reduce_tensor (reference utils/utils.py:43-54): SUM onto rank 0 in place, others untouched
+        t = torch.tensor([float(rank + 1), 10.0 * (rank + 1)])
+        out = utils.reduce_tensor(t.clone())
+        # epoch-end meter reduction (train._reduce_meters): one all-reduce of the stacked sums / world
+        meters = {'a': utils.AverageMeter(), 'b': utils.AverageMeter()}
+        meters['a'].update(torch.tensor(2.0 * (rank + 1)))
+        meters['b'].update(torch.tensor(-1.0 * (rank + 1)), 3)
+        train._reduce_meters(meters, ['a', 'b'], world)
+        q.put((rank, out.tolist(), float(meters['a'].sum), float(meters['b'].sum)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_reduce_tensor_and_meters_gloo_world2():
+    """utils.reduce_tensor and the epoch-end meter all-reduce at world size 2 (reference utils/utils.py:43-54,
+    train.py:53-59,109-114)."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_meters_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][0] == [3.0, 30.0]          # rank 0 holds the sum
+    assert res[1][0] == [2.0, 20.0]          # rank 1's tensor is not the destination
+    assert res[0][1] == res[1][1] == 3.0     # (2 + 4) / 2
+    assert res[0][2] == res[1][2] == -4.5    # (-3 + -6) / 2

@@ -308,3 +308,76 @@ def test_train_step_vs_oracle_unet_r50(hip_device, f32_mode, H):
         worst32 = max(worst32, float(np.abs(c - b).max() / (np.abs(b).max() + 1e-12)))
     print(f'params after 2 steps, worst rel err vs fp64: hip {worst:.2e} ref32 {worst32:.2e}')
     assert worst < max(1e-3, 2 * worst32), (worst, worst32)
+
+
+def test_checkpoint_resume_continues_identically(hip_device, f32_mode):
+    """Checkpoint dict of distributed_trainer.py:117-118 (state_dict, ema_state_dict, optimizer) after three
+    steps, loaded into fresh modules and a fresh ssseg SGD (momentum buffers copied into its flat arena,
+    reference resume at distributed_trainer.py:74-85): the next step equals the uninterrupted run's bit for bit."""
+    import copy
+    import cowmix
+    import losses
+    import train
+    from models import simple_unet
+    from models.adapters import ListOutput
+    from ssseg import arena, optim
+    from ssseg import nn as snn
+
+    def build():
+        torch.manual_seed(0)
+        s = ListOutput(simple_unet.UNet(2, num_blocks=2, first_channels=8, max_width=16)).to(hip_device)
+        torch.manual_seed(0)
+        t = ListOutput(simple_unet.UNet(2, num_blocks=2, first_channels=8, max_width=16)).to(hip_device)
+        for p in t.parameters():
+            p.detach_()
+        t.eval()
+        arena.attach(s)
+        arena.attach(t, with_grads=False)
+        return s, t, optim.SGD(s.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
+
+    cfg = {'train': dict(loss=losses.CalculateLoss([
+        {'loss_fn': losses.DenseBinaryCrossEntropyLossWithLogits(reduction='mean'), 'weight': [0.5]}]),
+        virtual_batch_size_multiplier=1, use_semi_supervised=True, mask_proportion_range=(0.45, 0.55),
+        sigma_range=(2, 4), confidence_threshold=0.0, consistency_loss_weight=10, ema_model_alpha=0.99,
+        print_freq=1, gradient_clip_value=5.0)}
+    g = torch.Generator().manual_seed(3)
+    data = [(torch.rand(2, 3, 32, 32, generator=g).to(hip_device),
+             torch.rand(2, 2, 32, 32, generator=g).round().to(hip_device),
+             torch.rand(2, 3, 32, 32, generator=g).to(hip_device),
+             torch.rand(2, 3, 32, 32, generator=g).to(hip_device)) for _ in range(4)]
+    old = cowmix.NOISE_SOURCE
+    cowmix.NOISE_SOURCE = 'cpu'
+    try:
+        s, t, opt = build()
+        s.train()
+        opt.zero_grad()
+        for step in range(3):
+            torch.manual_seed(100 + step)
+            train.train_step(s, t, opt, *data[step], 30, step, cfg)
+        ck = copy.deepcopy({'state_dict': {k: v.cpu() for k, v in s.state_dict().items()},
+                            'ema_state_dict': {k: v.cpu() for k, v in t.state_dict().items()},
+                            'optimizer': opt.state_dict()})
+        torch.manual_seed(103)
+        train.train_step(s, t, opt, *data[3], 30, 3, cfg)
+        want_s, want_t = s.state_dict(), t.state_dict()
+
+        s2, t2, opt2 = build()
+        s2.load_state_dict(ck['state_dict'])
+        t2.load_state_dict(ck['ema_state_dict'])
+        opt2.load_state_dict(ck['optimizer'])
+        # the uninterrupted teacher's BN buffers ARE the student's (update_ema_variables aliases them, reference
+        # mean_teacher.py:13-18); a resumed teacher holds loaded copies until its first EMA update -- the
+        # reference's own resume behaviour.  Alias them here so the comparison isolates parameter + momentum state.
+        for eb, b in zip(t2.buffers(), s2.buffers()):
+            eb.data = b.data
+        snn.invalidate_packed(s2)
+        snn.invalidate_packed(t2)
+        s2.train()
+        torch.manual_seed(103)
+        train.train_step(s2, t2, opt2, *data[3], 30, 3, cfg)
+        got_s, got_t = s2.state_dict(), t2.state_dict()
+    finally:
+        cowmix.NOISE_SOURCE = old
+    for k in want_s:
+        assert torch.equal(got_s[k], want_s[k]), k
+        assert torch.equal(got_t[k], want_t[k]), k
