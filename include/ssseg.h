@@ -365,6 +365,14 @@ int ssseg_bn_eval_bwd_grad(const void* dy, const void* y, const void* aux, void*
                            int64_t ld, const float* scale, const float* mean_eff, const float* invstd, int relu, int dt,
                            double* sums, void* ws, size_t ws_bytes, float* dgamma, float* dbeta, float* dconv_bias,
                            ssseg_stream_t stream);
+/* ssseg_bn_eval_bwd_grad without the raw accumulator copy, for a layer WITHOUT a residual: wherever the output
+ * gradient survives the activation, y itself is the pre-activation scale*aux + shift, so x_hat is recovered from y
+ * (x_hat = (y - (shift + mean_eff*scale)) * invstd / scale; a channel with scale == 0 gets x_hat = 0).  The
+ * differentiated eval pass (train.py:90-92) then does not write aux in the forward nor read it here. */
+int ssseg_bn_eval_bwd_grad_y(const void* dy, const void* y, void* dconv, void* dres, int64_t P, int64_t C, int64_t ld,
+                             const float* scale, const float* shift, const float* mean_eff, const float* invstd,
+                             int relu, int dt, double* sums, void* ws, size_t ws_bytes, float* dgamma, float* dbeta,
+                             float* dconv_bias, ssseg_stream_t stream);
 /* y = act(gamma*(x-mean)*invstd + beta [+ residual]); channels [C, rup(C, 16 bytes)) of y are written 0; relu = 1 for ReLU (unet.py:10, Bottleneck add+relu) */
 int ssseg_bn_apply(const void* x, const void* residual, void* y, int64_t P, int64_t C, int64_t ldx, int64_t ldr,
                    int64_t ldy, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu,

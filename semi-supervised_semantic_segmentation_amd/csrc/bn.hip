@@ -364,13 +364,17 @@ __global__ void bn_fold_batch_kernel(const ssseg_fold_desc* __restrict__ descs) 
 }
 
 // backward of a folded eval BN: dyr = relu ? dy*[y>0] : dy, dconv = scale*dyr, dres = dyr, and per-block
-// partial sums (dyr, dyr*xhat), xhat = (aux - mean_eff)*invstd
+// partial sums (dyr, dyr*xhat), xhat = (aux - mean_eff)*invstd.  y-mode (shift given, no aux; layers without a
+// residual): wherever dyr != 0 the stored y IS the pre-activation scale*aux + shift, so xhat = (y - beta')/gamma'
+// with beta' = shift + mean_eff*scale (= beta) and 1/gamma' = invstd/scale -- the raw accumulator copy is not
+// needed (saves its write in the forward and its read here); a channel with scale == 0 gets xhat = 0.
 template <typename T, int V>
 __global__ void __launch_bounds__(256) bn_eval_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ y,
                                                           const T* __restrict__ aux, T* __restrict__ dconv,
                                                           T* __restrict__ dres, int64_t P, int C, int64_t ld,
                                                           Layout L, const float* scale, const float* mean_eff,
-                                                          const float* invstd, int relu, double* part) {
+                                                          const float* invstd, int relu, double* part,
+                                                          const float* shift) {
   __shared__ double red[2][256][V];
   const int t = threadIdx.x;
   const int cl = t % L.cpb, pl = t / L.cpb;
@@ -396,6 +400,18 @@ __global__ void __launch_bounds__(256) bn_eval_bwd_kernel(const T* __restrict__ 
       me[e] = live[e] ? me[e] : 0.f;
       is[e] = live[e] ? is[e] : 0.f;
     }
+    const bool ymode = shift != nullptr;
+    if (ymode) {
+      float sh[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) sh[e] = shift[min(c0 + e, C - 1)];
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        me[e] = live[e] ? fmaf(me[e], sc[e], sh[e]) : 0.f;
+        is[e] = (live[e] && sc[e] != 0.f) ? is[e] / sc[e] : 0.f;
+      }
+    }
+    const T* __restrict__ xsrc = ymode ? y : aux;   // the pre-BN value source of xhat
     using CK = Chunk<T, V>;
     const int64_t stride = (int64_t)gridDim.x * L.ppb;
     for (int64_t p0 = (int64_t)blockIdx.x * L.ppb + pl; p0 < P; p0 += stride * U) {
@@ -404,10 +420,10 @@ __global__ void __launch_bounds__(256) bn_eval_bwd_kernel(const T* __restrict__ 
       for (int u = 0; u < U; ++u) {
         const int64_t p = clampp(p0 + u * stride, P);
         qg[u] = CK::ld(dy + p * ld + c0);
-        qa[u] = CK::ld(aux + p * ld + c0);
+        qa[u] = CK::ld(xsrc + p * ld + c0);
         qy[u] = CK::zero();
       }
-      if (relu)
+      if (relu && !ymode)
 #pragma unroll
         for (int u = 0; u < U; ++u) qy[u] = CK::ld(y + clampp(p0 + u * stride, P) * ld + c0);
 #pragma unroll
@@ -416,8 +432,13 @@ __global__ void __launch_bounds__(256) bn_eval_bwd_kernel(const T* __restrict__ 
         if (p >= P) continue;
         float g[U][V], yv[U][V], a[U][V];
         CK::cvt(qg[u], g[u]);
-        CK::cvt(qy[u], yv[u]);
         CK::cvt(qa[u], a[u]);
+        if (ymode) {
+#pragma unroll
+          for (int e = 0; e < V; ++e) yv[u][e] = a[u][e];
+        } else {
+          CK::cvt(qy[u], yv[u]);
+        }
         float od[V], oc[V];
 #pragma unroll
         for (int e = 0; e < V; ++e) {
@@ -765,23 +786,24 @@ extern "C" int ssseg_bn_fold_batch(const ssseg_fold_desc* descs, int64_t n, ssse
 template <typename T>
 static void eval_bwd(const T* dy, const T* y, const T* aux, T* dconv, T* dres, int64_t P, int64_t C, int64_t ld,
                      const float* scale, const float* mean_eff, const float* invstd, int relu, double* sums, void* ws,
-                     hipStream_t s, FinalEpi fe) {
+                     hipStream_t s, FinalEpi fe, const float* shift) {
   constexpr int V16 = 16 / sizeof(T);
   const bool wide = wide_ok<T>(C, {ld});
   const Layout L = layout_for(C, wide ? V16 : V16 / 2);
   const int64_t gx = pixel_blocks(P, L, MAXG);
   if (wide)
     hipLaunchKernelGGL((bn_eval_bwd_kernel<T, V16>), dim3((unsigned)gx, L.cblocks), dim3(256), 0, s, dy, y, aux, dconv,
-                       dres, P, (int)C, ld, L, scale, mean_eff, invstd, relu, (double*)ws);
+                       dres, P, (int)C, ld, L, scale, mean_eff, invstd, relu, (double*)ws, shift);
   else
     hipLaunchKernelGGL((bn_eval_bwd_kernel<T, V16 / 2>), dim3((unsigned)gx, L.cblocks), dim3(256), 0, s, dy, y, aux,
-                       dconv, dres, P, (int)C, ld, L, scale, mean_eff, invstd, relu, (double*)ws);
+                       dconv, dres, P, (int)C, ld, L, scale, mean_eff, invstd, relu, (double*)ws, shift);
   launch_partial_final((const double*)ws, gx, C, sums, s, fe);
 }
 
 static int eval_bwd_entry(const void* dy, const void* y, const void* aux, void* dconv, void* dres, int64_t P, int64_t C,
                           int64_t ld, const float* scale, const float* mean_eff, const float* invstd, int relu, int dt,
-                          double* sums, void* ws, size_t ws_bytes, ssseg_stream_t stream, FinalEpi fe);
+                          double* sums, void* ws, size_t ws_bytes, ssseg_stream_t stream, FinalEpi fe,
+                          const float* shift = nullptr);
 
 extern "C" int ssseg_bn_eval_bwd(const void* dy, const void* y, const void* aux, void* dconv, void* dres, int64_t P,
                                  int64_t C, int64_t ld, const float* scale, const float* mean_eff, const float* invstd,
@@ -804,9 +826,25 @@ extern "C" int ssseg_bn_eval_bwd_grad(const void* dy, const void* y, const void*
                         stream, fe);
 }
 
+extern "C" int ssseg_bn_eval_bwd_grad_y(const void* dy, const void* y, void* dconv, void* dres, int64_t P, int64_t C,
+                                        int64_t ld, const float* scale, const float* shift, const float* mean_eff,
+                                        const float* invstd, int relu, int dt, double* sums, void* ws, size_t ws_bytes,
+                                        float* dgamma, float* dbeta, float* dconv_bias, ssseg_stream_t stream) {
+  if (!shift || !y) return SSSEG_EINVAL;
+  FinalEpi fe{};
+  fe.mode = (dgamma || dbeta || dconv_bias) ? 2 : 0;
+  fe.dgamma = dgamma;
+  fe.dbeta = dbeta;
+  fe.scale = scale;
+  fe.dbias = dconv_bias;
+  return eval_bwd_entry(dy, y, y, dconv, dres, P, C, ld, scale, mean_eff, invstd, relu, dt, sums, ws, ws_bytes,
+                        stream, fe, shift);
+}
+
 static int eval_bwd_entry(const void* dy, const void* y, const void* aux, void* dconv, void* dres, int64_t P, int64_t C,
                           int64_t ld, const float* scale, const float* mean_eff, const float* invstd, int relu, int dt,
-                          double* sums, void* ws, size_t ws_bytes, ssseg_stream_t stream, FinalEpi fe) {
+                          double* sums, void* ws, size_t ws_bytes, ssseg_stream_t stream, FinalEpi fe,
+                          const float* shift) {
   if (!dy || !aux || !dconv || !sums || !scale || !mean_eff || !invstd || (relu && !y) || P < 1 || C < 1 ||
       ld_bad(C, ld))
     return SSSEG_EINVAL;
@@ -814,13 +852,13 @@ static int eval_bwd_entry(const void* dy, const void* y, const void* aux, void* 
   hipStream_t s = (hipStream_t)stream;
   if (dt == SSSEG_BF16)
     eval_bwd<bf16_t>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)aux, (bf16_t*)dconv, (bf16_t*)dres, P, C, ld,
-                     scale, mean_eff, invstd, relu, sums, ws, s, fe);
+                     scale, mean_eff, invstd, relu, sums, ws, s, fe, shift);
   else if (dt == SSSEG_F16)
     eval_bwd<f16_t>((const f16_t*)dy, (const f16_t*)y, (const f16_t*)aux, (f16_t*)dconv, (f16_t*)dres, P, C, ld,
-                     scale, mean_eff, invstd, relu, sums, ws, s, fe);
+                     scale, mean_eff, invstd, relu, sums, ws, s, fe, shift);
   else if (dt == SSSEG_F32)
     eval_bwd<float>((const float*)dy, (const float*)y, (const float*)aux, (float*)dconv, (float*)dres, P, C, ld, scale,
-                    mean_eff, invstd, relu, sums, ws, s, fe);
+                    mean_eff, invstd, relu, sums, ws, s, fe, shift);
   else
     return SSSEG_EUNSUPPORTED;
   SSSEG_LAUNCH_CHECK();

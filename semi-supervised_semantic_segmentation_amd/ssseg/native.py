@@ -78,6 +78,8 @@ SIGS = {
     'ssseg_bn_fold': (i32, [vp, vp, vp, vp, vp, f32, i64, i64, vp, vp, vp, vp, vp]),
     'ssseg_bn_fold_batch': (i32, [vp, i64, vp]),
     'ssseg_bn_eval_bwd': (i32, [vp, vp, vp, vp, vp, i64, i64, i64, vp, vp, vp, i32, i32, vp, vp, sz, vp]),
+    'ssseg_bn_eval_bwd_grad_y': (i32, [vp, vp, vp, vp, i64, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp, sz, vp, vp, vp,
+                                      vp]),
     'ssseg_bn_eval_bwd_grad': (i32, [vp, vp, vp, vp, vp, i64, i64, i64, vp, vp, vp, i32, i32, vp, vp, sz, vp, vp,
                                       vp, vp]),
     'ssseg_bn_eval_param_grad': (i32, [vp, i64, vp, vp, vp, vp, vp]),

@@ -18,7 +18,13 @@ import torch.nn as nn
 
 from . import native as N
 
-_CFG = {'grad_join': True, 'stem': True, 'phases': True, 'dtype': torch.bfloat16, 'sync_bn': True, 'fuse_stats': True}
+_CFG = {'grad_join': True, 'stem': True, 'phases': True, 'eval_bwd_y': True, 'dtype': torch.bfloat16, 'sync_bn': True, 'fuse_stats': True}
+
+
+def set_eval_bwd_from_y(on):
+    """Differentiated eval pass: recover the BN x_hat from y on layers without a residual (default on) instead of
+    keeping the raw accumulator copy."""
+    _CFG['eval_bwd_y'] = bool(on)
 
 
 def set_phase_launch(on):
@@ -453,7 +459,7 @@ class _ConvBase:
 
     def _fold(self, bn, residual, cout, aux=None):
         """Eval BatchNorm (+ this conv's bias) as the epilogue's per-channel affine.  Returns the epilogue
-        tuple and the (scale, mean_eff, invstd) vectors the backward of a differentiated pass uses.
+        tuple and the (scale, mean_eff, invstd, shift) vectors the backward of a differentiated pass uses.
         Inside `folded(model)` the vectors come from that context's single batched launch."""
         if bn.num_features != self.out_channels:
             raise ValueError('conv_bn_act: BatchNorm width != conv out_channels')
@@ -461,7 +467,8 @@ class _ConvBase:
         pre = bn.__dict__.get('_ssseg_fold_live')
         if pre is not None and pre[0] is self and pre[1].numel() == 4 * cout:
             v = pre[1]
-            return (v[:cout], v[cout:2 * cout], residual, aux), (v[:cout], v[2 * cout:3 * cout], v[3 * cout:])
+            return ((v[:cout], v[cout:2 * cout], residual, aux),
+                    (v[:cout], v[2 * cout:3 * cout], v[3 * cout:], v[cout:2 * cout]))
         dev = self.weight.device
         v = torch.empty(4 * cout, dtype=torch.float32, device=dev)
         scale, shift, mean_eff, invstd = v[:cout], v[cout:2 * cout], v[2 * cout:3 * cout], v[3 * cout:]
@@ -469,7 +476,7 @@ class _ConvBase:
         N.call('ssseg_bn_fold', N.dev_ptr(bn.running_mean), N.dev_ptr(bn.running_var), opt(bn.weight), opt(bn.bias),
                opt(self.bias), float(bn.eps), bn.num_features, cout, N.dev_ptr(scale), N.dev_ptr(shift),
                N.dev_ptr(mean_eff), N.dev_ptr(invstd), N.stream())
-        return (scale, shift, residual, aux), (scale, mean_eff, invstd)
+        return (scale, shift, residual, aux), (scale, mean_eff, invstd, shift)
 
 
 def ctypes_ref(d):
@@ -544,7 +551,7 @@ class Conv2d(nn.Conv2d, _ConvBase):
         R, S = self.kernel_size
         return self._pack('dw', 1, 1, self.in_channels, cin, 1, 0, 1, R, 0, 1, S)
 
-    def _dw_forward(self, x, relu, bn, residual, keep_pre):
+    def _dw_forward(self, x, relu, bn, residual, keep_pre, aux_copy=True):
         cin, cout = self._dims()
         n, _, H, W = x.shape
         d = self._dw_desc(n, H, W)
@@ -552,7 +559,7 @@ class Conv2d(nn.Conv2d, _ConvBase):
         aux = bwd = None
         if bn is not None:
             _need_res(residual, y)
-            aux = torch.empty_like(y) if keep_pre else None
+            aux = torch.empty_like(y) if keep_pre and aux_copy else None
             fold, bwd = self._fold(bn, residual, cout, aux)
         else:
             fold = (None, self.bias, None, None)
@@ -568,13 +575,13 @@ class Conv2d(nn.Conv2d, _ConvBase):
                    N.dt_code(x), ctypes_ref(ep), N.stream())
         return (y, aux, bwd) if keep_pre else y
 
-    def _ssseg_forward(self, x, relu, bn=None, residual=None, keep_pre=False, stats=None):
+    def _ssseg_forward(self, x, relu, bn=None, residual=None, keep_pre=False, stats=None, aux_copy=True):
         cin, cout = self._dims()
         _need_act(x, cin, 'Conv2d')
         if self._ssseg_dw:
             if stats is not None:
                 raise NotImplementedError('ssseg: fused BN statistics on a depthwise conv')
-            return self._dw_forward(x, relu, bn, residual, keep_pre)
+            return self._dw_forward(x, relu, bn, residual, keep_pre, aux_copy)
         n, _, H, W = x.shape
         d = self._fwd_desc(n, H, W)
         R, S = self.kernel_size
@@ -588,7 +595,7 @@ class Conv2d(nn.Conv2d, _ConvBase):
         if bn is not None:
             y = new_act(n, cout, d.OH, d.OW, _CFG['dtype'], x.device)
             _need_res(residual, y)
-            aux = torch.empty_like(y) if keep_pre else None
+            aux = torch.empty_like(y) if keep_pre and aux_copy else None
             fold, bwd = self._fold(bn, residual, cout, aux)
             with _Timed(fl, 'fwd', tg):
                 self._igemm(x, w, y, d, N.dt_code(y), relu=relu, fold=fold, stem=stem)
@@ -749,7 +756,7 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
         (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
         return (H - 1) * sh - 2 * ph + R, (W - 1) * sw - 2 * pw + S
 
-    def _ssseg_forward(self, x, relu, bn=None, residual=None, keep_pre=False, stats=None):
+    def _ssseg_forward(self, x, relu, bn=None, residual=None, keep_pre=False, stats=None, aux_copy=True):
         cin, cout = self._dims()
         _need_act(x, cin, 'ConvTranspose2d')
         n, _, H, W = x.shape
@@ -759,7 +766,7 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
         fold = aux = bwd = None
         if bn is not None:
             _need_res(residual, y)
-            aux = torch.empty_like(y) if keep_pre else None
+            aux = torch.empty_like(y) if keep_pre and aux_copy else None
             fold, bwd = self._fold(bn, residual, cout, aux)
         timer = _Timed(_conv_flops(n, H, W, self.out_channels, self.in_channels, R, S), 'fwd', _tag(self, n, H, W))
         timer.__enter__()
@@ -976,15 +983,19 @@ class _ConvBNEvalFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, cweight, cbias, gamma, beta, residual, conv, bn, relu, grad_in=None, grad_out=None, join=None):
-        y, aux, (scale, mean_eff, invstd) = conv._ssseg_forward(x, relu, bn=bn, residual=residual, keep_pre=True)
-        ctx.save_for_backward(x, y, aux, scale, mean_eff, invstd)
+        # without a residual, y itself carries the pre-activation wherever the gradient survives the activation:
+        # no raw accumulator copy (ssseg_bn_eval_bwd_grad_y recovers x_hat from y)
+        ycopy = residual is None and _CFG['eval_bwd_y']
+        y, aux, (scale, mean_eff, invstd, shift) = conv._ssseg_forward(x, relu, bn=bn, residual=residual,
+                                                                       keep_pre=True, aux_copy=not ycopy)
+        ctx.save_for_backward(x, y, aux, scale, mean_eff, invstd, shift)
         ctx.conv, ctx.bn, ctx.relu, ctx.has_res = conv, bn, relu, residual is not None
         ctx.grad_in, ctx.grad_out, ctx.join = grad_in, grad_out, join
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, y, aux, scale, mean_eff, invstd = ctx.saved_tensors
+        x, y, aux, scale, mean_eff, invstd, shift = ctx.saved_tensors
         conv, bn = ctx.conv, ctx.bn
         n, cp, h, w = y.shape
         C = bn.num_features
@@ -998,12 +1009,19 @@ class _ConvBNEvalFn(torch.autograd.Function):
         ws = N.workspace(nb, dev)
         want = lambda p: p is not None and p.requires_grad  # noqa: E731
         # dconv/dres + the BN (and conv-bias) parameter grads in one reduction (ssseg_bn_eval_bwd_grad)
-        N.call('ssseg_bn_eval_bwd_grad', N.dev_ptr(gy), N.dev_ptr(y), N.dev_ptr(aux), N.dev_ptr(dconv),
-               N.dev_ptr(dres) if dres is not None else None, n * h * w, C, cp, N.dev_ptr(scale), N.dev_ptr(mean_eff),
-               N.dev_ptr(invstd), _act(ctx.relu)[0], N.dt_code(y), N.dev_ptr(sums), N.dev_ptr(ws), nb,
-               N.dev_ptr(_grad_of(bn.weight)) if want(bn.weight) else None,
-               N.dev_ptr(_grad_of(bn.bias)) if want(bn.bias) else None,
-               N.dev_ptr(_grad_of(conv.bias)) if want(conv.bias) else None, N.stream())
+        grads = (N.dev_ptr(_grad_of(bn.weight)) if want(bn.weight) else None,
+                 N.dev_ptr(_grad_of(bn.bias)) if want(bn.bias) else None,
+                 N.dev_ptr(_grad_of(conv.bias)) if want(conv.bias) else None)
+        if aux is None:   # x_hat from y (no residual): ssseg_bn_eval_bwd_grad_y
+            N.call('ssseg_bn_eval_bwd_grad_y', N.dev_ptr(gy), N.dev_ptr(y), N.dev_ptr(dconv),
+                   N.dev_ptr(dres) if dres is not None else None, n * h * w, C, cp, N.dev_ptr(scale), N.dev_ptr(shift),
+                   N.dev_ptr(mean_eff), N.dev_ptr(invstd), _act(ctx.relu)[0], N.dt_code(y), N.dev_ptr(sums),
+                   N.dev_ptr(ws), nb, *grads, N.stream())
+        else:
+            N.call('ssseg_bn_eval_bwd_grad', N.dev_ptr(gy), N.dev_ptr(y), N.dev_ptr(aux), N.dev_ptr(dconv),
+                   N.dev_ptr(dres) if dres is not None else None, n * h * w, C, cp, N.dev_ptr(scale),
+                   N.dev_ptr(mean_eff), N.dev_ptr(invstd), _act(ctx.relu)[0], N.dt_code(y), N.dev_ptr(sums),
+                   N.dev_ptr(ws), nb, *grads, N.stream())
         if want(bn.weight) or want(bn.bias):
             _ready(*[p for p in (bn.weight, bn.bias) if want(p)])
         conv._ssseg_wgrad(x, dconv, bias_grad=False)

@@ -642,3 +642,39 @@ def test_convT_phase_launch_bitwise(hip_device, cin, cout, H):
             assert torch.allclose(a, b, rtol=1e-6, atol=1e-8), name
         else:
             assert torch.equal(a, b), name
+
+
+@pytest.mark.parametrize('relu', [True, False])
+def test_eval_bn_backward_from_y_matches_aux(hip_device, mode, relu):
+    """Differentiated eval pass without a residual: x_hat recovered from y (ssseg_bn_eval_bwd_grad_y, no raw
+    accumulator copy) vs the raw-copy path: input, weight, gamma, beta gradients agree to the mode's rounding."""
+    from ssseg import nn as snn
+    torch.manual_seed(9)
+    conv = snn.Conv2d(64, 96, 3, 1, 1, bias=True).to(hip_device)
+    bn = snn.BatchNorm2d(96).to(hip_device)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.3, 0.3)
+        bn.running_mean.uniform_(-0.2, 0.2)
+        bn.running_var.uniform_(0.5, 1.5)
+    bn.eval()
+    x0 = _act_in(torch.randn(2, 64, 15, 17), hip_device)
+    gy = _act_in(torch.randn(2, 96, 15, 17), hip_device)
+    outs = {}
+    try:
+        for ymode in (False, True):
+            snn.set_eval_bwd_from_y(ymode)
+            for p in (conv.weight, conv.bias, bn.weight, bn.bias):
+                p.grad = None
+            x = x0.detach().clone().requires_grad_(True)
+            y = snn.conv_bn_act(conv, x, bn, relu=relu)
+            y.backward(gy)
+            torch.cuda.synchronize()
+            outs[ymode] = [t.detach().float().cpu().clone() for t in
+                           (y, x.grad, conv.weight.grad, conv.bias.grad, bn.weight.grad, bn.bias.grad)]
+    finally:
+        snn.set_eval_bwd_from_y(True)
+    tol = {'f32': 1e-5, 'bf16': 2e-2, 'f16': 4e-3}[mode]
+    for name, a, b in zip(('y', 'dx', 'dW', 'db', 'dgamma', 'dbeta'), outs[False], outs[True]):
+        err = float((a - b).abs().max()) / (float(a.abs().max()) + 1e-12)
+        assert err <= tol, (name, err)
