@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 
 #include "../../include/ssseg.h"
 
@@ -177,7 +178,18 @@ __device__ __forceinline__ T block_sum(T v, T* scratch) {
   return t;
 }
 
-static inline int ssseg_grid(int64_t n, int block, int cap = 256 * 16) {
+// grid-stride launch size: one thread per element up to `cap` workgroups (SSSEG_GRID_CAP overrides the default
+// cap for sweeps)
+static inline int ssseg_grid_cap() {
+  static const int cap = [] {
+    const char* e = getenv("SSSEG_GRID_CAP");
+    const int v = e ? atoi(e) : 256 * 16;
+    return v > 0 ? v : 256 * 16;
+  }();
+  return cap;
+}
+static inline int ssseg_grid(int64_t n, int block, int cap = -1) {
+  if (cap < 0) cap = ssseg_grid_cap();
   int64_t g = (n + block - 1) / block;
   if (g > cap) g = cap;
   if (g < 1) g = 1;

@@ -276,7 +276,7 @@ extern "C" int ssseg_maxpool_fwd(const void* x, void* y, uint8_t* idx, int64_t N
     SSSEG_LAUNCH_CHECK();
     return 0;
   }
-  const dim3 g(ssseg_grid(total, 256, 256 * 16)), b(256);
+  const dim3 g(ssseg_grid(total, 256)), b(256);
   if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(maxpool_fwd_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)x, (bf16_t*)y, idx, (int)N, (int)H,
                        (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
@@ -322,7 +322,7 @@ extern "C" int ssseg_maxpool_bwd_res(const void* gy, const uint8_t* idx, const v
     SSSEG_LAUNCH_CHECK();
     return 0;
   }
-  const dim3 g(ssseg_grid(total, 256, 256 * 16)), b(256);
+  const dim3 g(ssseg_grid(total, 256)), b(256);
   if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(maxpool_bwd_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)gy, idx, (const bf16_t*)res, (bf16_t*)gx, (int)N, (int)H,
                        (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p);
@@ -351,19 +351,19 @@ extern "C" int ssseg_nhwc_copy(const void* src, void* dst, int64_t N, int64_t H,
   const int v = 16 / esz;
   if (C % v == 0 && sld % v == 0 && dld % v == 0 && (((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
     const int64_t t4 = total / v;
-    hipLaunchKernelGGL(nhwc_copy_v16_kernel, dim3(ssseg_grid(t4, 256, 256 * 16)), dim3(256), 0, st, (const uint4*)src,
+    hipLaunchKernelGGL(nhwc_copy_v16_kernel, dim3(ssseg_grid(t4, 256)), dim3(256), 0, st, (const uint4*)src,
                        (uint4*)dst, (int)N, (int)H, (int)W, (int)(C / v), (int)sH, (int)sW, sld / v, (int)soy, (int)sox,
                        (int)dH, (int)dW, dld / v, (int)doy, (int)dox);
   } else if (dt == SSSEG_BF16) {
-    hipLaunchKernelGGL(nhwc_copy_kernel<bf16_t>, dim3(ssseg_grid(total, 256, 256 * 16)), dim3(256), 0, st,
+    hipLaunchKernelGGL(nhwc_copy_kernel<bf16_t>, dim3(ssseg_grid(total, 256)), dim3(256), 0, st,
                        (const bf16_t*)src, (bf16_t*)dst, (int)N, (int)H, (int)W, (int)C, (int)sH, (int)sW, sld, (int)soy,
                        (int)sox, (int)dH, (int)dW, dld, (int)doy, (int)dox);
   } else if (dt == SSSEG_F16) {
-    hipLaunchKernelGGL(nhwc_copy_kernel<f16_t>, dim3(ssseg_grid(total, 256, 256 * 16)), dim3(256), 0, st,
+    hipLaunchKernelGGL(nhwc_copy_kernel<f16_t>, dim3(ssseg_grid(total, 256)), dim3(256), 0, st,
                        (const f16_t*)src, (f16_t*)dst, (int)N, (int)H, (int)W, (int)C, (int)sH, (int)sW, sld, (int)soy,
                        (int)sox, (int)dH, (int)dW, dld, (int)doy, (int)dox);
   } else if (dt == SSSEG_F32) {
-    hipLaunchKernelGGL(nhwc_copy_kernel<float>, dim3(ssseg_grid(total, 256, 256 * 16)), dim3(256), 0, st,
+    hipLaunchKernelGGL(nhwc_copy_kernel<float>, dim3(ssseg_grid(total, 256)), dim3(256), 0, st,
                        (const float*)src, (float*)dst, (int)N, (int)H, (int)W, (int)C, (int)sH, (int)sW, sld, (int)soy,
                        (int)sox, (int)dH, (int)dW, dld, (int)doy, (int)dox);
   } else {
@@ -394,7 +394,7 @@ extern "C" int ssseg_act_bwd(const void* gy, const void* y, void* gx, int64_t n,
   if (!gy || !y || !gx || n < 0 || act < 0 || act > SSSEG_ACT_LEAKY) return SSSEG_EINVAL;
   if (n == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  const dim3 g(ssseg_grid(n, 256, 256 * 16)), b(256);
+  const dim3 g(ssseg_grid(n, 256)), b(256);
   if (dt == SSSEG_BF16)
     hipLaunchKernelGGL(act_bwd_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)gy, (const bf16_t*)y, (bf16_t*)gx, n, act,
                        slope);
