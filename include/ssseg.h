@@ -270,6 +270,16 @@ size_t ssseg_conv_wgrad_workspace_bytes(const ssseg_conv_desc* desc_host, int dt
 int ssseg_conv_wgrad(const void* x, const void* dy, float* dw, const ssseg_conv_desc* desc_host, int dt, int64_t c_real,
                      int64_t k_real, int layout, int accumulate, void* ws, size_t ws_bytes, ssseg_stream_t stream);
 
+/* The same weight gradient over TWO pixel sets in one launch: dw (+)= sum over (x, dy) of batch desc.N plus
+ * (x2, dy2) of batch n2 (same geometry and strides otherwise).  The supervised and the consistency backward
+ * of a student conv (train.py:61 and :115, accumulated into one .grad before clip + SGD) become one
+ * contraction: one split plan over the union of the pixels, one deterministic reduce.  Kernels without the
+ * LDS-DMA path run the two contributions one after the other. */
+size_t ssseg_conv_wgrad2_workspace_bytes(const ssseg_conv_desc* desc_host, int64_t n2, int dt);
+int ssseg_conv_wgrad2(const void* x, const void* dy, const void* x2, const void* dy2, int64_t n2, float* dw,
+                      const ssseg_conv_desc* desc_host, int dt, int64_t c_real, int64_t k_real, int layout,
+                      int accumulate, void* ws, size_t ws_bytes, ssseg_stream_t stream);
+
 /* Pack fp32 master weights into the engine's [Kd][Rn][Sn][Cp] layout (dtype dt; rows >= Kr and
  * channels >= Cd zero): layout 0 reads src[k][c][r][s] (src is [Kr][Cd][Rs][Ss]), layout 1 reads
  * src[c][k][r][s] (src is [Cd][Kr][Rs][Ss]); r = r0 + rr*rstep, s = s0 + ss*sstep. */

@@ -283,10 +283,22 @@ __device__ __forceinline__ int wswz(int r) {
 }
 __device__ __forceinline__ int wkp(int g, int j) { return 16 * (g >> 1) + 8 * (g & 1) + 4 * (j >> 2) + (j & 3); }
 
+// Second pixel segment of a merged launch (ssseg_conv_wgrad2): the supervised and the consistency backward of
+// one conv have the same geometry and differ only in their pixel sets, so their weight gradients are ONE
+// contraction over the union of the pixels.  Splits [0, s1) read (x, dy, g.M), splits [s1, s1 + s2) read
+// (x, dy, M) of this segment; every split writes its own slab and the reduce sums all of them in order.
+struct WSeg2 {
+  const void* x;
+  const void* dy;
+  long long M;
+  unsigned xbytes, dbytes;
+  int s1;   // first split of this segment (0: no second segment)
+};
+
 template <typename T16, int BMW, int BNW, int NS>
 __global__ void __launch_bounds__(256) wgrad_glds_kernel(const T16* __restrict__ x, const T16* __restrict__ dy,
                                                          float* __restrict__ slab, ConvGeom g, long long pix_per_split,
-                                                         WDirect dd, unsigned xbytes, unsigned dbytes) {
+                                                         WDirect dd, unsigned xbytes, unsigned dbytes, WSeg2 sg) {
   constexpr int BKP = 64;                                    // pixels per k-tile
   constexpr int ROWX = BMW * 2, ROWD = BNW * 2;              // LDS row bytes
   constexpr int XCPR = ROWX / 16, DCPR = ROWD / 16;          // 16-byte chunks per row
@@ -305,13 +317,16 @@ __global__ void __launch_bounds__(256) wgrad_glds_kernel(const T16* __restrict__
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
   const int split = tile / (mt * nt), rem = tile - split * (mt * nt);
   const int kk0 = (rem % mt) * BMW, co0 = (rem / mt) * BNW;
-  const long long p_begin = (long long)split * pix_per_split;
-  const long long p_end = min(p_begin + pix_per_split, g.M);
+  const bool seg2 = sg.s1 > 0 && split >= sg.s1;   // block-uniform
+  const long long p_begin = (long long)(seg2 ? split - sg.s1 : split) * pix_per_split;
+  const long long p_end = min(p_begin + pix_per_split, seg2 ? sg.M : g.M);
   const int tap = kk0 / g.C, c0 = kk0 - tap * g.C;
   const int tr = tap / g.S, ts = tap - tr * g.S;
   const int offy = tr * g.dy + g.py, offx = ts * g.dx + g.px;
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)xbytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc((void*)dy, (short)0, (int)dbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(seg2 ? (void*)sg.x : (void*)x, (short)0,
+                                                                      (int)(seg2 ? sg.xbytes : xbytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(seg2 ? (void*)sg.dy : (void*)dy, (short)0,
+                                                                      (int)(seg2 ? sg.dbytes : dbytes), 0x00020000);
 
   // x slot ii of this lane: LDS row (wave*XI + ii)*(64/XCPR) + lane/XCPR, logical chunk (lane%XCPR)^swz;
   // its pixel advances by BKP per k-tile (incremental decode, no per-tile division)
@@ -322,7 +337,7 @@ __global__ void __launch_bounds__(256) wgrad_glds_kernel(const T16* __restrict__
     const int row = (wave * XI + ii) * (64 / XCPR) + lane / XCPR;
     xcb[ii] = (c0 + ((lane % XCPR) ^ wswz<ROWX>(row)) * 8) * 2;
     xp[ii] = p_begin + row;
-    const long long pp = xp[ii] < g.M ? xp[ii] : 0;
+    const long long pp = xp[ii] < p_end ? xp[ii] : 0;
     xox[ii] = (int)(pp % g.OW);
     const long long q = pp / g.OW;
     xoy[ii] = (int)(q % g.OH);
@@ -552,20 +567,20 @@ static WgradPlan choose_wgrad(const ConvGeom& g, int dt) {
 
 template <typename T16, int BMW, int BNW>
 void launch_wgrad_glds_t(const void* x, const void* dy, float* slab, const ConvGeom& g, const WgradPlan& p, WDirect dd,
-                         hipStream_t s) {
+                         hipStream_t s, const WSeg2& sg) {
   constexpr int NS = 64 * (BMW + BNW) * 2 <= 24576 ? 3 : 2;   // 48 / 72 / 64 KB of LDS: 2-3 blocks per CU
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.ldx * 2), db = (unsigned)(g.M * g.ldy * 2);
   hipLaunchKernelGGL((wgrad_glds_kernel<T16, BMW, BNW, NS>), dim3(p.mt * p.nt * p.splits), dim3(256), 0, s,
-                     (const T16*)x, (const T16*)dy, slab, g, p.pps, dd, xb, db);
+                     (const T16*)x, (const T16*)dy, slab, g, p.pps, dd, xb, db, sg);
 }
 
 template <typename T16>
 void launch_wgrad_glds(const void* x, const void* dy, float* slab, const ConvGeom& g, const WgradPlan& p, WDirect dd,
-                       hipStream_t s) {
-  if (p.bmw == 128 && p.bnw == 128) launch_wgrad_glds_t<T16, 128, 128>(x, dy, slab, g, p, dd, s);
-  else if (p.bmw == 128) launch_wgrad_glds_t<T16, 128, 64>(x, dy, slab, g, p, dd, s);
-  else if (p.bnw == 128) launch_wgrad_glds_t<T16, 64, 128>(x, dy, slab, g, p, dd, s);
-  else launch_wgrad_glds_t<T16, 64, 64>(x, dy, slab, g, p, dd, s);
+                       hipStream_t s, const WSeg2& sg = WSeg2{nullptr, nullptr, 0, 0, 0, 0}) {
+  if (p.bmw == 128 && p.bnw == 128) launch_wgrad_glds_t<T16, 128, 128>(x, dy, slab, g, p, dd, s, sg);
+  else if (p.bmw == 128) launch_wgrad_glds_t<T16, 128, 64>(x, dy, slab, g, p, dd, s, sg);
+  else if (p.bnw == 128) launch_wgrad_glds_t<T16, 64, 128>(x, dy, slab, g, p, dd, s, sg);
+  else launch_wgrad_glds_t<T16, 64, 64>(x, dy, slab, g, p, dd, s, sg);
 }
 
 
@@ -627,3 +642,78 @@ extern "C" int ssseg_conv_wgrad(const void* x, const void* dy, float* dw, const 
   return 0;
 }
 
+
+namespace {
+
+// merged launch plan of ssseg_conv_wgrad2: one split plan over the union of both pixel sets (as if the batch were
+// n1 + n2), each segment cut into whole splits of that size.  False when either segment is not LDS-DMA eligible.
+bool merged_plan(const ConvGeom& g1, int64_t n2, int dt, WgradPlan& p, int& s1, ConvGeom& g2) {
+  if (n2 < 1 || n2 > 0x7fffffff || !wgrad_glds_ok(g1, dt)) return false;
+  g2 = g1;
+  g2.N = (int)n2;
+  g2.M = n2 * (long long)g1.OH * g1.OW;
+  if (g2.M >= 0x7fffffffLL || !wgrad_glds_ok(g2, dt)) return false;
+  ConvGeom gm = g1;
+  gm.M = g1.M + g2.M;
+  p = plan_wgrad<bf16_t>(gm, (g1.C % 128 == 0 && g1.KK > 64) ? 128 : 64);
+  p.glds = true;
+  s1 = (int)((g1.M + p.pps - 1) / p.pps);
+  p.splits = s1 + (int)((g2.M + p.pps - 1) / p.pps);
+  return true;
+}
+
+void launch_reduce(const float* slab, const ConvGeom& g, int splits, int64_t c_real, int64_t k_real, float* dw,
+                   int layout, int accumulate, hipStream_t s) {
+  const long long total = (long long)g.K * g.KK;
+  if (splits >= 64)
+    hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)((total + 63) / 64)), dim3(1024), 0, s, slab, splits,
+                       g.K, g.R, g.S, g.C, (int)c_real, (int)k_real, dw, layout, accumulate);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ssseg_grid(total, 256)), dim3(256), 0, s, slab, splits, g.K, g.R, g.S,
+                       g.C, (int)c_real, (int)k_real, dw, layout, accumulate);
+}
+
+}  // namespace
+
+extern "C" size_t ssseg_conv_wgrad2_workspace_bytes(const ssseg_conv_desc* d, int64_t n2, int dt) {
+  ConvGeom g, g2;
+  if (!make_geom(d, g)) return 0;
+  WgradPlan p;
+  int s1;
+  if (merged_plan(g, n2, dt, p, s1, g2)) return (size_t)p.splits * g.K * g.KK * sizeof(float) + 256;
+  ssseg_conv_desc d2 = *d;
+  d2.N = n2;
+  return std::max(ssseg_conv_wgrad_workspace_bytes(d, dt), ssseg_conv_wgrad_workspace_bytes(&d2, dt));
+}
+
+extern "C" int ssseg_conv_wgrad2(const void* x, const void* dy, const void* x2, const void* dy2, int64_t n2, float* dw,
+                                 const ssseg_conv_desc* d, int dt, int64_t c_real, int64_t k_real, int layout,
+                                 int accumulate, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
+  ConvGeom g, g2;
+  if (!make_geom(d, g) || !x || !dy || !x2 || !dy2 || !dw || n2 < 1) return SSSEG_EINVAL;
+  const int vec = dt == SSSEG_F32 ? 4 : 8;
+  if (!wg_geom_ok(g, dt) || g.ldy % vec || g.K % vec) return SSSEG_EINVAL;
+  if (c_real < 1 || c_real > g.C || k_real < 1 || k_real > g.K || (layout != 0 && layout != 1)) return SSSEG_EINVAL;
+  if (!ws || ws_bytes < ssseg_conv_wgrad2_workspace_bytes(d, n2, dt)) return SSSEG_EWORKSPACE;
+  WgradPlan p;
+  int s1;
+  if (!merged_plan(g, n2, dt, p, s1, g2)) {   // other kernels: the two contributions one after the other
+    ssseg_conv_desc d2 = *d;
+    d2.N = n2;
+    const int rc = ssseg_conv_wgrad(x, dy, dw, d, dt, c_real, k_real, layout, accumulate, ws, ws_bytes, stream);
+    if (rc) return rc;
+    return ssseg_conv_wgrad(x2, dy2, dw, &d2, dt, c_real, k_real, layout, 1, ws, ws_bytes, stream);
+  }
+  hipStream_t s = (hipStream_t)stream;
+  float* slab = (float*)ws;
+  const WSeg2 sg{x2, dy2, g2.M, (unsigned)((long long)g2.N * g2.H * g2.W * g2.ldx * 2), (unsigned)(g2.M * g2.ldy * 2),
+                 s1};
+  const WDirect dd{nullptr, (int)c_real, (int)k_real, layout, accumulate};
+  if (dt == SSSEG_F16)
+    launch_wgrad_glds<f16_t>(x, dy, slab, g, p, dd, s, sg);
+  else
+    launch_wgrad_glds<bf16_t>(x, dy, slab, g, p, dd, s, sg);
+  launch_reduce(slab, g, p.splits, c_real, k_real, dw, layout, accumulate, s);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}

@@ -68,6 +68,8 @@ SIGS = {
     'ssseg_set_knob': (i32, [i32, i32]),
     'ssseg_conv_wgrad_workspace_bytes': (sz, [vp, i32]),
     'ssseg_conv_wgrad': (i32, [vp, vp, vp, vp, i32, i64, i64, i32, i32, vp, sz, vp]),
+    'ssseg_conv_wgrad2_workspace_bytes': (sz, [vp, i64, i32]),
+    'ssseg_conv_wgrad2': (i32, [vp, vp, vp, vp, i64, vp, vp, i32, i64, i64, i32, i32, vp, sz, vp]),
     'ssseg_weight_pack': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, i32, i64, i64, i64, i64, i64, i64, i32, vp]),
     # batch norm
     'ssseg_bn_workspace_bytes': (sz, [i64]),

@@ -11,6 +11,7 @@ a registered reducer (ssseg.ddp) is told when each parameter's gradient is compl
 all-reduce of its bucket can start during the rest of the backward pass.
 """
 import contextlib
+import os
 
 import torch
 import torch.distributed as dist
@@ -54,6 +55,48 @@ def compute_dtype():
 
 def set_sync_bn(flag):
     _CFG['sync_bn'] = bool(flag)
+
+
+_WGRAD = {'merge': os.environ.get('SSSEG_WGRAD_MERGE', '1') != '0', 'defer': False, 'pending': []}
+
+
+def set_wgrad_merge(on):
+    """Merge a conv's deferred weight gradient with its next one into a single launch (default on; see
+    defer_wgrad).  Off: defer_wgrad is a no-op and every backward launches its own weight gradients."""
+    _WGRAD['merge'] = bool(on)
+
+
+@contextlib.contextmanager
+def defer_wgrad():
+    """Inside: conv weight gradients are not launched; each conv keeps its (input, output-gradient) pair until
+    its NEXT weight gradient, which then runs as ONE launch over both pixel sets (ssseg_conv_wgrad2).  The
+    training step wraps the supervised backward (reference train.py:61) in this: the consistency backward
+    (train.py:115) accumulates into the same .grad before clip + SGD, so dW_sup + dW_cons is one contraction
+    over the union of the two batches' pixels -- one split plan, half the launches and half the fp32 slab
+    traffic per flop on the small-map layers.  Whatever is still pending when the step needs its gradients is
+    launched by flush_wgrad()."""
+    if not _WGRAD['merge']:
+        yield
+        return
+    prev = _WGRAD['defer']
+    _WGRAD['defer'] = True
+    try:
+        yield
+    finally:
+        _WGRAD['defer'] = prev
+
+
+def flush_wgrad():
+    """Launch every deferred weight gradient on its own (convs that ran no second backward)."""
+    pending, _WGRAD['pending'] = _WGRAD['pending'], []
+    for mod in pending:
+        pair = mod.__dict__.pop('_ssseg_wg_pending', None)
+        if pair is not None:
+            mod._ssseg_wgrad(*pair, bias_grad=False)
+
+
+def wgrad_pending():
+    return sum(1 for m in _WGRAD['pending'] if '_ssseg_wg_pending' in m.__dict__)
 
 
 def set_fused_bn_stats(flag):
@@ -408,6 +451,33 @@ _PACK_EPOCH = [0]   # bumped whenever any conv's set of packed layouts changes (
 
 class _ConvBase:
     """Shared host logic of Conv2d / ConvTranspose2d: packed-weight cache and launches."""
+    def _wg_defer(self, a, b):
+        """Inside defer_wgrad(): keep this weight gradient's operands for a merged launch later."""
+        if not _WGRAD['defer']:
+            return False
+        if '_ssseg_wg_pending' in self.__dict__:   # a second use inside the same deferred pass: run the first
+            _WGRAD['defer'] = False
+            try:
+                self._ssseg_wgrad(*self.__dict__.pop('_ssseg_wg_pending'), bias_grad=False)
+            finally:
+                _WGRAD['defer'] = True
+        self.__dict__['_ssseg_wg_pending'] = (a, b)
+        _WGRAD['pending'].append(self)
+        return True
+
+    def _wg_take(self, a, b):
+        """The deferred (input, output-gradient) pair to merge with (a, b): same spatial geometry, channel
+        padding and dtype (only the batch may differ); an incompatible one is launched on its own first."""
+        pend = self.__dict__.pop('_ssseg_wg_pending', None)
+        if pend is None:
+            return None
+        a1, b1 = pend
+        if (a1.shape[1:] == a.shape[1:] and b1.shape[1:] == b.shape[1:] and a1.dtype == a.dtype
+                and b1.dtype == b.dtype and a1.stride()[1:] == a.stride()[1:] and b1.stride()[1:] == b.stride()[1:]):
+            return pend
+        self._ssseg_wgrad(a1, b1, bias_grad=False)
+        return None
+
 
     def _ssseg_init(self, head=False):
         self._ssseg_head = head           # writes fp32 logits with the real channel count visible
@@ -651,13 +721,30 @@ class Conv2d(nn.Conv2d, _ConvBase):
                        ctypes_ref(d), N.dt_code(x), self.in_channels, 1, N.dev_ptr(ws), nb, N.stream())
             _ready(*[p for p in (self.weight, self.bias) if p is not None])
             return
-        d = self._fwd_desc(n, H, W)
-        nb = N.lib().ssseg_conv_wgrad_workspace_bytes(ctypes_ref(d), N.dt_code(x))
-        ws = N.workspace(nb, x.device)
+        if self._wg_defer(x, gy):
+            return
+        pend = self._wg_take(x, gy)
         R, S = self.kernel_size
-        with _Timed(_conv_flops(n, d.OH, d.OW, self.out_channels, self.in_channels, R, S), 'wgrad', _tag(self, n, H, W)):
-            N.call('ssseg_conv_wgrad', N.dev_ptr(x), N.dev_ptr(gy), N.dev_ptr(_grad_of(self.weight)), ctypes_ref(d),
-                   N.dt_code(x), self.in_channels, self.out_channels, 1, 1, N.dev_ptr(ws), nb, N.stream())
+        if pend is None:
+            d = self._fwd_desc(n, H, W)
+            nb = N.lib().ssseg_conv_wgrad_workspace_bytes(ctypes_ref(d), N.dt_code(x))
+            ws = N.workspace(nb, x.device)
+            with _Timed(_conv_flops(n, d.OH, d.OW, self.out_channels, self.in_channels, R, S), 'wgrad',
+                        _tag(self, n, H, W)):
+                N.call('ssseg_conv_wgrad', N.dev_ptr(x), N.dev_ptr(gy), N.dev_ptr(_grad_of(self.weight)),
+                       ctypes_ref(d), N.dt_code(x), self.in_channels, self.out_channels, 1, 1, N.dev_ptr(ws), nb,
+                       N.stream())
+        else:   # the deferred pass and this one: one launch over both pixel sets
+            x1, gy1 = pend
+            n1 = x1.shape[0]
+            d = self._fwd_desc(n1, H, W)
+            nb = N.lib().ssseg_conv_wgrad2_workspace_bytes(ctypes_ref(d), n, N.dt_code(x))
+            ws = N.workspace(nb, x.device)
+            with _Timed(_conv_flops(n1 + n, d.OH, d.OW, self.out_channels, self.in_channels, R, S), 'wgrad',
+                        _tag(self, n1 + n, H, W)):
+                N.call('ssseg_conv_wgrad2', N.dev_ptr(x1), N.dev_ptr(gy1), N.dev_ptr(x), N.dev_ptr(gy), n,
+                       N.dev_ptr(_grad_of(self.weight)), ctypes_ref(d), N.dt_code(x), self.in_channels,
+                       self.out_channels, 1, 1, N.dev_ptr(ws), nb, N.stream())
         if self.bias is not None:
             _ready(self.weight, self.bias)
         else:
@@ -817,19 +904,34 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
         if bias_grad:
             _bias_grad(self, gy)
         if self.weight.requires_grad:
+            if self._wg_defer(x, gy):
+                return
+            pend = self._wg_take(x, gy)
             cin, cout = self._dims()
             n, _, H, W = x.shape
             (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
             OH, OW = gy.shape[2], gy.shape[3]
+            n1 = pend[0].shape[0] if pend is not None else n
             # dW[ci][co][r][s] = sum_p x[p][ci] * gy[p*s - pad + r][co]: a conv over gy with x as its output grad
-            d = _desc(N=n, H=OH, W=OW, C=cout, ldx=cout, OH=H, OW=W, K=cin, R=R, S=S, sy=sh, sx=sw, dy=1, dx=1,
+            d = _desc(N=n1, H=OH, W=OW, C=cout, ldx=cout, OH=H, OW=W, K=cin, R=R, S=S, sy=sh, sx=sw, dy=1, dx=1,
                       py=-ph, px=-pw, outH=H, outW=W, osy=1, osx=1, ooy=0, oox=0, ldy=cin, ldw=R * S * cout)
-            nb = N.lib().ssseg_conv_wgrad_workspace_bytes(ctypes_ref(d), N.dt_code(x))
-            ws = N.workspace(nb, x.device)
-            with _Timed(_conv_flops(n, H, W, self.out_channels, self.in_channels, R, S), 'wgrad', _tag(self, n, H, W)):
-                N.call('ssseg_conv_wgrad', N.dev_ptr(gy), N.dev_ptr(x), N.dev_ptr(_grad_of(self.weight)),
-                       ctypes_ref(d), N.dt_code(x), self.out_channels, self.in_channels, 1, 1, N.dev_ptr(ws), nb,
-                       N.stream())
+            if pend is None:
+                nb = N.lib().ssseg_conv_wgrad_workspace_bytes(ctypes_ref(d), N.dt_code(x))
+                ws = N.workspace(nb, x.device)
+                with _Timed(_conv_flops(n, H, W, self.out_channels, self.in_channels, R, S), 'wgrad',
+                            _tag(self, n, H, W)):
+                    N.call('ssseg_conv_wgrad', N.dev_ptr(gy), N.dev_ptr(x), N.dev_ptr(_grad_of(self.weight)),
+                           ctypes_ref(d), N.dt_code(x), self.out_channels, self.in_channels, 1, 1, N.dev_ptr(ws), nb,
+                           N.stream())
+            else:   # the deferred pass and this one: one launch over both pixel sets (operands in (gy, x) order)
+                x1, gy1 = pend
+                nb = N.lib().ssseg_conv_wgrad2_workspace_bytes(ctypes_ref(d), n, N.dt_code(x))
+                ws = N.workspace(nb, x.device)
+                with _Timed(_conv_flops(n1 + n, H, W, self.out_channels, self.in_channels, R, S), 'wgrad',
+                            _tag(self, n1 + n, H, W)):
+                    N.call('ssseg_conv_wgrad2', N.dev_ptr(gy1), N.dev_ptr(x1), N.dev_ptr(gy), N.dev_ptr(x), n,
+                           N.dev_ptr(_grad_of(self.weight)), ctypes_ref(d), N.dt_code(x), self.out_channels,
+                           self.in_channels, 1, 1, N.dev_ptr(ws), nb, N.stream())
         _ready(*[p for p in (self.weight, self.bias) if p is not None])
 
     def _ssseg_dgrad(self, gy, xshape):

@@ -10,6 +10,7 @@ Deliberate differences: loss scalars stay on the device and are redu
 print steps (the reference syncs 4x per step for logging only); the DDP gradient all-reduce runs once
 per step, armed on the last backward pass (linear, so the averaged gradient is the same).
 """
+import contextlib
 import time
 
 import torch
@@ -124,7 +125,10 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
         sup_loss = sup_loss + adv_loss
     if ddp is not None and not semi:
         ddp.arm()
-    _scaled(sup_loss / tc['virtual_batch_size_multiplier'], optimizer).backward()
+    # with a consistency backward to follow, each conv's supervised weight gradient is merged into that pass's
+    # (one launch over both batches' pixels; ssseg.nn.defer_wgrad) -- the .grad sum is the same
+    with (snn.defer_wgrad() if semi else contextlib.nullcontext()):
+        _scaled(sup_loss / tc['virtual_batch_size_multiplier'], optimizer).backward()
     del pred_maps, features
     if adv is not None:
         adv['last_loss_d'] = discriminator_step(mask, prob, adv)
@@ -162,6 +166,7 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
         if ddp is not None:
             ddp.arm()
         _scaled(unsup_loss, optimizer).backward()
+    snn.flush_wgrad()
     if ddp is not None:
         ddp.finish()
     if step % tc['virtual_batch_size_multiplier'] == 0 and step != 0:

@@ -4,6 +4,8 @@ max-pool, concat/crop) against the plain PyTorch-CPU fp32 reference of the same 
 Tolerances: fp32 compute mode 1e-4 relative to the output's max magnitude (f32 MFMA is an exact
 fp32 fma chain; the residual difference is summation order); bf16 mode 2e-2, fp16 mode 4e-3 relative RMS.
 """
+import contextlib
+
 import numpy as np
 import pytest
 import torch
@@ -678,3 +680,54 @@ def test_eval_bn_backward_from_y_matches_aux(hip_device, mode, relu):
     for name, a, b in zip(('y', 'dx', 'dW', 'db', 'dgamma', 'dbeta'), outs[False], outs[True]):
         err = float((a - b).abs().max()) / (float(a.abs().max()) + 1e-12)
         assert err <= tol, (name, err)
+
+
+@pytest.mark.parametrize('kind,cin,cout,k,s,H,n1,n2', [('conv', 64, 128, 3, 1, 19, 2, 3), ('conv', 128, 64, 1, 1, 17, 3, 3),
+                                                       ('conv', 128, 256, 3, 2, 18, 2, 1), ('conv', 3, 64, 7, 2, 21, 2, 2),
+                                                       ('convT', 128, 64, 4, 2, 7, 2, 3), ('conv', 64, 64, 3, 1, 64, 4, 4)])
+def test_wgrad_merged_two_passes(hip_device, mode, kind, cin, cout, k, s, H, n1, n2):
+    """defer_wgrad + the next backward: ONE ssseg_conv_wgrad2 launch over both passes' pixels gives the summed
+    weight gradient of the two backward passes (reference train.py:61,115 accumulate into one .grad):
+    checked against fp32 PyTorch-CPU of both passes, and against the two separate launches (merge off)."""
+    from ssseg import nn as snn
+    torch.manual_seed(5)
+    if kind == 'conv':
+        mod = snn.Conv2d(cin, cout, k, s, k // 2, bias=True).to(hip_device)
+        ref = torch.nn.Conv2d(cin, cout, k, s, k // 2, bias=True)
+    else:
+        mod = snn.ConvTranspose2d(cin, cout, k, s, 1, bias=True).to(hip_device)
+        ref = torch.nn.ConvTranspose2d(cin, cout, k, s, 1, bias=True)
+    ref.load_state_dict({kk: v.cpu() for kk, v in mod.state_dict().items()})
+    xs = [torch.randn(n, cin, H, H) for n in (n1, n2)]
+    gs = []
+    for x in xs:
+        y = ref(_q(x, mode))
+        gs.append(torch.randn_like(y))
+        (_q(gs[-1], mode) * y).sum().backward()
+    ref_w = ref.weight.grad.clone()
+
+    def run(merge):
+        snn.set_wgrad_merge(merge)
+        mod.weight.grad = None
+        mod.bias.grad = None
+        try:
+            for i, (x, g) in enumerate(zip(xs, gs)):
+                xa = snn.to_act(x.to(hip_device))
+                y = mod(xa)
+                with (snn.defer_wgrad() if i == 0 else contextlib.nullcontext()):
+                    y.backward(snn.to_act(g.to(hip_device)))
+                if i == 0 and merge:
+                    assert snn.wgrad_pending() == 1
+            snn.flush_wgrad()
+            assert snn.wgrad_pending() == 0
+            return mod.weight.grad.clone(), mod.bias.grad.clone()
+        finally:
+            snn.set_wgrad_merge(True)
+
+    w_m, b_m = run(True)
+    w_s, b_s = run(False)
+    _close(w_m, ref_w, mode, 'merged dW')
+    _close(b_m, ref.bias.grad, mode, 'merged db')
+    _close(w_s, ref_w, mode, 'separate dW')
+    scale = float(w_s.abs().max())
+    assert float((w_m - w_s).abs().max()) <= 1e-5 * scale + 1e-7, 'merged vs separate launches'

@@ -82,10 +82,14 @@ def main():
           f'algorithmic bytes {tot_b / 1e9:.2f} GB ({tot_b / tot_ms / 1e9:.2f} TB/s over the conv time)')
     for k, (ms, fl) in sorted(by_kind.items(), key=lambda kv: -kv[1][0]):
         print(f'  {k:6s} {ms:8.3f} ms  {fl / 1e9:8.1f} GFLOP  {fl / ms / 1e9:7.1f} TF/s')
-    print(f'{"ms":>8s} {"pct":>6s} {"calls":>5s} {"GFLOP":>8s} {"TF/s":>7s} {"alg MB":>8s} {"TB/s":>6s}  kind   layer')
+    # roofline floor per layer: max(flops / dense bf16 peak, algorithmic bytes / 8 TB/s)
+    roof = {key: max(v[1] / 2.5e12, v[3] / 8e9) for key, v in agg.items()}
+    tot_roof = sum(roof.values())
+    print(f'roofline floor (max of 2.5 PF/s and 8 TB/s per layer): {tot_roof:.3f} ms = {tot_roof / tot_ms:.3f} of the conv time')
+    print(f'{"ms":>8s} {"pct":>6s} {"calls":>5s} {"GFLOP":>8s} {"TF/s":>7s} {"alg MB":>8s} {"TB/s":>6s} {"roof":>5s}  kind   layer')
     for (kind, tag), (ms, fl, n, by) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:a.top]:
         print(f'{ms:8.3f} {100 * ms / tot_ms:6.2f} {n:5d} {fl / 1e9:8.1f} {fl / ms / 1e9:7.1f} {by / 1e6:8.1f} '
-              f'{by / ms / 1e9:6.2f}  {kind:6s} {tag}')
+              f'{by / ms / 1e9:6.2f} {roof[(kind, tag)] / ms:5.2f}  {kind:6s} {tag}')
 
 
 if __name__ == '__main__':
