@@ -320,10 +320,17 @@ template <> struct Out8<float> {
   }
 };
 
-template <typename TO, int BM, int BN, int FM, int FN, int NT, bool STATS>
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+template <int NP> struct PreRes {   // residual chunks an epilogue thread loaded ahead of the main loop
+  u32x4 v[NP];
+  bool on;
+};
+
+template <typename TO, int BM, int BN, int FM, int FN, int NT, bool STATS, int NPRE = 1>
 __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char* smem, long long m0, int n0, int wmo,
                                                int wno, int lane, const ConvGeom& g, TO* __restrict__ y,
-                                               const Epi<TO>& ep) {
+                                               const Epi<TO>& ep, PreRes<NPRE> pre = PreRes<NPRE>{{}, false}) {
+  // pre: this thread's residual chunks, already loaded by the caller (one per pass; used where `full`)
   constexpr int LDR = BN * 4 + 16;   // bytes per staged pixel row
   __syncthreads();                   // every wave is done with the LDS ring
 #pragma unroll
@@ -365,9 +372,18 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
 #pragma unroll
       for (int e = 0; e < 8; ++e) r[p][e] = 0.f;
       if (ep.res && op[p] >= 0) {
-        if (full)
-          Out8<TO>::ld(ep.res + op[p] * ep.ldr + n, r[p]);
-        else
+        if (full) {
+          if constexpr (sizeof(TO) == 2) {
+            if (pre.on) {
+              const u32x4 q = pre.v[p < NPRE ? p : 0];
+              Chunk<TO, 8>::cvt(make_uint4(q.x, q.y, q.z, q.w), r[p]);
+            } else {
+              Out8<TO>::ld(ep.res + op[p] * ep.ldr + n, r[p]);
+            }
+          } else {
+            Out8<TO>::ld(ep.res + op[p] * ep.ldr + n, r[p]);
+          }
+        } else
           for (int e = 0; e < 8 && n + e < g.K; ++e) r[p][e] = io<TO>::ld(ep.res, op[p] * ep.ldr + n + e);
       }
     }
@@ -798,6 +814,33 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
 #pragma unroll
     for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // single-slot configs (one or two k-tiles: the 1x1 layers) with a residual: the LDS-staged epilogue's
+  // residual chunks are loaded here, in flight with the operand DMA, instead of after the MFMAs -- one dependent
+  // HBM round trip less per tile in a kernel whose tiles are a load -> multiply -> store chain
+  constexpr int EP_CPR = BN / 8, EP_RPP = NW * 64 / EP_CPR, EP_NP = (BM + EP_RPP - 1) / EP_RPP;
+  constexpr bool PRE = NS == 1 && EPI <= SMEM && (NW * 64) % EP_CPR == 0 && 64 % EP_CPR == 0;
+  PreRes<PRE ? EP_NP : 1> pre;
+  pre.on = false;
+  if constexpr (PRE) {
+    if (g_epi_lds && ep.res && splits == 1) {
+      const int ch = t % EP_CPR, r0 = t / EP_CPR;
+      const int n = n0 + ch * 8;
+      pre.on = (g.ldy & 7) == 0 && (ep.ldr & 7) == 0 && n + 7 < g.K;
+#pragma unroll
+      for (int p = 0; p < EP_NP; ++p) {
+        const int row = r0 + p * EP_RPP;
+        const long long m = m0 + row;
+        pre.v[p] = u32x4{0u, 0u, 0u, 0u};
+        if (pre.on && row < BM && m < g.M) {
+          const int ox = (int)m % g.OW;
+          const int q = (int)m / g.OW;
+          const int oy = q % g.OH, img = q / g.OH;
+          const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+          pre.v[p] = *(const u32x4*)(ep.res + op * ep.ldr + n);
+        }
+      }
+    }
+  }
   const int rsw = ((lane & 15) >> 1) & 7;   // read-side swizzle of this lane's fragment row
   auto compute = [&](int buf) {
     const char* As = smem + buf * STAGE;
@@ -858,7 +901,8 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
   }
   if constexpr (EPI <= SMEM) {
     if (g_epi_lds) {
-      store_tile_lds<TO, BM, BN, FM, FN, NW * 64, STATS>(acc, smem, m0, n0, wm * WTM, wn * WTN, lane, g, y, ep);
+      store_tile_lds<TO, BM, BN, FM, FN, NW * 64, STATS, PRE ? EP_NP : 1>(acc, smem, m0, n0, wm * WTM, wn * WTN,
+                                                                          lane, g, y, ep, pre);
       return;
     }
   }
