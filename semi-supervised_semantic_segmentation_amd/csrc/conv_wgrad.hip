@@ -510,7 +510,7 @@ struct WgradPlan {
 };
 
 template <typename T>
-WgradPlan plan_wgrad(const ConvGeom& g, int bmw = 0) {
+WgradPlan plan_wgrad(const ConvGeom& g, int bmw = 0, long long slots = 0) {
   WgradPlan p;
   p.glds = false;
   p.bnw = g.K <= 64 ? 64 : 128;
@@ -521,6 +521,13 @@ WgradPlan plan_wgrad(const ConvGeom& g, int bmw = 0) {
   const int bkp = WG<T>::BKP;
   const long long max_splits_by_work = std::max<long long>(1, g.M / (bkp * 8));   // >= 8 k-tiles per split
   long long want = std::max<long long>(1, (1024 + tiles - 1) / tiles);
+  if (slots > 0 && tiles < 1024) {
+    // every split does the same work, so blocks run in whole rounds of `slots` (resident blocks on the chip):
+    // round the block count DOWN to R full rounds (R ~ 1024 / slots) -- 1026 blocks over 512 slots ran a
+    // third, 2 %-full round (measured 0.70 of the rounds busy on the 128->64 3x3 @256^2 weight gradient)
+    const long long rounds = std::max<long long>(1, (1024 + slots / 2) / slots);
+    want = std::max<long long>(1, rounds * slots / tiles);
+  }
   const long long slab_cap = std::max<long long>(1, (64ll << 20) / (4ll * g.K * g.KK + 1));  // <= 64 MiB of slabs
   // (capping splits by slab traffic measured slower: layer3/4 wgrads need the parallelism, 58 -> 150 us)
   long long sp = std::min(std::min(want, max_splits_by_work), slab_cap);
@@ -554,15 +561,42 @@ static bool wgrad_glds_ok(const ConvGeom& g, int dt) {
   return xb < 0x7fffffffLL && db < 0x7fffffffLL;
 }
 
+long long wgrad_slots(int bmw, int bnw);
+
 static WgradPlan choose_wgrad(const ConvGeom& g, int dt) {
   WgradPlan p;
   if (wgrad_glds_ok(g, dt)) {
-    p = plan_wgrad<bf16_t>(g, (g.C % 128 == 0 && g.KK > 64) ? 128 : 64);
+    const int bmw = (g.C % 128 == 0 && g.KK > 64) ? 128 : 64;
+    p = plan_wgrad<bf16_t>(g, bmw, wgrad_slots(bmw, g.K <= 64 ? 64 : 128));
     p.glds = true;
   } else {
     p = dt != SSSEG_F32 ? plan_wgrad<bf16_t>(g) : plan_wgrad<float>(g);
   }
   return p;
+}
+
+// resident blocks of the LDS-DMA wgrad kernel chosen for (bmw, bnw) on the whole device (cached per config)
+template <typename T16, int BMW, int BNW>
+long long wgrad_slots_t() {
+  static long long slots = -1;
+  if (slots < 0) {
+    constexpr int NS = 64 * (BMW + BNW) * 2 <= 24576 ? 3 : 2;
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wgrad_glds_kernel<T16, BMW, BNW, NS>, 256, 0) !=
+            hipSuccess)
+      return 0;   // unknown: the unquantized plan
+    slots = (long long)per_cu * cus;
+  }
+  return slots;
+}
+
+long long wgrad_slots(int bmw, int bnw) {
+  if (bmw == 128 && bnw == 128) return wgrad_slots_t<bf16_t, 128, 128>();
+  if (bmw == 128) return wgrad_slots_t<bf16_t, 128, 64>();
+  if (bnw == 128) return wgrad_slots_t<bf16_t, 64, 128>();
+  return wgrad_slots_t<bf16_t, 64, 64>();
 }
 
 template <typename T16, int BMW, int BNW>
@@ -655,10 +689,18 @@ bool merged_plan(const ConvGeom& g1, int64_t n2, int dt, WgradPlan& p, int& s1, 
   if (g2.M >= 0x7fffffffLL || !wgrad_glds_ok(g2, dt)) return false;
   ConvGeom gm = g1;
   gm.M = g1.M + g2.M;
-  p = plan_wgrad<bf16_t>(gm, (g1.C % 128 == 0 && g1.KK > 64) ? 128 : 64);
+  const int bmw = (g1.C % 128 == 0 && g1.KK > 64) ? 128 : 64;
+  p = plan_wgrad<bf16_t>(gm, bmw, wgrad_slots(bmw, g1.K <= 64 ? 64 : 128));
   p.glds = true;
-  s1 = (int)((g1.M + p.pps - 1) / p.pps);
-  p.splits = s1 + (int)((g2.M + p.pps - 1) / p.pps);
+  // the plan's split count shared out in proportion to the segments' pixels, never more splits in total
+  // (a split past the plan's rounds would start a nearly empty extra round)
+  const long long sp = std::max(2, p.splits);
+  long long a = std::min(sp - 1, std::max(1LL, (long long)((double)sp * g1.M / gm.M + 0.5)));
+  long long pps = std::max((g1.M + a - 1) / a, (g2.M + (sp - a) - 1) / (sp - a));
+  pps = (pps + 63) / 64 * 64;
+  p.pps = pps;
+  s1 = (int)((g1.M + pps - 1) / pps);
+  p.splits = s1 + (int)((g2.M + pps - 1) / pps);
   return true;
 }
 
