@@ -150,6 +150,10 @@ int ssseg_ema_update(float* ema, const float* param, int64_t n, double alpha, ss
 int ssseg_sigmoid_fwd(const float* x, float* y, int64_t n, ssseg_stream_t stream);
 int ssseg_sigmoid_bwd(const float* y, const float* gy, float* gx, int64_t n, ssseg_stream_t stream);
 
+/* out = a*x + b*y over n fp32 (y may be NULL: out = a*x; out may alias x or y): the weighted sums of the
+ * loss terms (CalculateLoss weights losses.py:19, 1/virtual_batch_size_multiplier train.py:61, consistency
+ * weight x float(epoch > 25) train.py:112) and their backward. */
+int ssseg_axpby(const float* x, float a, const float* y, float b, float* out, int64_t n, ssseg_stream_t stream);
 /* x[i] *= a (in place): the 1/world average after a SUM all-reduce on backends without AVG (gloo). */
 int ssseg_scale_f32(float* x, int64_t n, float a, ssseg_stream_t stream);
 

@@ -276,6 +276,14 @@ __global__ void scale_by_kernel(const float* __restrict__ x, const float* __rest
     y[i] = x[i] * a;
 }
 
+// out = a*x + b*y (y optional): the loss-term arithmetic of the step (weights, 1/virtual batch, epoch gate) and
+// its backward, so no framework elementwise kernel runs on the hot path
+__global__ void axpby_kernel(const float* __restrict__ x, float a, const float* __restrict__ y, float b,
+                             float* __restrict__ out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = y ? fmaf(a, x[i], b * y[i]) : a * x[i];
+}
+
 __global__ void scale_kernel(float* __restrict__ x, int64_t n, float a) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     x[i] = __fmul_rn(x[i], a);
@@ -312,6 +320,15 @@ extern "C" int ssseg_scale_by(const float* x, const float* s, float* y, int64_t 
   if (!x || !s || !y || n < 0) return SSSEG_EINVAL;
   if (n == 0) return 0;
   hipLaunchKernelGGL(scale_by_kernel, dim3(ssseg_grid(n, 256)), dim3(256), 0, (hipStream_t)stream, x, s, y, n);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_axpby(const float* x, float a, const float* y, float b, float* out, int64_t n,
+                           ssseg_stream_t stream) {
+  if (!x || !out || n < 0) return SSSEG_EINVAL;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(axpby_kernel, dim3(ssseg_grid(n, 256)), dim3(256), 0, (hipStream_t)stream, x, a, y, b, out, n);
   SSSEG_LAUNCH_CHECK();
   return 0;
 }

@@ -18,13 +18,15 @@ class CalculateLoss:
         self.losses = losses
 
     def __call__(self, predictions_list, target):
-        total = 0
+        total = None
         size = (target.size(2), target.size(3))
         for idx, prediction in enumerate(predictions_list):
             prediction = ops.interpolate_bilinear(prediction, size, align_corners=False)
             for spec in self.losses:
-                total = total + spec['loss_fn'](prediction, target) * spec['weight'][idx]
-        return total
+                term, w = spec['loss_fn'](prediction, target), float(spec['weight'][idx])
+                # total + term * w on the device (ssseg_axpby): same fp32 arithmetic as the reference's
+                total = ops.scale(term, w) if total is None else ops.add_scaled(total, term, w)
+        return total if total is not None else 0
 
 
 class DenseBinaryCrossEntropyLossWithLogits(nn.Module):

@@ -48,6 +48,7 @@ SIGS = {
     'ssseg_seg_metrics': (i32, [vp, I64P, i64, i64, vp, I64P, i64, i64, i64, vp, vp, vp, vp]),
     'ssseg_ema_update': (i32, [vp, vp, i64, f64, vp]),
     'ssseg_scale_f32': (i32, [vp, i64, f32, vp]),
+    'ssseg_axpby': (i32, [vp, f32, vp, f32, vp, i64, vp]),
     'ssseg_sigmoid_fwd': (i32, [vp, vp, i64, vp]),
     'ssseg_sigmoid_bwd': (i32, [vp, vp, vp, i64, vp]),
     'ssseg_sqnorm_accum': (i32, [vp, i64, vp, vp, sz, vp]),

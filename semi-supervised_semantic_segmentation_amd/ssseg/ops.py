@@ -58,6 +58,53 @@ def mix(a, b, mask):
 # ------------------------------------------------------------------------------------------------
 # Bilinear interpolation (F.interpolate mode='bilinear')
 # ------------------------------------------------------------------------------------------------
+def _axpby(x, a, y=None, b=0.0):
+    out = torch.empty_like(x)
+    N.call('ssseg_axpby', N.dev_ptr(x), float(a), N.dev_ptr(y) if y is not None else None, float(b), N.dev_ptr(out),
+           x.numel(), N.stream())
+    return out
+
+
+class _Axpby(torch.autograd.Function):
+    """a*x (+ b*y): the loss-term arithmetic on the device (no framework elementwise kernels)"""
+    @staticmethod
+    def forward(ctx, x, a, y, b):
+        ctx.a, ctx.b, ctx.has_y = a, b, y is not None
+        return _axpby(_c(x), a, _c(y) if y is not None else None, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _c(g)
+        gx = _axpby(g, ctx.a) if ctx.a != 1.0 else g
+        gy = None
+        if ctx.has_y:
+            gy = _axpby(g, ctx.b) if ctx.b != 1.0 else g
+        return gx, None, gy, None
+
+
+def scale(x, a):
+    """a * x for a device loss tensor (autograd)."""
+    return _Axpby.apply(x, float(a), None, 0.0)
+
+
+def add_scaled(x, y, b=1.0):
+    """x + b * y for device loss tensors (autograd)."""
+    return _Axpby.apply(x, 1.0, y, float(b))
+
+
+_ONES = {}
+
+
+def backward(loss):
+    """loss.backward() seeded from a cached device 1.0 (autograd's own seed is a framework fill kernel)."""
+    key = (loss.device, loss.dtype, tuple(loss.shape))
+    one = _ONES.get(key)
+    if one is None:
+        one = torch.ones_like(loss)
+        _ONES[key] = one
+    loss.backward(one)
+
+
 class _Bilinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, size, align_corners):
@@ -175,6 +222,7 @@ class _Consistency(torch.autograd.Function):
         ctx.save_for_backward(s, t, out)
         ctx.meta = (B, C, HW, float(thr))
         ctx.mark_non_differentiable(out)
+        ctx.set_materialize_grads(False)   # no zero-filled gradient for the cm output (a framework fill kernel)
         return out[0], out[1]
 
     @staticmethod

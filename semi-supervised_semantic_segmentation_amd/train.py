@@ -74,7 +74,7 @@ def adversarial_terms(pred_maps, mask, adv):
     prob = ops.sigmoid(logits)
     _set_requires_grad(D, False)
     d_fake = D(prob)
-    adv_loss = ops.bce_with_logits_mean(d_fake, _target(d_fake, 1.0)) * adv['weight']
+    adv_loss = ops.scale(ops.bce_with_logits_mean(d_fake, _target(d_fake, 1.0)), adv['weight'])
     _set_requires_grad(D, True)
     return adv_loss, prob.detach()
 
@@ -88,11 +88,11 @@ def discriminator_step(mask, prob, adv):
     ddp = D if isinstance(D, _DDP) else None
     d_real = D(mask)
     d_fake = D(prob)
-    loss_d = ops.bce_with_logits_mean(d_real, _target(d_real, 1.0)) + \
-        ops.bce_with_logits_mean(d_fake, _target(d_fake, 0.0))
+    loss_d = ops.add_scaled(ops.bce_with_logits_mean(d_real, _target(d_real, 1.0)),
+                            ops.bce_with_logits_mean(d_fake, _target(d_fake, 0.0)))
     if ddp is not None:
         ddp.arm()
-    _scaled(loss_d, opt).backward()
+    ops.backward(_scaled(loss_d, opt))
     if ddp is not None:
         ddp.finish()
     opt.step()
@@ -122,13 +122,14 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
     prob = None
     if adv is not None:
         adv_loss, prob = adversarial_terms(pred_maps, mask, adv)
-        sup_loss = sup_loss + adv_loss
+        sup_loss = ops.add_scaled(sup_loss, adv_loss)
     if ddp is not None and not semi:
         ddp.arm()
     # with a consistency backward to follow, each conv's supervised weight gradient is merged into that pass's
     # (one launch over both batches' pixels; ssseg.nn.defer_wgrad) -- the .grad sum is the same
     with (snn.defer_wgrad() if semi else contextlib.nullcontext()):
-        _scaled(sup_loss / tc['virtual_batch_size_multiplier'], optimizer).backward()
+        vbm = tc['virtual_batch_size_multiplier']
+        ops.backward(_scaled(ops.scale(sup_loss, 1.0 / vbm) if vbm != 1 else sup_loss, optimizer))
     del pred_maps, features
     if adv is not None:
         adv['last_loss_d'] = discriminator_step(mask, prob, adv)
@@ -162,10 +163,11 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
         model.train()
         student_pred = ops.interpolate_bilinear(student_pred, mixed_images.shape[2:4], align_corners=False)
         consistency, cm_mean = ops.consistency_loss(student_pred, mixed_ema_pred, tc['confidence_threshold'])
-        unsup_loss = consistency * tc['consistency_loss_weight'] * float(epoch > 25)
+        # consistency * weight * float(epoch > 25) (train.py:112; a 0/0 NaN survives the 0.0 gate, as there)
+        unsup_loss = ops.scale(consistency, float(tc['consistency_loss_weight']) * float(epoch > 25))
         if ddp is not None:
             ddp.arm()
-        _scaled(unsup_loss, optimizer).backward()
+        ops.backward(_scaled(unsup_loss, optimizer))
     snn.flush_wgrad()
     if ddp is not None:
         ddp.finish()
