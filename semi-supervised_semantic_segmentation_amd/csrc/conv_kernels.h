@@ -52,7 +52,29 @@ struct ConvGeom {
   int ldw;
   long long M;   // N*OH*OW
   int KK;        // R*S*C
+  // division by OW / OH as multiply-high + shift (set by make_geom; exact for 0 <= n < 2^31): the output-pixel
+  // decode m -> (img, oy, ox) of every tile row otherwise costs two integer divisions (~40 VALU each)
+  unsigned mow, moh;
+  int sow, soh;
 };
+
+// magic multiplier for unsigned division by d >= 1: n / d = (umulhi(n, m) + n) >> s for n < 2^31
+static inline void fdiv_init(int d, unsigned& m, int& s) {
+  int l = 0;
+  while ((1ll << l) < (long long)d) ++l;
+  m = (unsigned)((((unsigned long long)1 << (32 + l)) / (unsigned long long)d) - ((unsigned long long)1 << 32) + 1);
+  s = l;
+}
+__device__ __forceinline__ int fdiv(int n, unsigned m, int s) {
+  return (int)((__umulhi((unsigned)n, m) + (unsigned)n) >> s);
+}
+// output-pixel decode of GEMM row m (0 <= m < M < 2^31)
+__device__ __forceinline__ void decode_m(const ConvGeom& g, int m, int& img, int& oy, int& ox) {
+  const int q = fdiv(m, g.mow, g.sow);
+  ox = m - q * g.OW;
+  img = fdiv(q, g.moh, g.soh);
+  oy = q - img * g.OH;
+}
 
 static inline bool make_geom(const ssseg_conv_desc* d, ConvGeom& g) {
   if (!d) return false;
@@ -68,6 +90,8 @@ static inline bool make_geom(const ssseg_conv_desc* d, ConvGeom& g) {
   g.oox = (int)d->oox; g.ldy = (int)d->ldy; g.ldw = (int)d->ldw;
   g.M = (long long)d->N * d->OH * d->OW;
   g.KK = (int)(d->R * d->S * d->C);
+  fdiv_init(g.OW > 0 ? g.OW : 1, g.mow, g.sow);
+  fdiv_init(g.OH > 0 ? g.OH : 1, g.moh, g.soh);
   return true;
 }
 
@@ -218,9 +242,8 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[FN][FM], long long
     const long long m = mb + j * 16 + (lane & 15);
     op[j] = -1;
     if (m < g.M) {
-      const int ox = (int)m % g.OW;    // 32-bit decode: geom_ok guarantees M < 2^31
-      const int q = (int)m / g.OW;
-      const int oy = q % g.OH, img = q / g.OH;
+      int img, oy, ox;   // M < 2^31 (geom_ok): 32-bit decode
+      decode_m(g, (int)m, img, oy, ox);
       op[j] = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
     }
   }
@@ -364,9 +387,8 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
       const long long m = m0 + row;
       op[p] = -1;
       if (row < BM && m < g.M) {
-        const int ox = (int)m % g.OW;    // 32-bit decode: geom_ok guarantees M < 2^31
-        const int q = (int)m / g.OW;
-        const int oy = q % g.OH, img = q / g.OH;
+        int img, oy, ox;   // M < 2^31 (geom_ok): 32-bit decode
+        decode_m(g, (int)m, img, oy, ox);
         op[p] = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
       }
 #pragma unroll
@@ -548,10 +570,7 @@ __global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __res
     const long long m = m0 + (t >> 2) + 64 * i;
     a_ok[i] = m < g.M;
     const long long mm = a_ok[i] ? m : 0;
-    a_ox[i] = (int)mm % g.OW;
-    const int q = (int)mm / g.OW;
-    a_oy[i] = q % g.OH;
-    a_n[i] = q / g.OH;
+    decode_m(g, (int)mm, a_n[i], a_oy[i], a_ox[i]);
   }
   // k-state of this thread's chunk: k = tap*C + kc, tap = r*S + s (advanced by every load, in order)
   const int k_first = kt0 * BK + chunk * VEC;
@@ -757,9 +776,8 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
     const int ch = c_even ^ ((inst & 1) * 4);
     const long long m = m0 + 8 * inst + (lane >> 3);
     if (m < g.M) {
-      const int ox = (int)m % g.OW;
-      const int q = (int)m / g.OW;
-      const int oy = q % g.OH, img = q / g.OH;
+      int img, oy, ox;   // M < 2^31 (geom_ok): 32-bit decode
+      decode_m(g, (int)m, img, oy, ox);
       a_iy[ii] = oy * g.sy + g.py;
       a_ix[ii] = ox * g.sx + g.px;
       a_off[ii] = ((img * g.H + a_iy[ii]) * g.W + a_ix[ii]) * g.ldx * 2 + ch * 16;
@@ -832,9 +850,8 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
         const long long m = m0 + row;
         pre.v[p] = u32x4{0u, 0u, 0u, 0u};
         if (pre.on && row < BM && m < g.M) {
-          const int ox = (int)m % g.OW;
-          const int q = (int)m / g.OW;
-          const int oy = q % g.OH, img = q / g.OH;
+          int img, oy, ox;   // M < 2^31 (geom_ok): 32-bit decode
+          decode_m(g, (int)m, img, oy, ox);
           const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
           pre.v[p] = *(const u32x4*)(ep.res + op * ep.ldr + n);
         }
@@ -926,9 +943,8 @@ __global__ void splitk_finalize_kernel(const float* __restrict__ ws, TO* __restr
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
     const int n = (int)(i % g.K);
     const long long m = i / g.K;
-    const int ox = (int)m % g.OW;    // 32-bit decode: geom_ok guarantees M < 2^31
-    const int q = (int)m / g.OW;
-    const int oy = q % g.OH, img = q / g.OH;
+    int img, oy, ox;   // M < 2^31 (geom_ok): 32-bit decode
+    decode_m(g, (int)m, img, oy, ox);
     const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
     float v = ws[i];
     if (ep.aux) io<TO>::st(ep.aux, op * g.ldy + n, v);
@@ -949,9 +965,8 @@ __global__ void phase_zero_vec_kernel(TO* y, ConvGeom g, Epi<TO> ep) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
     const int n = (int)(i % kc) * 8;
     const long long m = i / kc;
-    const int ox = (int)m % g.OW;    // 32-bit decode: geom_ok guarantees M < 2^31
-    const int q = (int)m / g.OW;
-    const int oy = q % g.OH, img = q / g.OH;
+    int img, oy, ox;   // M < 2^31 (geom_ok): 32-bit decode
+    decode_m(g, (int)m, img, oy, ox);
     const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
     float r[8], v[8];
     if (ep.res) Out8<TO>::ld(ep.res + op * ep.ldr + n, r);
@@ -975,9 +990,8 @@ __global__ void phase_zero_kernel(TO* y, ConvGeom g, Epi<TO> ep) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
     const int n = (int)(i % g.K);
     const long long m = i / g.K;
-    const int ox = (int)m % g.OW;    // 32-bit decode: geom_ok guarantees M < 2^31
-    const int q = (int)m / g.OW;
-    const int oy = q % g.OH, img = q / g.OH;
+    int img, oy, ox;   // M < 2^31 (geom_ok): 32-bit decode
+    decode_m(g, (int)m, img, oy, ox);
     const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
     float v = ep.shift ? ep.shift[n] : 0.f;
     if (ep.aux) io<TO>::st(ep.aux, op * g.ldy + n, 0.f);

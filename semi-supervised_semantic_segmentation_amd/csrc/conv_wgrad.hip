@@ -66,10 +66,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ x, con
   for (int i = 0; i < X_IT; ++i) {
     xp[i] = p_begin + t / XCH + i * (256 / XCH);
     const long long pp = xp[i] < g.M ? xp[i] : 0;
-    xox[i] = (int)(pp % g.OW);
-    const long long q = pp / g.OW;
-    xoy[i] = (int)(q % g.OH);
-    ximg[i] = (int)(q / g.OH);
+    decode_m(g, (int)pp, ximg[i], xoy[i], xox[i]);   // M < 2^31 (wg_geom_ok)
   }
 #pragma unroll
   for (int i = 0; i < D_IT; ++i) dp[i] = p_begin + t / DCH + i * (256 / DCH);
@@ -338,10 +335,7 @@ __global__ void __launch_bounds__(256) wgrad_glds_kernel(const T16* __restrict__
     xcb[ii] = (c0 + ((lane % XCPR) ^ wswz<ROWX>(row)) * 8) * 2;
     xp[ii] = p_begin + row;
     const long long pp = xp[ii] < p_end ? xp[ii] : 0;
-    xox[ii] = (int)(pp % g.OW);
-    const long long q = pp / g.OW;
-    xoy[ii] = (int)(q % g.OH);
-    ximg[ii] = (int)(q / g.OH);
+    decode_m(g, (int)pp, ximg[ii], xoy[ii], xox[ii]);   // M < 2^31 (wg_geom_ok)
   }
   long long dp[DI];
   int dcb[DI];
