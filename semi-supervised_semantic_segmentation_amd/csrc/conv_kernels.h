@@ -56,6 +56,8 @@ struct ConvGeom {
   // decode m -> (img, oy, ox) of every tile row otherwise costs two integer divisions (~40 VALU each)
   unsigned mow, moh;
   int sow, soh;
+  int oident;   // output pixel == GEMM row (stride-1 output grid, no offsets): no decode in the epilogue
+  int aident;   // 1x1 stride-1 unpadded gather over the same grid: A row m is input pixel m
 };
 
 // magic multiplier for unsigned division by d >= 1: n / d = (umulhi(n, m) + n) >> s for n < 2^31
@@ -75,6 +77,13 @@ __device__ __forceinline__ void decode_m(const ConvGeom& g, int m, int& img, int
   img = fdiv(q, g.moh, g.soh);
   oy = q - img * g.OH;
 }
+// output pixel (row of y) of GEMM row m: m itself on the identity grid (every forward conv, stride-1 dgrad)
+__device__ __forceinline__ long long out_pixel(const ConvGeom& g, int m) {
+  if (g.oident) return m;
+  int img, oy, ox;
+  decode_m(g, m, img, oy, ox);
+  return ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+}
 
 static inline bool make_geom(const ssseg_conv_desc* d, ConvGeom& g) {
   if (!d) return false;
@@ -92,6 +101,9 @@ static inline bool make_geom(const ssseg_conv_desc* d, ConvGeom& g) {
   g.KK = (int)(d->R * d->S * d->C);
   fdiv_init(g.OW > 0 ? g.OW : 1, g.mow, g.sow);
   fdiv_init(g.OH > 0 ? g.OH : 1, g.moh, g.soh);
+  g.oident = g.osy == 1 && g.osx == 1 && g.ooy == 0 && g.oox == 0 && g.outH == g.OH && g.outW == g.OW;
+  g.aident = g.R == 1 && g.S == 1 && g.sy == 1 && g.sx == 1 && g.py == 0 && g.px == 0 && g.H == g.OH &&
+             g.W == g.OW;
   return true;
 }
 
@@ -242,9 +254,7 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[FN][FM], long long
     const long long m = mb + j * 16 + (lane & 15);
     op[j] = -1;
     if (m < g.M) {
-      int img, oy, ox;   // M < 2^31 (geom_ok): 32-bit decode
-      decode_m(g, (int)m, img, oy, ox);
-      op[j] = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+      op[j] = out_pixel(g, (int)m);   // M < 2^31 (geom_ok)
     }
   }
 #pragma unroll
@@ -387,9 +397,7 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
       const long long m = m0 + row;
       op[p] = -1;
       if (row < BM && m < g.M) {
-        int img, oy, ox;   // M < 2^31 (geom_ok): 32-bit decode
-        decode_m(g, (int)m, img, oy, ox);
-        op[p] = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+        op[p] = out_pixel(g, (int)m);   // M < 2^31 (geom_ok)
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) r[p][e] = 0.f;
@@ -775,7 +783,11 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
     const int inst = wave * AI + ii;
     const int ch = c_even ^ ((inst & 1) * 4);
     const long long m = m0 + 8 * inst + (lane >> 3);
-    if (m < g.M) {
+    if (m < g.M && g.aident) {   // 1x1 / stride 1 / no padding: input pixel m, always in bounds
+      a_iy[ii] = 0;
+      a_ix[ii] = 0;
+      a_off[ii] = (int)m * g.ldx * 2 + ch * 16;
+    } else if (m < g.M) {
       int img, oy, ox;   // M < 2^31 (geom_ok): 32-bit decode
       decode_m(g, (int)m, img, oy, ox);
       a_iy[ii] = oy * g.sy + g.py;
@@ -850,9 +862,7 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
         const long long m = m0 + row;
         pre.v[p] = u32x4{0u, 0u, 0u, 0u};
         if (pre.on && row < BM && m < g.M) {
-          int img, oy, ox;   // M < 2^31 (geom_ok): 32-bit decode
-          decode_m(g, (int)m, img, oy, ox);
-          const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+          const long long op = out_pixel(g, (int)m);   // M < 2^31 (geom_ok)
           pre.v[p] = *(const u32x4*)(ep.res + op * ep.ldr + n);
         }
       }
@@ -943,9 +953,7 @@ __global__ void splitk_finalize_kernel(const float* __restrict__ ws, TO* __restr
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
     const int n = (int)(i % g.K);
     const long long m = i / g.K;
-    int img, oy, ox;   // M < 2^31 (geom_ok): 32-bit decode
-    decode_m(g, (int)m, img, oy, ox);
-    const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+    const long long op = out_pixel(g, (int)m);   // M < 2^31 (geom_ok)
     float v = ws[i];
     if (ep.aux) io<TO>::st(ep.aux, op * g.ldy + n, v);
     if (ep.scale) v *= ep.scale[n];
@@ -965,9 +973,7 @@ __global__ void phase_zero_vec_kernel(TO* y, ConvGeom g, Epi<TO> ep) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
     const int n = (int)(i % kc) * 8;
     const long long m = i / kc;
-    int img, oy, ox;   // M < 2^31 (geom_ok): 32-bit decode
-    decode_m(g, (int)m, img, oy, ox);
-    const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+    const long long op = out_pixel(g, (int)m);   // M < 2^31 (geom_ok)
     float r[8], v[8];
     if (ep.res) Out8<TO>::ld(ep.res + op * ep.ldr + n, r);
 #pragma unroll
@@ -990,9 +996,7 @@ __global__ void phase_zero_kernel(TO* y, ConvGeom g, Epi<TO> ep) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
     const int n = (int)(i % g.K);
     const long long m = i / g.K;
-    int img, oy, ox;   // M < 2^31 (geom_ok): 32-bit decode
-    decode_m(g, (int)m, img, oy, ox);
-    const long long op = ((long long)img * g.outH + oy * g.osy + g.ooy) * g.outW + ox * g.osx + g.oox;
+    const long long op = out_pixel(g, (int)m);   // M < 2^31 (geom_ok)
     float v = ep.shift ? ep.shift[n] : 0.f;
     if (ep.aux) io<TO>::st(ep.aux, op * g.ldy + n, 0.f);
     if (ep.res) v += io<TO>::ld(ep.res, op * ep.ldr + n);

@@ -27,6 +27,7 @@ def main(d):
     for i in ids:
         if lo < i < hi:
             n = disp[i]['name']
+            n = n.replace('(anonymous namespace)::', '')
             key = (n[:n.find('(')] if '(' in n else n).replace('void ', '')[:78]
             c = agg[key]
             c['launches'] += 1
