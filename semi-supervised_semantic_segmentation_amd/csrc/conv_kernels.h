@@ -56,6 +56,8 @@ struct ConvGeom {
   // decode m -> (img, oy, ox) of every tile row otherwise costs two integer divisions (~40 VALU each)
   unsigned mow, moh;
   int sow, soh;
+  unsigned mn64, mn128, mS;   // magic divisors: n-tile counts ceil(K/64), ceil(K/128) and the filter width S
+  int sn64, sn128, sS;
   int oident;   // output pixel == GEMM row (stride-1 output grid, no offsets): no decode in the epilogue
   int aident;   // 1x1 stride-1 unpadded gather over the same grid: A row m is input pixel m
 };
@@ -101,6 +103,9 @@ static inline bool make_geom(const ssseg_conv_desc* d, ConvGeom& g) {
   g.KK = (int)(d->R * d->S * d->C);
   fdiv_init(g.OW > 0 ? g.OW : 1, g.mow, g.sow);
   fdiv_init(g.OH > 0 ? g.OH : 1, g.moh, g.soh);
+  fdiv_init(g.K > 0 ? (g.K + 63) / 64 : 1, g.mn64, g.sn64);
+  fdiv_init(g.K > 0 ? (g.K + 127) / 128 : 1, g.mn128, g.sn128);
+  fdiv_init(g.S > 0 ? g.S : 1, g.mS, g.sS);
   g.oident = g.osy == 1 && g.osx == 1 && g.ooy == 0 && g.oox == 0 && g.outH == g.OH && g.outW == g.OW;
   g.aident = g.R == 1 && g.S == 1 && g.sy == 1 && g.sx == 1 && g.py == 0 && g.px == 0 && g.H == g.OH &&
              g.W == g.OW;
@@ -753,8 +758,10 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
   const int wm = wave / WN, wn = wave % WN;
   const int nnt = (g.K + BN - 1) / BN;
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
-  const long long m0 = (long long)(tile / nnt) * BM;
-  const int n0 = (tile % nnt) * BN;
+  static_assert(BN == 64 || BN == 128, "n-tile divisor magic");
+  const int mt_ = fdiv(tile, BN == 64 ? g.mn64 : g.mn128, BN == 64 ? g.sn64 : g.sn128);   // tile / nnt
+  const long long m0 = (long long)mt_ * BM;
+  const int n0 = (tile - mt_ * nnt) * BN;
   if (ph.n > 1) {   // this block's output phase: offsets, sub-grid, weights, statistics rows
     const int p = blockIdx.y;
     g.py = ph.py[p];
@@ -768,9 +775,12 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
   const int cpt = g.C >> 6;                      // k-tiles per tap
   // split-K (low-tile layers, blockIdx.y = split): this block reduces k-tiles [kt0, kt1) in order
   const int nk_all = RS * cpt;
-  const int kper = (nk_all + splits - 1) / splits;
-  const int kt0 = min(nk_all, (ph.n > 1 ? 0 : (int)blockIdx.y) * kper);
-  const int nk = min(nk_all, kt0 + kper) - kt0;
+  int kt0 = 0, nk = nk_all;   // the common unsplit launch: no divisions
+  if (splits > 1) {
+    const int kper = (nk_all + splits - 1) / splits;
+    kt0 = min(nk_all, (ph.n > 1 ? 0 : (int)blockIdx.y) * kper);
+    nk = min(nk_all, kt0 + kper) - kt0;
+  }
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, (int)wbytes, 0x00020000);
 
@@ -810,7 +820,7 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
 
   unsigned a_cur[AI];   // byte offsets of this lane's A rows for the current tap (OOB = padding)
   auto set_tap = [&](int tap) {
-    const int r = tap / g.S, s_ = tap - (tap / g.S) * g.S;
+    const int r = fdiv(tap, g.mS, g.sS), s_ = tap - r * g.S;
     const int dyy = r * g.dy, dxx = s_ * g.dx;
     const int toff = (dyy * g.W + dxx) * g.ldx * 2;
 #pragma unroll
@@ -821,7 +831,7 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
     }
   };
 
-  int ld_tap = kt0 / cpt, ld_c = kt0 - (kt0 / cpt) * cpt, ld_kt = kt0;   // k-tile staged next: tap, block, index
+  int ld_tap = kt0 ? kt0 / cpt : 0, ld_c = kt0 ? kt0 - (kt0 / cpt) * cpt : 0, ld_kt = kt0;   // next: tap, block, index
   set_tap(min(ld_tap, RS - 1));
   auto issue = [&](int buf) {
     char* As = smem + buf * STAGE;
