@@ -325,6 +325,20 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[FN][FM], long long
 // conflict-free float4 writes), then each thread finishes 8 consecutive channels of one pixel with 16-byte
 // residual loads and 16-byte (bf16) / 2x16-byte (f32) stores, so a pixel row is written in full lines.
 // Same arithmetic as store_tile (fp32 acc*scale + shift + res, then act, then one rounding).
+// act_fwd over 8 values with the (uniform) activation code tested once, not per value
+__device__ __forceinline__ void act8(float (&v)[8], int act, float slope) {
+  if (act == SSSEG_ACT_RELU) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+  } else if (act == SSSEG_ACT_RELU6) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = fminf(fmaxf(v[e], 0.f), 6.f);
+  } else if (act == SSSEG_ACT_LEAKY) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * slope;
+  }
+}
+
 template <typename TO> struct Out8;
 template <> struct Out8<bf16_t> {
   __device__ __forceinline__ static void ld(const bf16_t* p, float (&v)[8]) {
@@ -429,15 +443,10 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
       float v[8];
       const float4 a0 = *(const float4*)a, a1 = *(const float4*)(a + 4);
       const float raw[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      // affine + residual, then ONE uniform activation switch per chunk (not one per value)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float t = raw[e];
-        if (ep.scale) t *= sc[e];
-        if (ep.shift) t += sh[e];
-        t += r[p][e];
-        t = act_fwd(t, ep.relu, ep.slope);
-        v[e] = t;
-      }
+      for (int e = 0; e < 8; ++e) v[e] = raw[e] * sc[e] + sh[e] + r[p][e];   // scale 1 / shift 0 when absent
+      act8(v, ep.relu, ep.slope);
       const long long o = op[p] * g.ldy + n;
       if (full) {
         Out8<TO>::st(y + o, v);
