@@ -359,13 +359,17 @@ __global__ void __launch_bounds__(256) wgrad_glds_kernel(const T16* __restrict__
       }
       bldslds16(xr, Xs + (wave * XI + ii) * 1024, off, 0);
       xp[ii] += BKP;
-      xox[ii] += BKP;
-      while (xox[ii] >= g.OW) {
-        xox[ii] -= g.OW;
-        if (++xoy[ii] == g.OH) {
-          xoy[ii] = 0;
-          ++ximg[ii];
+      if (BKP < g.OW) {   // at most one row wrap (wave-uniform test)
+        xox[ii] += BKP;
+        if (xox[ii] >= g.OW) {
+          xox[ii] -= g.OW;
+          if (++xoy[ii] == g.OH) {
+            xoy[ii] = 0;
+            ++ximg[ii];
+          }
         }
+      } else if (xp[ii] < p_end) {   // small maps: several rows per k-tile -- decode again (magic divisors)
+        decode_m(g, (int)xp[ii], ximg[ii], xoy[ii], xox[ii]);
       }
     }
 #pragma unroll
