@@ -763,7 +763,8 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
   constexpr int SMEM = (NS == 1 && EPI > STAGE) ? EPI : NS * STAGE;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  // wave index as a scalar: the LDS-DMA destinations (per-wave LDS bases) then need no readfirstlane per load
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int nnt = (g.K + BN - 1) / BN;
   const int tile = xcd_tile(blockIdx.x, gridDim.x);

@@ -306,7 +306,8 @@ __global__ void __launch_bounds__(256) wgrad_glds_kernel(const T16* __restrict__
   static_assert(XI >= 1 && DI >= 1 && NS >= 2 && NS <= 3, "wgrad glds tile");
   __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
 
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  // wave index as a scalar: the LDS-DMA destinations (per-wave LDS bases) then need no readfirstlane per load
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   // 1-D grid, XCD-aware: consecutive logical ids (the mt x nt tiles of one pixel split, which gather the
   // same x and dY rows) run on one XCD and share its L2
