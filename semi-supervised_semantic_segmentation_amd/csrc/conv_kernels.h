@@ -402,11 +402,19 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
     // this thread's 8 channels are the same in every pass: the affine is loaded once, and all residual
     // rows are in flight before the first store
     float sc[8], sh[8];
+    if (full && ep.scale && ((reinterpret_cast<uintptr_t>(ep.scale) & 15) == 0)) {   // two 16-byte loads
+      const float4 a = *(const float4*)(ep.scale + n), b = *(const float4*)(ep.scale + n + 4);
+      sc[0] = a.x; sc[1] = a.y; sc[2] = a.z; sc[3] = a.w; sc[4] = b.x; sc[5] = b.y; sc[6] = b.z; sc[7] = b.w;
+    } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const bool in = n + e < g.K;
-      sc[e] = (ep.scale && in) ? ep.scale[n + e] : 1.f;
-      sh[e] = (ep.shift && in) ? ep.shift[n + e] : 0.f;
+      for (int e = 0; e < 8; ++e) sc[e] = (ep.scale && n + e < g.K) ? ep.scale[n + e] : 1.f;
+    }
+    if (full && ep.shift && ((reinterpret_cast<uintptr_t>(ep.shift) & 15) == 0)) {
+      const float4 a = *(const float4*)(ep.shift + n), b = *(const float4*)(ep.shift + n + 4);
+      sh[0] = a.x; sh[1] = a.y; sh[2] = a.z; sh[3] = a.w; sh[4] = b.x; sh[5] = b.y; sh[6] = b.z; sh[7] = b.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sh[e] = (ep.shift && n + e < g.K) ? ep.shift[n + e] : 0.f;
     }
     long long op[NP];
     float r[NP][8];
