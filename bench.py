@@ -90,35 +90,111 @@ def synthetic_batches(n_batches, batch, size, device, rank):
     return data
 
 
-def cpu_baseline(size, batch=2, steps=2):
-    """The oracle's torch-CPU restatement of the same step (oracle/train_ref.py), bounded sample."""
+def _cpu_threads():
+    """the node's host cores (sched_getaffinity), capped by OMP_NUM_THREADS when the launcher
+    sets it (the GPU box gives each GPU a share of the host: 16 threads, set there)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get('OMP_NUM_THREADS')
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_baseline(size, batch=2, steps=3):
+    """The oracle's torch-CPU restatement of the same step (oracle/train_ref.py), bounded sample: batch 2,
+    1 warm-up + `steps` timed steps on the host's cores.  tests/golden/time_cpu_baseline.py
+    shows, in the build container, that this restatement runs at the reference train.train's own speed
+    (profiles/r3_cpu_baseline_check.json)."""
     from oracle import models_ref, train_ref
-    threads = torch.get_num_threads()
-    torch.manual_seed(0)
-    s = models_ref.ListOutput(models_ref.UNet(2, models_ref.resnet50_encoder(), 128, train_upsampling=True))
-    t = models_ref.ListOutput(models_ref.UNet(2, models_ref.resnet50_encoder(), 128, train_upsampling=True))
-    for p in t.parameters():
-        p.detach_()
-    t.eval()
-    opt = torch.optim.SGD(s.parameters(), lr=0.0001 * 9 / 4, momentum=0.9, weight_decay=0.0005)
-    g = torch.Generator().manual_seed(7)
-    n = steps + 1
-    imgs = torch.rand(n, batch, 3, size, size, generator=g)
-    fg = (torch.rand(n, batch, 1, size, size, generator=g) > 0.5).float()
-    masks = torch.cat([1 - fg, fg], 2)
-    unl = torch.rand(2 * n, batch, 3, size, size, generator=g)
-    cfg = train_ref.default_cfg()
-    times = []
+    threads = _cpu_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        torch.manual_seed(0)
+        s = models_ref.ListOutput(models_ref.UNet(2, models_ref.resnet50_encoder(), 128, train_upsampling=True))
+        t = models_ref.ListOutput(models_ref.UNet(2, models_ref.resnet50_encoder(), 128, train_upsampling=True))
+        t.load_state_dict(s.state_dict())
+        for p in t.parameters():
+            p.detach_()
+        t.eval()
+        opt = torch.optim.SGD(s.parameters(), lr=0.0001 * 9 / 4, momentum=0.9, weight_decay=0.0005)
+        g = torch.Generator().manual_seed(7)
+        n = steps + 1
+        imgs = torch.rand(n, batch, 3, size, size, generator=g)
+        fg = (torch.rand(n, batch, 1, size, size, generator=g) > 0.5).float()
+        masks = torch.cat([1 - fg, fg], 2)
+        unl = torch.rand(2 * n, batch, 3, size, size, generator=g)
+        cfg = train_ref.default_cfg(confidence_threshold=THRESHOLD)
+        times = []
+        t0 = time.perf_counter()
+        train_ref.train_epoch(s, t, opt, list(zip(imgs, masks)), iter(unl), 30, cfg,
+                              on_step=lambda step, rec: times.append(time.perf_counter()))
+        dt = (times[-1] - times[0]) / steps     # the first step is the warm-up
+        return {'value': round(batch / dt, 4), 'unit': 'images/sec', 'cores': threads, 'kind': 'port',
+                'sample': f'oracle/train_ref.py torch-CPU fp32 semi-supervised step (the same C2 step), UNet-R50 '
+                          f'{size}x{size}, batch {batch}, {steps} timed steps after 1 warm-up '
+                          f'({time.perf_counter() - t0:.1f} s total)'}
+    finally:
+        torch.set_num_threads(prev)
 
-    def on_step(step, rec):
-        times.append(time.perf_counter())
 
-    t0 = time.perf_counter()
-    train_ref.train_epoch(s, t, opt, list(zip(imgs, masks)), iter(unl), 30, cfg, on_step=on_step)
-    dt = (times[-1] - times[0]) / steps     # first step is warm-up
-    return {'value': round(batch / dt, 4), 'unit': 'images/sec', 'cores': threads, 'kind': 'port',
-            'sample': f'oracle/train_ref.py torch-CPU fp32 semi-supervised step, UNet-R50 {size}x{size}, batch {batch}, '
-                      f'{steps} timed steps after 1 warm-up ({time.perf_counter() - t0:.1f} s total)'}
+def parity_leg(student, size, device, n_img=4):
+    """mIoU / Dice parity (BASELINE.json metric '...; mIoU parity'): the benched student (after
+    its timed steps, running BN statistics included) validated on the same synthetic validation images by the
+    HIP path (ssseg_seg_metrics: argmax -> nearest resize -> Dice counts + lovasz.iou confusion counts,
+    train.validate) in the fp32 parity mode and in the bf16 throughput mode, and by the oracle (torch-CPU fp32
+    restatement of the network, numpy restatement of the metrics, reference train.py:171-176, metrics.py:1-7,
+    lovasz.py:54-73) on the same weights.  Part of the CPU-baseline leg (the oracle is the checker)."""
+    from oracle import losses_ref, models_ref
+    from ssseg import nn as snn
+    from ssseg import ops
+    import numpy as np
+    g = torch.Generator().manual_seed(4242)
+    imgs = torch.rand(n_img, 3, size, size, generator=g)
+    noise = torch.randn(n_img, 1, size, size, generator=g).to(device)
+    fg = ops.cowmix_mask(noise, torch.full((n_img,), 16.0, device=device), torch.full((n_img,), 0.6, device=device))
+    mask = torch.cat([1 - fg, fg], 1).contiguous()
+    inner = student.module if hasattr(student, 'module') else student
+    sd = {k: v.detach().float().cpu() for k, v in inner.state_dict().items()}
+    inner.eval()
+    out = {}
+    logits = {}
+    try:
+        for name, dt in (('hip_fp32', torch.float32), ('hip_bf16', torch.bfloat16)):
+            snn.set_compute_dtype(dt)
+            seg = ops.SegMetrics(device)
+            with torch.no_grad():
+                lg = inner(imgs.to(device))[-1][-1].float()
+                res = seg.update(lg, mask)
+            r = res.cpu().double().numpy()
+            out[name] = {'dice': round(float(r[0]), 6), 'miou': round(float(r[3]), 6)}
+            logits[name] = lg.cpu()
+    finally:
+        snn.set_compute_dtype(torch.bfloat16)
+        inner.train()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(_cpu_threads())
+    try:
+        ref = models_ref.ListOutput(models_ref.UNet(2, models_ref.resnet50_encoder(), 128, train_upsampling=True))
+        ref.load_state_dict(sd)
+        ref.eval()
+        with torch.no_grad():
+            rl = ref(imgs)[-1][-1].float()
+    finally:
+        torch.set_num_threads(prev)
+    dice, ious, _ = losses_ref.seg_metrics(rl.numpy(), mask.cpu().numpy())
+    out['oracle_fp32'] = {'dice': round(float(np.mean(dice)), 6), 'miou': round(float(np.mean(ious)), 6)}
+    scale = float(rl.abs().max()) or 1.0
+    for name in ('hip_fp32', 'hip_bf16'):
+        d = (logits[name] - rl).abs()
+        lab = (logits[name][:, 1] > logits[name][:, 0]) != (rl[:, 1] > rl[:, 0])
+        out[name]['logits_max_err_rel'] = float(d.max()) / scale
+        out[name]['argmax_mismatch_frac'] = float(lab.float().mean())
+    out['data'] = (f'{n_img} synthetic {size}x{size} validation images (U[0,1)), blob masks (CowMix kernel, sigma 16, '
+                   f'p 0.6); student weights after the timed steps')
+    out['miou_abs_diff_fp32'] = abs(out['hip_fp32']['miou'] - out['oracle_fp32']['miou'])
+    out['dice_abs_diff_fp32'] = abs(out['hip_fp32']['dice'] - out['oracle_fp32']['dice'])
+    return out
 
 
 def _spawn_ranks(n):
@@ -184,7 +260,7 @@ def timed_run(args, world, rank, device, dtype, probe=True):
         elapsed = float(t)
     live = torch.stack([torch.stack([c.float(), u.float(), m.float()]) for c, u, m in recs]).cpu()
     snn.set_compute_dtype(torch.bfloat16)
-    return elapsed, rows, live
+    return elapsed, rows, live, model
 
 
 def main():
@@ -211,7 +287,7 @@ def main():
               f'{dist.get_backend()}, device cuda:{local}', file=sys.stderr, flush=True)
     device = torch.device('cuda', local)
 
-    elapsed, rows, live = timed_run(args, world, rank, device, torch.bfloat16)
+    elapsed, rows, live, model = timed_run(args, world, rank, device, torch.bfloat16)
     finite = bool(torch.isfinite(live).all())
     if not finite:
         raise RuntimeError(f'bench: non-finite loss in the timed steps (rank {rank}): {live.tolist()}')
@@ -242,7 +318,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_fp32:
         try:
-            f_el, _, f_live = timed_run(argparse.Namespace(**dict(vars(args), steps=min(args.steps, 5), warmup=2)),
+            f_el, _, f_live, _ = timed_run(argparse.Namespace(**dict(vars(args), steps=min(args.steps, 5), warmup=2)),
                                         world, rank, device, torch.float32, probe=False)
             n = min(args.steps, 5)
             result['fp32_mode'] = {'value': round(args.batch * n / f_el, 3), 'unit': 'images/sec',
@@ -256,6 +332,10 @@ def main():
             result['cpu_baseline'] = cpu_baseline(args.size)
         except Exception as exc:  # report, never hide
             result['cpu_baseline'] = {'error': repr(exc)}
+        try:
+            result['parity'] = parity_leg(model, args.size, device)
+        except Exception as exc:  # report, never hide
+            result['parity'] = {'error': repr(exc)}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -254,7 +254,9 @@ __global__ void amp_update_kernel(float* state, const float* sqnorm, float growt
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   float sc = state[0];
   if (!isfinite(sqnorm[0])) {
-    sc *= backoff;
+    // floor at 1: a persistently non-finite loss (the reference's 0/0 consistency NaN survives its epoch gate)
+    // would otherwise halve S to 0 in ~150 steps, and 1/S = inf then turns the next finite step's update into NaN
+    sc = fmaxf(sc * backoff, 1.f);
     state[1] = 0.f;
     state[2] = 1.f;
   } else {

@@ -29,6 +29,27 @@ def _writer(path, step):
         return None
 
 
+def attach_grad_scaler(optimizer, device):
+    """fp16 mode: the device-side GradScaler.  Only ssseg's fused SGD unscales by 1/S and skips a non-finite
+    step; any other optimizer would apply S-scaled gradients, so it is refused."""
+    if not isinstance(optimizer, soptim.SGD):
+        raise NotImplementedError(f'fp16 compute mode needs ssseg.optim.SGD (loss-scaled gradients are unscaled in '
+                                  f'its fused step); got {type(optimizer).__name__}')
+    optimizer.grad_scaler = amp.GradScaler(device)
+    return optimizer.grad_scaler
+
+
+def _scaler_state(opt):
+    sc = getattr(opt, 'grad_scaler', None)
+    return sc.state_dict() if sc is not None else None
+
+
+def _load_scaler_state(opt, sd):
+    sc = getattr(opt, 'grad_scaler', None)
+    if sc is not None and sd is not None:
+        sc.load_state_dict(sd)
+
+
 def distributed_train(rank, cfg_path):
     utils.seed_everything(0)
     cfg = config.fromfile(cfg_path)
@@ -48,7 +69,7 @@ def distributed_train(rank, cfg_path):
     optimizer = soptim.from_config(cfg['train']['optimizer'], utils.get_trainable_params(model))
     fp16 = snn.compute_dtype() == torch.float16
     if fp16:   # dynamic loss scaling on the device (ssseg.amp): fp16's exponent range flushes small gradients
-        optimizer.grad_scaler = amp.GradScaler(device)
+        attach_grad_scaler(optimizer, device)
     disc = None
     if cfg['model'].get('discriminator') is not None and cfg['train'].get('adversarial_loss_weight'):
         # config C5: the discriminator the reference config names (default_config.py:116-120) trained by the
@@ -56,7 +77,7 @@ def distributed_train(rank, cfg_path):
         disc = DistributedDataParallel(cfg['model']['discriminator']().to(device))
         disc_opt = soptim.from_config(cfg['train']['discriminator_optimizer'], disc.parameters())
         if fp16:
-            disc_opt.grad_scaler = amp.GradScaler(device)
+            attach_grad_scaler(disc_opt, device)
         cfg['train']['adversarial'] = dict(discriminator=disc, optimizer=disc_opt,
                                            weight=float(cfg['train']['adversarial_loss_weight']))
 
@@ -76,9 +97,11 @@ def distributed_train(rank, cfg_path):
         model.module.load_state_dict(ck['state_dict'], strict=False)
         ema_model.load_state_dict(ck['ema_state_dict'], strict=False)
         optimizer.load_state_dict(ck['optimizer'])
+        _load_scaler_state(optimizer, ck.get('grad_scaler'))
         if disc is not None and 'discriminator_state_dict' in ck:
             disc.module.load_state_dict(ck['discriminator_state_dict'])
             cfg['train']['adversarial']['optimizer'].load_state_dict(ck['discriminator_optimizer'])
+            _load_scaler_state(cfg['train']['adversarial']['optimizer'], ck.get('discriminator_grad_scaler'))
             snn.invalidate_packed(disc.module)
         best_metric, last_epoch = ck['best_metric'], ck['epoch']
         snn.invalidate_packed(model.module)
@@ -116,9 +139,13 @@ def distributed_train(rank, cfg_path):
             os.makedirs(train_dir, exist_ok=True)
             ck = {'epoch': epoch + 1, 'best_metric': val_loss, 'state_dict': model.module.state_dict(),
                   'ema_state_dict': ema_model.state_dict(), 'optimizer': optimizer.state_dict()}
-            if disc is not None:   # extra keys only; the reference's five keys are unchanged
+            if fp16:   # extra keys only; the reference's five keys are unchanged
+                ck['grad_scaler'] = _scaler_state(optimizer)
+            if disc is not None:
                 ck['discriminator_state_dict'] = disc.module.state_dict()
                 ck['discriminator_optimizer'] = cfg['train']['adversarial']['optimizer'].state_dict()
+                if fp16:
+                    ck['discriminator_grad_scaler'] = _scaler_state(cfg['train']['adversarial']['optimizer'])
             torch.save(ck, latest)
             if best_metric is None or val_loss < best_metric:
                 best_metric = val_loss

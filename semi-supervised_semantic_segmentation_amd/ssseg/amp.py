@@ -6,7 +6,7 @@ its smallest normal (6.1e-5) and flush in the fp16 activation gradients.  The st
 before the optimizer step, skipping steps whose gradients overflowed and adapting S.  Here everything stays
 on the device (no host sync per step): the backward's incoming gradient is multiplied by S in a native
 kernel (ssseg_scale_by), the fused clip + SGD kernel unscales by 1/S and skips a non-finite step, and
-ssseg_amp_update adapts S (x0.5 on overflow, x2 after `growth_interval` finite steps).  bf16 / fp32 modes do not
+ssseg_amp_update adapts S (x0.5 on overflow, floored at 1; x2 after `growth_interval` finite steps).  bf16 / fp32 modes do not
 use it (bf16 keeps fp32's exponent range)."""
 import torch
 
@@ -40,6 +40,17 @@ class GradScaler:
     def update(self, sqnorm):
         N.call('ssseg_amp_update', N.dev_ptr(self.state), N.dev_ptr(sqnorm), self.growth, self.backoff, self.interval,
                N.stream())
+
+    def state_dict(self):
+        """Checkpointable state (scale, growth counter, last-step overflow flag): resume continues the schedule."""
+        return {'state': self.state.detach().cpu().clone(), 'growth_factor': self.growth,
+                'backoff_factor': self.backoff, 'growth_interval': self.interval}
+
+    def load_state_dict(self, sd):
+        self.state.copy_(sd['state'].to(self.state.device, torch.float32))
+        self.growth = float(sd.get('growth_factor', self.growth))
+        self.backoff = float(sd.get('backoff_factor', self.backoff))
+        self.interval = int(sd.get('growth_interval', self.interval))
 
     def get_scale(self):
         return float(self.state[0])

@@ -92,7 +92,7 @@ def flush_wgrad():
     for mod in pending:
         pair = mod.__dict__.pop('_ssseg_wg_pending', None)
         if pair is not None:
-            mod._ssseg_wgrad(*pair, bias_grad=False)
+            mod._ssseg_wgrad(*pair, bias_grad=False, want=(True, False))
 
 
 def wgrad_pending():
@@ -413,7 +413,9 @@ class _ConvFn(torch.autograd.Function):
             N.call('ssseg_act_bwd', N.dev_ptr(gy), N.dev_ptr(y), N.dev_ptr(gm), gy.numel(), code, slope, N.dt_code(gy),
                    N.stream())
             gy = gm
-        mod._ssseg_wgrad(x, gy)
+        # parameter gradients as autograd decided at forward time (a module frozen for this forward, e.g. the
+        # discriminator under the student's adversarial term, stays frozen in its backward whatever its flag is now)
+        mod._ssseg_wgrad(x, gy, want=(ctx.needs_input_grad[1], ctx.needs_input_grad[2]))
         joined, last = _join_take(ctx.join)
         pending = _sum_pending(_take(ctx.handoff), joined)
         if not ctx.needs_input_grad[0]:
@@ -432,9 +434,9 @@ def _dgrad_acc(mod, gy, xshape, pending):
     return mod._ssseg_dgrad(gy, xshape) + pending
 
 
-def _bias_grad(mod, gy):
-    """d bias += per-channel sum of gy (NHWC)."""
-    if mod.bias is None or not mod.bias.requires_grad:
+def _bias_grad(mod, gy, want=None):
+    """d bias += per-channel sum of gy (NHWC).  want: forward-time requires_grad (None: the live flag)."""
+    if mod.bias is None or not (mod.bias.requires_grad if want is None else want):
         return
     n, cp, h, w = gy.shape
     C = mod.bias.numel()
@@ -458,7 +460,7 @@ class _ConvBase:
         if '_ssseg_wg_pending' in self.__dict__:   # a second use inside the same deferred pass: run the first
             _WGRAD['defer'] = False
             try:
-                self._ssseg_wgrad(*self.__dict__.pop('_ssseg_wg_pending'), bias_grad=False)
+                self._ssseg_wgrad(*self.__dict__.pop('_ssseg_wg_pending'), bias_grad=False, want=(True, False))
             finally:
                 _WGRAD['defer'] = True
         self.__dict__['_ssseg_wg_pending'] = (a, b)
@@ -475,7 +477,7 @@ class _ConvBase:
         if (a1.shape[1:] == a.shape[1:] and b1.shape[1:] == b.shape[1:] and a1.dtype == a.dtype
                 and b1.dtype == b.dtype and a1.stride()[1:] == a.stride()[1:] and b1.stride()[1:] == b.stride()[1:]):
             return pend
-        self._ssseg_wgrad(a1, b1, bias_grad=False)
+        self._ssseg_wgrad(a1, b1, bias_grad=False, want=(True, False))
         return None
 
 
@@ -703,11 +705,13 @@ class Conv2d(nn.Conv2d, _ConvBase):
         _need_act(gy, cout, 'Conv2d backward')
         return gy
 
-    def _ssseg_wgrad(self, x, gy, bias_grad=True):
+    def _ssseg_wgrad(self, x, gy, bias_grad=True, want=None):
+        """dW (+ db) of this conv; want = (weight, bias) requires_grad as captured at forward time (None: live)."""
+        ww = self.weight.requires_grad if want is None else want[0]
         if bias_grad:
-            _bias_grad(self, gy)
-        if not self.weight.requires_grad:
-            if self.bias is not None:
+            _bias_grad(self, gy, None if want is None else want[1])
+        if not ww:
+            if self.bias is not None and (self.bias.requires_grad if want is None else want[1]):
                 _ready(self.bias)
             return
         n, _, H, W = x.shape
@@ -900,10 +904,11 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
         _need_act(gy, self._dims()[1], 'ConvTranspose2d backward')
         return gy
 
-    def _ssseg_wgrad(self, x, gy, bias_grad=True):
+    def _ssseg_wgrad(self, x, gy, bias_grad=True, want=None):
+        ww = self.weight.requires_grad if want is None else want[0]
         if bias_grad:
-            _bias_grad(self, gy)
-        if self.weight.requires_grad:
+            _bias_grad(self, gy, None if want is None else want[1])
+        if ww:
             if self._wg_defer(x, gy):
                 return
             pend = self._wg_take(x, gy)
@@ -932,7 +937,8 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
                     N.call('ssseg_conv_wgrad2', N.dev_ptr(gy1), N.dev_ptr(x1), N.dev_ptr(gy), N.dev_ptr(x), n,
                            N.dev_ptr(_grad_of(self.weight)), ctypes_ref(d), N.dt_code(x), self.out_channels,
                            self.in_channels, 1, 1, N.dev_ptr(ws), nb, N.stream())
-        _ready(*[p for p in (self.weight, self.bias) if p is not None])
+        wb = self.bias is not None and (self.bias.requires_grad if want is None else want[1])
+        _ready(*[p for p, on in ((self.weight, ww), (self.bias, wb)) if on])
 
     def _ssseg_dgrad(self, gy, xshape):
         cin, cout = self._dims()
@@ -1034,7 +1040,7 @@ class _BNFn(torch.autograd.Function):
         nb = N.lib().ssseg_bn_workspace_bytes(C)
         ws = N.workspace(nb, dev)
         res_p = N.dev_ptr(residual) if residual is not None else None
-        pgrad = mod.weight is not None and mod.weight.requires_grad
+        pgrad = mod.weight is not None and ctx.needs_input_grad[1]   # forward-time requires_grad
         # reduction + (dgamma, dbeta) from the local sums in one launch (ssseg_bn_bwd_reduce_grad)
         N.call('ssseg_bn_bwd_reduce_grad', N.dev_ptr(gy), N.dev_ptr(x), res_p, P, C, cp, cp, cp, N.dev_ptr(mean),
                N.dev_ptr(invstd), N.dev_ptr(wt) if wt is not None else None,
@@ -1109,7 +1115,11 @@ class _ConvBNEvalFn(torch.autograd.Function):
         sums = torch.empty(2 * C, dtype=torch.float64, device=dev)
         nb = N.lib().ssseg_bn_workspace_bytes(C)
         ws = N.workspace(nb, dev)
-        want = lambda p: p is not None and p.requires_grad  # noqa: E731
+        # parameter gradients as autograd decided at forward time (inputs 1-4: conv.weight, conv.bias, bn.weight,
+        # bn.bias)
+        fw = {id(p): ctx.needs_input_grad[i] for i, p in ((1, conv.weight), (2, conv.bias), (3, bn.weight),
+                                                           (4, bn.bias)) if p is not None}
+        want = lambda p: p is not None and fw.get(id(p), False)  # noqa: E731
         # dconv/dres + the BN (and conv-bias) parameter grads in one reduction (ssseg_bn_eval_bwd_grad)
         grads = (N.dev_ptr(_grad_of(bn.weight)) if want(bn.weight) else None,
                  N.dev_ptr(_grad_of(bn.bias)) if want(bn.bias) else None,
@@ -1126,7 +1136,7 @@ class _ConvBNEvalFn(torch.autograd.Function):
                    N.dev_ptr(ws), nb, *grads, N.stream())
         if want(bn.weight) or want(bn.bias):
             _ready(*[p for p in (bn.weight, bn.bias) if want(p)])
-        conv._ssseg_wgrad(x, dconv, bias_grad=False)
+        conv._ssseg_wgrad(x, dconv, bias_grad=False, want=(ctx.needs_input_grad[1], False))
         joined, last = _join_take(ctx.join)
         pending = _sum_pending(_take(ctx.grad_in), joined)
         if not ctx.needs_input_grad[0]:

@@ -65,7 +65,10 @@ def adversarial_terms(pred_maps, mask, adv):
     calls it; the formulation follows Hung et al. 2018, "Adversarial Learning for Semi-Supervised Semantic
     Segmentation").  The discriminator sees the student's probability map p = sigmoid(up(logits)) at the mask
     resolution (the reference's BCE treats each of the 2 channels as an independent sigmoid, losses.py:41-48).
-    Student term: weight * BCE(D(p), 1) with D frozen (its native layers skip their weight gradients).
+    Student term: weight * BCE(D(p), 1) with D frozen: D's parameters are built with requires_grad off for this
+    forward, and the native layers take their parameter-gradient decision from forward time (ctx.needs_input_grad),
+    so the student's backward never writes D's gradient arena.  D stays frozen until the caller has run that
+    backward (train_step re-enables it right before discriminator_step).
     Returns (student adversarial loss, detached p for the discriminator update)."""
     D = adv['discriminator']
     logits = pred_maps[-1]
@@ -75,7 +78,6 @@ def adversarial_terms(pred_maps, mask, adv):
     _set_requires_grad(D, False)
     d_fake = D(prob)
     adv_loss = ops.scale(ops.bce_with_logits_mean(d_fake, _target(d_fake, 1.0)), adv['weight'])
-    _set_requires_grad(D, True)
     return adv_loss, prob.detach()
 
 
@@ -132,6 +134,7 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
         ops.backward(_scaled(ops.scale(sup_loss, 1.0 / vbm) if vbm != 1 else sup_loss, optimizer))
     del pred_maps, features
     if adv is not None:
+        _set_requires_grad(adv['discriminator'], True)   # frozen since adversarial_terms; the student backward is done
         adv['last_loss_d'] = discriminator_step(mask, prob, adv)
         adv['last_loss_adv'] = adv_loss.detach()
         del prob

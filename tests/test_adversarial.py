@@ -110,3 +110,42 @@ def test_adversarial_branch_vs_oracle(hip_device):
         assert not bad_s and not bad_d, (bad_s[:5], bad_d[:5])
     finally:
         snn.set_compute_dtype(torch.bfloat16)
+
+
+def test_frozen_discriminator_gets_no_student_gradient(hip_device):
+    """The student's adversarial term weight*BCE(D(p), 1) must not reach D's parameters: after the student's
+    supervised backward (the adversarial term included, weight gradients deferred as in train_step) and a flush
+    of every deferred weight gradient, D's whole gradient arena is exactly zero -- whatever D's requires_grad
+    flags are by the time the backward runs (train.adversarial_terms freezes D for its forward only)."""
+    import losses
+    import train
+    from models import simple_unet
+    from models.adapters import ListOutput
+    from models.discriminator import Discriminator
+    from ssseg import arena, ops
+    from ssseg import nn as snn
+    snn.set_compute_dtype(torch.float32)
+    try:
+        torch.manual_seed(0)
+        student = ListOutput(simple_unet.UNet(2, 3, 8, 32)).to(hip_device)
+        D = Discriminator(5, 2, 64, 512, 1).to(hip_device)
+        sa = arena.attach(student)
+        da = arena.attach(D)
+        imgs, masks, _ = _data()
+        image, mask = imgs[0].to(hip_device), masks[0].to(hip_device)
+        loss_fn = losses.CalculateLoss([{'loss_fn': losses.DenseBinaryCrossEntropyLossWithLogits('mean'),
+                                         'weight': [0.5]}])
+        adv = dict(discriminator=D, optimizer=None, weight=0.01)
+        student.train()
+        _, pred_maps = student(image)
+        sup = loss_fn(pred_maps, mask)
+        adv_loss, _ = train.adversarial_terms(pred_maps, mask, adv)
+        train._set_requires_grad(D, True)      # live flags back on BEFORE the backward: must not matter
+        with snn.defer_wgrad():
+            ops.backward(ops.add_scaled(sup, adv_loss))
+        snn.flush_wgrad()
+        torch.cuda.synchronize()
+        assert float(da.grad.abs().max()) == 0.0
+        assert float(sa.grad.abs().max()) > 0.0     # the student did get its gradients
+    finally:
+        snn.set_compute_dtype(torch.bfloat16)

@@ -103,3 +103,28 @@ def test_grad_scaler_skips_overflowed_step(hip_device):
     torch.cuda.synchronize()
     np.testing.assert_allclose((before[0] - m.weight.detach()).cpu().numpy(), 0.1, rtol=1e-6)
     assert opt.grad_scaler.get_scale() == 1024.0 and not opt.grad_scaler.found_inf()   # growth_interval 1
+
+
+def test_grad_scaler_floor_after_many_overflows(hip_device):
+    """A persistently non-finite loss backs the scale off to its floor (1.0), never to 0: 1/S stays finite, and
+    the next finite step unscales and updates normally (no 0*inf NaN in the fused SGD)."""
+    from ssseg import amp, arena, optim
+    m = torch.nn.Linear(16, 4).to(hip_device)
+    arena.attach(m)
+    opt = optim.SGD(m.parameters(), lr=0.1, momentum=0.0)
+    opt.grad_scaler = amp.GradScaler(hip_device, init_scale=2.0 ** 16, growth_interval=10 ** 6)
+    before = [p.detach().clone() for p in m.parameters()]
+    for _ in range(200):
+        opt.zero_grad()
+        m.weight.grad.fill_(float('nan'))
+        opt.step()
+    torch.cuda.synchronize()
+    assert opt.grad_scaler.get_scale() == 1.0
+    assert all(torch.equal(a, p.detach()) for a, p in zip(before, m.parameters()))
+    opt.zero_grad()
+    m.weight.grad.fill_(1.0)            # S = 1: unscaled 1.0
+    opt.step()
+    torch.cuda.synchronize()
+    w = m.weight.detach()
+    assert bool(torch.isfinite(w).all())
+    np.testing.assert_allclose((before[0] - w).cpu().numpy(), 0.1, rtol=1e-6)

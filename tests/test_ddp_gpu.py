@@ -30,12 +30,12 @@ def _free_port():
     return p
 
 
-def _data():
+def _data(world=WORLD):
     g = torch.Generator().manual_seed(11)
-    imgs = torch.rand(STEPS, WORLD, B, 3, H, H, generator=g)
-    fg = (torch.rand(STEPS, WORLD, B, 1, H, H, generator=g) > 0.5).float()
+    imgs = torch.rand(STEPS, world, B, 3, H, H, generator=g)
+    fg = (torch.rand(STEPS, world, B, 1, H, H, generator=g) > 0.5).float()
     masks = torch.cat([1 - fg, fg], 3)
-    unl = torch.rand(STEPS, WORLD, 2, B, 3, H, H, generator=g)
+    unl = torch.rand(STEPS, world, 2, B, 3, H, H, generator=g)
     if 'same' in os.environ.get('SSSEG_DDP_DIAG', ''):
         imgs[:] = imgs[0].clone()
         masks[:] = masks[0].clone()
@@ -58,11 +58,27 @@ def _cfg(semi=True):
                 print_freq=1, gradient_clip_value=5.0)
 
 
-def _worker(rank, port, q, semi):
+class _CollectiveLog:
+    """Counts every torch.distributed.all_reduce of the step (ssseg.ddp's gradient buckets, ssseg.nn's SyncBN
+    statistic sums, utils.reduce_tensor): (tensor dtype, bytes) per call."""
+    def __init__(self, dist):
+        self.calls, self._orig, self._dist = [], dist.all_reduce, dist
+
+        def wrapped(tensor, *a, **k):
+            self.calls.append((str(tensor.dtype), tensor.numel() * tensor.element_size()))
+            return self._orig(tensor, *a, **k)
+        dist.all_reduce = wrapped
+
+    def take(self):
+        c, self.calls = self.calls, []
+        return c
+
+
+def _worker(rank, port, q, semi, world=WORLD):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     import torch.distributed as dist
-    dist.init_process_group('gloo', rank=rank, world_size=WORLD)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
         import cowmix
         import train
@@ -85,8 +101,11 @@ def _worker(rank, port, q, semi):
         model = DistributedDataParallel(student, bucket_cap_mb=0.02)
         arena.attach(teacher, with_grads=False)
         opt = optim.SGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
-        imgs, masks, unl = _data()
+        imgs, masks, unl = _data(world)
         cowmix.NOISE_SOURCE = 'cpu'
+        import utils.utils as utils
+        log = _CollectiveLog(dist)
+        collectives, reduced = [], []
         torch.manual_seed(3)
         model.train()
         opt.zero_grad()
@@ -102,6 +121,10 @@ def _worker(rank, port, q, semi):
                                        unl[step, rank, 0].to(dev), unl[step, rank, 1].to(dev), 30, step,
                                        {'train': _cfg(semi)})
             torch.cuda.synchronize()
+            collectives.append(log.take())
+            # the reference's logging reduction (utils.py:43-54) on the device loss scalars: sum over ranks
+            red = utils.reduce_tensor(c.clone())
+            reduced.append((str(red.device), float(red) / world))
             losses.append((float(c), float(u) if u is not None else 0.0))
             early.append(model.last_early)
             if step == 0:    # no optimizer step at step 0 (train.py:121): its gradients stay accumulated
@@ -109,7 +132,11 @@ def _worker(rank, port, q, semi):
                 if os.environ.get('SSSEG_DDP_DIAG') == 'zero':
                     opt.zero_grad()
         # numpy (pickled by value): torch CPU tensors would travel as shared-memory fds that die with this process
-        out = dict(losses=losses, early=early, nbuckets=len(model.buckets), grads=grads,
+        n_bn = sum(1 for m in student.modules() if isinstance(m, snn.BatchNorm2d))
+        out = dict(losses=losses, early=early, nbuckets=len(model.buckets), grads=grads, collectives=collectives,
+                   reduced=reduced, n_bn=n_bn, bn_channels=[m.num_features for m in student.modules()
+                                                             if isinstance(m, snn.BatchNorm2d)],
+                   bucket_bytes=[4 * (e - s0) for s0, e, _ in model.buckets],
                    student={k: v.detach().cpu().numpy().copy() for k, v in student.state_dict().items()},
                    teacher={k: v.detach().cpu().numpy().copy() for k, v in teacher.state_dict().items()})
         q.put((rank, out))
@@ -120,7 +147,7 @@ def _worker(rank, port, q, semi):
         dist.destroy_process_group()
 
 
-def _oracle(dt=torch.float32, semi=True, pert=0.0):
+def _oracle(dt=torch.float32, semi=True, pert=0.0, world=WORLD):
     from oracle import models_ref, train_ref
     torch.manual_seed(0)
     s = models_ref.ListOutput(models_ref.SimpleUNet(2, 3, 8, 32))
@@ -132,7 +159,7 @@ def _oracle(dt=torch.float32, semi=True, pert=0.0):
         p.detach_()
     t.eval()
     opt = torch.optim.SGD(s.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
-    imgs, masks, unl = (v.to(dt) for v in _data())
+    imgs, masks, unl = (v.to(dt) for v in _data(world))
     if pert:    # the step's own sensitivity: inputs moved by ~fp32 rounding after a few layers
         g = torch.Generator().manual_seed(99)
         imgs = imgs * (1 + pert * torch.randn(imgs.shape, generator=g, dtype=dt))
@@ -145,49 +172,53 @@ def _oracle(dt=torch.float32, semi=True, pert=0.0):
         if step == 0 and os.environ.get('SSSEG_DDP_DIAG') == 'zero':
             opt.zero_grad()
     torch.manual_seed(3)
-    logs = train_ref.train_epoch_dp(s, t, opt, [[(imgs[k, r], masks[k, r]) for r in range(WORLD)] for k in range(STEPS)],
-                                    [[(unl[k, r, 0], unl[k, r, 1]) for r in range(WORLD)] for k in range(STEPS)], 30,
+    logs = train_ref.train_epoch_dp(s, t, opt, [[(imgs[k, r], masks[k, r]) for r in range(world)] for k in range(STEPS)],
+                                    [[(unl[k, r, 0], unl[k, r, 1]) for r in range(world)] for k in range(STEPS)], 30,
                                     cfg, on_step=on_step)
     return logs, grads, s.state_dict(), t.state_dict()
 
 
-@pytest.mark.parametrize('semi', [False, True])
-def test_ddp_syncbn_world2_product_path(hip_device, semi):
+@pytest.mark.parametrize('semi,world', [(False, WORLD), (True, WORLD), (True, 4)])
+def test_ddp_syncbn_product_path(hip_device, semi, world):
+    """world 2 (both step kinds) and world 4 (semi-supervised): 4 ranks share the one GPU over gloo -- the same
+    product code an 8-GPU node runs over RCCL."""
     import torch.multiprocessing as mp
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, q, semi)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, port, q, semi, world)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
     try:
-        for _ in range(WORLD):
-            r, out = q.get(timeout=100)
+        for _ in range(world):
+            r, out = q.get(timeout=110)
             res[r] = out
     finally:
         for p in procs:
             p.join(30)
             if p.is_alive():
                 p.kill()
-    for r in range(WORLD):
+    for r in range(world):
         assert not isinstance(res[r], str), res[r]
+    _check_collectives(res, world)
     failures = []
-    logs, g_ref, s_ref, t_ref = _oracle(semi=semi)
-    _, g64, s64, t64 = _oracle(torch.float64, semi=semi)
+    logs, g_ref, s_ref, t_ref = _oracle(semi=semi, world=world)
+    logs64, g64, s64, t64 = _oracle(torch.float64, semi=semi, world=world)
     # ReLU / max-pool switches sit within ~1e-6 of these tiny-batch activations: a 1e-6 relative input
     # perturbation moves the fp64 oracle's step-1 gradients by ~1 % (measured).  After step 0 the bound is
     # therefore 2x the larger of the fp32 oracle's drift and this perturbation drift (tests/parity.py's rule).
-    _, gp, sp, tp = _oracle(torch.float64, semi=semi, pert=1e-6)
-    for r in range(WORLD):
+    _, gp, sp, tp = _oracle(torch.float64, semi=semi, pert=1e-6, world=world)
+    for r in range(world):
         out = res[r]
         for k, (c, u) in enumerate(out['losses']):
             np.testing.assert_allclose(c, logs[k]['sup_loss'][r], rtol=1e-4)
-            if semi:
-                np.testing.assert_allclose(u, logs[k]['unsup_loss'][r], rtol=2e-3, atol=1e-6)
+            if semi:   # tests/parity.py's loss rule: within max(1e-3 rel, 2x the fp32 oracle's own drift) of fp64
+                u64, u32 = logs64[k]['unsup_loss'][r], logs[k]['unsup_loss'][r]
+                assert abs(u - u64) <= max(1e-3 * abs(u64), 2 * abs(u32 - u64)) + 1e-9, (k, r, u, u32, u64)
         assert out['nbuckets'] > 2
         assert out['early'][0] == 0                       # first armed backward learns the counts
-        if os.environ.get('SSSEG_DDP_OVERLAP', '1') != '0' and WORLD > 1:
+        if os.environ.get('SSSEG_DDP_OVERLAP', '1') != '0' and world > 1:
             assert all(e > 0 for e in out['early'][1:]), out['early']   # later ones launch from the backward
         # averaged gradients of every step vs fp64: per tensor within max(1e-3, 2x the fp32 oracle's own drift)
         # of the tensor's scale, floored at 1e-3 of the model's largest gradient (a conv bias feeding a
@@ -209,7 +240,7 @@ def test_ddp_syncbn_world2_product_path(hip_device, semi):
             worst = max((float(np.abs(out['grads'][k][n] - g.numpy()).max()) / max(float(g.abs().max()), 1e-3 * gmax), n)
                         for n, g in g64[k].items())
             print(f'rank {r} step {k} worst grad err vs fp64 {worst}')
-        if r == 1 and WORLD == 2:
+        if r == 1 and world == 2:
             for k in range(STEPS):
                 d = max(float(np.abs(res[0]['grads'][k][n] - res[1]['grads'][k][n]).max()) for n in g64[k])
                 print(f'step {k} max |grad rank0 - grad rank1| = {d}')
@@ -237,4 +268,27 @@ def test_ddp_syncbn_world2_product_path(hip_device, semi):
     assert not failures, failures
     # both ranks hold identical weights (averaged gradients, broadcast init)
     for k in res[0]['student']:
-        assert np.array_equal(res[0]['student'][k], res[WORLD - 1]['student'][k]), k
+        assert np.array_equal(res[0]['student'][k], res[world - 1]['student'][k]), k
+    # utils.reduce_tensor on the device loss scalars (reference utils.py:43-54, dist.reduce SUM to rank 0): rank 0
+    # holds the mean of every rank's supervised loss
+    for k in range(STEPS):
+        dev, mean = res[0]['reduced'][k]
+        assert dev.startswith('cuda'), dev
+        np.testing.assert_allclose(mean, np.mean([res[r]['losses'][k][0] for r in range(world)]), rtol=1e-6)
+
+
+def _check_collectives(res, world):
+    """Per-step collective count and bytes on every rank: one all-reduce per gradient bucket (fp32,
+    together exactly the flat gradient arena) + 2 SyncBN all-reduces per training BatchNorm (forward (sum, sum^2)
+    and backward (sum dy, sum dy*xhat), fp64 [2C] each) -- the eval-mode consistency pass and the teacher run none."""
+    for r in range(world):
+        out = res[r]
+        n_bn, bn_c = out['n_bn'], out['bn_channels']
+        for k, calls in enumerate(out['collectives']):
+            f64 = [b for d, b in calls if d == 'torch.float64']
+            f32 = [b for d, b in calls if d == 'torch.float32']
+            assert len(calls) == len(f64) + len(f32), calls
+            assert len(f64) == 2 * n_bn, (r, k, len(f64), n_bn)
+            assert sum(f64) == 2 * sum(2 * c * 8 for c in bn_c), (r, k, sum(f64))
+            assert len(f32) == out['nbuckets'], (r, k, len(f32), out['nbuckets'])
+            assert sum(f32) == sum(out['bucket_bytes']), (r, k, sum(f32))

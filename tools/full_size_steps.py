@@ -5,9 +5,14 @@ and 32-bit offsets at the real geometries (every kernel entry validates its offs
 finiteness of losses and parameters, ms/step of the last two steps, peak device memory.
 
     python tools/full_size_steps.py [--configs c3,c4,c5] > gpurun_out/full_size.log
-The confidence threshold is set to 0.0 (every pixel confident): with random init the teachers' max sigmoid is
-<= 0.5 on whole batches (HRNet-MSA's eval logits are ~1e-14: tools/diag_c4.py), so the reference's 0.97 -- and even
-bench.py's 0.5 -- gives an all-zero mask and the reference's own 0/0 NaN.
+Teacher liveness: a random-init network normalised with the init running statistics (mean 0, var 1) is
+degenerate in eval mode (HRNet-MSA's eval logits are ~1e-14: tools/diag_c4.py), so at any threshold >= 0.5 no
+pixel is confident and the consistency loss is the reference's own 0/0 NaN.  Before the timed steps
+the student's BatchNorm running statistics are therefore calibrated by ONE train-mode forward (no grad) with
+momentum 1 (running stats = that batch's statistics; the teacher's buffers alias the student's, mean_teacher.py:
+13-18), which is what training does to them anyway; the steps then run at confidence threshold 0.5 and the record
+carries cm_mean (the confident-pixel fraction) so a degenerate mean-teacher path is visible.  --threshold 0 and
+--no-calibrate restore the round-2 smoke.
 """
 import argparse
 import json
@@ -22,10 +27,27 @@ sys.path[:0] = [ROOT, PKG]
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+# semi-supervised step GFLOP per labelled image (3F sup fwd+bwd + 2F teacher + 3F consistency fwd+bwd)
+STEP_GFLOP_PER_IMAGE = {'c3': 3855.8, 'c4': 3904.2, 'c5': 85.2}
+PEAK = {'bfloat16': 2.5e15, 'float16': 2.5e15, 'float32': 0.16e15}   # dense MFMA (MI355X_MICROARCH.md)
 CFGS = {'c3': 'configs/c3_deeplabv3_r101.py', 'c4': 'configs/c4_msa_hrnet.py', 'c5': 'configs/c5_hardnet_disc.py'}
 
 
-def run(name, path, dev):
+def calibrate_bn(model, x):
+    """One train-mode forward with BN momentum 1: running statistics := this batch's statistics."""
+    from ssseg import nn as snn
+    bns = [m for m in model.modules() if isinstance(m, (snn.BatchNorm2d, torch.nn.BatchNorm2d))]
+    saved = [m.momentum for m in bns]
+    for m in bns:
+        m.momentum = 1.0
+    model.train()
+    with torch.no_grad():
+        model(x)
+    for m, mo in zip(bns, saved):
+        m.momentum = mo
+
+
+def run(name, path, dev, threshold=0.5, calibrate=True):
     import config
     import mean_teacher
     import train
@@ -46,7 +68,7 @@ def run(name, path, dev):
     if snn.compute_dtype() == torch.float16:
         opt.grad_scaler = amp.GradScaler(dev)
     tc = cfg['train']
-    tc['confidence_threshold'] = 0.0
+    tc['confidence_threshold'] = threshold
     tc['print_freq'] = 10 ** 9
     if cfg['model'].get('discriminator') is not None and tc.get('adversarial_loss_weight'):
         disc = DistributedDataParallel(cfg['model']['discriminator']().to(dev))
@@ -61,6 +83,8 @@ def run(name, path, dev):
     mask = torch.cat([1 - fg, fg], 1).contiguous()
     ua = torch.rand(b, 3, s, s, generator=g).to(dev)
     ub = torch.rand(b, 3, s, s, generator=g).to(dev)
+    if calibrate:
+        calibrate_bn(model.module, ua)
     torch.cuda.reset_peak_memory_stats(dev)
     times, out = [], []
     for step in range(3):
@@ -73,9 +97,14 @@ def run(name, path, dev):
     params_finite = all(bool(torch.isfinite(p).all()) for p in model.parameters())
     losses_finite = all(v is None or v == v and abs(v) != float('inf') for row in out for v in row)
     rec = {'config': name, 'image_size': s, 'batch': b, 'dtype': str(snn.compute_dtype()).replace('torch.', ''),
-           'losses': out, 'losses_finite': losses_finite, 'params_finite': params_finite,
+           'confidence_threshold': threshold, 'bn_calibrated': calibrate,
+           'cm_mean': [row[2] for row in out], 'losses': out, 'losses_finite': losses_finite, 'params_finite': params_finite,
            'ms_per_step_last2': round(1e3 * sum(times[1:]) / 2, 1), 'first_step_s': round(times[0], 1),
            'peak_mem_GB': round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)}
+    step_s = sum(times[1:]) / 2
+    tf = STEP_GFLOP_PER_IMAGE[name] * b / step_s / 1e3
+    rec['conv_tflops'] = round(tf, 1)
+    rec['frac_of_dense_peak'] = round(tf * 1e12 / PEAK[rec['dtype']], 4)
     if 'adversarial' in tc:
         rec['loss_d'] = float(tc['adversarial']['last_loss_d'])
     print(json.dumps(rec), flush=True)
@@ -85,13 +114,15 @@ def run(name, path, dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--configs', default='c3,c4,c5')
+    ap.add_argument('--threshold', type=float, default=0.5)
+    ap.add_argument('--no-calibrate', action='store_true')
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     dist.init_process_group('nccl', init_method='tcp://127.0.0.1:29533', rank=0, world_size=1)
     ok = True
     for name in a.configs.split(','):
-        ok &= run(name, CFGS[name], dev)
+        ok &= run(name, CFGS[name], dev, a.threshold, not a.no_calibrate)
         torch.cuda.empty_cache()
     dist.destroy_process_group()
     sys.exit(0 if ok else 1)
