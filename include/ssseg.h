@@ -235,6 +235,23 @@ typedef struct ssseg_conv_epilogue {
 } ssseg_conv_epilogue;
 int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const ssseg_conv_desc* desc_host, int dt, int dt_out,
                          const ssseg_conv_epilogue* epi, void* ws, size_t ws_bytes, ssseg_stream_t stream);
+/* Virtual channel concat of a conv input (reference models/unet.py:44-45, torch.cat((x, skip), 1) feeding
+ * UpBlock.conv3_0): input channels [0, c1) are read from x (pixel stride desc.ldx) and [c1, desc.C) from x2
+ * (pixel stride ldx2, channel 0 of x2 = input channel c1); same N x H x W.  c1 and C - c1 are multiples of 64
+ * (the LDS-DMA engine takes whole 64-channel k-blocks from one source).  The concatenated tensor is never
+ * written: forward, input-gradient and weight-gradient launches read the two parts where they lie. */
+typedef struct {
+  const void* x2;
+  int64_t c1;
+  int64_t ldx2;
+} ssseg_vcat;
+
+/* ssseg_conv_igemm_epi over a virtual concat input (16-bit dt == dt_out; SSSEG_EUNSUPPORTED where the LDS-DMA
+ * engine cannot run the geometry: the caller then materialises the concat).  Bit-identical to the same launch on
+ * the materialised tensor. */
+int ssseg_conv_igemm_epi_vcat(const void* x, const ssseg_vcat* vc, const void* w, void* y,
+                              const ssseg_conv_desc* desc_host, int dt, int dt_out, const ssseg_conv_epilogue* epi,
+                              void* ws, size_t ws_bytes, ssseg_stream_t stream);
 /* The output phases of a transposed conv in ONE launch (ConvTranspose2d(4,2,1): four 2x2-tap phases over the same
  * input; on 16x16..32x32 inputs a single phase has too few tiles to fill 256 CUs).  desc describes a phase's GEMM
  * (every phase: same K, taps R x S, weight stride ldw, output sub-grid OH x OW); phase_geom[4*p .. 4*p+3] =
@@ -263,7 +280,10 @@ size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* desc_host, int dt
  * (0 = on, -1 = off); knob 4: bf16 variant (0 = auto, 1..10 = an LDS-DMA tile config, 11 = register-staged);
  * knob 5: autotune unseen geometries once on the caller's stream (1 = on, default; 0 = static rule);
  * knob 6 (write 1): clear the per-geometry variant cache; knob 7: LDS-staged coalesced epilogue of the LDS-DMA
- * kernel (0 = on, default; -1 = off).  Variants never change results.  Not thread-safe. */
+ * kernel (0 = on, default; -1 = off); knob 8: LDS-DMA weight gradient (0 = on, -1 = register-staged);
+ * knob 9: LDS-DMA weight-gradient tile config (0 = the static plan, n = config n); knob 10: weight-gradient
+ * split count in percent of the plan's (100 = default).  Forward variants never change results; the
+ * weight-gradient knobs change the fp32 summation order of dW.  Not thread-safe. */
 int ssseg_set_knob(int id, int value);
 
 /* dW = sum over output pixels of dY[p][k] * x_col[p][(r,s,c)] (split-K fp32 slabs + deterministic
@@ -283,6 +303,17 @@ size_t ssseg_conv_wgrad2_workspace_bytes(const ssseg_conv_desc* desc_host, int64
 int ssseg_conv_wgrad2(const void* x, const void* dy, const void* x2, const void* dy2, int64_t n2, float* dw,
                       const ssseg_conv_desc* desc_host, int dt, int64_t c_real, int64_t k_real, int layout,
                       int accumulate, void* ws, size_t ws_bytes, ssseg_stream_t stream);
+
+/* Weight gradients over a virtual concat input (ssseg_vcat, same contract as ssseg_conv_igemm_epi_vcat; vc / vc2
+ * describe the second part of x / x2, with the same c1 and ldx2).  The workspace queries above cover them.
+ * SSSEG_EUNSUPPORTED where the LDS-DMA weight-gradient kernel cannot run the geometry. */
+int ssseg_conv_wgrad_vcat(const void* x, const ssseg_vcat* vc, const void* dy, float* dw,
+                          const ssseg_conv_desc* desc_host, int dt, int64_t c_real, int64_t k_real, int layout,
+                          int accumulate, void* ws, size_t ws_bytes, ssseg_stream_t stream);
+int ssseg_conv_wgrad2_vcat(const void* x, const ssseg_vcat* vc, const void* dy, const void* x2, const ssseg_vcat* vc2,
+                           const void* dy2, int64_t n2, float* dw, const ssseg_conv_desc* desc_host, int dt,
+                           int64_t c_real, int64_t k_real, int layout, int accumulate, void* ws, size_t ws_bytes,
+                           ssseg_stream_t stream);
 
 /* Pack fp32 master weights into the engine's [Kd][Rn][Sn][Cp] layout (dtype dt; rows >= Kr and
  * channels >= Cd zero): layout 0 reads src[k][c][r][s] (src is [Kr][Cd][Rs][Ss]), layout 1 reads

@@ -5,7 +5,7 @@
 
 #include "conv_kernels.h"
 
-int g_knobs[9] = {0, -1, 0, 0, 0, 1, 0, 0, 0};   // split-K off: measured a net loss on the C2 step (r2u)   // runtime variant switches (ssseg_set_knob)
+int g_knobs[12] = {0, -1, 0, 0, 0, 1, 0, 0, 0, 0, 100, 0};   // split-K off: measured a net loss on the C2 step (r2u)   // runtime variant switches (ssseg_set_knob)
 
 // ------------------------------------------------------------------------------------------------
 // weight packing: dst[k][rr][ss][c] (c < Cp; zero for c >= Cd) from an fp32 source
@@ -69,40 +69,39 @@ namespace {
 // returns the tile height BM of the launched config (the fused BN statistics write ceil(M / BM) partial rows)
 template <typename TO>
 int launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep,
-                    unsigned xb, unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph) {
+                    unsigned xb, unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2 = nullptr,
+                    unsigned x2b = 0) {
   switch (cfg) {
-    case 1: return launch_glds_grp_a<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
-    case 2: return launch_glds_grp_a<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
-    case 3: return launch_glds_grp_a<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
-    case 4: return launch_glds_grp_d<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
-    case 5: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
-    case 6: return launch_glds_grp_d<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
-    case 7: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
-    case 8: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
-    case 9: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
-    case 12: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
-    case 13: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
-    case 14: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
-    case 15: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
-    case 16: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
-    case 17: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
-    default: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 1:
+    case 2:
+    case 3: return launch_glds_grp_a<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
+    case 4:
+    case 6:
+    case 18:
+    case 19:
+    case 20: return launch_glds_grp_d<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
+    case 5:
+    case 7:
+    case 8:
+    case 9:
+    case 12: return launch_glds_grp_b<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
+    default: return launch_glds_grp_c<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
   }
 }
 
 // ---- bf16 variant choice: per-geometry autotune cache ----------------------------------------
 // Every variant accumulates the same 32-deep MFMA k-sequence in the same order, so the choice changes
 // speed, never results (tests/test_hip_layers.py::test_conv_variants_bitwise).  Variant 0 is the
-// register-staged kernel, 1..10 and 12..17 the LDS-DMA configs.  With knob 5 on (default) an unseen geometry is
+// register-staged kernel, 1..10 and 12..20 the LDS-DMA configs.  With knob 5 on (default) an unseen geometry is
 // timed once over the candidates on the caller's stream (HIP events) and the fastest is cached.
 constexpr int kSplitBit = 256;   // cached choice flag: run the variant with its split-K plan
-constexpr int kCandidates[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 14, 15, 16, 17};
+constexpr int kCandidates[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 14, 15, 16, 17, 18, 19, 20};
 std::unordered_map<unsigned long long, int> g_variant;
 std::mutex g_variant_mu;
 
 static unsigned long long geom_key(const ConvGeom& g, int tag) {
   const long long v[] = {g.N, g.H, g.W, g.C, g.ldx, g.OH, g.OW, g.K, g.R, g.S, g.sy, g.sx, g.dy, g.dx, g.py, g.px,
-                         g.outH, g.outW, g.osy, g.osx, g.ldy, g.ldw, tag};
+                         g.outH, g.outW, g.osy, g.osx, g.ldy, g.ldw, g.c1b, g.ldx2, tag};
   unsigned long long h = 1469598103934665603ull;
   for (long long e : v) h = (h ^ (unsigned long long)e) * 1099511628211ull;
   return h;
@@ -115,12 +114,15 @@ static int heuristic_variant(const ConvGeom& g) {
   return tiles(64, 64) < 512 ? 10 : 0;
 }
 
+// x2: second source of a virtual concat input (LDS-DMA configs only: the register-staged kernel returns -1)
 template <typename T, typename TO>
 int run_variant(int v, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph = nullptr) {
+                unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph = nullptr, const void* x2 = nullptr,
+                unsigned x2b = 0) {
   if constexpr (sizeof(TO) == 2) {
-    if (v != 0) return launch_glds_cfg<TO>(v, x, w, y, g, ep, xb, wb, s, ws, ph);
+    if (v != 0) return launch_glds_cfg<TO>(v, x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
   }
+  if (x2) return -1;
   if (ph && ph->n > 1) {   // register-staged kernel: one launch per phase
     int bm = 0;
     long long rows = 0;
@@ -143,16 +145,18 @@ int run_variant(int v, const void* x, const void* w, void* y, const ConvGeom& g,
 
 template <typename T, typename TO>
 int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                 unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph) {
+                 unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2 = nullptr,
+                 unsigned x2b = 0) {
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return heuristic_variant(g);
+  const int heur = x2 && heuristic_variant(g) == 0 ? 5 : heuristic_variant(g);
+  if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return heur;
   hipEvent_t e0, e1;
   if (hipEventCreate(&e0) != hipSuccess) return heuristic_variant(g);
   if (hipEventCreate(&e1) != hipSuccess) {
     (void)hipEventDestroy(e0);
     return heuristic_variant(g);
   }
-  int best = heuristic_variant(g);
+  int best = heur;
   float best_ms = 1e30f;
   static const bool log = getenv("SSSEG_TUNE_LOG") != nullptr;   // one line per tuned geometry (stderr)
   char line[512];
@@ -164,11 +168,12 @@ int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const
   for (int split = 0; split < (ws ? 2 : 1); ++split) {
     float* wsv = split ? ws : nullptr;
     for (int v : kCandidates) {
-      run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, ph ? nullptr : wsv, ph);   // warm (code load, caches)
+      // warm (code load, caches); a variant that cannot run this launch (-1) is skipped
+      if (run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, ph ? nullptr : wsv, ph, x2, x2b) <= 0) continue;
       float ms = 1e30f;
       for (int rep = 0; rep < 3; ++rep) {
         (void)hipEventRecord(e0, s);
-        run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, ph ? nullptr : wsv, ph);
+        run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, ph ? nullptr : wsv, ph, x2, x2b);
         (void)hipEventRecord(e1, s);
         float t = 1e30f;
         if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&t, e0, e1) == hipSuccess) ms = std::min(ms, t);
@@ -187,37 +192,44 @@ int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const
   return best;
 }
 
+// x2 (virtual concat, g.c1b / g.ldx2 set): LDS-DMA configs only; returns -1 where they cannot run the launch
 template <typename T, typename TO>
 int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, float* ws,
-                   hipStream_t s, const PhaseTab* ph = nullptr) {
+                   hipStream_t s, const PhaseTab* ph = nullptr, const void* x2 = nullptr) {
   if constexpr (sizeof(T) == 2 && sizeof(TO) == 2) {
     const long long xb = (long long)g.N * g.H * g.W * g.ldx * 2, wb = (long long)g.K * g.ldw * 2;
+    const long long x2b = x2 ? (long long)g.N * g.H * g.W * g.ldx2 * 2 : 0;
     if (sizeof(TO) == 2 && g_knobs[3] == 0 && g.C % 64 == 0 && g.ldx % 8 == 0 && g.ldw % 8 == 0 && g.ldw == g.KK &&
-        g.K > 16 && xb < 0x7fffffffLL && wb < 0x7fffffffLL) {
+        g.K > 16 && xb < 0x7fffffffLL && wb < 0x7fffffffLL && x2b < 0x7fffffffLL && (!x2 || g.ldx2 % 8 == 0)) {
       int v = g_knobs[4];
       if (v < 0) v = 0;
       if (v == 0) {
         const unsigned long long key =
             geom_key(g, (int)sizeof(TO) * 8 + (ws ? 8 : 0) + (ep.stats ? 4 : 0) + (ep.res ? 2 : 0) + (ep.scale ? 1 : 0) +
-                        64 * (ph ? ph->n : 1));
+                        64 * (ph ? ph->n : 1) + (x2 ? 4096 * (g.c1b + 1) : 0));
         std::lock_guard<std::mutex> lk(g_variant_mu);
         auto it = g_variant.find(key);
         if (it != g_variant.end()) {
           v = it->second;
         } else {
-          v = g_knobs[5] ? tune_variant<T, TO>(x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, ws, ph)
+          v = g_knobs[5] ? tune_variant<T, TO>(x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, ws, ph, x2,
+                                               (unsigned)x2b)
                          : heuristic_variant(g);
+          if (x2 && (v & ~kSplitBit) == 0) v = 5;   // the register-staged kernel has no second source
           g_variant[key] = v;
         }
       } else if (g_knobs[4] == 11) {
         v = 0;   // forced register-staged
+        if (x2) return -1;
       }
       // split-K only where the autotuner measured it faster (its fp32 atomics reorder the sums); a variant
       // forced by knob 4 runs unsplit, so forced variants stay bit-comparable
       float* wsv = (g_knobs[4] == 0 && (v & kSplitBit)) ? ws : nullptr;
-      return run_variant<T, TO>(v & ~kSplitBit, x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, ph ? nullptr : wsv, ph);
+      return run_variant<T, TO>(v & ~kSplitBit, x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, ph ? nullptr : wsv, ph,
+                                x2, (unsigned)x2b);
     }
   }
+  if (x2) return -1;
   return run_variant<T, TO>(0, x, w, y, g, ep, 0, 0, s, ph ? nullptr : ws, ph);
 }
 
@@ -233,7 +245,7 @@ bool geom_ok(const ConvGeom& g, int dt) {
 }  // namespace
 
 extern "C" int ssseg_set_knob(int id, int value) {
-  if (id < 0 || id >= 9) return SSSEG_EINVAL;
+  if (id < 0 || id >= 12) return SSSEG_EINVAL;
   if (id == 6 && value) {
     std::lock_guard<std::mutex> lk(g_variant_mu);
     g_variant.clear();
@@ -256,11 +268,20 @@ extern "C" size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* d, int
   return sp > 1 ? (size_t)g.M * g.K * sizeof(float) : 0;
 }
 
-extern "C" int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const ssseg_conv_desc* d, int dt, int dt_out,
-                                    const ssseg_conv_epilogue* epi, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
+static int conv_igemm_epi(const void* x, const void* x2, int64_t c1, int64_t ldx2, const void* w, void* y,
+                          const ssseg_conv_desc* d, int dt, int dt_out, const ssseg_conv_epilogue* epi, void* ws,
+                          size_t ws_bytes, ssseg_stream_t stream) {
   ConvGeom g;
   if (!make_geom(d, g) || !y) return SSSEG_EINVAL;
   if (!geom_ok(g, dt)) return SSSEG_EINVAL;
+  if (x2) {   // virtual concat: channels [0, c1) from x, [c1, C) from x2 (both whole 64-channel blocks)
+    if (c1 <= 0 || c1 >= g.C || c1 % 64 || (g.C - c1) % 64 || g.ldx < c1 || ldx2 < g.C - c1 || ldx2 % 8 ||
+        ldx2 > 0x7fffffff)
+      return SSSEG_EINVAL;
+    if (dt != dt_out || (dt != SSSEG_BF16 && dt != SSSEG_F16) || g.KK == 0) return SSSEG_EUNSUPPORTED;
+    g.c1b = (int)(c1 / 64);
+    g.ldx2 = (int)ldx2;
+  }
   const ssseg_conv_epilogue none = {nullptr, nullptr, nullptr, 0, nullptr, 0, 0.f, nullptr, 0, nullptr};
   const ssseg_conv_epilogue& e = epi ? *epi : none;
   if (e.residual && (e.ldr < g.K || e.ldr > 0x7fffffff)) return SSSEG_EINVAL;
@@ -308,7 +329,11 @@ extern "C" int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const
   // no workspace: no split-K (and never with fused statistics: the split partials are summed after the tiles)
   float* wsf = (need > 0 && ws && ws_bytes >= need && !e.stats) ? (float*)ws : nullptr;
   int bm;
-  if (dt == SSSEG_BF16 && dt_out == SSSEG_BF16)
+  if (x2 && dt == SSSEG_BF16)
+    bm = dispatch_igemm<bf16_t, bf16_t>(x, w, y, g, eb, wsf, s, nullptr, x2);
+  else if (x2)
+    bm = dispatch_igemm<f16_t, f16_t>(x, w, y, g, eh, wsf, s, nullptr, x2);
+  else if (dt == SSSEG_BF16 && dt_out == SSSEG_BF16)
     bm = dispatch_igemm<bf16_t, bf16_t>(x, w, y, g, eb, wsf, s);
   else if (dt == SSSEG_BF16 && dt_out == SSSEG_F32)
     bm = dispatch_igemm<bf16_t, float>(x, w, y, g, ef, wsf, s);
@@ -324,6 +349,18 @@ extern "C" int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const
   if (e.stats_rows_host && e.stats) *e.stats_rows_host = (g.M + bm - 1) / bm;
   SSSEG_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const ssseg_conv_desc* d, int dt, int dt_out,
+                                    const ssseg_conv_epilogue* epi, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
+  return conv_igemm_epi(x, nullptr, 0, 0, w, y, d, dt, dt_out, epi, ws, ws_bytes, stream);
+}
+
+extern "C" int ssseg_conv_igemm_epi_vcat(const void* x, const ssseg_vcat* vc, const void* w, void* y,
+                                         const ssseg_conv_desc* d, int dt, int dt_out, const ssseg_conv_epilogue* epi,
+                                         void* ws, size_t ws_bytes, ssseg_stream_t stream) {
+  if (!vc || !vc->x2) return SSSEG_EINVAL;
+  return conv_igemm_epi(x, vc->x2, vc->c1, vc->ldx2, w, y, d, dt, dt_out, epi, ws, ws_bytes, stream);
 }
 
 extern "C" int ssseg_conv_igemm(const void* x, const void* w, void* y, const ssseg_conv_desc* d, int dt, int dt_out,

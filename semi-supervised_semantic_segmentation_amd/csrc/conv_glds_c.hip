@@ -3,18 +3,21 @@
 
 template <typename TO>
 int launch_glds_grp_c(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                      unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph) {
+                      unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2,
+                      unsigned x2b) {
   switch (cfg) {
-    case 13: return launch_glds<TO, 256, 64, 4, 1, 4, 2>(x, w, y, g, ep, xb, wb, s, ws, ph);
-    case 14: return launch_glds<TO, 128, 64, 2, 2, 4, 2>(x, w, y, g, ep, xb, wb, s, ws, ph);
-    case 15: return launch_glds<TO, 128, 64, 2, 2, 4, 1>(x, w, y, g, ep, xb, wb, s, ws, ph);
-    case 16: return launch_glds<TO, 64, 64, 2, 2, 4, 1>(x, w, y, g, ep, xb, wb, s, ws, ph);
-    case 17: return launch_glds<TO, 64, 64, 2, 2, 4, 2>(x, w, y, g, ep, xb, wb, s, ws, ph);
-    default: return launch_glds<TO, 64, 64, 2, 2, 4, 4>(x, w, y, g, ep, xb, wb, s, ws, ph);
+    case 13: return launch_glds<TO, 256, 64, 4, 1, 4, 2>(x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
+    case 14: return launch_glds<TO, 128, 64, 2, 2, 4, 2>(x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
+    case 15: return launch_glds<TO, 128, 64, 2, 2, 4, 1>(x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
+    case 16: return launch_glds<TO, 64, 64, 2, 2, 4, 1>(x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
+    case 17: return launch_glds<TO, 64, 64, 2, 2, 4, 2>(x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
+    default: return launch_glds<TO, 64, 64, 2, 2, 4, 4>(x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
   }
 }
 
 template int launch_glds_grp_c<bf16_t>(int, const void*, const void*, void*, const ConvGeom&, const Epi<bf16_t>&,
-                                        unsigned, unsigned, hipStream_t, float*, const PhaseTab*);
+                                        unsigned, unsigned, hipStream_t, float*, const PhaseTab*,
+                                        const void*, unsigned);
 template int launch_glds_grp_c<f16_t>(int, const void*, const void*, void*, const ConvGeom&, const Epi<f16_t>&,
-                                       unsigned, unsigned, hipStream_t, float*, const PhaseTab*);
+                                       unsigned, unsigned, hipStream_t, float*, const PhaseTab*,
+                                        const void*, unsigned);

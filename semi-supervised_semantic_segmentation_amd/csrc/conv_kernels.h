@@ -60,6 +60,10 @@ struct ConvGeom {
   int sn64, sn128, sS;
   int oident;   // output pixel == GEMM row (stride-1 output grid, no offsets): no decode in the epilogue
   int aident;   // 1x1 stride-1 unpadded gather over the same grid: A row m is input pixel m
+  // virtual channel concat of the input (unet.py:44 torch.cat feeding conv3_0): channels [0, 64*c1b) come from x
+  // (pixel stride ldx), channels [64*c1b, C) from a second tensor x2 (pixel stride ldx2), same N x H x W.  No
+  // second source: c1b >= C / 64.
+  int c1b, ldx2;
 };
 
 // magic multiplier for unsigned division by d >= 1: n / d = (umulhi(n, m) + n) >> s for n < 2^31
@@ -109,6 +113,8 @@ static inline bool make_geom(const ssseg_conv_desc* d, ConvGeom& g) {
   g.oident = g.osy == 1 && g.osx == 1 && g.ooy == 0 && g.oox == 0 && g.outH == g.OH && g.outW == g.OW;
   g.aident = g.R == 1 && g.S == 1 && g.sy == 1 && g.sx == 1 && g.py == 0 && g.px == 0 && g.H == g.OH &&
              g.W == g.OW;
+  g.c1b = 0x40000000;
+  g.ldx2 = 0;
   return true;
 }
 
@@ -555,13 +561,15 @@ constexpr int ROWB = 80;   // 64 data bytes + 16 pad per LDS row
 // ------------------------------------------------------------------------------------------------
 // forward / dgrad / transposed-conv gather GEMM
 // ------------------------------------------------------------------------------------------------
-extern int g_knobs[9];   // runtime variant switches (ssseg_set_knob), defined in conv.hip
+extern int g_knobs[12];   // runtime variant switches (ssseg_set_knob), defined in conv.hip
 // 0: reg-staged pipeline depth; 1: split-K cap (-1 off = default, 0 auto: the autotuner also times each variant with
 // its split plan, fp32-atomic partials + finalize, and keeps it where faster); 2: 64x64 small-M tiles (reg-staged path);
-// 3: bf16 LDS-DMA path (0 on, -1 off); 4: variant (0 auto, 1..10 / 12..17 LDS-DMA config, 11 register-staged);
+// 3: bf16 LDS-DMA path (0 on, -1 off); 4: variant (0 auto, 1..10 / 12..20 LDS-DMA config, 11 register-staged);
 // 5: autotune unseen geometries (1 on, 0 = static heuristic); knob 6 = 1 clears the variant cache;
 // 7: LDS-staged coalesced epilogue in the LDS-DMA kernel (0 on, -1 off);
-// 8: bf16 weight gradient on the LDS-DMA kernel (0 on, -1 = register-staged wgrad_kernel)
+// 8: bf16 weight gradient on the LDS-DMA kernel (0 on, -1 = register-staged wgrad_kernel);
+// 9: LDS-DMA weight-gradient tile variant (0 = the static plan, 1.. = a forced WGRAD_CFGS entry, conv_wgrad.hip);
+// 10: weight-gradient split count scale in percent (100 = the plan's); 11: reserved
 
 // STATS: the epilogue also writes the fused BatchNorm statistics partials (a separate instantiation: the fp64
 // sums raise the register count, which must not cost the launches that do not need them)
@@ -752,12 +760,15 @@ __device__ __forceinline__ void vmcnt_wait() {
 
 constexpr unsigned OOB = 0x80000000u;   // > any num_records we build: the load returns zeros
 
-template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS, bool STATS>
+// VC: virtual concat input (ConvGeom.c1b / ldx2): k-tiles of channel block >= c1b gather from x2 (a scalar choice
+// per k-tile: the block never straddles the seam because both parts are whole 64-channel blocks)
+template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS, bool STATS, bool VC = false>
 __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __restrict__ x,
                                                                 const TO* __restrict__ w, TO* __restrict__ y,
                                                                 ConvGeom g, Epi<TO> ep, unsigned xbytes,
                                                                 unsigned wbytes, int g_epi_lds, int splits,
-                                                                float* __restrict__ ws, PhaseTab ph) {
+                                                                float* __restrict__ ws, PhaseTab ph,
+                                                                const TO* __restrict__ x2, unsigned x2bytes) {
   constexpr int ROW = 128;                       // bytes per LDS row = 64 bf16 of k
   constexpr int STAGE = (BM + BN) * ROW;
   constexpr int AI = BM / 8 / NW;                // A (pixel) wave-instructions per wave per stage
@@ -801,31 +812,36 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
   }
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, (int)wbytes, 0x00020000);
+  __amdgpu_buffer_rsrc_t xr2 = xr;
+  if constexpr (VC) xr2 = __builtin_amdgcn_make_buffer_rsrc((void*)x2, (short)0, (int)x2bytes, 0x00020000);
 
   // lane rows: A row 8*(wave*AI + ii) + (lane>>3), B row 8*(wave*BI + jj) + (lane>>3); the lane loads
   // logical chunk (lane & 7) ^ swz(row) = (lane & 7) ^ (lane >> 4) ^ 4*(instruction parity)
   const int c_even = (lane & 7) ^ (lane >> 4);
   int a_off[AI], a_iy[AI], a_ix[AI];
+  int a_pix[VC ? AI : 1];   // VC: input pixel index of the row (the byte offset differs per source)
 #pragma unroll
   for (int ii = 0; ii < AI; ++ii) {
     const int inst = wave * AI + ii;
     const int ch = c_even ^ ((inst & 1) * 4);
     const long long m = m0 + 8 * inst + (lane >> 3);
+    int pix = 0;
     if (m < g.M && g.aident) {   // 1x1 / stride 1 / no padding: input pixel m, always in bounds
       a_iy[ii] = 0;
       a_ix[ii] = 0;
-      a_off[ii] = (int)m * g.ldx * 2 + ch * 16;
+      pix = (int)m;
     } else if (m < g.M) {
       int img, oy, ox;   // M < 2^31 (geom_ok): 32-bit decode
       decode_m(g, (int)m, img, oy, ox);
       a_iy[ii] = oy * g.sy + g.py;
       a_ix[ii] = ox * g.sx + g.px;
-      a_off[ii] = ((img * g.H + a_iy[ii]) * g.W + a_ix[ii]) * g.ldx * 2 + ch * 16;
+      pix = (img * g.H + a_iy[ii]) * g.W + a_ix[ii];
     } else {
       a_iy[ii] = -0x40000000;   // never in bounds
       a_ix[ii] = 0;
-      a_off[ii] = 0;
     }
+    a_off[ii] = pix * g.ldx * 2 + ch * 16;
+    if constexpr (VC) a_pix[ii] = pix * g.ldx2 * 2 + ch * 16;
   }
   unsigned b_off[BI];
 #pragma unroll
@@ -837,6 +853,7 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
   }
 
   unsigned a_cur[AI];   // byte offsets of this lane's A rows for the current tap (OOB = padding)
+  unsigned a_cur2[VC ? AI : 1];   // VC: the same rows in x2
   auto set_tap = [&](int tap) {
     const int r = fdiv(tap, g.mS, g.sS), s_ = tap - r * g.S;
     const int dyy = r * g.dy, dxx = s_ * g.dx;
@@ -846,6 +863,7 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
       const int iy = a_iy[ii] + dyy, ix = a_ix[ii] + dxx;
       const bool ok = (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
       a_cur[ii] = ok ? (unsigned)(a_off[ii] + toff) : OOB;
+      if constexpr (VC) a_cur2[ii] = ok ? (unsigned)(a_pix[ii] + (dyy * g.W + dxx) * g.ldx2 * 2) : OOB;
     }
   };
 
@@ -855,8 +873,14 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
     char* As = smem + buf * STAGE;
     char* Bs = As + BM * ROW;
     const unsigned sa = (unsigned)ld_c * 128u, sb = (unsigned)ld_kt * 128u;
+    if (VC && ld_c >= g.c1b) {   // channel block of the second source (scalar branch)
+      const unsigned sa2 = (unsigned)(ld_c - g.c1b) * 128u;
 #pragma unroll
-    for (int ii = 0; ii < AI; ++ii) bldslds16(xr, As + (wave * AI + ii) * 1024, a_cur[ii], sa);
+      for (int ii = 0; ii < AI; ++ii) bldslds16(xr2, As + (wave * AI + ii) * 1024, a_cur2[ii], sa2);
+    } else {
+#pragma unroll
+      for (int ii = 0; ii < AI; ++ii) bldslds16(xr, As + (wave * AI + ii) * 1024, a_cur[ii], sa);
+    }
 #pragma unroll
     for (int jj = 0; jj < BI; ++jj) bldslds16(wr, Bs + (wave * BI + jj) * 1024, b_off[jj], sb);
     ++ld_kt;
@@ -1039,20 +1063,22 @@ inline int plan_splits(const ConvGeom& g);
 template <typename TO>
 __global__ void splitk_finalize_kernel(const float* __restrict__ ws, TO* __restrict__ y, ConvGeom g, Epi<TO> ep);
 
-template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS>
-int launch_glds(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb, unsigned wb,
-                hipStream_t s, float* ws, const PhaseTab* ph) {
+template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS, bool VC>
+int launch_glds_vc(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
+                   unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2, unsigned x2b) {
   static_assert(sizeof(TO) == 2, "LDS-DMA configs: 16-bit activations in and out (fp32-output heads have K <= 16)");
   const long long tiles = ((g.M + BM - 1) / BM) * ((g.K + BN - 1) / BN);
+  const int epi = (int)(g_knobs[7] == 0);
+  const TO* xa = (const TO*)x2;
   if (ph && ph->n > 1) {   // all phases in one launch (no split-K)
     if (ep.stats)
-      hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, true>), dim3((unsigned)tiles, (unsigned)ph->n),
-                         dim3(NW * 64), 0, s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb,
-                         (int)(g_knobs[7] == 0), 1, nullptr, *ph);
+      hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, true, VC>),
+                         dim3((unsigned)tiles, (unsigned)ph->n), dim3(NW * 64), 0, s, (const TO*)x, (const TO*)w,
+                         (TO*)y, g, ep, xb, wb, epi, 1, nullptr, *ph, xa, x2b);
     else
-      hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, false>), dim3((unsigned)tiles, (unsigned)ph->n),
-                         dim3(NW * 64), 0, s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb,
-                         (int)(g_knobs[7] == 0), 1, nullptr, *ph);
+      hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, false, VC>),
+                         dim3((unsigned)tiles, (unsigned)ph->n), dim3(NW * 64), 0, s, (const TO*)x, (const TO*)w,
+                         (TO*)y, g, ep, xb, wb, epi, 1, nullptr, *ph, xa, x2b);
     return BM;
   }
   const PhaseTab one{1, {0}, {0}, {0}, {0}, {nullptr}};
@@ -1060,18 +1086,28 @@ int launch_glds(const void* x, const void* w, void* y, const ConvGeom& g, const 
   const int sp = (ws && !ep.stats) ? plan_splits<TO, BM, BN>(g) : 1;
   if (sp > 1) {
     (void)hipMemsetAsync(ws, 0, sizeof(float) * g.M * g.K, s);
-    hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, false>), dim3((unsigned)tiles, (unsigned)sp),
-                       dim3(NW * 64), 0, s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, 0, sp, ws, one);
+    hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, false, VC>), dim3((unsigned)tiles, (unsigned)sp),
+                       dim3(NW * 64), 0, s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, 0, sp, ws, one, xa,
+                       x2b);
     hipLaunchKernelGGL(splitk_finalize_kernel<TO>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, ws, (TO*)y, g,
                        ep);
   } else if (ep.stats) {
-    hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, true>), dim3((unsigned)tiles), dim3(NW * 64), 0,
-                       s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, (int)(g_knobs[7] == 0), 1, nullptr, one);
+    hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, true, VC>), dim3((unsigned)tiles), dim3(NW * 64),
+                       0, s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, epi, 1, nullptr, one, xa, x2b);
   } else {
-    hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, false>), dim3((unsigned)tiles), dim3(NW * 64), 0,
-                       s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, (int)(g_knobs[7] == 0), 1, nullptr, one);
+    hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, false, VC>), dim3((unsigned)tiles),
+                       dim3(NW * 64), 0, s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, epi, 1, nullptr, one,
+                       xa, x2b);
   }
   return BM;
+}
+
+// x2 != nullptr: the virtual-concat instantiation (second input source, ConvGeom.c1b / ldx2)
+template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS>
+int launch_glds(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb, unsigned wb,
+                hipStream_t s, float* ws, const PhaseTab* ph, const void* x2 = nullptr, unsigned x2b = 0) {
+  if (x2) return launch_glds_vc<TO, BM, BN, WM, WN, NW, NS, true>(x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
+  return launch_glds_vc<TO, BM, BN, WM, WN, NW, NS, false>(x, w, y, g, ep, xb, wb, s, ws, ph, nullptr, 0);
 }
 
 
@@ -1079,16 +1115,20 @@ int launch_glds(const void* x, const void* w, void* y, const ConvGeom& g, const 
 // Each returns the tile height BM of the launched config (the fused BN statistics write ceil(M/BM) rows).
 template <typename TO>
 int launch_glds_grp_a(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                      unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph);
+                      unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2 = nullptr,
+                      unsigned x2b = 0);
 template <typename TO>
 int launch_glds_grp_b(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                      unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph);
+                      unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2 = nullptr,
+                      unsigned x2b = 0);
 template <typename TO>
 int launch_glds_grp_d(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                      unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph);
+                      unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2 = nullptr,
+                      unsigned x2b = 0);
 template <typename TO>
 int launch_glds_grp_c(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                      unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph);
+                      unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2 = nullptr,
+                      unsigned x2b = 0);
 
 
 template <typename T, int BM, int BN>

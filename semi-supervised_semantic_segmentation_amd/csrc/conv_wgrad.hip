@@ -290,25 +290,33 @@ struct WSeg2 {
   long long M;
   unsigned xbytes, dbytes;
   int s1;   // first split of this segment (0: no second segment)
+  // virtual concat input (ssseg_vcat): channels >= c1 of segment 1 / 2 come from xa / xb (pixel stride ldx2);
+  // c1 = 0: none.  A kk-tile never straddles c1 (c1 % BMW == 0), so the source is a block-uniform choice.
+  int c1, ldx2;
+  const void* xa;
+  const void* xb;
+  unsigned xabytes, xbbytes;
 };
 
-template <typename T16, int BMW, int BNW, int NS>
-__global__ void __launch_bounds__(256) wgrad_glds_kernel(const T16* __restrict__ x, const T16* __restrict__ dy,
-                                                         float* __restrict__ slab, ConvGeom g, long long pix_per_split,
-                                                         WDirect dd, unsigned xbytes, unsigned dbytes, WSeg2 sg) {
-  constexpr int BKP = 64;                                    // pixels per k-tile
+template <typename T16, int BMW, int BNW, int NS, int WM = 2, int WN = 2, int BKP = 64>
+__global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const T16* __restrict__ x, const T16* __restrict__ dy,
+                                                                   float* __restrict__ slab, ConvGeom g,
+                                                                   long long pix_per_split, WDirect dd, unsigned xbytes,
+                                                                   unsigned dbytes, WSeg2 sg) {
+  // BKP pixels per k-tile; WM x WN waves, each owning a (BMW / WM) x (BNW / WN) block of dW
+  constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int ROWX = BMW * 2, ROWD = BNW * 2;              // LDS row bytes
   constexpr int XCPR = ROWX / 16, DCPR = ROWD / 16;          // 16-byte chunks per row
-  constexpr int XI = BKP * XCPR / 256, DI = BKP * DCPR / 256;   // wave-instructions per wave per stage
+  constexpr int XI = BKP * XCPR / NT, DI = BKP * DCPR / NT;  // wave-instructions per wave per stage
   constexpr int NL = XI + DI;
   constexpr int STAGE = BKP * (ROWX + ROWD);
-  constexpr int WTM = BMW / 2, WTN = BNW / 2, FM = WTM / 16, FN = WTN / 16;
-  static_assert(XI >= 1 && DI >= 1 && NS >= 2 && NS <= 3, "wgrad glds tile");
+  constexpr int WTM = BMW / WM, WTN = BNW / WN, FM = WTM / 16, FN = WTN / 16;
+  static_assert(XI >= 1 && DI >= 1 && NS >= 2 && NS <= 4 && FM >= 1 && FN >= 1 && BKP % 32 == 0, "wgrad glds tile");
   __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
 
   // wave index as a scalar: the LDS-DMA destinations (per-wave LDS bases) then need no readfirstlane per load
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   // 1-D grid, XCD-aware: consecutive logical ids (the mt x nt tiles of one pixel split, which gather the
   // same x and dY rows) run on one XCD and share its L2
   const int mt = (g.KK + BMW - 1) / BMW, nt = (g.K + BNW - 1) / BNW;
@@ -321,8 +329,11 @@ __global__ void __launch_bounds__(256) wgrad_glds_kernel(const T16* __restrict__
   const int tap = kk0 / g.C, c0 = kk0 - tap * g.C;
   const int tr = tap / g.S, ts = tap - tr * g.S;
   const int offy = tr * g.dy + g.py, offx = ts * g.dx + g.px;
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(seg2 ? (void*)sg.x : (void*)x, (short)0,
-                                                                      (int)(seg2 ? sg.xbytes : xbytes), 0x00020000);
+  const bool src2 = sg.c1 > 0 && c0 >= sg.c1;      // block-uniform: this kk-tile reads the concat's second part
+  const void* xbase = src2 ? (seg2 ? sg.xb : sg.xa) : (seg2 ? sg.x : (const void*)x);
+  const unsigned xbyt = src2 ? (seg2 ? sg.xbbytes : sg.xabytes) : (seg2 ? sg.xbytes : xbytes);
+  const int ldx = src2 ? sg.ldx2 : g.ldx, cb0 = src2 ? c0 - sg.c1 : c0;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)xbase, (short)0, (int)xbyt, 0x00020000);
   const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(seg2 ? (void*)sg.dy : (void*)dy, (short)0,
                                                                       (int)(seg2 ? sg.dbytes : dbytes), 0x00020000);
 
@@ -333,7 +344,7 @@ __global__ void __launch_bounds__(256) wgrad_glds_kernel(const T16* __restrict__
 #pragma unroll
   for (int ii = 0; ii < XI; ++ii) {
     const int row = (wave * XI + ii) * (64 / XCPR) + lane / XCPR;
-    xcb[ii] = (c0 + ((lane % XCPR) ^ wswz<ROWX>(row)) * 8) * 2;
+    xcb[ii] = (cb0 + ((lane % XCPR) ^ wswz<ROWX>(row)) * 8) * 2;
     xp[ii] = p_begin + row;
     const long long pp = xp[ii] < p_end ? xp[ii] : 0;
     decode_m(g, (int)pp, ximg[ii], xoy[ii], xox[ii]);   // M < 2^31 (wg_geom_ok)
@@ -356,7 +367,7 @@ __global__ void __launch_bounds__(256) wgrad_glds_kernel(const T16* __restrict__
       if (xp[ii] < p_end) {
         const int iy = xoy[ii] * g.sy + offy, ix = xox[ii] * g.sx + offx;
         if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
-          off = (unsigned)(((ximg[ii] * g.H + iy) * g.W + ix) * g.ldx) * 2u + (unsigned)xcb[ii];
+          off = (unsigned)(((ximg[ii] * g.H + iy) * g.W + ix) * ldx) * 2u + (unsigned)xcb[ii];
       }
       bldslds16(xr, Xs + (wave * XI + ii) * 1024, off, 0);
       xp[ii] += BKP;
@@ -427,7 +438,10 @@ __global__ void __launch_bounds__(256) wgrad_glds_kernel(const T16* __restrict__
   for (int p = 0; p < D; ++p)
     if (p < nk) issue(p);
   for (int kt = 0; kt < nk; ++kt) {
-    if (D >= 2 && kt + 1 < nk) vmcnt_wait<NL>();   // tile kt landed, tile kt+1 may stay in flight
+    // tile kt landed; the tiles issued after it (at most D - 1) may stay in flight
+    const int ahead = min(nk - 1, kt + D - 1) - kt;
+    if (D >= 3 && ahead >= 2) vmcnt_wait<2 * NL>();
+    else if (D >= 2 && ahead >= 1) vmcnt_wait<NL>();
     else vmcnt_wait<0>();
     __builtin_amdgcn_s_barrier();                  // every wave's tile kt landed; slot (kt+D)%NS is free
     if (kt + D < nk) issue((kt + D) % NS);
@@ -506,18 +520,48 @@ struct WgradPlan {
   int bmw, bnw, mt, nt, splits;
   long long pps;
   bool glds;
+  int cfg;   // LDS-DMA config (WGRAD_CFGS index), 0 = register-staged
 };
 
+// LDS-DMA weight-gradient configs: tile (kk x co), ring depth, waves (WM x WN), pixels per k-tile.
+// The static plan uses 1-4 (bmw by C % 128, bnw by K); 5.. are A/B candidates (knob 9).
+struct WgradCfg {
+  int bmw, bnw, ns, wm, wn, bkp;
+};
+constexpr WgradCfg WGRAD_CFGS[] = {
+    {0, 0, 0, 0, 0, 0},
+    {64, 64, 3, 2, 2, 64},     // 1: 48 KB LDS
+    {128, 64, 3, 2, 2, 64},    // 2: 72 KB
+    {64, 128, 3, 2, 2, 64},    // 3: 72 KB
+    {128, 128, 2, 2, 2, 64},   // 4: 64 KB
+    {128, 64, 3, 4, 2, 64},    // 5: 8 waves, 32x32 per wave
+    {128, 128, 2, 2, 4, 64},   // 6: 8 waves, 64x32 per wave
+    {128, 64, 2, 2, 2, 128},   // 7: 128-pixel k-tiles, 96 KB
+    {64, 64, 3, 2, 2, 128},    // 8: 128-pixel k-tiles, 96 KB
+    {256, 64, 2, 4, 2, 64},    // 9: 8 waves, 80 KB
+    {128, 128, 3, 2, 4, 64},   // 10: 8 waves, 96 KB
+    {64, 64, 4, 2, 2, 64},     // 11: 4-deep ring, 64 KB
+    {128, 64, 4, 2, 2, 64},    // 12: 4-deep ring, 96 KB
+    {64, 128, 4, 2, 2, 64},    // 13: 4-deep ring, 96 KB
+    {64, 64, 3, 2, 4, 64},     // 14: 8 waves, 32x16 per wave
+    {64, 128, 3, 2, 4, 64},    // 15: 8 waves, 32x32 per wave
+    {64, 128, 3, 4, 2, 64},    // 16: 8 waves, 16x64 per wave
+    {128, 128, 2, 4, 2, 64},   // 17: 8 waves, 32x64 per wave
+    {128, 64, 2, 4, 2, 64},    // 18: 8 waves, 2-deep ring, 48 KB
+};
+constexpr int N_WGRAD_CFGS = (int)(sizeof(WGRAD_CFGS) / sizeof(WGRAD_CFGS[0]));
+
 template <typename T>
-WgradPlan plan_wgrad(const ConvGeom& g, int bmw = 0, long long slots = 0) {
+WgradPlan plan_wgrad(const ConvGeom& g, int bmw = 0, long long slots = 0, int bnw = 0, int bkp_ = 0) {
   WgradPlan p;
   p.glds = false;
-  p.bnw = g.K <= 64 ? 64 : 128;
+  p.cfg = 0;
+  p.bnw = bnw ? bnw : (g.K <= 64 ? 64 : 128);
   p.bmw = bmw ? bmw : (g.KK <= 64 ? 64 : 128);   // (a 256x64 tile for Cout <= 64 measured slower: 263 -> 208 TF)
   p.mt = (g.KK + p.bmw - 1) / p.bmw;
   p.nt = (g.K + p.bnw - 1) / p.bnw;
   const long long tiles = (long long)p.mt * p.nt;
-  const int bkp = WG<T>::BKP;
+  const int bkp = bkp_ ? bkp_ : WG<T>::BKP;
   const long long max_splits_by_work = std::max<long long>(1, g.M / (bkp * 8));   // >= 8 k-tiles per split
   long long want = std::max<long long>(1, (1024 + tiles - 1) / tiles);
   if (slots > 0 && tiles < 1024) {
@@ -527,6 +571,7 @@ WgradPlan plan_wgrad(const ConvGeom& g, int bmw = 0, long long slots = 0) {
     const long long rounds = std::max<long long>(1, (1024 + slots / 2) / slots);
     want = std::max<long long>(1, rounds * slots / tiles);
   }
+  if (g_knobs[10] != 100 && g_knobs[10] > 0) want = std::max<long long>(1, want * g_knobs[10] / 100);
   const long long slab_cap = std::max<long long>(1, (64ll << 20) / (4ll * g.K * g.KK + 1));  // <= 64 MiB of slabs
   // (capping splits by slab traffic measured slower: layer3/4 wgrads need the parallelism, 58 -> 150 us)
   long long sp = std::min(std::min(want, max_splits_by_work), slab_cap);
@@ -560,60 +605,93 @@ static bool wgrad_glds_ok(const ConvGeom& g, int dt) {
   return xb < 0x7fffffffLL && db < 0x7fffffffLL;
 }
 
-long long wgrad_slots(int bmw, int bnw);
+long long wgrad_slots(int cfg);
 
-static WgradPlan choose_wgrad(const ConvGeom& g, int dt) {
-  WgradPlan p;
-  if (wgrad_glds_ok(g, dt)) {
-    const int bmw = (g.C % 128 == 0 && g.KK > 64) ? 128 : 64;
-    p = plan_wgrad<bf16_t>(g, bmw, wgrad_slots(bmw, g.K <= 64 ? 64 : 128));
-    p.glds = true;
-  } else {
-    p = dt != SSSEG_F32 ? plan_wgrad<bf16_t>(g) : plan_wgrad<float>(g);
-  }
+// the static LDS-DMA config choice: kk-tile 128 where a tap holds whole 128-channel blocks, co-tile by K
+static int static_wgrad_cfg(const ConvGeom& g) {
+  const int bmw = (g.C % 128 == 0 && g.KK > 64) ? 128 : 64;
+  const int bnw = g.K <= 64 ? 64 : 128;
+  return bmw == 64 ? (bnw == 64 ? 1 : 3) : (bnw == 64 ? 2 : 4);
+}
+
+// c1 > 0 (virtual concat input): the kk-tile must not straddle channel c1 -> a 64-wide tile where c1 % 128 != 0
+static int wgrad_cfg_for(const ConvGeom& g, int c1 = 0) {
+  int c = g_knobs[9];
+  if (!(c > 0 && c < N_WGRAD_CFGS && g.C % WGRAD_CFGS[c].bmw == 0)) c = static_wgrad_cfg(g);
+  if (c1 > 0 && c1 % WGRAD_CFGS[c].bmw) c = WGRAD_CFGS[c].bnw == 64 ? 1 : 3;
+  return c;
+}
+
+static WgradPlan plan_for_cfg(const ConvGeom& g, int c) {
+  const WgradCfg& wc = WGRAD_CFGS[c];
+  WgradPlan p = plan_wgrad<bf16_t>(g, wc.bmw, wgrad_slots(c), wc.bnw, wc.bkp);
+  p.glds = true;
+  p.cfg = c;
   return p;
 }
 
-// resident blocks of the LDS-DMA wgrad kernel chosen for (bmw, bnw) on the whole device (cached per config)
-template <typename T16, int BMW, int BNW>
+static WgradPlan choose_wgrad(const ConvGeom& g, int dt) {
+  if (wgrad_glds_ok(g, dt)) return plan_for_cfg(g, wgrad_cfg_for(g));
+  return dt != SSSEG_F32 ? plan_wgrad<bf16_t>(g) : plan_wgrad<float>(g);
+}
+
+template <typename T16, int C>
+constexpr auto wgrad_kernel_of() {
+  return &wgrad_glds_kernel<T16, WGRAD_CFGS[C].bmw, WGRAD_CFGS[C].bnw, WGRAD_CFGS[C].ns, WGRAD_CFGS[C].wm,
+                            WGRAD_CFGS[C].wn, WGRAD_CFGS[C].bkp>;
+}
+
+// resident blocks of an LDS-DMA wgrad config on the whole device (cached per config)
+template <int C>
 long long wgrad_slots_t() {
   static long long slots = -1;
   if (slots < 0) {
-    constexpr int NS = 64 * (BMW + BNW) * 2 <= 24576 ? 3 : 2;
     int per_cu = 0, dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wgrad_glds_kernel<T16, BMW, BNW, NS>, 256, 0) !=
-            hipSuccess)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wgrad_kernel_of<bf16_t, C>(),
+                                                     WGRAD_CFGS[C].wm * WGRAD_CFGS[C].wn * 64, 0) != hipSuccess)
       return 0;   // unknown: the unquantized plan
     slots = (long long)per_cu * cus;
   }
   return slots;
 }
 
-long long wgrad_slots(int bmw, int bnw) {
-  if (bmw == 128 && bnw == 128) return wgrad_slots_t<bf16_t, 128, 128>();
-  if (bmw == 128) return wgrad_slots_t<bf16_t, 128, 64>();
-  if (bnw == 128) return wgrad_slots_t<bf16_t, 64, 128>();
-  return wgrad_slots_t<bf16_t, 64, 64>();
+template <int C = 1>
+long long wgrad_slots_dispatch(int c) {
+  if constexpr (C < N_WGRAD_CFGS) {
+    if (c == C) return wgrad_slots_t<C>();
+    return wgrad_slots_dispatch<C + 1>(c);
+  } else {
+    return 0;
+  }
 }
 
-template <typename T16, int BMW, int BNW>
+long long wgrad_slots(int cfg) { return wgrad_slots_dispatch<1>(cfg); }
+
+template <typename T16, int C>
 void launch_wgrad_glds_t(const void* x, const void* dy, float* slab, const ConvGeom& g, const WgradPlan& p, WDirect dd,
                          hipStream_t s, const WSeg2& sg) {
-  constexpr int NS = 64 * (BMW + BNW) * 2 <= 24576 ? 3 : 2;   // 48 / 72 / 64 KB of LDS: 2-3 blocks per CU
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.ldx * 2), db = (unsigned)(g.M * g.ldy * 2);
-  hipLaunchKernelGGL((wgrad_glds_kernel<T16, BMW, BNW, NS>), dim3(p.mt * p.nt * p.splits), dim3(256), 0, s,
-                     (const T16*)x, (const T16*)dy, slab, g, p.pps, dd, xb, db, sg);
+  hipLaunchKernelGGL((wgrad_kernel_of<T16, C>()), dim3(p.mt * p.nt * p.splits),
+                     dim3(WGRAD_CFGS[C].wm * WGRAD_CFGS[C].wn * 64), 0, s, (const T16*)x, (const T16*)dy, slab, g,
+                     p.pps, dd, xb, db, sg);
+}
+
+template <typename T16, int C = 1>
+void launch_wgrad_glds_dispatch(const void* x, const void* dy, float* slab, const ConvGeom& g, const WgradPlan& p,
+                                WDirect dd, hipStream_t s, const WSeg2& sg) {
+  if constexpr (C < N_WGRAD_CFGS) {
+    if (p.cfg == C) return launch_wgrad_glds_t<T16, C>(x, dy, slab, g, p, dd, s, sg);
+    return launch_wgrad_glds_dispatch<T16, C + 1>(x, dy, slab, g, p, dd, s, sg);
+  }
 }
 
 template <typename T16>
 void launch_wgrad_glds(const void* x, const void* dy, float* slab, const ConvGeom& g, const WgradPlan& p, WDirect dd,
-                       hipStream_t s, const WSeg2& sg = WSeg2{nullptr, nullptr, 0, 0, 0, 0}) {
-  if (p.bmw == 128 && p.bnw == 128) launch_wgrad_glds_t<T16, 128, 128>(x, dy, slab, g, p, dd, s, sg);
-  else if (p.bmw == 128) launch_wgrad_glds_t<T16, 128, 64>(x, dy, slab, g, p, dd, s, sg);
-  else if (p.bnw == 128) launch_wgrad_glds_t<T16, 64, 128>(x, dy, slab, g, p, dd, s, sg);
-  else launch_wgrad_glds_t<T16, 64, 64>(x, dy, slab, g, p, dd, s, sg);
+                       hipStream_t s, const WSeg2& sg = WSeg2{nullptr, nullptr, 0, 0, 0, 0, 0, 0, nullptr, nullptr, 0,
+                                                               0}) {
+  launch_wgrad_glds_dispatch<T16, 1>(x, dy, slab, g, p, dd, s, sg);
 }
 
 
@@ -628,85 +706,30 @@ bool wg_geom_ok(const ConvGeom& g, int dt) {
 
 }  // namespace
 
+// largest slab workspace over the configs a launch of this geometry may use (the 64-wide kk-tile one is taken for a
+// virtual concat input whose seam is not 128-aligned)
+static size_t wgrad_ws_bytes(const ConvGeom& g, int dt) {
+  const WgradPlan p = choose_wgrad(g, dt);
+  size_t b = (size_t)p.splits * g.K * g.KK * sizeof(float);
+  if (p.glds) {
+    const WgradPlan q = plan_for_cfg(g, wgrad_cfg_for(g, 64));
+    b = std::max(b, (size_t)q.splits * g.K * g.KK * sizeof(float));
+  }
+  return b + 256;
+}
+
 extern "C" size_t ssseg_conv_wgrad_workspace_bytes(const ssseg_conv_desc* d, int dt) {
   ConvGeom g;
   if (!make_geom(d, g)) return 0;
-  const WgradPlan p = choose_wgrad(g, dt);
-  return (size_t)p.splits * g.K * g.KK * sizeof(float) + 256;
+  return wgrad_ws_bytes(g, dt);
 }
-
-extern "C" int ssseg_conv_wgrad(const void* x, const void* dy, float* dw, const ssseg_conv_desc* d, int dt,
-                                int64_t c_real, int64_t k_real, int layout, int accumulate, void* ws, size_t ws_bytes,
-                                ssseg_stream_t stream) {
-  ConvGeom g;
-  if (!make_geom(d, g) || !x || !dy || !dw) return SSSEG_EINVAL;
-  const int vec = dt == SSSEG_F32 ? 4 : 8;
-  if (!wg_geom_ok(g, dt) || g.ldy % vec || g.K % vec) return SSSEG_EINVAL;
-  if (c_real < 1 || c_real > g.C || k_real < 1 || k_real > g.K || (layout != 0 && layout != 1)) return SSSEG_EINVAL;
-  if (!ws || ws_bytes < ssseg_conv_wgrad_workspace_bytes(d, dt)) return SSSEG_EWORKSPACE;
-  hipStream_t s = (hipStream_t)stream;
-  float* slab = (float*)ws;
-  WgradPlan p;
-  if (dt != SSSEG_BF16 && dt != SSSEG_F16 && dt != SSSEG_F32) return SSSEG_EUNSUPPORTED;
-  p = choose_wgrad(g, dt);
-  const WDirect dd{p.splits == 1 ? dw : nullptr, (int)c_real, (int)k_real, layout, accumulate};
-  if (p.glds && dt == SSSEG_F16)
-    launch_wgrad_glds<f16_t>(x, dy, slab, g, p, dd, s);
-  else if (p.glds)
-    launch_wgrad_glds<bf16_t>(x, dy, slab, g, p, dd, s);
-  else if (dt == SSSEG_BF16)
-    launch_wgrad<bf16_t>(x, dy, slab, g, p, dd, s);
-  else if (dt == SSSEG_F16)
-    launch_wgrad<f16_t>(x, dy, slab, g, p, dd, s);
-  else
-    launch_wgrad<float>(x, dy, slab, g, p, dd, s);
-  if (p.splits == 1) {
-    SSSEG_LAUNCH_CHECK();
-    return 0;
-  }
-  const long long total = (long long)g.K * g.KK;
-  if (p.splits >= 64)   // many splits: spread them over the 16 waves of a block
-    hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)((total + 63) / 64)), dim3(1024), 0, s, slab, p.splits,
-                       g.K, g.R, g.S, g.C, (int)c_real, (int)k_real, dw, layout, accumulate);
-  else
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ssseg_grid(total, 256)), dim3(256), 0, s, slab, p.splits, g.K, g.R, g.S,
-                       g.C, (int)c_real, (int)k_real, dw, layout, accumulate);
-  SSSEG_LAUNCH_CHECK();
-  return 0;
-}
-
 
 namespace {
-
-// merged launch plan of ssseg_conv_wgrad2: one split plan over the union of both pixel sets (as if the batch were
-// n1 + n2), each segment cut into whole splits of that size.  False when either segment is not LDS-DMA eligible.
-bool merged_plan(const ConvGeom& g1, int64_t n2, int dt, WgradPlan& p, int& s1, ConvGeom& g2) {
-  if (n2 < 1 || n2 > 0x7fffffff || !wgrad_glds_ok(g1, dt)) return false;
-  g2 = g1;
-  g2.N = (int)n2;
-  g2.M = n2 * (long long)g1.OH * g1.OW;
-  if (g2.M >= 0x7fffffffLL || !wgrad_glds_ok(g2, dt)) return false;
-  ConvGeom gm = g1;
-  gm.M = g1.M + g2.M;
-  const int bmw = (g1.C % 128 == 0 && g1.KK > 64) ? 128 : 64;
-  p = plan_wgrad<bf16_t>(gm, bmw, wgrad_slots(bmw, g1.K <= 64 ? 64 : 128));
-  p.glds = true;
-  // the plan's split count shared out in proportion to the segments' pixels, never more splits in total
-  // (a split past the plan's rounds would start a nearly empty extra round)
-  const long long sp = std::max(2, p.splits);
-  long long a = std::min(sp - 1, std::max(1LL, (long long)((double)sp * g1.M / gm.M + 0.5)));
-  long long pps = std::max((g1.M + a - 1) / a, (g2.M + (sp - a) - 1) / (sp - a));
-  pps = (pps + 63) / 64 * 64;
-  p.pps = pps;
-  s1 = (int)((g1.M + pps - 1) / pps);
-  p.splits = s1 + (int)((g2.M + pps - 1) / pps);
-  return true;
-}
 
 void launch_reduce(const float* slab, const ConvGeom& g, int splits, int64_t c_real, int64_t k_real, float* dw,
                    int layout, int accumulate, hipStream_t s) {
   const long long total = (long long)g.K * g.KK;
-  if (splits >= 64)
+  if (splits >= 64)   // many splits: spread them over the 16 waves of a block
     hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)((total + 63) / 64)), dim3(1024), 0, s, slab, splits,
                        g.K, g.R, g.S, g.C, (int)c_real, (int)k_real, dw, layout, accumulate);
   else
@@ -714,41 +737,129 @@ void launch_reduce(const float* slab, const ConvGeom& g, int splits, int64_t c_r
                        g.C, (int)c_real, (int)k_real, dw, layout, accumulate);
 }
 
-}  // namespace
-
-extern "C" size_t ssseg_conv_wgrad2_workspace_bytes(const ssseg_conv_desc* d, int64_t n2, int dt) {
-  ConvGeom g, g2;
-  if (!make_geom(d, g)) return 0;
-  WgradPlan p;
-  int s1;
-  if (merged_plan(g, n2, dt, p, s1, g2)) return (size_t)p.splits * g.K * g.KK * sizeof(float) + 256;
-  ssseg_conv_desc d2 = *d;
-  d2.N = n2;
-  return std::max(ssseg_conv_wgrad_workspace_bytes(d, dt), ssseg_conv_wgrad_workspace_bytes(&d2, dt));
+// validates a virtual concat descriptor against the geometry and fills the WSeg2 second-source fields of one segment
+bool vcat_ok(const ssseg_vcat* vc, const ConvGeom& g, int dt) {
+  if (!vc) return true;
+  return vc->x2 && vc->c1 > 0 && vc->c1 < g.C && vc->c1 % 64 == 0 && (g.C - vc->c1) % 64 == 0 && g.ldx >= vc->c1 &&
+         vc->ldx2 >= g.C - vc->c1 && vc->ldx2 % 8 == 0 && vc->ldx2 <= 0x7fffffff && (dt == SSSEG_BF16 || dt == SSSEG_F16) &&
+         (long long)g.N * g.H * g.W * vc->ldx2 * 2 < 0x7fffffffLL;
 }
 
-extern "C" int ssseg_conv_wgrad2(const void* x, const void* dy, const void* x2, const void* dy2, int64_t n2, float* dw,
-                                 const ssseg_conv_desc* d, int dt, int64_t c_real, int64_t k_real, int layout,
-                                 int accumulate, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
-  ConvGeom g, g2;
-  if (!make_geom(d, g) || !x || !dy || !x2 || !dy2 || !dw || n2 < 1) return SSSEG_EINVAL;
+int wgrad_one(const void* x, const ssseg_vcat* vc, const void* dy, float* dw, const ssseg_conv_desc* d, int dt,
+              int64_t c_real, int64_t k_real, int layout, int accumulate, void* ws, size_t ws_bytes,
+              ssseg_stream_t stream) {
+  ConvGeom g;
+  if (!make_geom(d, g) || !x || !dy || !dw) return SSSEG_EINVAL;
   const int vec = dt == SSSEG_F32 ? 4 : 8;
   if (!wg_geom_ok(g, dt) || g.ldy % vec || g.K % vec) return SSSEG_EINVAL;
   if (c_real < 1 || c_real > g.C || k_real < 1 || k_real > g.K || (layout != 0 && layout != 1)) return SSSEG_EINVAL;
-  if (!ws || ws_bytes < ssseg_conv_wgrad2_workspace_bytes(d, n2, dt)) return SSSEG_EWORKSPACE;
+  if (!vcat_ok(vc, g, dt)) return SSSEG_EINVAL;
+  if (!ws || ws_bytes < wgrad_ws_bytes(g, dt)) return SSSEG_EWORKSPACE;
+  if (dt != SSSEG_BF16 && dt != SSSEG_F16 && dt != SSSEG_F32) return SSSEG_EUNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  float* slab = (float*)ws;
+  WgradPlan p = choose_wgrad(g, dt);
+  if (vc) {
+    if (!p.glds) return SSSEG_EUNSUPPORTED;   // the register-staged kernel has no second source
+    p = plan_for_cfg(g, wgrad_cfg_for(g, (int)vc->c1));
+  }
+  const WDirect dd{p.splits == 1 ? dw : nullptr, (int)c_real, (int)k_real, layout, accumulate};
+  WSeg2 sg{nullptr, nullptr, 0, 0, 0, 0, 0, 0, nullptr, nullptr, 0, 0};
+  if (vc) {
+    sg.c1 = (int)vc->c1;
+    sg.ldx2 = (int)vc->ldx2;
+    sg.xa = vc->x2;
+    sg.xabytes = (unsigned)((long long)g.N * g.H * g.W * vc->ldx2 * 2);
+  }
+  if (p.glds && dt == SSSEG_F16)
+    launch_wgrad_glds<f16_t>(x, dy, slab, g, p, dd, s, sg);
+  else if (p.glds)
+    launch_wgrad_glds<bf16_t>(x, dy, slab, g, p, dd, s, sg);
+  else if (dt == SSSEG_BF16)
+    launch_wgrad<bf16_t>(x, dy, slab, g, p, dd, s);
+  else if (dt == SSSEG_F16)
+    launch_wgrad<f16_t>(x, dy, slab, g, p, dd, s);
+  else
+    launch_wgrad<float>(x, dy, slab, g, p, dd, s);
+  if (p.splits > 1) launch_reduce(slab, g, p.splits, c_real, k_real, dw, layout, accumulate, s);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+// merged launch plan of ssseg_conv_wgrad2: one split plan over the union of both pixel sets (as if the batch were
+// n1 + n2), each segment cut into whole splits of that size.  False when either segment is not LDS-DMA eligible.
+bool merged_plan(const ConvGeom& g1, int64_t n2, int dt, WgradPlan& p, int& s1, ConvGeom& g2, int c1 = 0) {
+  if (n2 < 1 || n2 > 0x7fffffff || !wgrad_glds_ok(g1, dt)) return false;
+  g2 = g1;
+  g2.N = (int)n2;
+  g2.M = n2 * (long long)g1.OH * g1.OW;
+  if (g2.M >= 0x7fffffffLL || !wgrad_glds_ok(g2, dt)) return false;
+  ConvGeom gm = g1;
+  gm.M = g1.M + g2.M;
+  p = plan_for_cfg(gm, wgrad_cfg_for(g1, c1));
+  const int bkp = WGRAD_CFGS[p.cfg].bkp;
+  // the plan's split count shared out in proportion to the segments' pixels, never more splits in total
+  // (a split past the plan's rounds would start a nearly empty extra round)
+  const long long sp = std::max(2, p.splits);
+  long long a = std::min(sp - 1, std::max(1LL, (long long)((double)sp * g1.M / gm.M + 0.5)));
+  long long pps = std::max((g1.M + a - 1) / a, (g2.M + (sp - a) - 1) / (sp - a));
+  pps = (pps + bkp - 1) / bkp * bkp;
+  p.pps = pps;
+  s1 = (int)((g1.M + pps - 1) / pps);
+  p.splits = s1 + (int)((g2.M + pps - 1) / pps);
+  return true;
+}
+
+size_t wgrad2_ws_bytes(const ConvGeom& g, int64_t n2, int dt) {
+  ConvGeom g2;
   WgradPlan p;
   int s1;
-  if (!merged_plan(g, n2, dt, p, s1, g2)) {   // other kernels: the two contributions one after the other
+  size_t b = 0;
+  for (int c1 : {0, 64})   // the static config and the 64-wide one a virtual concat may need
+    if (merged_plan(g, n2, dt, p, s1, g2, c1)) b = std::max(b, (size_t)p.splits * g.K * g.KK * sizeof(float) + 256);
+  if (b) return b;
+  ConvGeom gb = g;
+  gb.N = (int)n2;
+  gb.M = n2 * (long long)g.OH * g.OW;
+  return std::max(wgrad_ws_bytes(g, dt), wgrad_ws_bytes(gb, dt));
+}
+
+int wgrad_two(const void* x, const ssseg_vcat* vc, const void* dy, const void* x2, const ssseg_vcat* vc2,
+              const void* dy2, int64_t n2, float* dw, const ssseg_conv_desc* d, int dt, int64_t c_real, int64_t k_real,
+              int layout, int accumulate, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
+  ConvGeom g, g2;
+  if (!make_geom(d, g) || !x || !dy || !x2 || !dy2 || !dw || n2 < 1 || n2 > 0x7fffffff) return SSSEG_EINVAL;
+  const int vec = dt == SSSEG_F32 ? 4 : 8;
+  if (!wg_geom_ok(g, dt) || g.ldy % vec || g.K % vec) return SSSEG_EINVAL;
+  if (c_real < 1 || c_real > g.C || k_real < 1 || k_real > g.K || (layout != 0 && layout != 1)) return SSSEG_EINVAL;
+  if ((vc == nullptr) != (vc2 == nullptr) || (vc && (vc->c1 != vc2->c1 || vc->ldx2 != vc2->ldx2))) return SSSEG_EINVAL;
+  ConvGeom gb = g;
+  gb.N = (int)n2;
+  gb.M = n2 * (long long)g.OH * g.OW;
+  if (!vcat_ok(vc, g, dt) || !vcat_ok(vc2, gb, dt)) return SSSEG_EINVAL;
+  if (!ws || ws_bytes < wgrad2_ws_bytes(g, n2, dt)) return SSSEG_EWORKSPACE;
+  WgradPlan p;
+  int s1;
+  if (!merged_plan(g, n2, dt, p, s1, g2, vc ? (int)vc->c1 : 0)) {   // the two contributions one after the other
+    if (vc) return SSSEG_EUNSUPPORTED;
     ssseg_conv_desc d2 = *d;
     d2.N = n2;
-    const int rc = ssseg_conv_wgrad(x, dy, dw, d, dt, c_real, k_real, layout, accumulate, ws, ws_bytes, stream);
+    const int rc = wgrad_one(x, nullptr, dy, dw, d, dt, c_real, k_real, layout, accumulate, ws, ws_bytes, stream);
     if (rc) return rc;
-    return ssseg_conv_wgrad(x2, dy2, dw, &d2, dt, c_real, k_real, layout, 1, ws, ws_bytes, stream);
+    return wgrad_one(x2, nullptr, dy2, dw, &d2, dt, c_real, k_real, layout, 1, ws, ws_bytes, stream);
   }
   hipStream_t s = (hipStream_t)stream;
   float* slab = (float*)ws;
-  const WSeg2 sg{x2, dy2, g2.M, (unsigned)((long long)g2.N * g2.H * g2.W * g2.ldx * 2), (unsigned)(g2.M * g2.ldy * 2),
-                 s1};
+  WSeg2 sg{x2, dy2, g2.M, (unsigned)((long long)g2.N * g2.H * g2.W * g2.ldx * 2), (unsigned)(g2.M * g2.ldy * 2), s1,
+           0, 0, nullptr, nullptr, 0, 0};
+  if (vc) {
+    sg.c1 = (int)vc->c1;
+    sg.ldx2 = (int)vc->ldx2;
+    sg.xa = vc->x2;
+    sg.xb = vc2->x2;
+    sg.xabytes = (unsigned)((long long)g.N * g.H * g.W * vc->ldx2 * 2);
+    sg.xbbytes = (unsigned)((long long)g2.N * g2.H * g2.W * vc->ldx2 * 2);
+  }
   const WDirect dd{nullptr, (int)c_real, (int)k_real, layout, accumulate};
   if (dt == SSSEG_F16)
     launch_wgrad_glds<f16_t>(x, dy, slab, g, p, dd, s, sg);
@@ -757,4 +868,40 @@ extern "C" int ssseg_conv_wgrad2(const void* x, const void* dy, const void* x2, 
   launch_reduce(slab, g, p.splits, c_real, k_real, dw, layout, accumulate, s);
   SSSEG_LAUNCH_CHECK();
   return 0;
+}
+
+}  // namespace
+
+extern "C" int ssseg_conv_wgrad(const void* x, const void* dy, float* dw, const ssseg_conv_desc* d, int dt,
+                                int64_t c_real, int64_t k_real, int layout, int accumulate, void* ws, size_t ws_bytes,
+                                ssseg_stream_t stream) {
+  return wgrad_one(x, nullptr, dy, dw, d, dt, c_real, k_real, layout, accumulate, ws, ws_bytes, stream);
+}
+
+extern "C" int ssseg_conv_wgrad_vcat(const void* x, const ssseg_vcat* vc, const void* dy, float* dw,
+                                     const ssseg_conv_desc* d, int dt, int64_t c_real, int64_t k_real, int layout,
+                                     int accumulate, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
+  if (!vc) return SSSEG_EINVAL;
+  return wgrad_one(x, vc, dy, dw, d, dt, c_real, k_real, layout, accumulate, ws, ws_bytes, stream);
+}
+
+extern "C" size_t ssseg_conv_wgrad2_workspace_bytes(const ssseg_conv_desc* d, int64_t n2, int dt) {
+  ConvGeom g;
+  if (!make_geom(d, g) || n2 < 1 || n2 > 0x7fffffff) return 0;
+  return wgrad2_ws_bytes(g, n2, dt);
+}
+
+extern "C" int ssseg_conv_wgrad2(const void* x, const void* dy, const void* x2, const void* dy2, int64_t n2, float* dw,
+                                 const ssseg_conv_desc* d, int dt, int64_t c_real, int64_t k_real, int layout,
+                                 int accumulate, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
+  return wgrad_two(x, nullptr, dy, x2, nullptr, dy2, n2, dw, d, dt, c_real, k_real, layout, accumulate, ws, ws_bytes,
+                   stream);
+}
+
+extern "C" int ssseg_conv_wgrad2_vcat(const void* x, const ssseg_vcat* vc, const void* dy, const void* x2,
+                                      const ssseg_vcat* vc2, const void* dy2, int64_t n2, float* dw,
+                                      const ssseg_conv_desc* d, int dt, int64_t c_real, int64_t k_real, int layout,
+                                      int accumulate, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
+  if (!vc || !vc2) return SSSEG_EINVAL;
+  return wgrad_two(x, vc, dy, x2, vc2, dy2, n2, dw, d, dt, c_real, k_real, layout, accumulate, ws, ws_bytes, stream);
 }

@@ -3,7 +3,8 @@
 Constructor signatures and submodule names follow the reference (ConvBlock unet.py:4-14, UpBlock
 unet.py:16-50, _center_crop unet.py:52-60, UNet unet.py:63-102), so reference state_dicts load.  The
 forward runs on the native kernels: ConvTranspose2d(4,2,1)+bias+ReLU in one epilogue, bilinear
-x2 (align_corners=True) + 1x1 conv with a fused ReLU, concat/crop in one copy, Conv+BN+ReLU blocks.
+x2 (align_corners=True) + 1x1 conv with a fused ReLU, the concat read part by part by conv3_0 (virtual concat,
+ssseg_vcat; one copy where the parts do not qualify), Conv+BN+ReLU blocks.
 The input may be an NCHW image batch (converted once to NHWC) and the logits come back fp32.
 """
 import torch.nn as nn
@@ -35,7 +36,8 @@ class UpBlock(nn.Module):
 
     def forward(self, x, skip):
         x = self._upsample(x)
-        x = snn.cat_crop(x, skip, self.out_channels, self.skip_channels)
+        # conv3_0 is the concat's only consumer: it reads [x | skip] part by part (virtual concat, no copy)
+        x = snn.cat_crop(x, skip, self.out_channels, self.skip_channels, lazy=True)
         return self.conv3_1(self.conv3_0(x))
 
 

@@ -71,6 +71,10 @@ SIGS = {
     'ssseg_conv_wgrad': (i32, [vp, vp, vp, vp, i32, i64, i64, i32, i32, vp, sz, vp]),
     'ssseg_conv_wgrad2_workspace_bytes': (sz, [vp, i64, i32]),
     'ssseg_conv_wgrad2': (i32, [vp, vp, vp, vp, i64, vp, vp, i32, i64, i64, i32, i32, vp, sz, vp]),
+    # virtual concat inputs (ssseg_vcat)
+    'ssseg_conv_igemm_epi_vcat': (i32, [vp, vp, vp, vp, vp, i32, i32, vp, vp, sz, vp]),
+    'ssseg_conv_wgrad_vcat': (i32, [vp, vp, vp, vp, vp, i32, i64, i64, i32, i32, vp, sz, vp]),
+    'ssseg_conv_wgrad2_vcat': (i32, [vp, vp, vp, vp, vp, vp, i64, vp, vp, i32, i64, i64, i32, i32, vp, sz, vp]),
     'ssseg_weight_pack': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, i32, i64, i64, i64, i64, i64, i64, i32, vp]),
     # batch norm
     'ssseg_bn_workspace_bytes': (sz, [i64]),
@@ -129,6 +133,11 @@ class ConvEpilogue(ctypes.Structure):
                 ('stats', ctypes.c_void_p), ('stats_ld', ctypes.c_int64), ('stats_rows', ctypes.c_void_p)]
 
 
+class VCat(ctypes.Structure):
+    """Mirror of ssseg_vcat (include/ssseg.h): second source of a virtual channel concat."""
+    _fields_ = [('x2', ctypes.c_void_p), ('c1', ctypes.c_int64), ('ldx2', ctypes.c_int64)]
+
+
 _lib = None
 
 
@@ -159,6 +168,19 @@ def call(name, *args):
     rc = getattr(lib(), name)(*args)
     if rc != 0:
         raise RuntimeError(f'ssseg: {name} failed with {_ERRS.get(rc, "hipError " + str(rc))}')
+
+
+EUNSUPPORTED = -2
+
+
+def call_or_unsupported(name, *args):
+    """call(), except that SSSEG_EUNSUPPORTED is returned (False) instead of raised: the caller has another way."""
+    rc = getattr(lib(), name)(*args)
+    if rc == EUNSUPPORTED:
+        return False
+    if rc != 0:
+        raise RuntimeError(f'ssseg: {name} failed with {_ERRS.get(rc, "hipError " + str(rc))}')
+    return True
 
 
 def stream():

@@ -19,7 +19,14 @@ import torch.nn as nn
 
 from . import native as N
 
-_CFG = {'grad_join': True, 'stem': True, 'phases': True, 'eval_bwd_y': True, 'dtype': torch.bfloat16, 'sync_bn': True, 'fuse_stats': True}
+_CFG = {'grad_join': True, 'stem': True, 'phases': True, 'eval_bwd_y': True, 'dtype': torch.bfloat16, 'sync_bn': True,
+        'fuse_stats': True, 'vcat': os.environ.get('SSSEG_VCAT', '1') != '0'}
+
+
+def set_virtual_concat(on):
+    """cat_crop(lazy=True) returns a virtual concat the consuming conv reads part by part (default on); off: the
+    concat is materialised by two copies."""
+    _CFG['vcat'] = bool(on)
 
 
 def set_eval_bwd_from_y(on):
@@ -398,13 +405,14 @@ class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, mod, relu, handoff=None, stats=None, join=None):
         y = mod._ssseg_forward(x, relu, stats=stats)
-        ctx.mod, ctx.relu, ctx.handoff, ctx.join = mod, relu, handoff, join
+        ctx.mod, ctx.relu, ctx.handoff, ctx.join, ctx.vcat = mod, relu, handoff, join, _vcat_of(x)
         ctx.save_for_backward(x, y if _act(relu)[0] else None)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, y = ctx.saved_tensors
+        _vcat_restore(x, ctx.vcat)
         mod = ctx.mod
         gy = mod._grad_in(gy)
         code, slope = _act(ctx.relu)
@@ -520,10 +528,18 @@ class _ConvBase:
                             N.dev_ptr(shift) if shift is not None else None,
                             N.dev_ptr(res) if res is not None else None, res.shape[1] if res is not None else 0,
                             N.dev_ptr(aux) if aux is not None else None, *_act(relu), *sf)
+        vc = _vcat_of(x)
         if stem:
             N.call('ssseg_conv_stem_epi', N.dev_ptr(x), N.dev_ptr(w), N.dev_ptr(y), dref, N.dt_code(x),
                    ctypes_ref(ep), N.stream())
+        elif vc is not None and vc.ready(desc) and N.call_or_unsupported(
+                'ssseg_conv_igemm_epi_vcat', N.dev_ptr(vc.a), ctypes_ref(vc.desc2()), N.dev_ptr(w), N.dev_ptr(y),
+                ctypes_ref(vc.desc_for(desc)), N.dt_code(x), out_dt, ctypes_ref(ep),
+                N.dev_ptr(ws) if ws is not None else None, nb, N.stream()):
+            pass   # read the two parts of the virtual concat where they lie
         else:
+            if vc is not None:
+                materialize(x)
             N.call('ssseg_conv_igemm_epi', N.dev_ptr(x), N.dev_ptr(w) if w is not None else None, N.dev_ptr(y), dref,
                    N.dt_code(x), out_dt, ctypes_ref(ep), N.dev_ptr(ws) if ws is not None else None, nb, N.stream())
         if stats is not None:
@@ -733,22 +749,39 @@ class Conv2d(nn.Conv2d, _ConvBase):
             d = self._fwd_desc(n, H, W)
             nb = N.lib().ssseg_conv_wgrad_workspace_bytes(ctypes_ref(d), N.dt_code(x))
             ws = N.workspace(nb, x.device)
+            vc = _vcat_of(x)
             with _Timed(_conv_flops(n, d.OH, d.OW, self.out_channels, self.in_channels, R, S), 'wgrad',
                         _tag(self, n, H, W)):
-                N.call('ssseg_conv_wgrad', N.dev_ptr(x), N.dev_ptr(gy), N.dev_ptr(_grad_of(self.weight)),
-                       ctypes_ref(d), N.dt_code(x), self.in_channels, self.out_channels, 1, 1, N.dev_ptr(ws), nb,
-                       N.stream())
+                if not (vc is not None and vc.ready(d) and N.call_or_unsupported(
+                        'ssseg_conv_wgrad_vcat', N.dev_ptr(vc.a), ctypes_ref(vc.desc2()), N.dev_ptr(gy),
+                        N.dev_ptr(_grad_of(self.weight)), ctypes_ref(vc.desc_for(d)), N.dt_code(x), self.in_channels,
+                        self.out_channels, 1, 1, N.dev_ptr(ws), nb, N.stream())):
+                    if vc is not None:
+                        materialize(x)
+                    N.call('ssseg_conv_wgrad', N.dev_ptr(x), N.dev_ptr(gy), N.dev_ptr(_grad_of(self.weight)),
+                           ctypes_ref(d), N.dt_code(x), self.in_channels, self.out_channels, 1, 1, N.dev_ptr(ws), nb,
+                           N.stream())
         else:   # the deferred pass and this one: one launch over both pixel sets
             x1, gy1 = pend
             n1 = x1.shape[0]
             d = self._fwd_desc(n1, H, W)
             nb = N.lib().ssseg_conv_wgrad2_workspace_bytes(ctypes_ref(d), n, N.dt_code(x))
             ws = N.workspace(nb, x.device)
+            v1, v2 = _vcat_of(x1), _vcat_of(x)
             with _Timed(_conv_flops(n1 + n, d.OH, d.OW, self.out_channels, self.in_channels, R, S), 'wgrad',
                         _tag(self, n1 + n, H, W)):
-                N.call('ssseg_conv_wgrad2', N.dev_ptr(x1), N.dev_ptr(gy1), N.dev_ptr(x), N.dev_ptr(gy), n,
-                       N.dev_ptr(_grad_of(self.weight)), ctypes_ref(d), N.dt_code(x), self.in_channels,
-                       self.out_channels, 1, 1, N.dev_ptr(ws), nb, N.stream())
+                both = v1 is not None and v2 is not None and v1.same_split(v2) and v1.ready(d)
+                if not (both and N.call_or_unsupported(
+                        'ssseg_conv_wgrad2_vcat', N.dev_ptr(v1.a), ctypes_ref(v1.desc2()), N.dev_ptr(gy1),
+                        N.dev_ptr(v2.a), ctypes_ref(v2.desc2()), N.dev_ptr(gy), n, N.dev_ptr(_grad_of(self.weight)),
+                        ctypes_ref(v1.desc_for(d)), N.dt_code(x), self.in_channels, self.out_channels, 1, 1,
+                        N.dev_ptr(ws), nb, N.stream())):
+                    for t in (x1, x):
+                        if _vcat_of(t) is not None:
+                            materialize(t)
+                    N.call('ssseg_conv_wgrad2', N.dev_ptr(x1), N.dev_ptr(gy1), N.dev_ptr(x), N.dev_ptr(gy), n,
+                           N.dev_ptr(_grad_of(self.weight)), ctypes_ref(d), N.dt_code(x), self.in_channels,
+                           self.out_channels, 1, 1, N.dev_ptr(ws), nb, N.stream())
         if self.bias is not None:
             _ready(self.weight, self.bias)
         else:
@@ -1098,12 +1131,13 @@ class _ConvBNEvalFn(torch.autograd.Function):
                                                                        keep_pre=True, aux_copy=not ycopy)
         ctx.save_for_backward(x, y, aux, scale, mean_eff, invstd, shift)
         ctx.conv, ctx.bn, ctx.relu, ctx.has_res = conv, bn, relu, residual is not None
-        ctx.grad_in, ctx.grad_out, ctx.join = grad_in, grad_out, join
+        ctx.grad_in, ctx.grad_out, ctx.join, ctx.vcat = grad_in, grad_out, join, _vcat_of(x)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, y, aux, scale, mean_eff, invstd, shift = ctx.saved_tensors
+        _vcat_restore(x, ctx.vcat)
         conv, bn = ctx.conv, ctx.bn
         n, cp, h, w = y.shape
         C = bn.num_features
@@ -1250,23 +1284,76 @@ class Upsample(nn.Upsample):
         return interpolate_bilinear(x, (oh, ow), align_corners=bool(self.align_corners))
 
 
+class VirtualCat:
+    """The two parts of a virtual channel concat (cat_crop(lazy=True)): the consuming conv's kernels read channels
+    [0, ca) from a and [ca, ca + cb) from b where they lie (ssseg_vcat); the concat tensor itself is allocated but
+    not written unless materialize() runs (a consumer that cannot read it part by part)."""
+    __slots__ = ('a', 'b', 'ca', 'cb', '_d2')
+
+    def __init__(self, a, b, ca, cb):
+        self.a, self.b, self.ca, self.cb = a, b, ca, cb
+        self._d2 = None
+
+    def desc2(self):
+        if self._d2 is None:
+            self._d2 = N.VCat(N.dev_ptr(self.b), self.ca, self.b.shape[1])
+        return self._d2
+
+    def ready(self, desc):
+        """the engine reads x as [a | b]: desc.C is the concat's width"""
+        return int(desc.C) == self.ca + self.cb
+
+    def desc_for(self, desc):
+        """the launch descriptor with x = a (its own pixel stride)"""
+        d = N.ConvDesc.from_buffer_copy(desc)
+        d.ldx = self.a.shape[1]
+        return d
+
+    def same_split(self, other):
+        return self.ca == other.ca and self.b.shape[1] == other.b.shape[1]
+
+
+def _vcat_of(x):
+    return x.__dict__.get('_ssseg_vcat') if isinstance(x, torch.Tensor) else None
+
+
+def _vcat_restore(x, vc):
+    if vc is not None and '_ssseg_vcat' not in x.__dict__ and not getattr(x, '_ssseg_materialized', False):
+        x.__dict__['_ssseg_vcat'] = vc
+
+
+def materialize(x):
+    """Write a virtual concat's two parts into its own tensor (the copy path); afterwards x is an ordinary
+    activation."""
+    vc = x.__dict__.pop('_ssseg_vcat', None)
+    if vc is None:
+        return x
+    n, cp, H, W = x.shape
+    for t, c, c0 in ((vc.a, vc.ca, 0), (vc.b, vc.cb, vc.ca)):
+        N.call('ssseg_nhwc_copy', N.dev_ptr(t), N.dev_ptr(x) + c0 * x.element_size(), n, H, W, c, H, W, t.shape[1],
+               0, 0, H, W, cp, 0, 0, N.dt_code(t), N.stream())
+    x.__dict__['_ssseg_materialized'] = True
+    return x
+
+
 class _CatFn(torch.autograd.Function):
     """torch.cat((a, b), 1) with a center-crop of whichever map is larger (unet.py:40-45)."""
 
     @staticmethod
-    def forward(ctx, a, b, ca, cb, ja=None, jb=None):
+    def forward(ctx, a, b, ca, cb, ja=None, jb=None, virtual=False):
         ctx.joins = (ja, jb)
         n = a.shape[0]
         H, W = min(a.shape[2], b.shape[2]), min(a.shape[3], b.shape[3])
         v = vec()
         cp = rup(ca + cb, v)
-        y = new_act(n, cp, H, W, a.dtype, a.device, zero=cp != ca + cb)
+        y = new_act(n, cp, H, W, a.dtype, a.device, zero=cp != ca + cb and not virtual)
         offs = []
         for t, c, c0 in ((a, ca, 0), (b, cb, ca)):
             oy, ox = (t.shape[2] - H) // 2, (t.shape[3] - W) // 2
             offs.append((oy, ox))
-            N.call('ssseg_nhwc_copy', N.dev_ptr(t), N.dev_ptr(y) + c0 * y.element_size(), n, H, W, c, t.shape[2],
-                   t.shape[3], t.shape[1], oy, ox, H, W, cp, 0, 0, N.dt_code(t), N.stream())
+            if not virtual:
+                N.call('ssseg_nhwc_copy', N.dev_ptr(t), N.dev_ptr(y) + c0 * y.element_size(), n, H, W, c, t.shape[2],
+                       t.shape[3], t.shape[1], oy, ox, H, W, cp, 0, 0, N.dt_code(t), N.stream())
         ctx.meta = (a.shape, b.shape, ca, cb, offs, H, W, cp)
         return y
 
@@ -1284,13 +1371,25 @@ class _CatFn(torch.autograd.Function):
             if joined is not None:   # the concat usually runs first (it is downstream): rare
                 g = g + joined
             grads.append(_join_give(j, last, g))
-        return grads[0], grads[1], None, None, None, None
+        return grads[0], grads[1], None, None, None, None, None
 
 
-def cat_crop(a, b, ca, cb):
+def _vcat_eligible(a, b, ca, cb):
+    return (_CFG['vcat'] and _CFG['dtype'] in (torch.bfloat16, torch.float16) and ca % 64 == 0 and cb % 64 == 0
+            and a.shape[1] == ca and b.shape[1] == cb and tuple(a.shape[2:]) == tuple(b.shape[2:])
+            and a.shape[0] == b.shape[0] and a.dtype == b.dtype and _is_act(a) and _is_act(b))
+
+
+def cat_crop(a, b, ca, cb, lazy=False):
     """Concatenate NHWC activations a (ca real channels) and b (cb) along channels; the larger map is
-    center-cropped to the smaller (unet.py:40-45 compares dim 2; both dims are cropped to match here)."""
-    return _CatFn.apply(a, b, ca, cb, _join_fwd(a), _join_fwd(b))
+    center-cropped to the smaller (unet.py:40-45 compares dim 2; both dims are cropped to match here).
+    lazy=True: the caller's only consumer is a conv that reads a virtual concat (UpBlock.conv3_0); where the parts
+    qualify (16-bit, whole 64-channel parts, no crop) nothing is copied and the returned tensor carries the parts."""
+    virtual = lazy and _vcat_eligible(a, b, ca, cb)
+    y = _CatFn.apply(a, b, ca, cb, _join_fwd(a), _join_fwd(b), virtual)
+    if virtual:
+        y.__dict__['_ssseg_vcat'] = VirtualCat(a, b, ca, cb)
+    return y
 
 
 @contextlib.contextmanager

@@ -50,16 +50,20 @@ def test_c1_config_supervised_steps_vs_oracle(hip_device):
         fg = (torch.rand(steps, B, 1, H, H, generator=g) > 0.5).float()
         masks = torch.cat([1 - fg, fg], 2)
 
-        def oracle(dt):
+        def oracle(dt, pert=0.0):
             import copy
             s = copy.deepcopy(ref).to(dt)
             o = torch.optim.SGD(s.parameters(), lr=tc['base_lr'], momentum=0.9, weight_decay=0.0005)
-            logs = train_ref.train_epoch(s, None, o, list(zip(imgs.to(dt), masks.to(dt))), iter(()), 0,
+            x = imgs.to(dt)
+            if pert:   # the step's own sensitivity (tests/parity.py): inputs moved by ~fp32 rounding
+                x = x * (1 + pert * torch.randn(x.shape, generator=torch.Generator().manual_seed(99), dtype=dt))
+            logs = train_ref.train_epoch(s, None, o, list(zip(x, masks.to(dt))), iter(()), 0,
                                          train_ref.default_cfg(use_semi_supervised=False,
                                                                gradient_clip_value=tc['gradient_clip_value']))
             return logs, s
         r32, s32 = oracle(torch.float32)
         r64, s64 = oracle(torch.float64)
+        _, sp = oracle(torch.float64, pert=1e-6)
         model.train()
         opt.zero_grad()
         logs = []
@@ -70,7 +74,13 @@ def test_c1_config_supervised_steps_vs_oracle(hip_device):
             logs.append((float(c),))
         check_losses(logs, [(r['sup_loss'],) for r in r32], [(r['sup_loss'],) for r in r64], names=('sup',))
         np_sd = lambda m: {k: v.detach().cpu().double().numpy() for k, v in m.state_dict().items()}  # noqa: E731
-        bad = tensor_outliers(np_sd(model), np_sd(s32), np_sd(s64))
+        # the deepest blocks normalise 2 and 1 pixels per channel (batch 2 at 2x2 / 1x1 after ceil-mode pools): their
+        # batch statistics and every gradient through them are dominated by rounding, so the bound includes the
+        # fp64 drift under a 1e-6 input perturbation and a floor at 1e-3 of each parameter group's scale
+        # (tests/parity.py rules, as the UNet-R50 / DDP tests)
+        sd64 = np_sd(s64)
+        floor = 1e-3 * max(float(np.abs(v).max()) for k, v in sd64.items() if 'running' not in k and v.ndim)
+        bad = tensor_outliers(np_sd(model), np_sd(s32), sd64, np_sd(sp), floor=floor)
         print('C1 parameter outliers after 3 steps:', bad[:5])
         assert not bad, bad[:5]
     finally:

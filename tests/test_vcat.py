@@ -1,0 +1,82 @@
+"""Virtual channel concat (ssseg_vcat; reference models/unet.py:44-45 torch.cat((x, skip), 1) feeding
+UpBlock.conv3_0): the consuming conv's forward (LDS-DMA A-loader), weight gradient and merged two-pass weight
+gradient read the two parts where they lie.  Every engine launch accumulates the same MFMA k-sequence from the
+same bytes as on the materialised concat, so outputs, input gradients and weight gradients must be BIT-identical
+to the copy path (snn.set_virtual_concat(False))."""
+import contextlib
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _upblock(dev, cin, skip, cout, seed=3):
+    from models.unet import UpBlock
+    torch.manual_seed(seed)
+    return UpBlock(cin, skip, cout, shrink=False, train_upsampling=True).to(dev)
+
+
+def _run(block, x, skip, mode, vcat, gy=None):
+    from ssseg import nn as snn
+    snn.set_virtual_concat(vcat)
+    try:
+        block.zero_grad(set_to_none=True)
+        xa = snn.to_act(x).detach().requires_grad_(mode != 'nograd')
+        sa = snn.to_act(skip).detach().requires_grad_(mode != 'nograd')
+        if mode == 'nograd':
+            block.eval()
+            with torch.no_grad():
+                y = block(xa, sa)
+            return [y.clone()]
+        block.train(mode == 'train')
+        if mode == 'merged':   # two backward passes, the first one's weight gradients deferred (train_step)
+            outs = []
+            for i in range(2):
+                with (snn.defer_wgrad() if i == 0 else contextlib.nullcontext()):
+                    y = block(xa, sa)
+                    y.backward(gy)
+                outs.append(y.detach().clone())
+            snn.flush_wgrad()
+        else:
+            y = block(xa, sa)
+            y.backward(gy)
+            outs = [y.detach().clone()]
+        return outs + [xa.grad.clone(), sa.grad.clone()] + [p.grad.clone() for p in block.parameters()]
+    finally:
+        snn.set_virtual_concat(True)
+        block.train()
+
+
+@pytest.mark.parametrize('cin,skip,cout,H', [(256, 256, 128, 16), (128, 64, 64, 33), (512, 1024, 128, 9)])
+@pytest.mark.parametrize('mode', ['train', 'eval', 'nograd', 'merged'])
+def test_upblock_virtual_concat_bitwise(hip_device, cin, skip, cout, H, mode):
+    from ssseg import nn as snn
+    snn.set_compute_dtype(torch.bfloat16)
+    block = _upblock(hip_device, cin, skip, cout)
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(2, cin, H, H, generator=g).to(hip_device)
+    s = torch.randn(2, skip, 2 * H, 2 * H, generator=g).to(hip_device)
+    gy = snn.to_act(torch.randn(2, cout, 2 * H, 2 * H, generator=g).to(hip_device)) if mode != 'nograd' else None
+    ref = _run(block, x, s, mode, False, gy)
+    got = _run(block, x, s, mode, True, gy)
+    assert len(ref) == len(got)
+    for i, (a, b) in enumerate(zip(got, ref)):
+        assert torch.equal(a, b), f'{mode}: tensor {i} differs (max |d| {float((a.float() - b.float()).abs().max())})'
+
+
+def test_virtual_concat_is_not_copied(hip_device):
+    """The lazy concat of an eligible UpBlock carries its parts and its memory is never written by the forward."""
+    from ssseg import nn as snn
+    snn.set_compute_dtype(torch.bfloat16)
+    a = snn.to_act(torch.randn(2, 128, 8, 8, device=hip_device))
+    b = snn.to_act(torch.randn(2, 64, 8, 8, device=hip_device))
+    y = snn.cat_crop(a, b, 128, 64, lazy=True)
+    assert snn._vcat_of(y) is not None
+    snn.materialize(y)
+    assert snn._vcat_of(y) is None
+    ref = snn.cat_crop(a, b, 128, 64)
+    assert torch.equal(y, ref)
+    # not eligible (fp32 mode / 64-unaligned part): an ordinary concat
+    c = snn.to_act(torch.randn(2, 40, 8, 8, device=hip_device))
+    assert snn._vcat_of(snn.cat_crop(a, c, 128, 40, lazy=True)) is None
