@@ -527,6 +527,7 @@ struct WgradPlan {
 // The static plan uses 1-4 (bmw by C % 128, bnw by K); 5.. are A/B candidates (knob 9).
 struct WgradCfg {
   int bmw, bnw, ns, wm, wn, bkp;
+  int pct = 100;   // split count in percent of plan_wgrad's (fewer, longer splits: less slab traffic)
 };
 constexpr WgradCfg WGRAD_CFGS[] = {
     {0, 0, 0, 0, 0, 0},
@@ -548,11 +549,15 @@ constexpr WgradCfg WGRAD_CFGS[] = {
     {64, 128, 3, 4, 2, 64},    // 16: 8 waves, 16x64 per wave
     {128, 128, 2, 4, 2, 64},   // 17: 8 waves, 32x64 per wave
     {128, 64, 2, 4, 2, 64},    // 18: 8 waves, 2-deep ring, 48 KB
+    // the static plan's picks (tools/wgrad_variants.py on the C2 geometries, profiles/r3_wgrad_variants.txt): the
+    // 8-wave tiles at half the splits beat the round-2 4-wave plan by 15-35 % on every layer with C % 128 == 0
+    {128, 128, 2, 2, 4, 64, 50},   // 19: cfg 6 at 50 % of the splits
+    {64, 128, 3, 4, 2, 64, 50},    // 20: cfg 16 at 50 % of the splits
 };
 constexpr int N_WGRAD_CFGS = (int)(sizeof(WGRAD_CFGS) / sizeof(WGRAD_CFGS[0]));
 
 template <typename T>
-WgradPlan plan_wgrad(const ConvGeom& g, int bmw = 0, long long slots = 0, int bnw = 0, int bkp_ = 0) {
+WgradPlan plan_wgrad(const ConvGeom& g, int bmw = 0, long long slots = 0, int bnw = 0, int bkp_ = 0, int pct = 100) {
   WgradPlan p;
   p.glds = false;
   p.cfg = 0;
@@ -571,6 +576,7 @@ WgradPlan plan_wgrad(const ConvGeom& g, int bmw = 0, long long slots = 0, int bn
     const long long rounds = std::max<long long>(1, (1024 + slots / 2) / slots);
     want = std::max<long long>(1, rounds * slots / tiles);
   }
+  if (pct != 100) want = std::max<long long>(1, want * pct / 100);
   if (g_knobs[10] != 100 && g_knobs[10] > 0) want = std::max<long long>(1, want * g_knobs[10] / 100);
   const long long slab_cap = std::max<long long>(1, (64ll << 20) / (4ll * g.K * g.KK + 1));  // <= 64 MiB of slabs
   // (capping splits by slab traffic measured slower: layer3/4 wgrads need the parallelism, 58 -> 150 us)
@@ -607,24 +613,25 @@ static bool wgrad_glds_ok(const ConvGeom& g, int dt) {
 
 long long wgrad_slots(int cfg);
 
-// the static LDS-DMA config choice: kk-tile 128 where a tap holds whole 128-channel blocks, co-tile by K
+// the static LDS-DMA config choice: kk-tile 128 where a tap holds whole 128-channel blocks, co-tile by K; 8-wave
+// tiles (measured: profiles/r3_wgrad_variants.txt)
 static int static_wgrad_cfg(const ConvGeom& g) {
   const int bmw = (g.C % 128 == 0 && g.KK > 64) ? 128 : 64;
   const int bnw = g.K <= 64 ? 64 : 128;
-  return bmw == 64 ? (bnw == 64 ? 1 : 3) : (bnw == 64 ? 2 : 4);
+  return bmw == 64 ? (bnw == 64 ? 1 : 20) : (bnw == 64 ? 18 : 19);
 }
 
 // c1 > 0 (virtual concat input): the kk-tile must not straddle channel c1 -> a 64-wide tile where c1 % 128 != 0
 static int wgrad_cfg_for(const ConvGeom& g, int c1 = 0) {
   int c = g_knobs[9];
   if (!(c > 0 && c < N_WGRAD_CFGS && g.C % WGRAD_CFGS[c].bmw == 0)) c = static_wgrad_cfg(g);
-  if (c1 > 0 && c1 % WGRAD_CFGS[c].bmw) c = WGRAD_CFGS[c].bnw == 64 ? 1 : 3;
+  if (c1 > 0 && c1 % WGRAD_CFGS[c].bmw) c = WGRAD_CFGS[c].bnw == 64 ? 1 : 20;
   return c;
 }
 
 static WgradPlan plan_for_cfg(const ConvGeom& g, int c) {
   const WgradCfg& wc = WGRAD_CFGS[c];
-  WgradPlan p = plan_wgrad<bf16_t>(g, wc.bmw, wgrad_slots(c), wc.bnw, wc.bkp);
+  WgradPlan p = plan_wgrad<bf16_t>(g, wc.bmw, wgrad_slots(c), wc.bnw, wc.bkp, wc.pct);
   p.glds = true;
   p.cfg = c;
   return p;

@@ -30,12 +30,13 @@ def check_losses(hip, r32, r64, names=('sup', 'unsup')):
     return lines
 
 
-def tensor_outliers(got, ref32, ref64, refp=None, rel=1e-3, floor=None):
+def tensor_outliers(got, ref32, ref64, refp=None, rel=1e-3, floor=None, factor=2.0):
     """Per-tensor parity of parameters / gradients after a few optimizer steps: max |got - ref64| relative to
     the tensor's scale must stay within max(rel, 2x the fp32 oracle's drift, 2x the drift of an fp64 run on
     inputs perturbed by ~1e-6 (ReLU / max-pool switches of tiny-batch activations)).  Dicts of numpy
     arrays; `floor` (a global scale) keeps mathematically-zero tensors (a bias feeding a BatchNorm) from
-    being judged on rounding noise.  Returns the violating (name, err, drift32, drift_pert) rows."""
+    being judged on rounding noise; `factor` (default 2) multiplies the two drifts.  Returns the violating
+    (name, err, drift32, drift_pert) rows."""
     import numpy as np
     bad = []
     for k, b in ref64.items():
@@ -46,6 +47,6 @@ def tensor_outliers(got, ref32, ref64, refp=None, rel=1e-3, floor=None):
         e = float(np.abs(np.asarray(got[k], np.float64) - b).max()) / scale
         d32 = float(np.abs(np.asarray(ref32[k], np.float64) - b).max()) / scale
         dp = float(np.abs(np.asarray(refp[k], np.float64) - b).max()) / scale if refp is not None else 0.0
-        if e > max(rel, 2 * d32, 2 * dp):
+        if e > max(rel, factor * d32, factor * dp):
             bad.append((k, e, d32, dp))
     return bad

@@ -20,7 +20,7 @@ from ssseg import nn as snn  # noqa: E402
 LAYERS = [(128, 64, 3, 256), (384, 128, 3, 128), (256, 256, 3, 32), (64, 64, 3, 256), (128, 128, 3, 64),
           (64, 64, 3, 128), (64, 256, 1, 128), (256, 1024, 1, 32), (640, 128, 3, 64), (1024, 256, 1, 32),
           (128, 512, 1, 64), (512, 512, 3, 16), (1152, 128, 3, 32), (2048, 512, 1, 16), (512, 2048, 1, 16)]
-CFG_C = {1: 64, 2: 128, 3: 64, 4: 128, 5: 128, 6: 128, 7: 128, 8: 64, 9: 256, 10: 128, 11: 64, 12: 128, 13: 64,
+CFG_C = {1: 64, 2: 128, 3: 64, 4: 128, 5: 128, 6: 128, 7: 128, 8: 64, 9: 256, 10: 128, 11: 64, 12: 128, 13: 64, 19: 128, 20: 64,
          14: 64, 15: 64, 16: 64, 17: 128, 18: 128}
 
 
