@@ -80,6 +80,9 @@ int launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvGe
     case 18:
     case 19:
     case 20: return launch_glds_grp_d<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
+    case 21:
+    case 22:
+    case 23: return launch_glds_grp_e<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
     case 5:
     case 7:
     case 8:
@@ -92,10 +95,10 @@ int launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvGe
 // ---- bf16 variant choice: per-geometry autotune cache ----------------------------------------
 // Every variant accumulates the same 32-deep MFMA k-sequence in the same order, so the choice changes
 // speed, never results (tests/test_hip_layers.py::test_conv_variants_bitwise).  Variant 0 is the
-// register-staged kernel, 1..10 and 12..20 the LDS-DMA configs.  With knob 5 on (default) an unseen geometry is
+// register-staged kernel, 1..10 and 12..23 the LDS-DMA configs.  With knob 5 on (default) an unseen geometry is
 // timed once over the candidates on the caller's stream (HIP events) and the fastest is cached.
 constexpr int kSplitBit = 256;   // cached choice flag: run the variant with its split-K plan
-constexpr int kCandidates[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 14, 15, 16, 17, 18, 19, 20};
+constexpr int kCandidates[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23};
 std::unordered_map<unsigned long long, int> g_variant;
 std::mutex g_variant_mu;
 

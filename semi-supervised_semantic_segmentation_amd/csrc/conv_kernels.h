@@ -56,8 +56,8 @@ struct ConvGeom {
   // decode m -> (img, oy, ox) of every tile row otherwise costs two integer divisions (~40 VALU each)
   unsigned mow, moh;
   int sow, soh;
-  unsigned mn64, mn128, mS;   // magic divisors: n-tile counts ceil(K/64), ceil(K/128) and the filter width S
-  int sn64, sn128, sS;
+  unsigned mn64, mn128, mn256, mS;   // magic divisors: n-tile counts ceil(K/64), ceil(K/128), ceil(K/256), filter width S
+  int sn64, sn128, sn256, sS;
   int oident;   // output pixel == GEMM row (stride-1 output grid, no offsets): no decode in the epilogue
   int aident;   // 1x1 stride-1 unpadded gather over the same grid: A row m is input pixel m
   // virtual channel concat of the input (unet.py:44 torch.cat feeding conv3_0): channels [0, 64*c1b) come from x
@@ -109,6 +109,7 @@ static inline bool make_geom(const ssseg_conv_desc* d, ConvGeom& g) {
   fdiv_init(g.OH > 0 ? g.OH : 1, g.moh, g.soh);
   fdiv_init(g.K > 0 ? (g.K + 63) / 64 : 1, g.mn64, g.sn64);
   fdiv_init(g.K > 0 ? (g.K + 127) / 128 : 1, g.mn128, g.sn128);
+  fdiv_init(g.K > 0 ? (g.K + 255) / 256 : 1, g.mn256, g.sn256);
   fdiv_init(g.S > 0 ? g.S : 1, g.mS, g.sS);
   g.oident = g.osy == 1 && g.osx == 1 && g.ooy == 0 && g.oox == 0 && g.outH == g.OH && g.outW == g.OW;
   g.aident = g.R == 1 && g.S == 1 && g.sy == 1 && g.sx == 1 && g.py == 0 && g.px == 0 && g.H == g.OH &&
@@ -255,7 +256,7 @@ template <> struct Load4<bf16_t> {
 // The per-channel affine of a fragment column is loaded once, and every residual of the column is loaded
 // before the first store (the stores may alias the residual as far as the compiler knows, so it could not
 // batch those loads itself): one HBM round trip per column instead of one per pixel.
-template <typename TO, int FM, int FN>
+template <typename TO, int FM, int FN, bool ST = false>
 __device__ __forceinline__ void store_tile(const f32x4 (&acc)[FN][FM], long long mb, int nb, int lane,
                                            const ConvGeom& g, TO* __restrict__ y, const Epi<TO>& ep,
                                            double (*st1)[4] = nullptr, double (*st2)[4] = nullptr) {
@@ -289,7 +290,9 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[FN][FM], long long
         if (full && (ep.ldr & 3) == 0)
           Load4<TO>::ld(rp, r[j]);
         else
-          for (int e = 0; e < 4 && n + e < g.K; ++e) r[j][e] = io<TO>::ld(rp, e);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)   // fixed trip count: r stays in registers (a runtime bound spills it)
+            if (n + e < g.K) r[j][e] = io<TO>::ld(rp, e);
       }
     }
 #pragma unroll
@@ -300,7 +303,9 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[FN][FM], long long
         if (full && (g.ldy & 3) == 0)
           Store4<TO>::st(ep.aux + op[j] * g.ldy + n, a4);
         else
-          for (int e = 0; e < 4 && n + e < g.K; ++e) io<TO>::st(ep.aux, op[j] * g.ldy + n + e, a4[e]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (n + e < g.K) io<TO>::st(ep.aux, op[j] * g.ldy + n + e, a4[e]);
       }
       float v[4];
 #pragma unroll
@@ -311,17 +316,21 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[FN][FM], long long
         a += r[j][e];
         a = act_fwd(a, ep.relu, ep.slope);
         v[e] = a;
-        if (st1 && n + e < g.K) {
-          const double q = (double)stored<TO>(a);
-          st1[i][e] += q;
-          st2[i][e] += q * q;
+        if constexpr (ST) {   // compile-time: the statistics arrays stay in registers
+          if (n + e < g.K) {
+            const double q = (double)stored<TO>(a);
+            st1[i][e] += q;
+            st2[i][e] += q * q;
+          }
         }
       }
       TO* yp = y + op[j] * g.ldy;
       if (full && (g.ldy & 3) == 0) {
         Store4<TO>::st(yp + n, v);
       } else {
-        for (int e = 0; e < 4 && n + e < g.K; ++e) io<TO>::st(yp, n + e, v[e]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (n + e < g.K) io<TO>::st(yp, n + e, v[e]);
       }
     }
   }
@@ -447,7 +456,9 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
             Out8<TO>::ld(ep.res + op[p] * ep.ldr + n, r[p]);
           }
         } else
-          for (int e = 0; e < 8 && n + e < g.K; ++e) r[p][e] = io<TO>::ld(ep.res, op[p] * ep.ldr + n + e);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)   // fixed trip count: r stays in registers (a runtime bound spills it)
+            if (n + e < g.K) r[p][e] = io<TO>::ld(ep.res, op[p] * ep.ldr + n + e);
       }
     }
 #pragma unroll
@@ -466,7 +477,9 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
         Out8<TO>::st(y + o, v);
         if (ep.aux) Out8<TO>::st(ep.aux + o, raw);
       } else {
-        for (int e = 0; e < 8 && n + e < g.K; ++e) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if (n + e >= g.K) continue;
           io<TO>::st(y, o + e, v[e]);
           if (ep.aux) io<TO>::st(ep.aux, o + e, raw[e]);
         }
@@ -564,7 +577,7 @@ constexpr int ROWB = 80;   // 64 data bytes + 16 pad per LDS row
 extern int g_knobs[12];   // runtime variant switches (ssseg_set_knob), defined in conv.hip
 // 0: reg-staged pipeline depth; 1: split-K cap (-1 off = default, 0 auto: the autotuner also times each variant with
 // its split plan, fp32-atomic partials + finalize, and keeps it where faster); 2: 64x64 small-M tiles (reg-staged path);
-// 3: bf16 LDS-DMA path (0 on, -1 off); 4: variant (0 auto, 1..10 / 12..20 LDS-DMA config, 11 register-staged);
+// 3: bf16 LDS-DMA path (0 on, -1 off); 4: variant (0 auto, 1..10 / 12..23 LDS-DMA config, 11 register-staged);
 // 5: autotune unseen geometries (1 on, 0 = static heuristic); knob 6 = 1 clears the variant cache;
 // 7: LDS-staged coalesced epilogue in the LDS-DMA kernel (0 on, -1 off);
 // 8: bf16 weight gradient on the LDS-DMA kernel (0 on, -1 = register-staged wgrad_kernel);
@@ -729,7 +742,7 @@ __global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __res
     for (int i = 0; i < FN; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) st1[i][e] = st2[i][e] = 0.0;
-    store_tile<TO, FM, FN>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, g, y, ep, st1, st2);
+    store_tile<TO, FM, FN, true>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, g, y, ep, st1, st2);
     frag_stats<FN, BN, 4>(st1, st2, wn * WTN, smem, m0 / BM, n0, ep.stats, ep.sld);
     return;
   }
@@ -787,8 +800,9 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
   const int wm = wave / WN, wn = wave % WN;
   const int nnt = (g.K + BN - 1) / BN;
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
-  static_assert(BN == 64 || BN == 128, "n-tile divisor magic");
-  const int mt_ = fdiv(tile, BN == 64 ? g.mn64 : g.mn128, BN == 64 ? g.sn64 : g.sn128);   // tile / nnt
+  static_assert(BN == 64 || BN == 128 || BN == 256, "n-tile divisor magic");
+  const int mt_ = fdiv(tile, BN == 64 ? g.mn64 : (BN == 128 ? g.mn128 : g.mn256),
+                       BN == 64 ? g.sn64 : (BN == 128 ? g.sn128 : g.sn256));   // tile / nnt
   const long long m0 = (long long)mt_ * BM;
   const int n0 = (tile - mt_ * nnt) * BN;
   if (ph.n > 1) {   // this block's output phase: offsets, sub-grid, weights, statistics rows
@@ -904,7 +918,7 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
   PreRes<PRE ? EP_NP : 1> pre;
   pre.on = false;
   if constexpr (PRE) {
-    if (g_epi_lds && ep.res && splits == 1) {
+    if (ep.res && splits == 1) {
       const int ch = t % EP_CPR, r0 = t / EP_CPR;
       const int n = n0 + ch * 8;
       pre.on = (g.ldy & 7) == 0 && (ep.ldr & 7) == 0 && n + 7 < g.K;
@@ -979,23 +993,22 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
     return;
   }
   if constexpr (EPI <= SMEM) {
-    if (g_epi_lds) {
-      store_tile_lds<TO, BM, BN, FM, FN, NW * 64, STATS, PRE ? EP_NP : 1>(acc, smem, m0, n0, wm * WTM, wn * WTN,
-                                                                          lane, g, y, ep, pre);
-      return;
-    }
-  }
-  if constexpr (STATS) {
+    // the LDS-staged epilogue whenever the staged tile fits the ring (the register epilogue is not even compiled
+    // then: as dead code it cost the statistics instantiations a scratch frame)
+    (void)g_epi_lds;
+    store_tile_lds<TO, BM, BN, FM, FN, NW * 64, STATS, PRE ? EP_NP : 1>(acc, smem, m0, n0, wm * WTM, wn * WTN, lane,
+                                                                        g, y, ep, pre);
+  } else if constexpr (STATS) {
     double st1[FN][4], st2[FN][4];
 #pragma unroll
     for (int i = 0; i < FN; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) st1[i][e] = st2[i][e] = 0.0;
-    store_tile<TO, FM, FN>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, g, y, ep, st1, st2);
+    store_tile<TO, FM, FN, true>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, g, y, ep, st1, st2);
     frag_stats<FN, BN, NW>(st1, st2, wn * WTN, smem, m0 / BM, n0, ep.stats, ep.sld);
-    return;
+  } else {
+    store_tile<TO, FM, FN>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, g, y, ep);
   }
-  store_tile<TO, FM, FN>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, g, y, ep);
 }
 
 // split-K finalize: y[pixel(m)][n] = act(ws[m][n] * scale[n] + shift[n] + res[pixel(m)][n])
@@ -1123,6 +1136,10 @@ int launch_glds_grp_b(int cfg, const void* x, const void* w, void* y, const Conv
                       unsigned x2b = 0);
 template <typename TO>
 int launch_glds_grp_d(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
+                      unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2 = nullptr,
+                      unsigned x2b = 0);
+template <typename TO>
+int launch_glds_grp_e(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
                       unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2 = nullptr,
                       unsigned x2b = 0);
 template <typename TO>

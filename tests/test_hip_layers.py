@@ -283,7 +283,7 @@ def test_conv_bn_act_fused_eval_grad(hip_device, mode, monkeypatch, kind, cin, c
     _close(mb.bias.grad, rb.bias.grad, mode, 'dbeta')
 
 
-ALL_VARIANTS = [11] + list(range(1, 11)) + list(range(12, 21))
+ALL_VARIANTS = [11] + list(range(1, 11)) + list(range(12, 24))
 
 
 @pytest.mark.parametrize('kind,cin,cout,k,H', [('conv', 64, 128, 3, 19), ('conv', 128, 64, 1, 17), ('conv', 192, 256, 3, 9),
@@ -291,7 +291,7 @@ ALL_VARIANTS = [11] + list(range(1, 11)) + list(range(12, 21))
                                                ('conv', 256, 200, 1, 23), ('conv', 192, 1024, 1, 11),
                                                ('conv_s2', 128, 256, 1, 18), ('conv', 64, 64, 1, 64)])
 def test_conv_variants_bitwise(hip_device, kind, cin, cout, k, H):
-    """Every bf16 engine variant (register-staged, LDS-DMA tile configs 1..10 and 12..20) accumulates the
+    """Every bf16 engine variant (register-staged, LDS-DMA tile configs 1..10 and 12..23) accumulates the
     same MFMA k-sequence: forward and input-gradient outputs are bit-identical, so autotuning never changes
     results."""
     from ssseg import native as N
