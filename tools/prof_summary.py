@@ -1,5 +1,6 @@
 """Per-kernel summary (pct, total_us, calls, avg_us, name) from a rocprofv3 rocpd database
-(`rocprofv3 --kernel-trace --stats -d DIR -o run -- ...` writes DIR/run_results.db).
+(`rocprofv3 --kernel-trace --stats -d DIR -o run -- ...` writes DIR/run_results.db) or from the csv kernel
+trace (`--output-format csv`: DIR/run_kernel_trace.csv).
 
     python tools/prof_summary.py DB [--tail-ms MS] [--header TEXT] > profiles/rN_kernel_stats.tsv
 
@@ -10,7 +11,25 @@ import argparse
 import sqlite3
 
 
+def summary_csv(path, tail_ms=None):
+    """Same summary from a rocprofv3 `--output-format csv` kernel trace (DIR/<o>_kernel_trace.csv)."""
+    import csv
+    with open(path) as fh:
+        rows = [(r['Kernel_Name'], int(r['Start_Timestamp']), int(r['End_Timestamp'])) for r in csv.DictReader(fh)]
+    t0 = max(e for _, _, e in rows) - int(tail_ms * 1e6) if tail_ms else 0
+    agg = {}
+    for name, s, e in rows:
+        if s >= t0:
+            n, ns = agg.get(name, (0, 0))
+            agg[name] = (n + 1, ns + e - s)
+    total = sum(ns for _, ns in agg.values()) or 1
+    out = [(100.0 * ns / total, ns / 1e3, n, ns / 1e3 / n, name) for name, (n, ns) in agg.items()]
+    return sorted(out, key=lambda r: -r[1])
+
+
 def summary(db, tail_ms=None):
+    if db.endswith('.csv'):
+        return summary_csv(db, tail_ms)
     c = sqlite3.connect(db)
     t0 = 0
     if tail_ms:
