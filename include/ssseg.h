@@ -252,6 +252,15 @@ typedef struct {
 int ssseg_conv_igemm_epi_vcat(const void* x, const ssseg_vcat* vc, const void* w, void* y,
                               const ssseg_conv_desc* desc_host, int dt, int dt_out, const ssseg_conv_epilogue* epi,
                               void* ws, size_t ws_bytes, ssseg_stream_t stream);
+/* ssseg_conv_igemm_epi with a SPLIT output: channels [0, ysplit->c1) of each output pixel go to y (pixel stride
+ * desc.ldy >= c1), channels [c1, K) to ysplit->x2 at channel n - c1 (pixel stride ysplit->ldx2).  The input
+ * gradient of a virtual concat (the UNet decoder's conv3_0, unet.py:44-47: dgrad of torch.cat((up, skip), 1)) is
+ * written straight into the gradients of its two parts: no [up | skip] gradient tensor, no split copies.
+ * c1 % 8 == 0; 16-bit dt == dt_out; the epilogue may carry scale / shift / act but no residual, aux or statistics
+ * (SSSEG_EUNSUPPORTED).  Bit-identical to the unsplit launch followed by the two channel copies. */
+int ssseg_conv_igemm_epi_vsplit(const void* x, const void* w, void* y, const ssseg_vcat* ysplit,
+                                const ssseg_conv_desc* desc_host, int dt, int dt_out, const ssseg_conv_epilogue* epi,
+                                void* ws, size_t ws_bytes, ssseg_stream_t stream);
 /* The output phases of a transposed conv in ONE launch (ConvTranspose2d(4,2,1): four 2x2-tap phases over the same
  * input; on 16x16..32x32 inputs a single phase has too few tiles to fill 256 CUs).  desc describes a phase's GEMM
  * (every phase: same K, taps R x S, weight stride ldw, output sub-grid OH x OW); phase_geom[4*p .. 4*p+3] =

@@ -209,7 +209,7 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
       if (v == 0) {
         const unsigned long long key =
             geom_key(g, (int)sizeof(TO) * 8 + (ws ? 8 : 0) + (ep.stats ? 4 : 0) + (ep.res ? 2 : 0) + (ep.scale ? 1 : 0) +
-                        64 * (ph ? ph->n : 1) + (x2 ? 4096 * (g.c1b + 1) : 0));
+                        64 * (ph ? ph->n : 1) + (x2 ? 4096 * (g.c1b + 1) : 0) + (ep.y2 ? (1 << 24) : 0));
         std::lock_guard<std::mutex> lk(g_variant_mu);
         auto it = g_variant.find(key);
         if (it != g_variant.end()) {
@@ -273,7 +273,7 @@ extern "C" size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* d, int
 
 static int conv_igemm_epi(const void* x, const void* x2, int64_t c1, int64_t ldx2, const void* w, void* y,
                           const ssseg_conv_desc* d, int dt, int dt_out, const ssseg_conv_epilogue* epi, void* ws,
-                          size_t ws_bytes, ssseg_stream_t stream) {
+                          size_t ws_bytes, ssseg_stream_t stream, const ssseg_vcat* ysplit = nullptr) {
   ConvGeom g;
   if (!make_geom(d, g) || !y) return SSSEG_EINVAL;
   if (!geom_ok(g, dt)) return SSSEG_EINVAL;
@@ -297,10 +297,22 @@ static int conv_igemm_epi(const void* x, const void* x2, int64_t c1, int64_t ldx
   if (e.relu < 0 || e.relu > SSSEG_ACT_LEAKY) return SSSEG_EINVAL;
   const Epi<float> ef{e.scale, e.shift, (const float*)e.residual, (int)e.ldr, e.relu, (float*)e.aux, e.slope,
                       e.stats, (int)e.stats_ld};
-  const Epi<bf16_t> eb{e.scale, e.shift, (const bf16_t*)e.residual, (int)e.ldr, e.relu, (bf16_t*)e.aux, e.slope,
-                       e.stats, (int)e.stats_ld};
-  const Epi<f16_t> eh{e.scale, e.shift, (const f16_t*)e.residual, (int)e.ldr, e.relu, (f16_t*)e.aux, e.slope,
-                      e.stats, (int)e.stats_ld};
+  Epi<bf16_t> eb{e.scale, e.shift, (const bf16_t*)e.residual, (int)e.ldr, e.relu, (bf16_t*)e.aux, e.slope,
+                 e.stats, (int)e.stats_ld};
+  Epi<f16_t> eh{e.scale, e.shift, (const f16_t*)e.residual, (int)e.ldr, e.relu, (f16_t*)e.aux, e.slope,
+                e.stats, (int)e.stats_ld};
+  if (ysplit) {   // split output: channels [c1, K) to ysplit->x2 (pixel stride ldx2); 16-bit, plain epilogue
+    const int64_t oc1 = ysplit->c1, ld2 = ysplit->ldx2;
+    if (!ysplit->x2 || oc1 <= 0 || oc1 >= g.K || oc1 % 8 || g.ldy < oc1 || g.ldy % 8 || ld2 < g.K - oc1 || ld2 % 8 ||
+        ld2 > 0x7fffffff)
+      return SSSEG_EINVAL;
+    if (dt_out != dt || (dt != SSSEG_BF16 && dt != SSSEG_F16) || e.stats || e.aux || e.residual)
+      return SSSEG_EUNSUPPORTED;
+    eb.y2 = (bf16_t*)ysplit->x2;
+    eh.y2 = (f16_t*)ysplit->x2;
+    eb.oc1 = eh.oc1 = (int)oc1;
+    eb.ldy2 = eh.ldy2 = (int)ld2;
+  }
   if (g.KK == 0) {   // no taps reach this output phase: the contraction is zero
     if (e.stats) return SSSEG_EUNSUPPORTED;
     const bool v8 = g.K % 8 == 0 && g.ldy % 8 == 0 && (!e.residual || e.ldr % 8 == 0);
@@ -364,6 +376,13 @@ extern "C" int ssseg_conv_igemm_epi_vcat(const void* x, const ssseg_vcat* vc, co
                                          void* ws, size_t ws_bytes, ssseg_stream_t stream) {
   if (!vc || !vc->x2) return SSSEG_EINVAL;
   return conv_igemm_epi(x, vc->x2, vc->c1, vc->ldx2, w, y, d, dt, dt_out, epi, ws, ws_bytes, stream);
+}
+
+extern "C" int ssseg_conv_igemm_epi_vsplit(const void* x, const void* w, void* y, const ssseg_vcat* ysplit,
+                                           const ssseg_conv_desc* d, int dt, int dt_out, const ssseg_conv_epilogue* epi,
+                                           void* ws, size_t ws_bytes, ssseg_stream_t stream) {
+  if (!ysplit) return SSSEG_EINVAL;
+  return conv_igemm_epi(x, nullptr, 0, 0, w, y, d, dt, dt_out, epi, ws, ws_bytes, stream, ysplit);
 }
 
 extern "C" int ssseg_conv_igemm(const void* x, const void* w, void* y, const ssseg_conv_desc* d, int dt, int dt_out,

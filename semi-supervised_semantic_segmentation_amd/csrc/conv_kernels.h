@@ -175,7 +175,18 @@ struct Epi {
   float slope;
   double* stats;   // optional BatchNorm statistics partials of the stored output: row (2*mtile) = sum y,
   int sld;         // row (2*mtile+1) = sum y^2, channels [0, sld) (sld = the BN's channel count)
+  // split output (the input gradient of a virtual concat, ssseg_conv_igemm_epi_vsplit): channels [oc1, K) go to y2
+  // (pixel stride ldy2) at channel n - oc1; oc1 % 8 == 0, so no 4- or 8-channel group straddles the seam
+  TO* y2 = nullptr;
+  int oc1 = 0x40000000;
+  int ldy2 = 0;
 };
+
+// where output channel n of pixel op is stored (y, or the second part of a split output)
+template <typename TO>
+__device__ __forceinline__ TO* out_at(const Epi<TO>& ep, TO* y, int ldy, long long op, int n) {
+  return n >= ep.oc1 ? ep.y2 + op * ep.ldy2 + (n - ep.oc1) : y + op * ldy + n;
+}
 
 // the value a later pass reads back from the stored output (the BN statistics are those of that value)
 template <typename TO> __device__ __forceinline__ float stored(float v);
@@ -324,13 +335,13 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[FN][FM], long long
           }
         }
       }
-      TO* yp = y + op[j] * g.ldy;
+      TO* yp = out_at(ep, y, g.ldy, op[j], n);
       if (full && (g.ldy & 3) == 0) {
-        Store4<TO>::st(yp + n, v);
+        Store4<TO>::st(yp, v);
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          if (n + e < g.K) io<TO>::st(yp, n + e, v[e]);
+          if (n + e < g.K) io<TO>::st(yp, e, v[e]);
       }
     }
   }
@@ -473,14 +484,15 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
       for (int e = 0; e < 8; ++e) v[e] = raw[e] * sc[e] + sh[e] + r[p][e];   // scale 1 / shift 0 when absent
       act8(v, ep.relu, ep.slope);
       const long long o = op[p] * g.ldy + n;
+      TO* yp = out_at(ep, y, g.ldy, op[p], n);   // (a split output has no aux: host contract)
       if (full) {
-        Out8<TO>::st(y + o, v);
+        Out8<TO>::st(yp, v);
         if (ep.aux) Out8<TO>::st(ep.aux + o, raw);
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           if (n + e >= g.K) continue;
-          io<TO>::st(y, o + e, v[e]);
+          io<TO>::st(yp, e, v[e]);
           if (ep.aux) io<TO>::st(ep.aux, o + e, raw[e]);
         }
       }
@@ -623,9 +635,23 @@ __global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __res
     const long long mm = a_ok[i] ? m : 0;
     decode_m(g, (int)mm, a_n[i], a_oy[i], a_ox[i]);
   }
-  // k-state of this thread's chunk: k = tap*C + kc, tap = r*S + s (advanced by every load, in order)
-  const int k_first = kt0 * BK + chunk * VEC;
-  int tap = min(k_first / g.C, RS), kc = k_first - tap * g.C, r = tap / max(g.S, 1), s = tap - r * g.S;
+  // k-state of this thread's chunk: k = tap*C + kc, tap = r*S + s (advanced by every load, in order).
+  // 16-bit operands with C % 64 == 0 run the LDS-DMA kernel's order (64-channel block major, tap minor, two
+  // 32-deep halves per block and tap), so every variant accumulates the same MFMA k-sequence (bitwise equal).
+  const bool cm = sizeof(T) == 2 && (g.C & 63) == 0;
+  int tap, kc, r, s, half = 0;
+  if (cm) {
+    const int cb = kt0 / (2 * RS), rem = kt0 - cb * 2 * RS;
+    tap = rem >> 1;
+    half = rem & 1;
+    kc = cb * 64 + half * BK + chunk * VEC;
+  } else {
+    const int k_first = kt0 * BK + chunk * VEC;
+    tap = min(k_first / g.C, RS);
+    kc = k_first - tap * g.C;
+  }
+  r = tap / max(g.S, 1);
+  s = tap - r * g.S;
   const int nk = max(kt1 - kt0, 0);
 
   auto load = [&](uint4 (&ra)[A_PER], uint4 (&rb)[B_IT], int kt) {
@@ -636,20 +662,35 @@ __global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __res
       const bool ok = a_ok[i] && tap < RS && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
       ra[i] = ok ? *(const uint4*)(x + ((long long)(a_n[i] * g.H + iy) * g.W + ix) * g.ldx + kc) : make_uint4(0, 0, 0, 0);
     }
+    // B rows: the same k as this thread's A chunk (id & 3 == t & 3)
+    const int kb = tap < RS ? tap * g.C + kc : g.KK;
 #pragma unroll
     for (int j = 0; j < B_IT; ++j) {
       const int id = t + 256 * j;
       rb[j] = make_uint4(0, 0, 0, 0);
       if (id < BN * 4) {
         const int n = n0 + (id >> 2);
-        const int k = (kt0 + kt) * BK + (id & 3) * VEC;
-        if (n < g.K && k < g.KK) rb[j] = *(const uint4*)(w + (long long)n * g.ldw + k);
+        if (n < g.K && kb < g.KK) rb[j] = *(const uint4*)(w + (long long)n * g.ldw + kb);
       }
     }
-    kc += BK;
-    while (kc >= g.C && tap < RS) {
-      kc -= g.C; ++tap;
-      if (++s == g.S) { s = 0; ++r; }
+    (void)kt;
+    if (cm) {
+      if (!half) {
+        half = 1;
+        kc += BK;
+      } else {
+        half = 0;
+        kc -= BK;
+        ++tap;
+        if (++s == g.S) { s = 0; ++r; }
+        if (tap == RS) { tap = 0; r = 0; s = 0; kc += 2 * BK; }
+      }
+    } else {
+      kc += BK;
+      while (kc >= g.C && tap < RS) {
+        kc -= g.C; ++tap;
+        if (++s == g.S) { s = 0; ++r; }
+      }
     }
   };
   auto store = [&](const uint4 (&ra)[A_PER], const uint4 (&rb)[B_IT], int buf) {
@@ -751,7 +792,7 @@ __global__ void __launch_bounds__(256, DEEP ? 2 : 1) igemm_kernel(const T* __res
 
 // ------------------------------------------------------------------------------------------------
 // bf16 gather GEMM, LDS-DMA pipeline (gfx950), for C % 64 == 0.  Same contraction and epilogue as
-// igemm_kernel.  k runs tap-major (k = tap*C + c) and a k-tile (BK = 64) never straddles a tap, so the
+// igemm_kernel.  k runs channel-block major, tap minor, and a k-tile (BK = 64) never straddles a tap, so the
 // tap (r, s) and channel block c0 are wave-uniform scalars.  Tiles are staged by buffer_load ... lds
 // (16 B per lane straight into LDS, no VGPR round trip) into an NS-deep LDS ring: NS-1 tiles are in
 // flight while one is multiplied, one raw barrier per k-tile, counted vmcnt.  Per-lane byte offsets are
@@ -881,12 +922,19 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
     }
   };
 
-  int ld_tap = kt0 ? kt0 / cpt : 0, ld_c = kt0 ? kt0 - (kt0 / cpt) * cpt : 0, ld_kt = kt0;   // next: tap, block, index
-  set_tap(min(ld_tap, RS - 1));
+  // k-tile order: channel block major, tap minor (kt = cb * RS + tap).  The taps of one 64-channel block re-read
+  // the same input lines RS times in a row, so those re-reads hit L2 (PMC: a tap-major sweep over all C kept
+  // BM x C x 2 B per block live -- 50 MB over the chip at 384 channels -- and its re-reads went to the Infinity
+  // Cache at 2.6x the L2 latency, which is what bounds the LDS-DMA stream: ~90 outstanding lines per CU)
+  int ld_tap = kt0 ? kt0 % RS : 0, ld_c = kt0 ? kt0 / RS : 0;   // next: tap, channel block
+  set_tap(ld_tap);
   auto issue = [&](int buf) {
     char* As = smem + buf * STAGE;
     char* Bs = As + BM * ROW;
-    const unsigned sa = (unsigned)ld_c * 128u, sb = (unsigned)ld_kt * 128u;
+    // wave-uniform soffsets, stated as such (otherwise the compiler may keep the k-state in VGPRs and wrap every
+    // LDS-DMA issue in a readfirstlane waterfall loop)
+    const unsigned sa = (unsigned)__builtin_amdgcn_readfirstlane(ld_c * 128),
+                   sb = (unsigned)__builtin_amdgcn_readfirstlane((ld_tap * cpt + ld_c) * 128);
     if (VC && ld_c >= g.c1b) {   // channel block of the second source (scalar branch)
       const unsigned sa2 = (unsigned)(ld_c - g.c1b) * 128u;
 #pragma unroll
@@ -897,11 +945,11 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
     }
 #pragma unroll
     for (int jj = 0; jj < BI; ++jj) bldslds16(wr, Bs + (wave * BI + jj) * 1024, b_off[jj], sb);
-    ++ld_kt;
-    if (++ld_c == cpt) {
-      ld_c = 0;
-      if (++ld_tap < RS) set_tap(ld_tap);
+    if (++ld_tap == RS) {
+      ld_tap = 0;
+      ++ld_c;
     }
+    if (RS > 1) set_tap(ld_tap);
   };
 
   f32x4 acc[FN][FM];
@@ -1025,7 +1073,7 @@ __global__ void splitk_finalize_kernel(const float* __restrict__ ws, TO* __restr
     if (ep.shift) v += ep.shift[n];
     if (ep.res) v += io<TO>::ld(ep.res, op * ep.ldr + n);
     v = act_fwd(v, ep.relu, ep.slope);
-    io<TO>::st(y, op * g.ldy + n, v);
+    io<TO>::st(out_at(ep, y, g.ldy, op, n), 0, v);
   }
 }
 
@@ -1051,7 +1099,7 @@ __global__ void phase_zero_vec_kernel(TO* y, ConvGeom g, Epi<TO> ep) {
       const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       Out8<TO>::st(ep.aux + op * g.ldy + n, z);
     }
-    Out8<TO>::st(y + op * g.ldy + n, v);
+    Out8<TO>::st(out_at(ep, y, g.ldy, op, n), v);
   }
 }
 
@@ -1066,7 +1114,7 @@ __global__ void phase_zero_kernel(TO* y, ConvGeom g, Epi<TO> ep) {
     if (ep.aux) io<TO>::st(ep.aux, op * g.ldy + n, 0.f);
     if (ep.res) v += io<TO>::ld(ep.res, op * ep.ldr + n);
     v = act_fwd(v, ep.relu, ep.slope);
-    io<TO>::st(y, op * g.ldy + n, v);
+    io<TO>::st(out_at(ep, y, g.ldy, op, n), 0, v);
   }
 }
 

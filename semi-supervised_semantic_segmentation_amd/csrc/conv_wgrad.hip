@@ -298,7 +298,12 @@ struct WSeg2 {
   unsigned xabytes, xbbytes;
 };
 
-template <typename T16, int BMW, int BNW, int NS, int WM = 2, int WN = 2, int BKP = 64>
+// ST (straddle): the kk-tile may cross the seam of a virtual concat input (sg.c1 % BMW != 0, e.g. the UNet's
+// 256^2 conv3_0 over [up 64 | skip 64] with a 128-wide kk-tile): every x piece is issued twice, by the lanes whose
+// chunk lies before the seam from the first part and by the others from the second (EXEC-masked LDS-DMA: each
+// lane lands its 16 bytes in the same slot as in the unsplit issue), so the tile and its MFMA sequence are those of
+// the materialised concat.
+template <typename T16, int BMW, int BNW, int NS, int WM = 2, int WN = 2, int BKP = 64, bool ST = false>
 __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const T16* __restrict__ x, const T16* __restrict__ dy,
                                                                    float* __restrict__ slab, ConvGeom g,
                                                                    long long pix_per_split, WDirect dd, unsigned xbytes,
@@ -308,7 +313,7 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const T16* __r
   constexpr int ROWX = BMW * 2, ROWD = BNW * 2;              // LDS row bytes
   constexpr int XCPR = ROWX / 16, DCPR = ROWD / 16;          // 16-byte chunks per row
   constexpr int XI = BKP * XCPR / NT, DI = BKP * DCPR / NT;  // wave-instructions per wave per stage
-  constexpr int NL = XI + DI;
+  constexpr int NL = (ST ? 2 : 1) * XI + DI;                 // vmcnt units per stage
   constexpr int STAGE = BKP * (ROWX + ROWD);
   constexpr int WTM = BMW / WM, WTN = BNW / WN, FM = WTM / 16, FN = WTN / 16;
   static_assert(XI >= 1 && DI >= 1 && NS >= 2 && NS <= 4 && FM >= 1 && FN >= 1 && BKP % 32 == 0, "wgrad glds tile");
@@ -334,6 +339,12 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const T16* __r
   const unsigned xbyt = src2 ? (seg2 ? sg.xbbytes : sg.xabytes) : (seg2 ? sg.xbytes : xbytes);
   const int ldx = src2 ? sg.ldx2 : g.ldx, cb0 = src2 ? c0 - sg.c1 : c0;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)xbase, (short)0, (int)xbyt, 0x00020000);
+  // ST: this tile straddles the seam (block-uniform); the second part's resource
+  const bool strad = ST && sg.c1 > c0 && sg.c1 < c0 + BMW;
+  __amdgpu_buffer_rsrc_t xr2 = xr;
+  if constexpr (ST)
+    xr2 = __builtin_amdgcn_make_buffer_rsrc(seg2 ? (void*)sg.xb : (void*)sg.xa, (short)0,
+                                            (int)(seg2 ? sg.xbbytes : sg.xabytes), 0x00020000);
   const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(seg2 ? (void*)sg.dy : (void*)dy, (short)0,
                                                                       (int)(seg2 ? sg.dbytes : dbytes), 0x00020000);
 
@@ -341,10 +352,15 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const T16* __r
   // its pixel advances by BKP per k-tile (incremental decode, no per-tile division)
   long long xp[XI];
   int xoy[XI], xox[XI], ximg[XI], xcb[XI];
+  bool xin2[ST ? XI : 1];   // ST: this lane's chunk of piece ii lies past the seam (second part)
 #pragma unroll
   for (int ii = 0; ii < XI; ++ii) {
     const int row = (wave * XI + ii) * (64 / XCPR) + lane / XCPR;
     xcb[ii] = (cb0 + ((lane % XCPR) ^ wswz<ROWX>(row)) * 8) * 2;
+    if constexpr (ST) {
+      xin2[ii] = strad && c0 + ((lane % XCPR) ^ wswz<ROWX>(row)) * 8 >= sg.c1;
+      if (xin2[ii]) xcb[ii] -= sg.c1 * 2;   // channel offset inside the second part
+    }
     xp[ii] = p_begin + row;
     const long long pp = xp[ii] < p_end ? xp[ii] : 0;
     decode_m(g, (int)pp, ximg[ii], xoy[ii], xox[ii]);   // M < 2^31 (wg_geom_ok)
@@ -364,12 +380,27 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const T16* __r
 #pragma unroll
     for (int ii = 0; ii < XI; ++ii) {
       unsigned off = OOB;
+      if constexpr (ST) {
+        if (strad) {   // two EXEC-masked issues of the same piece (one vmcnt unit each, taken by every lane)
+          unsigned o1 = OOB, o2 = OOB;
+          if (xp[ii] < p_end) {
+            const int iy = xoy[ii] * g.sy + offy, ix = xox[ii] * g.sx + offx;
+            if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W) {
+              const unsigned pix = (unsigned)((ximg[ii] * g.H + iy) * g.W + ix);
+              o1 = pix * (unsigned)g.ldx * 2u + (unsigned)xcb[ii];
+              o2 = pix * (unsigned)sg.ldx2 * 2u + (unsigned)xcb[ii];
+            }
+          }
+          if (!xin2[ii]) bldslds16(xr, Xs + (wave * XI + ii) * 1024, o1, 0);
+          if (xin2[ii]) bldslds16(xr2, Xs + (wave * XI + ii) * 1024, o2, 0);
+        }
+      }
       if (xp[ii] < p_end) {
         const int iy = xoy[ii] * g.sy + offy, ix = xox[ii] * g.sx + offx;
         if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
           off = (unsigned)(((ximg[ii] * g.H + iy) * g.W + ix) * ldx) * 2u + (unsigned)xcb[ii];
       }
-      bldslds16(xr, Xs + (wave * XI + ii) * 1024, off, 0);
+      if (!strad) bldslds16(xr, Xs + (wave * XI + ii) * 1024, off, 0);
       xp[ii] += BKP;
       if (BKP < g.OW) {   // at most one row wrap (wave-uniform test)
         xox[ii] += BKP;
@@ -520,7 +551,8 @@ struct WgradPlan {
   int bmw, bnw, mt, nt, splits;
   long long pps;
   bool glds;
-  int cfg;   // LDS-DMA config (WGRAD_CFGS index), 0 = register-staged
+  int cfg;          // LDS-DMA config (WGRAD_CFGS index), 0 = register-staged
+  bool st = false;  // kk-tiles may straddle a virtual concat's seam (the ST kernel variant)
 };
 
 // LDS-DMA weight-gradient configs: tile (kk x co), ring depth, waves (WM x WN), pixels per k-tile.
@@ -621,11 +653,16 @@ static int static_wgrad_cfg(const ConvGeom& g) {
   return bmw == 64 ? (bnw == 64 ? 1 : 20) : (bnw == 64 ? 18 : 19);
 }
 
-// c1 > 0 (virtual concat input): the kk-tile must not straddle channel c1 -> a 64-wide tile where c1 % 128 != 0
-static int wgrad_cfg_for(const ConvGeom& g, int c1 = 0) {
+// c1 > 0 (virtual concat input) with c1 % bmw != 0: a 128-wide kk-tile straddles the seam and runs the ST variant
+// (st = true); other widths fall back to a 64-wide tile
+static int wgrad_cfg_for(const ConvGeom& g, int c1 = 0, bool* st = nullptr) {
   int c = g_knobs[9];
   if (!(c > 0 && c < N_WGRAD_CFGS && g.C % WGRAD_CFGS[c].bmw == 0)) c = static_wgrad_cfg(g);
-  if (c1 > 0 && c1 % WGRAD_CFGS[c].bmw) c = WGRAD_CFGS[c].bnw == 64 ? 1 : 20;
+  if (st) *st = false;
+  if (c1 > 0 && c1 % WGRAD_CFGS[c].bmw) {
+    if (WGRAD_CFGS[c].bmw == 128 && c1 % 64 == 0 && st) *st = true;
+    else c = WGRAD_CFGS[c].bnw == 64 ? 1 : 20;
+  }
   return c;
 }
 
@@ -642,10 +679,10 @@ static WgradPlan choose_wgrad(const ConvGeom& g, int dt) {
   return dt != SSSEG_F32 ? plan_wgrad<bf16_t>(g) : plan_wgrad<float>(g);
 }
 
-template <typename T16, int C>
+template <typename T16, int C, bool ST = false>
 constexpr auto wgrad_kernel_of() {
   return &wgrad_glds_kernel<T16, WGRAD_CFGS[C].bmw, WGRAD_CFGS[C].bnw, WGRAD_CFGS[C].ns, WGRAD_CFGS[C].wm,
-                            WGRAD_CFGS[C].wn, WGRAD_CFGS[C].bkp>;
+                            WGRAD_CFGS[C].wn, WGRAD_CFGS[C].bkp, ST>;
 }
 
 // resident blocks of an LDS-DMA wgrad config on the whole device (cached per config)
@@ -680,6 +717,14 @@ template <typename T16, int C>
 void launch_wgrad_glds_t(const void* x, const void* dy, float* slab, const ConvGeom& g, const WgradPlan& p, WDirect dd,
                          hipStream_t s, const WSeg2& sg) {
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.ldx * 2), db = (unsigned)(g.M * g.ldy * 2);
+  if constexpr (WGRAD_CFGS[C].bmw == 128) {
+    if (p.st) {   // kk-tiles straddling a virtual concat's seam
+      hipLaunchKernelGGL((wgrad_kernel_of<T16, C, true>()), dim3(p.mt * p.nt * p.splits),
+                         dim3(WGRAD_CFGS[C].wm * WGRAD_CFGS[C].wn * 64), 0, s, (const T16*)x, (const T16*)dy, slab, g,
+                         p.pps, dd, xb, db, sg);
+      return;
+    }
+  }
   hipLaunchKernelGGL((wgrad_kernel_of<T16, C>()), dim3(p.mt * p.nt * p.splits),
                      dim3(WGRAD_CFGS[C].wm * WGRAD_CFGS[C].wn * 64), 0, s, (const T16*)x, (const T16*)dy, slab, g,
                      p.pps, dd, xb, db, sg);
@@ -768,7 +813,9 @@ int wgrad_one(const void* x, const ssseg_vcat* vc, const void* dy, float* dw, co
   WgradPlan p = choose_wgrad(g, dt);
   if (vc) {
     if (!p.glds) return SSSEG_EUNSUPPORTED;   // the register-staged kernel has no second source
-    p = plan_for_cfg(g, wgrad_cfg_for(g, (int)vc->c1));
+    bool st = false;
+    p = plan_for_cfg(g, wgrad_cfg_for(g, (int)vc->c1, &st));
+    p.st = st;
   }
   const WDirect dd{p.splits == 1 ? dw : nullptr, (int)c_real, (int)k_real, layout, accumulate};
   WSeg2 sg{nullptr, nullptr, 0, 0, 0, 0, 0, 0, nullptr, nullptr, 0, 0};
@@ -795,7 +842,8 @@ int wgrad_one(const void* x, const ssseg_vcat* vc, const void* dy, float* dw, co
 
 // merged launch plan of ssseg_conv_wgrad2: one split plan over the union of both pixel sets (as if the batch were
 // n1 + n2), each segment cut into whole splits of that size.  False when either segment is not LDS-DMA eligible.
-bool merged_plan(const ConvGeom& g1, int64_t n2, int dt, WgradPlan& p, int& s1, ConvGeom& g2, int c1 = 0) {
+bool merged_plan(const ConvGeom& g1, int64_t n2, int dt, WgradPlan& p, int& s1, ConvGeom& g2, int c1 = 0,
+                 bool allow_st = true) {
   if (n2 < 1 || n2 > 0x7fffffff || !wgrad_glds_ok(g1, dt)) return false;
   g2 = g1;
   g2.N = (int)n2;
@@ -803,7 +851,9 @@ bool merged_plan(const ConvGeom& g1, int64_t n2, int dt, WgradPlan& p, int& s1, 
   if (g2.M >= 0x7fffffffLL || !wgrad_glds_ok(g2, dt)) return false;
   ConvGeom gm = g1;
   gm.M = g1.M + g2.M;
-  p = plan_for_cfg(gm, wgrad_cfg_for(g1, c1));
+  bool st = false;
+  p = plan_for_cfg(gm, wgrad_cfg_for(g1, c1, allow_st ? &st : nullptr));
+  p.st = st;
   const int bkp = WGRAD_CFGS[p.cfg].bkp;
   // the plan's split count shared out in proportion to the segments' pixels, never more splits in total
   // (a split past the plan's rounds would start a nearly empty extra round)

@@ -73,6 +73,7 @@ SIGS = {
     'ssseg_conv_wgrad2': (i32, [vp, vp, vp, vp, i64, vp, vp, i32, i64, i64, i32, i32, vp, sz, vp]),
     # virtual concat inputs (ssseg_vcat)
     'ssseg_conv_igemm_epi_vcat': (i32, [vp, vp, vp, vp, vp, i32, i32, vp, vp, sz, vp]),
+    'ssseg_conv_igemm_epi_vsplit': (i32, [vp, vp, vp, vp, vp, i32, i32, vp, vp, sz, vp]),
     'ssseg_conv_wgrad_vcat': (i32, [vp, vp, vp, vp, vp, i32, i64, i64, i32, i32, vp, sz, vp]),
     'ssseg_conv_wgrad2_vcat': (i32, [vp, vp, vp, vp, vp, vp, i64, vp, vp, i32, i64, i64, i32, i32, vp, sz, vp]),
     'ssseg_weight_pack': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, i32, i64, i64, i64, i64, i64, i64, i32, vp]),

@@ -429,12 +429,20 @@ class _ConvFn(torch.autograd.Function):
         if not ctx.needs_input_grad[0]:
             dx = None
         else:
-            dx = _dgrad_acc(mod, gy, x.shape, pending)
+            dx = _dgrad_acc(mod, gy, x.shape, pending, ctx.vcat)
         return _join_give(ctx.join, last, dx), None, None, None, None, None, None, None
 
 
-def _dgrad_acc(mod, gy, xshape, pending):
-    """dx (+ a pending gradient of x): fused as the dgrad epilogue's residual where the engine supports it"""
+def _dgrad_acc(mod, gy, xshape, pending, vc=None):
+    """dx (+ a pending gradient of x): fused as the dgrad epilogue's residual where the engine supports it.
+    vc: x is a virtual concat (its only consumer is this conv): the engine writes the gradients of the two parts
+    where they are needed (VirtualCat.grads, taken by the concat's backward) and dx is a placeholder."""
+    if pending is None and vc is not None and _CFG['vcat']:
+        parts = getattr(mod, '_ssseg_dgrad_vsplit', lambda *a: None)(gy, xshape, vc)
+        if parts is not None:
+            vc.grads = parts
+            # never read: an expanded 0-d tensor of x's shape (no memory, no kernel)
+            return torch.empty((), dtype=gy.dtype, device=gy.device).expand(*xshape)
     if pending is None:
         return mod._ssseg_dgrad(gy, xshape)
     if getattr(mod, '_ssseg_res_dgrad', lambda: False)():
@@ -833,6 +841,35 @@ class Conv2d(nn.Conv2d, _ConvBase):
         return dx
 
 
+    def _ssseg_dgrad_vsplit(self, gy, xshape, vc):
+        """dx of a virtual concat input [a | b] written straight into (da, db), the gradients of its parts
+        (ssseg_conv_igemm_epi_vsplit: channels [0, ca) to da, [ca, ca + cb) to db).  None where the engine cannot
+        (the caller runs the ordinary dgrad and the concat's backward splits it)."""
+        cin, cout = self._dims()
+        n, cp, H, W = xshape
+        if (self._ssseg_dw or self.stride != (1, 1) or cp != vc.ca + vc.cb or cin != cp
+                or _CFG['dtype'] not in (torch.bfloat16, torch.float16)):
+            return None
+        (R, S), (ph, pw), (dh, dw) = self.kernel_size, self.padding, self.dilation
+        OH, OW = gy.shape[2], gy.shape[3]
+        da = new_act(n, vc.ca, H, W, _CFG['dtype'], gy.device)
+        db = new_act(n, vc.cb, H, W, _CFG['dtype'], gy.device)
+        w = self._pack('dgrad', cin, self.in_channels, self.out_channels, cout, 1, R - 1, -1, R, S - 1, -1, S)
+        d = _desc(N=n, H=OH, W=OW, C=cout, ldx=cout, OH=H, OW=W, K=cin, R=R, S=S, sy=1, sx=1, dy=dh, dx=dw,
+                  py=ph - (R - 1) * dh, px=pw - (S - 1) * dw, outH=H, outW=W, osy=1, osx=1, ooy=0, oox=0,
+                  ldy=vc.ca, ldw=R * S * cout)
+        dref = ctypes_ref(d)
+        nb = N.lib().ssseg_conv_igemm_workspace_bytes(dref, N.dt_code(gy))
+        ws = N.workspace(nb, gy.device) if nb else None
+        ep = N.ConvEpilogue(None, None, None, 0, None, 0, 0.0, None, 0, None)
+        split = N.VCat(N.dev_ptr(db), vc.ca, vc.cb)
+        with _Timed(_conv_flops(n, OH, OW, self.out_channels, self.in_channels, R, S), 'dgrad', _tag(self, n, H, W)):
+            ok = N.call_or_unsupported('ssseg_conv_igemm_epi_vsplit', N.dev_ptr(gy), N.dev_ptr(w), N.dev_ptr(da),
+                                       ctypes_ref(split), dref, N.dt_code(gy), N.dt_code(gy), ctypes_ref(ep),
+                                       N.dev_ptr(ws) if ws is not None else None, nb, N.stream())
+        return (da, db) if ok else None
+
+
 class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
     """nn.ConvTranspose2d (output_padding 0, groups 1, dilation 1) with an optional fused ReLU."""
 
@@ -1176,7 +1213,7 @@ class _ConvBNEvalFn(torch.autograd.Function):
         if not ctx.needs_input_grad[0]:
             dx = None
         else:
-            dx = _dgrad_acc(conv, dconv, x.shape, pending)
+            dx = _dgrad_acc(conv, dconv, x.shape, pending, ctx.vcat)
         if dres is not None and ctx.grad_out is not None:
             ctx.grad_out.put(dres)
             dres = None
@@ -1288,11 +1325,12 @@ class VirtualCat:
     """The two parts of a virtual channel concat (cat_crop(lazy=True)): the consuming conv's kernels read channels
     [0, ca) from a and [ca, ca + cb) from b where they lie (ssseg_vcat); the concat tensor itself is allocated but
     not written unless materialize() runs (a consumer that cannot read it part by part)."""
-    __slots__ = ('a', 'b', 'ca', 'cb', '_d2')
+    __slots__ = ('a', 'b', 'ca', 'cb', '_d2', 'grads')
 
     def __init__(self, a, b, ca, cb):
         self.a, self.b, self.ca, self.cb = a, b, ca, cb
         self._d2 = None
+        self.grads = None   # (da, db) from the consumer's split-output dgrad, taken by the concat's backward
 
     def desc2(self):
         if self._d2 is None:
@@ -1340,8 +1378,9 @@ class _CatFn(torch.autograd.Function):
     """torch.cat((a, b), 1) with a center-crop of whichever map is larger (unet.py:40-45)."""
 
     @staticmethod
-    def forward(ctx, a, b, ca, cb, ja=None, jb=None, virtual=False):
+    def forward(ctx, a, b, ca, cb, ja=None, jb=None, virtual=False, vc=None):
         ctx.joins = (ja, jb)
+        ctx.vc = vc
         n = a.shape[0]
         H, W = min(a.shape[2], b.shape[2]), min(a.shape[3], b.shape[3])
         v = vec()
@@ -1362,16 +1401,23 @@ class _CatFn(torch.autograd.Function):
         ash, bsh, ca, cb, offs, H, W, cp = ctx.meta
         n = gy.shape[0]
         grads = []
-        for sh, c, c0, (oy, ox), j in ((ash, ca, 0, offs[0], ctx.joins[0]), (bsh, cb, ca, offs[1], ctx.joins[1])):
-            cropped = (sh[2], sh[3]) != (H, W)
-            g = new_act(n, sh[1], sh[2], sh[3], gy.dtype, gy.device, zero=cropped or sh[1] != c)
-            N.call('ssseg_nhwc_copy', N.dev_ptr(gy) + c0 * gy.element_size(), N.dev_ptr(g), n, H, W, c, H, W, cp, 0,
-                   0, sh[2], sh[3], sh[1], oy, ox, N.dt_code(gy), N.stream())
+        split = ctx.vc.grads if ctx.vc is not None else None   # the consumer wrote the parts' gradients itself
+        if split is not None:
+            ctx.vc.grads = None
+        for k, (sh, c, c0, (oy, ox), j) in enumerate(((ash, ca, 0, offs[0], ctx.joins[0]),
+                                                        (bsh, cb, ca, offs[1], ctx.joins[1]))):
+            if split is not None:
+                g = split[k]
+            else:
+                cropped = (sh[2], sh[3]) != (H, W)
+                g = new_act(n, sh[1], sh[2], sh[3], gy.dtype, gy.device, zero=cropped or sh[1] != c)
+                N.call('ssseg_nhwc_copy', N.dev_ptr(gy) + c0 * gy.element_size(), N.dev_ptr(g), n, H, W, c, H, W, cp,
+                       0, 0, sh[2], sh[3], sh[1], oy, ox, N.dt_code(gy), N.stream())
             joined, last = _join_take(j)
             if joined is not None:   # the concat usually runs first (it is downstream): rare
                 g = g + joined
             grads.append(_join_give(j, last, g))
-        return grads[0], grads[1], None, None, None, None, None
+        return grads[0], grads[1], None, None, None, None, None, None
 
 
 def _vcat_eligible(a, b, ca, cb):
@@ -1386,9 +1432,10 @@ def cat_crop(a, b, ca, cb, lazy=False):
     lazy=True: the caller's only consumer is a conv that reads a virtual concat (UpBlock.conv3_0); where the parts
     qualify (16-bit, whole 64-channel parts, no crop) nothing is copied and the returned tensor carries the parts."""
     virtual = lazy and _vcat_eligible(a, b, ca, cb)
-    y = _CatFn.apply(a, b, ca, cb, _join_fwd(a), _join_fwd(b), virtual)
+    vc = VirtualCat(a, b, ca, cb) if virtual else None
+    y = _CatFn.apply(a, b, ca, cb, _join_fwd(a), _join_fwd(b), virtual, vc)
     if virtual:
-        y.__dict__['_ssseg_vcat'] = VirtualCat(a, b, ca, cb)
+        y.__dict__['_ssseg_vcat'] = vc
     return y
 
 

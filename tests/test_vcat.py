@@ -80,3 +80,35 @@ def test_virtual_concat_is_not_copied(hip_device):
     # not eligible (fp32 mode / 64-unaligned part): an ordinary concat
     c = snn.to_act(torch.randn(2, 40, 8, 8, device=hip_device))
     assert snn._vcat_of(snn.cat_crop(a, c, 128, 40, lazy=True)) is None
+
+
+@pytest.mark.parametrize('mode', ['train', 'eval'])
+def test_virtual_concat_backward_writes_parts(hip_device, monkeypatch, mode):
+    """conv3_0's input gradient goes straight into the two parts' gradients (ssseg_conv_igemm_epi_vsplit): no
+    channel copy runs in the forward or the backward of an eligible UpBlock (the gradients themselves are checked
+    bitwise against the copy path by test_upblock_virtual_concat_bitwise)."""
+    from ssseg import native as N
+    from ssseg import nn as snn
+    snn.set_compute_dtype(torch.bfloat16)
+    block = _upblock(hip_device, 128, 64, 64)
+    block.train(mode == 'train')
+    x = snn.to_act(torch.randn(2, 128, 12, 12, device=hip_device)).requires_grad_(True)
+    s = snn.to_act(torch.randn(2, 64, 24, 24, device=hip_device)).requires_grad_(True)
+    calls = []
+    real = N.call
+
+    def spy(name, *args):
+        calls.append(name)
+        return real(name, *args)
+    monkeypatch.setattr(N, 'call', spy)
+    real_u = N.call_or_unsupported
+
+    def spy_u(name, *args):
+        calls.append(name)
+        return real_u(name, *args)
+    monkeypatch.setattr(N, 'call_or_unsupported', spy_u)
+    y = block(x, s)
+    y.backward(torch.ones_like(y))
+    torch.cuda.synchronize()
+    assert 'ssseg_conv_igemm_epi_vsplit' in calls
+    assert 'ssseg_nhwc_copy' not in calls

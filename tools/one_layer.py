@@ -24,9 +24,14 @@ def main():
     ap.add_argument('--hw', type=int, default=256)
     ap.add_argument('--batch', type=int, default=32)
     ap.add_argument('--reps', type=int, default=10)
+    ap.add_argument('--variant', type=int, default=0, help='forced LDS-DMA config (knob 4; 0 = autotune)')
+    ap.add_argument('--wvariant', type=int, default=0, help='forced weight-gradient config (knob 9)')
     a = ap.parse_args()
     dev = torch.device('cuda')
     snn.set_compute_dtype(torch.bfloat16)
+    from ssseg import native as N
+    N.lib().ssseg_set_knob(4, a.variant)
+    N.lib().ssseg_set_knob(9, a.wvariant)
     conv = snn.Conv2d(a.cin, a.cout, a.k, a.stride, a.k // 2, bias=False).to(dev)
     x = snn.to_act(torch.randn(a.batch, a.cin, a.hw, a.hw, device=dev))
     with torch.no_grad():
@@ -45,7 +50,7 @@ def main():
                 conv(x)
     e1.record()
     torch.cuda.synchronize()
-    print(f'{a.kind} {a.cin}->{a.cout} k{a.k} s{a.stride} @{a.batch}x{a.hw}^2: {e0.elapsed_time(e1) / a.reps * 1e3:.1f} us')
+    print(f'v{a.variant}/{a.wvariant} {a.kind} {a.cin}->{a.cout} k{a.k} s{a.stride} @{a.batch}x{a.hw}^2: {e0.elapsed_time(e1) / a.reps * 1e3:.1f} us')
 
 
 if __name__ == '__main__':
