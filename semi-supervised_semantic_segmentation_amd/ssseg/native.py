@@ -162,6 +162,11 @@ def lib():
             fn.restype = res
             fn.argtypes = args
         _lib = L
+        # engine knobs for experiments, e.g. SSSEG_KNOBS="11=1,10=50" (ssseg_set_knob id=value pairs)
+        for kv in filter(None, os.environ.get('SSSEG_KNOBS', '').split(',')):
+            k, v = kv.split('=')
+            if L.ssseg_set_knob(int(k), int(v)) != 0:
+                raise ValueError(f'SSSEG_KNOBS: bad knob {kv!r}')
     return _lib
 
 
