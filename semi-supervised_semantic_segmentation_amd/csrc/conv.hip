@@ -287,7 +287,7 @@ static int conv_igemm_epi(const void* x, const void* x2, int64_t c1, int64_t ldx
   }
   const ssseg_conv_epilogue none = {nullptr, nullptr, nullptr, 0, nullptr, 0, 0.f, nullptr, 0, nullptr};
   const ssseg_conv_epilogue& e = epi ? *epi : none;
-  if (e.residual && (e.ldr < g.K || e.ldr > 0x7fffffff)) return SSSEG_EINVAL;
+  if (e.residual && ((!ysplit && e.ldr < g.K) || e.ldr > 0x7fffffff)) return SSSEG_EINVAL;
   if (e.stats && (!e.stats_rows_host || e.stats_ld < 1 || e.stats_ld > g.K)) return SSSEG_EINVAL;
   // fused statistics are of acc + shift: the conv feeding a training BatchNorm has no affine / residual / act
   if (e.stats && (e.scale || e.residual || e.relu || e.aux)) return SSSEG_EINVAL;
@@ -306,8 +306,10 @@ static int conv_igemm_epi(const void* x, const void* x2, int64_t c1, int64_t ldx
     if (!ysplit->x2 || oc1 <= 0 || oc1 >= g.K || oc1 % 8 || g.ldy < oc1 || g.ldy % 8 || ld2 < g.K - oc1 || ld2 % 8 ||
         ld2 > 0x7fffffff)
       return SSSEG_EINVAL;
-    if (dt_out != dt || (dt != SSSEG_BF16 && dt != SSSEG_F16) || e.stats || e.aux || e.residual)
-      return SSSEG_EUNSUPPORTED;
+    if (dt_out != dt || (dt != SSSEG_BF16 && dt != SSSEG_F16) || e.stats || e.aux) return SSSEG_EUNSUPPORTED;
+    if (e.residual && (e.ldr < oc1 || e.ldr % 8)) return SSSEG_EINVAL;
+    // a residual here is the first part's ReLU mask (its producer's forward output), never an addend
+    eb.rmask = eh.rmask = e.residual ? 1 : 0;
     eb.y2 = (bf16_t*)ysplit->x2;
     eh.y2 = (f16_t*)ysplit->x2;
     eb.oc1 = eh.oc1 = (int)oc1;

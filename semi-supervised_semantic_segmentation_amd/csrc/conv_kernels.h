@@ -180,6 +180,9 @@ struct Epi {
   TO* y2 = nullptr;
   int oc1 = 0x40000000;
   int ldy2 = 0;
+  // rmask (split outputs only): res is not added but is the forward output of the first part's producer, whose
+  // ReLU backward is applied in place: channels [0, oc1) are stored as (res > 0 ? v : 0), channels >= oc1 read no res
+  int rmask = 0;
 };
 
 // where output channel n of pixel op is stored (y, or the second part of a split output)
@@ -296,7 +299,7 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[FN][FM], long long
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
       r[j][0] = r[j][1] = r[j][2] = r[j][3] = 0.f;
-      if (ep.res && op[j] >= 0) {
+      if (ep.res && op[j] >= 0 && n < ep.oc1) {
         const TO* rp = ep.res + op[j] * ep.ldr + n;
         if (full && (ep.ldr & 3) == 0)
           Load4<TO>::ld(rp, r[j]);
@@ -324,8 +327,9 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[FN][FM], long long
         float a = acc[i][j][e];
         if (ep.scale) a *= sc[e];
         if (ep.shift) a += sh[e];
-        a += r[j][e];
+        if (!ep.rmask) a += r[j][e];
         a = act_fwd(a, ep.relu, ep.slope);
+        if (ep.rmask && n < ep.oc1 && !(r[j][e] > 0.f)) a = 0.f;
         v[e] = a;
         if constexpr (ST) {   // compile-time: the statistics arrays stay in registers
           if (n + e < g.K) {
@@ -454,7 +458,7 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) r[p][e] = 0.f;
-      if (ep.res && op[p] >= 0) {
+      if (ep.res && op[p] >= 0 && n < ep.oc1) {
         if (full) {
           if constexpr (sizeof(TO) == 2) {
             if (pre.on) {
@@ -480,9 +484,18 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
       const float4 a0 = *(const float4*)a, a1 = *(const float4*)(a + 4);
       const float raw[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
       // affine + residual, then ONE uniform activation switch per chunk (not one per value)
+      if (ep.rmask) {   // split output with the first part's ReLU backward (no residual add)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = raw[e] * sc[e] + sh[e] + r[p][e];   // scale 1 / shift 0 when absent
-      act8(v, ep.relu, ep.slope);
+        for (int e = 0; e < 8; ++e) v[e] = raw[e] * sc[e] + sh[e];
+        act8(v, ep.relu, ep.slope);
+        if (n < ep.oc1)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = r[p][e] > 0.f ? v[e] : 0.f;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = raw[e] * sc[e] + sh[e] + r[p][e];   // scale 1 / shift 0 when absent
+        act8(v, ep.relu, ep.slope);
+      }
       const long long o = op[p] * g.ldy + n;
       TO* yp = out_at(ep, y, g.ldy, op[p], n);   // (a split output has no aux: host contract)
       if (full) {
@@ -969,7 +982,7 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
     if (ep.res && splits == 1) {
       const int ch = t % EP_CPR, r0 = t / EP_CPR;
       const int n = n0 + ch * 8;
-      pre.on = (g.ldy & 7) == 0 && (ep.ldr & 7) == 0 && n + 7 < g.K;
+      pre.on = (g.ldy & 7) == 0 && (ep.ldr & 7) == 0 && n + 7 < g.K && n < ep.oc1;
 #pragma unroll
       for (int p = 0; p < EP_NP; ++p) {
         const int row = r0 + p * EP_RPP;
@@ -1071,8 +1084,10 @@ __global__ void splitk_finalize_kernel(const float* __restrict__ ws, TO* __restr
     if (ep.aux) io<TO>::st(ep.aux, op * g.ldy + n, v);
     if (ep.scale) v *= ep.scale[n];
     if (ep.shift) v += ep.shift[n];
-    if (ep.res) v += io<TO>::ld(ep.res, op * ep.ldr + n);
+    const float r = (ep.res && n < ep.oc1) ? io<TO>::ld(ep.res, op * ep.ldr + n) : 0.f;
+    if (!ep.rmask) v += r;
     v = act_fwd(v, ep.relu, ep.slope);
+    if (ep.rmask && n < ep.oc1 && !(r > 0.f)) v = 0.f;
     io<TO>::st(out_at(ep, y, g.ldy, op, n), 0, v);
   }
 }

@@ -407,6 +407,10 @@ class _ConvFn(torch.autograd.Function):
         y = mod._ssseg_forward(x, relu, stats=stats)
         ctx.mod, ctx.relu, ctx.handoff, ctx.join, ctx.vcat = mod, relu, handoff, join, _vcat_of(x)
         ctx.save_for_backward(x, y if _act(relu)[0] else None)
+        if _act(relu)[0] == ACT_RELU:
+            # a ReLU output: a consumer's input-gradient launch may apply this ReLU's backward in place (the
+            # gradient then carries _ssseg_premasked and backward() skips ssseg_act_bwd)
+            y.__dict__['_ssseg_relu_out'] = True
         return y
 
     @staticmethod
@@ -416,7 +420,7 @@ class _ConvFn(torch.autograd.Function):
         mod = ctx.mod
         gy = mod._grad_in(gy)
         code, slope = _act(ctx.relu)
-        if code:
+        if code and not gy.__dict__.get('_ssseg_premasked', False):
             gm = torch.empty_like(gy)
             N.call('ssseg_act_bwd', N.dev_ptr(gy), N.dev_ptr(y), N.dev_ptr(gm), gy.numel(), code, slope, N.dt_code(gy),
                    N.stream())
@@ -861,13 +865,19 @@ class Conv2d(nn.Conv2d, _ConvBase):
         dref = ctypes_ref(d)
         nb = N.lib().ssseg_conv_igemm_workspace_bytes(dref, N.dt_code(gy))
         ws = N.workspace(nb, gy.device) if nb else None
-        ep = N.ConvEpilogue(None, None, None, 0, None, 0, 0.0, None, 0, None)
+        mask = vc.a if vc.mask_a else None   # the first part's ReLU mask (its forward output)
+        ep = N.ConvEpilogue(None, None, N.dev_ptr(mask) if mask is not None else None, vc.ca if mask is not None else 0,
+                            None, 0, 0.0, None, 0, None)
         split = N.VCat(N.dev_ptr(db), vc.ca, vc.cb)
         with _Timed(_conv_flops(n, OH, OW, self.out_channels, self.in_channels, R, S), 'dgrad', _tag(self, n, H, W)):
             ok = N.call_or_unsupported('ssseg_conv_igemm_epi_vsplit', N.dev_ptr(gy), N.dev_ptr(w), N.dev_ptr(da),
                                        ctypes_ref(split), dref, N.dt_code(gy), N.dt_code(gy), ctypes_ref(ep),
                                        N.dev_ptr(ws) if ws is not None else None, nb, N.stream())
-        return (da, db) if ok else None
+        if not ok:
+            return None
+        if mask is not None:
+            da.__dict__['_ssseg_premasked'] = True
+        return da, db
 
 
 class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
@@ -1325,12 +1335,15 @@ class VirtualCat:
     """The two parts of a virtual channel concat (cat_crop(lazy=True)): the consuming conv's kernels read channels
     [0, ca) from a and [ca, ca + cb) from b where they lie (ssseg_vcat); the concat tensor itself is allocated but
     not written unless materialize() runs (a consumer that cannot read it part by part)."""
-    __slots__ = ('a', 'b', 'ca', 'cb', '_d2', 'grads')
+    __slots__ = ('a', 'b', 'ca', 'cb', '_d2', 'grads', 'mask_a')
 
     def __init__(self, a, b, ca, cb):
         self.a, self.b, self.ca, self.cb = a, b, ca, cb
         self._d2 = None
         self.grads = None   # (da, db) from the consumer's split-output dgrad, taken by the concat's backward
+        # a is the output of a fused conv+ReLU (the UpBlock upsampler): da can be written with that ReLU's
+        # backward already applied (ssseg_conv_igemm_epi_vsplit's mask), which removes its ssseg_act_bwd pass
+        self.mask_a = bool(a.__dict__.get('_ssseg_relu_out', False))
 
     def desc2(self):
         if self._d2 is None:

@@ -84,9 +84,10 @@ def test_virtual_concat_is_not_copied(hip_device):
 
 @pytest.mark.parametrize('mode', ['train', 'eval'])
 def test_virtual_concat_backward_writes_parts(hip_device, monkeypatch, mode):
-    """conv3_0's input gradient goes straight into the two parts' gradients (ssseg_conv_igemm_epi_vsplit): no
-    channel copy runs in the forward or the backward of an eligible UpBlock (the gradients themselves are checked
-    bitwise against the copy path by test_upblock_virtual_concat_bitwise)."""
+    """conv3_0's input gradient goes straight into the two parts' gradients (ssseg_conv_igemm_epi_vsplit), the up
+    part's with the upsampler's ReLU backward applied: no channel copy and no ssseg_act_bwd pass run in the forward
+    or the backward of an eligible UpBlock (the gradients themselves are checked bitwise against the copy path by
+    test_upblock_virtual_concat_bitwise)."""
     from ssseg import native as N
     from ssseg import nn as snn
     snn.set_compute_dtype(torch.bfloat16)
@@ -112,3 +113,5 @@ def test_virtual_concat_backward_writes_parts(hip_device, monkeypatch, mode):
     torch.cuda.synchronize()
     assert 'ssseg_conv_igemm_epi_vsplit' in calls
     assert 'ssseg_nhwc_copy' not in calls
+    # the upsampler's ReLU backward runs inside the split launch (the up part's gradient arrives masked)
+    assert 'ssseg_act_bwd' not in calls
