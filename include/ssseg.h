@@ -375,10 +375,11 @@ int ssseg_bn_stats_finalize(const void* x, int64_t P, int64_t C, int64_t ldx, in
                             float* running_mean, float* running_var, int64_t* num_batches_tracked,
                             ssseg_stream_t stream);
 /* BatchNorm statistics from the partial rows a conv epilogue wrote (ssseg_conv_epilogue.stats): sums[0:C] /
- * sums[C:2C] = column sums over nparts rows of part[2*nparts][C] (fixed order, deterministic); when mean_out is
+ * sums[C:2C] = column sums over nparts rows of part[2*nparts][C] (fixed order, deterministic; part is scratch: a
+ * long table is folded in place before the column reduce, so its contents are undefined afterwards); when mean_out is
  * non-NULL the training finalize of ssseg_bn_finalize runs in the same launch (the single-process path; SyncBN
  * passes mean_out = NULL, all-reduces sums, then calls ssseg_bn_finalize). */
-int ssseg_bn_partials_finalize(const double* part, int64_t nparts, int64_t C, double* sums, double count, float eps,
+int ssseg_bn_partials_finalize(double* part, int64_t nparts, int64_t C, double* sums, double count, float eps,
                                float momentum, float* mean_out, float* invstd_out, float* running_mean,
                                float* running_var, int64_t* num_batches_tracked, ssseg_stream_t stream);
 /* eval mode: mean = running_mean, invstd = 1/sqrt(running_var + eps) */

@@ -245,9 +245,31 @@ __device__ __forceinline__ void finalize_channel(double s1, double s2, int c, do
 // sums over the per-block partials: block = CH channels x (256/CH) partial lanes, two accumulator chains
 // per lane, then a fixed-order LDS reduction (deterministic).  Narrow channel groups (CH = 2, 4) put more
 // workgroups and shorter load chains on the small-C layers, whose partial count is the largest.
+// Long tables (a conv epilogue's statistics rows: one per 128-pixel tile, 8192 rows at 16x256^2) are first folded
+// in place: block b sums rows [b*S, (b+1)*S) in order -- coalesced full-row reads, every thread one column of the
+// [2][C] row -- and leaves the sum in row b*S; the final kernel then reads every S-th row.  (The final kernel alone
+// gave such a table C/CH = 32 workgroups of strided 8-byte reads: 30 us for 8 MB.)
+__global__ void __launch_bounds__(256) bn_partial_rows_kernel(double* part, int nparts, int C, int S) {
+  const int r0 = blockIdx.x * S, r1 = min(nparts, r0 + S);
+  for (int k = threadIdx.x; k < 2 * C; k += 256) {
+    double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    int r = r0;
+    for (; r + 3 < r1; r += 4) {
+      const double q0 = part[(int64_t)(2 * r) * C + k], q1 = part[(int64_t)(2 * (r + 1)) * C + k];
+      const double q2 = part[(int64_t)(2 * (r + 2)) * C + k], q3 = part[(int64_t)(2 * (r + 3)) * C + k];
+      a0 += q0;
+      a1 += q1;
+      a2 += q2;
+      a3 += q3;
+    }
+    for (; r < r1; ++r) a0 += part[(int64_t)(2 * r) * C + k];
+    part[(int64_t)(2 * r0) * C + k] = (a0 + a1) + (a2 + a3);
+  }
+}
+
 template <int CH>
 __global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* part, int nparts, int C, double* sums,
-                                                               FinalEpi fe) {
+                                                               FinalEpi fe, int rs = 1) {
   constexpr int LN = 256 / CH;
   if (fe.mode == 1 && fe.nbt && blockIdx.x == 0 && threadIdx.x == 0) *fe.nbt += 1;
   __shared__ double red[2][LN][CH];
@@ -261,8 +283,8 @@ __global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* par
       double qa[4], qb[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        qa[k] = part[(int64_t)(2 * (i + k * LN)) * C + c];
-        qb[k] = part[(int64_t)(2 * (i + k * LN) + 1) * C + c];
+        qa[k] = part[(int64_t)(2 * (i + k * LN) * rs) * C + c];
+        qb[k] = part[(int64_t)(2 * (i + k * LN) * rs + 1) * C + c];
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -271,8 +293,8 @@ __global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* par
       }
     }
     for (; i < nparts; i += LN) {
-      a[0] += part[(int64_t)(2 * i) * C + c];
-      b[0] += part[(int64_t)(2 * i + 1) * C + c];
+      a[0] += part[(int64_t)(2 * i * rs) * C + c];
+      b[0] += part[(int64_t)(2 * i * rs + 1) * C + c];
     }
   }
   const double a0 = a[0] + a[2], a1 = a[1] + a[3], b0 = b[0] + b[2], b1 = b[1] + b[3];
@@ -298,17 +320,26 @@ __global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* par
 }
 
 // one launch of the partial reduction: channel group narrowed until the grid has >= 64 workgroups
+// part is consumed (a long table is folded in place first)
 static void launch_partial_final(const double* part, int64_t nparts, int64_t C, double* sums, hipStream_t s,
                                  FinalEpi fe = FinalEpi{}) {
+  int rs = 1;
+  if (nparts >= 1024) {   // fold to ~256 rows first
+    rs = (int)((nparts + 255) / 256);
+    const int64_t g = (nparts + rs - 1) / rs;
+    hipLaunchKernelGGL(bn_partial_rows_kernel, dim3((unsigned)g), dim3(256), 0, s, (double*)part, (int)nparts, (int)C,
+                       rs);
+    nparts = g;
+  }
   if (C >= 512 || nparts < 256)
     hipLaunchKernelGGL(bn_partial_final_kernel<8>, dim3((unsigned)((C + 7) / 8)), dim3(256), 0, s, part, (int)nparts,
-                       (int)C, sums, fe);
+                       (int)C, sums, fe, rs);
   else if (C >= 128)
     hipLaunchKernelGGL(bn_partial_final_kernel<4>, dim3((unsigned)((C + 3) / 4)), dim3(256), 0, s, part, (int)nparts,
-                       (int)C, sums, fe);
+                       (int)C, sums, fe, rs);
   else
     hipLaunchKernelGGL(bn_partial_final_kernel<2>, dim3((unsigned)((C + 1) / 2)), dim3(256), 0, s, part, (int)nparts,
-                       (int)C, sums, fe);
+                       (int)C, sums, fe, rs);
 }
 
 __global__ void bn_finalize_kernel(const double* sums, int C, double count, float eps, float momentum, float* mean_out,
@@ -729,7 +760,7 @@ extern "C" int ssseg_bn_stats_finalize(const void* x, int64_t P, int64_t C, int6
   return 0;
 }
 
-extern "C" int ssseg_bn_partials_finalize(const double* part, int64_t nparts, int64_t C, double* sums, double count,
+extern "C" int ssseg_bn_partials_finalize(double* part, int64_t nparts, int64_t C, double* sums, double count,
                                           float eps, float momentum, float* mean_out, float* invstd_out,
                                           float* running_mean, float* running_var, int64_t* num_batches_tracked,
                                           ssseg_stream_t stream) {
