@@ -10,7 +10,8 @@ degenerate in eval mode (HRNet-MSA's eval logits are ~1e-14: tools/diag_c4.py), 
 pixel is confident and the consistency loss is the reference's own 0/0 NaN.  Before the timed steps
 the student's BatchNorm running statistics are therefore calibrated by ONE train-mode forward (no grad) with
 momentum 1 (running stats = that batch's statistics; the teacher's buffers alias the student's, mean_teacher.py:
-13-18), which is what training does to them anyway; the steps then run at confidence threshold 0.5 and the record
+13-18), which is what training does to them anyway, and the teacher starts from the student's weights (the shared
+pretrained checkpoint of distributed_trainer.py:56-61); the steps then run at confidence threshold 0.5 and the record
 carries cm_mean (the confident-pixel fraction) so a degenerate mean-teacher path is visible.  --threshold 0 and
 --no-calibrate restore the round-2 smoke.
 """
@@ -31,6 +32,22 @@ import torch.distributed as dist  # noqa: E402
 STEP_GFLOP_PER_IMAGE = {'c3': 3855.8, 'c4': 3904.2, 'c5': 85.2}
 PEAK = {'bfloat16': 2.5e15, 'float16': 2.5e15, 'float32': 0.16e15}   # dense MFMA (MI355X_MICROARCH.md)
 CFGS = {'c3': 'configs/c3_deeplabv3_r101.py', 'c4': 'configs/c4_msa_hrnet.py', 'c5': 'configs/c5_hardnet_disc.py'}
+
+
+def rescale_heads(model, ncls=2):
+    """Re-initialise the class-logit convs (out_channels == ncls) with a unit-gain fan-in normal init: the configs'
+    own inits leave a random network's logits at ~0 (C4 MSA-HRNet and C5 HarDNet: sup loss exactly ln2 / 2 at step 0),
+    so p = 0.5 everywhere and no pixel is confident at any threshold.  A synthetic-data stand-in for a trained head."""
+    import math
+    with torch.no_grad():
+        for m in model.modules():
+            if isinstance(m, torch.nn.Conv2d) and m.out_channels == ncls:
+                fan_in = m.in_channels * m.kernel_size[0] * m.kernel_size[1] // m.groups
+                m.weight.normal_(0.0, 1.0 / math.sqrt(fan_in))
+                if m.bias is not None:
+                    m.bias.zero_()
+                if hasattr(m, 'invalidate_packed'):
+                    m.invalidate_packed()
 
 
 def calibrate_bn(model, x):
@@ -60,7 +77,12 @@ def run(name, path, dev, threshold=0.5, calibrate=True):
     snn.set_compute_dtype({'fp32': torch.float32, 'fp16': torch.float16}.get(cfg['common'].get('compute_dtype'),
                                                                              torch.bfloat16))
     model = DistributedDataParallel(cfg['model']['model_fn']().to(dev))
+    if calibrate:
+        rescale_heads(model.module)
     ema = cfg['model']['model_fn']().to(dev)
+    # the teacher starts from the student's weights: the stand-in for the pretrained checkpoint both models load in
+    # the reference (distributed_trainer.py:56-61); two independent random inits give a teacher whose eval logits do
+    # not match the (student-calibrated, aliased) BN statistics and are degenerate (C4: cm_mean 0, 0/0 NaN)
     mean_teacher.detach_model_parameters(ema)
     arena.attach(ema, with_grads=False)
     ema.eval()
@@ -85,6 +107,8 @@ def run(name, path, dev, threshold=0.5, calibrate=True):
     ub = torch.rand(b, 3, s, s, generator=g).to(dev)
     if calibrate:
         calibrate_bn(model.module, ua)
+    with torch.no_grad():   # after the calibration: the teacher's own BN buffers are used until the first EMA update
+        ema.load_state_dict(model.module.state_dict())
     torch.cuda.reset_peak_memory_stats(dev)
     times, out = [], []
     for step in range(3):
