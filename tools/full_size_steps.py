@@ -64,7 +64,7 @@ def calibrate_bn(model, x):
         m.momentum = mo
 
 
-def run(name, path, dev, threshold=0.5, calibrate=True):
+def run(name, path, dev, threshold=0.5, calibrate=True, layers=False):
     import config
     import mean_teacher
     import train
@@ -118,6 +118,19 @@ def run(name, path, dev, threshold=0.5, calibrate=True):
         torch.cuda.synchronize()
         times.append(time.time() - t0)
         out.append((float(cls), float(unsup) if unsup is not None else None, float(cm) if cm is not None else None))
+    if layers:   # one more step with HIP events around every conv-engine launch (tools/layer_report.py format)
+        sys.path.insert(0, os.path.join(ROOT, 'tools'))
+        import layer_report
+        rows = snn.probe(True)
+        train.train_step(model, ema, opt, img, mask, ua, ub, 30, 3, cfg)
+        snn.probe(False)
+        torch.cuda.synchronize()
+        print(f'== {name} conv layers', file=sys.stderr)
+        stdout, sys.stdout = sys.stdout, sys.stderr
+        try:
+            layer_report.report(rows, 40)
+        finally:
+            sys.stdout = stdout
     params_finite = all(bool(torch.isfinite(p).all()) for p in model.parameters())
     losses_finite = all(v is None or v == v and abs(v) != float('inf') for row in out for v in row)
     rec = {'config': name, 'image_size': s, 'batch': b, 'dtype': str(snn.compute_dtype()).replace('torch.', ''),
@@ -140,13 +153,14 @@ def main():
     ap.add_argument('--configs', default='c3,c4,c5')
     ap.add_argument('--threshold', type=float, default=0.5)
     ap.add_argument('--no-calibrate', action='store_true')
+    ap.add_argument('--layers', action='store_true', help='per-layer conv report of one extra step (stderr)')
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     dist.init_process_group('nccl', init_method='tcp://127.0.0.1:29533', rank=0, world_size=1)
     ok = True
     for name in a.configs.split(','):
-        ok &= run(name, CFGS[name], dev, a.threshold, not a.no_calibrate)
+        ok &= run(name, CFGS[name], dev, a.threshold, not a.no_calibrate, a.layers)
         torch.cuda.empty_cache()
     dist.destroy_process_group()
     sys.exit(0 if ok else 1)

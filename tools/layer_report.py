@@ -64,6 +64,11 @@ def main():
     train.train_step(model, teacher, opt, img, mask, ua, ub, 30, 3, cfg)
     snn.probe(False)
     torch.cuda.synchronize()
+    report(rows, a.top)
+
+
+def report(rows, top):
+    """Print the per-(kind, layer) aggregate of snn.probe rows (shared with tools/full_size_steps.py --layers)."""
     agg = collections.defaultdict(lambda: [0.0, 0.0, 0, 0])
     by_kind = collections.defaultdict(lambda: [0.0, 0.0])
     for e0, e1, fl, kind, tag in rows:
@@ -87,7 +92,7 @@ def main():
     tot_roof = sum(roof.values())
     print(f'roofline floor (max of 2.5 PF/s and 8 TB/s per layer): {tot_roof:.3f} ms = {tot_roof / tot_ms:.3f} of the conv time')
     print(f'{"ms":>8s} {"pct":>6s} {"calls":>5s} {"GFLOP":>8s} {"TF/s":>7s} {"alg MB":>8s} {"TB/s":>6s} {"roof":>5s}  kind   layer')
-    for (kind, tag), (ms, fl, n, by) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:a.top]:
+    for (kind, tag), (ms, fl, n, by) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:top]:
         print(f'{ms:8.3f} {100 * ms / tot_ms:6.2f} {n:5d} {fl / 1e9:8.1f} {fl / ms / 1e9:7.1f} {by / 1e6:8.1f} '
               f'{by / ms / 1e9:6.2f} {roof[(kind, tag)] / ms:5.2f}  {kind:6s} {tag}')
 
