@@ -113,6 +113,7 @@ static unsigned long long geom_key(const ConvGeom& g, int tag) {
 static int heuristic_variant(const ConvGeom& g) {
   auto tiles = [&](int bm, int bn) { return ((g.M + bm - 1) / bm) * ((g.K + bn - 1) / bn); };
   if (g.KK <= 128) return 0;
+  if (g.C % 64) return 5;   // general-k loader: 64-wide n-tiles only
   if (g.K > 64) return tiles(256, 128) >= 128 ? 6 : (tiles(128, 128) >= 256 ? 8 : 5);
   return tiles(64, 64) < 512 ? 10 : 0;
 }
@@ -202,7 +203,8 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
   if constexpr (sizeof(T) == 2 && sizeof(TO) == 2) {
     const long long xb = (long long)g.N * g.H * g.W * g.ldx * 2, wb = (long long)g.K * g.ldw * 2;
     const long long x2b = x2 ? (long long)g.N * g.H * g.W * g.ldx2 * 2 : 0;
-    if (sizeof(TO) == 2 && g_knobs[3] == 0 && g.C % 64 == 0 && g.ldx % 8 == 0 && g.ldw % 8 == 0 && g.ldw == g.KK &&
+    // C % 64 != 0 (general-k loader, 64-wide n-tiles): any C % 8 == 0 (geom_ok), no virtual concat
+    if (sizeof(TO) == 2 && g_knobs[3] == 0 && (g.C % 64 == 0 || !x2) && g.ldx % 8 == 0 && g.ldw % 8 == 0 && g.ldw == g.KK &&
         g.K > 16 && xb < 0x7fffffffLL && wb < 0x7fffffffLL && x2b < 0x7fffffffLL && (!x2 || g.ldx2 % 8 == 0)) {
       int v = g_knobs[4];
       if (v < 0) v = 0;
@@ -228,8 +230,11 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
       // split-K only where the autotuner measured it faster (its fp32 atomics reorder the sums); a variant
       // forced by knob 4 runs unsplit, so forced variants stay bit-comparable
       float* wsv = (g_knobs[4] == 0 && (v & kSplitBit)) ? ws : nullptr;
-      return run_variant<T, TO>(v & ~kSplitBit, x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, ph ? nullptr : wsv, ph,
-                                x2, (unsigned)x2b);
+      const int r = run_variant<T, TO>(v & ~kSplitBit, x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s,
+                                       ph ? nullptr : wsv, ph, x2, (unsigned)x2b);
+      // a forced config without a general-k instantiation (128/256-wide n-tiles, C % 64 != 0): register-staged
+      if (r == -1 && g_knobs[4] != 0 && !x2 && g.C % 64) return run_variant<T, TO>(0, x, w, y, g, ep, 0, 0, s, nullptr, ph);
+      return r;
     }
   }
   if (x2) return -1;

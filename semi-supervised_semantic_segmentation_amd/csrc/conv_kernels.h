@@ -64,6 +64,8 @@ struct ConvGeom {
   // (pixel stride ldx), channels [64*c1b, C) from a second tensor x2 (pixel stride ldx2), same N x H x W.  No
   // second source: c1b >= C / 64.
   int c1b, ldx2;
+  unsigned mC;   // magic divisor: channel count C (the general-k LDS-DMA loader's k -> (tap, channel) split)
+  int sC;
 };
 
 // magic multiplier for unsigned division by d >= 1: n / d = (umulhi(n, m) + n) >> s for n < 2^31
@@ -111,6 +113,7 @@ static inline bool make_geom(const ssseg_conv_desc* d, ConvGeom& g) {
   fdiv_init(g.K > 0 ? (g.K + 127) / 128 : 1, g.mn128, g.sn128);
   fdiv_init(g.K > 0 ? (g.K + 255) / 256 : 1, g.mn256, g.sn256);
   fdiv_init(g.S > 0 ? g.S : 1, g.mS, g.sS);
+  fdiv_init(g.C > 0 ? g.C : 1, g.mC, g.sC);
   g.oident = g.osy == 1 && g.osx == 1 && g.ooy == 0 && g.oox == 0 && g.outH == g.OH && g.outW == g.OW;
   g.aident = g.R == 1 && g.S == 1 && g.sy == 1 && g.sx == 1 && g.py == 0 && g.px == 0 && g.H == g.OH &&
              g.W == g.OW;
@@ -827,9 +830,13 @@ __device__ __forceinline__ void vmcnt_wait() {
 
 constexpr unsigned OOB = 0x80000000u;   // > any num_records we build: the load returns zeros
 
-// VC: virtual concat input (ConvGeom.c1b / ldx2): k-tiles of channel block >= c1b gather from x2 (a scalar choice
-// per k-tile: the block never straddles the seam because both parts are whole 64-channel blocks)
-template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS, bool STATS, bool VC = false>
+// KM (k mode): 0 = 64-channel k-tiles (C % 64 == 0, channel block major, tap minor: the tile's tap and channel block
+// are scalars); 1 = the same over a virtual concat input (ConvGeom.c1b / ldx2): k-tiles of channel block >= c1b
+// gather from x2 (a scalar choice per k-tile: the block never straddles the seam because both parts are whole
+// 64-channel blocks); 2 = general k (any C % 8 == 0: HRNet-W32's 32-channel branches, HarDNet's growth layers):
+// k runs linearly, k = tap * C + c, exactly like the register-staged kernel, so a 64-deep k-tile may hold several
+// taps -- every lane splits its own 16-byte chunk's k into (tap, channel) and gathers from that tap's pixel
+template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS, bool STATS, int KM = 0>
 __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __restrict__ x,
                                                                 const TO* __restrict__ w, TO* __restrict__ y,
                                                                 ConvGeom g, Epi<TO> ep, unsigned xbytes,
@@ -837,6 +844,7 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
                                                                 float* __restrict__ ws, PhaseTab ph,
                                                                 const TO* __restrict__ x2, unsigned x2bytes) {
   constexpr int ROW = 128;                       // bytes per LDS row = 64 bf16 of k
+  constexpr bool VC = KM == 1, GK = KM == 2;
   constexpr int STAGE = (BM + BN) * ROW;
   constexpr int AI = BM / 8 / NW;                // A (pixel) wave-instructions per wave per stage
   constexpr int BI = BN / 8 / NW;                // B (weight) wave-instructions per wave per stage
@@ -871,7 +879,7 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
   const int RS = g.R * g.S;
   const int cpt = g.C >> 6;                      // k-tiles per tap
   // split-K (low-tile layers, blockIdx.y = split): this block reduces k-tiles [kt0, kt1) in order
-  const int nk_all = RS * cpt;
+  const int nk_all = GK ? (g.KK + 63) >> 6 : RS * cpt;
   int kt0 = 0, nk = nk_all;   // the common unsplit launch: no divisions
   if (splits > 1) {
     const int kper = (nk_all + splits - 1) / splits;
@@ -888,6 +896,7 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
   const int c_even = (lane & 7) ^ (lane >> 4);
   int a_off[AI], a_iy[AI], a_ix[AI];
   int a_pix[VC ? AI : 1];   // VC: input pixel index of the row (the byte offset differs per source)
+  int a_k[GK ? AI : 1];     // GK: k of this lane's chunk in the next k-tile to issue
 #pragma unroll
   for (int ii = 0; ii < AI; ++ii) {
     const int inst = wave * AI + ii;
@@ -908,8 +917,9 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
       a_iy[ii] = -0x40000000;   // never in bounds
       a_ix[ii] = 0;
     }
-    a_off[ii] = pix * g.ldx * 2 + ch * 16;
+    a_off[ii] = pix * g.ldx * 2 + (GK ? 0 : ch * 16);
     if constexpr (VC) a_pix[ii] = pix * g.ldx2 * 2 + ch * 16;
+    if constexpr (GK) a_k[ii] = kt0 * 64 + ch * 8;
   }
   unsigned b_off[BI];
 #pragma unroll
@@ -939,11 +949,39 @@ __global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __rest
   // the same input lines RS times in a row, so those re-reads hit L2 (PMC: a tap-major sweep over all C kept
   // BM x C x 2 B per block live -- 50 MB over the chip at 384 channels -- and its re-reads went to the Infinity
   // Cache at 2.6x the L2 latency, which is what bounds the LDS-DMA stream: ~90 outstanding lines per CU)
+  // GK: the (tap, channel) of each lane's chunk k; k >= KK (the last tile's tail) is a padding tap (zeros), so
+  // the weight bytes loaded there (the next row's head) only ever meet zeros
+  auto set_k = [&]() {
+#pragma unroll
+    for (int ii = 0; ii < AI; ++ii) {
+      const int k = a_k[ii];
+      const int tap = fdiv(k, g.mC, g.sC), c = k - tap * g.C;
+      const int r = fdiv(tap, g.mS, g.sS), s_ = tap - r * g.S;
+      const int dyy = r * g.dy, dxx = s_ * g.dx;
+      const int iy = a_iy[ii] + dyy, ix = a_ix[ii] + dxx;
+      const bool ok = tap < RS && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+      a_cur[ii] = ok ? (unsigned)(a_off[ii] + ((dyy * g.W + dxx) * g.ldx + c) * 2) : OOB;
+    }
+  };
   int ld_tap = kt0 ? kt0 % RS : 0, ld_c = kt0 ? kt0 / RS : 0;   // next: tap, channel block
-  set_tap(ld_tap);
+  int ld_kt = kt0;                                              // GK: next k-tile
+  if constexpr (GK) set_k();
+  else set_tap(ld_tap);
   auto issue = [&](int buf) {
     char* As = smem + buf * STAGE;
     char* Bs = As + BM * ROW;
+    if constexpr (GK) {
+      const unsigned sb = (unsigned)__builtin_amdgcn_readfirstlane(ld_kt * 128);
+#pragma unroll
+      for (int ii = 0; ii < AI; ++ii) bldslds16(xr, As + (wave * AI + ii) * 1024, a_cur[ii], 0u);
+#pragma unroll
+      for (int jj = 0; jj < BI; ++jj) bldslds16(wr, Bs + (wave * BI + jj) * 1024, b_off[jj], sb);
+      ++ld_kt;
+#pragma unroll
+      for (int ii = 0; ii < AI; ++ii) a_k[ii] += 64;
+      set_k();
+      return;
+    }
     // wave-uniform soffsets, stated as such (otherwise the compiler may keep the k-state in VGPRs and wrap every
     // LDS-DMA issue in a readfirstlane waterfall loop)
     const unsigned sa = (unsigned)__builtin_amdgcn_readfirstlane(ld_c * 128),
@@ -1139,7 +1177,7 @@ inline int plan_splits(const ConvGeom& g);
 template <typename TO>
 __global__ void splitk_finalize_kernel(const float* __restrict__ ws, TO* __restrict__ y, ConvGeom g, Epi<TO> ep);
 
-template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS, bool VC>
+template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS, int VC>
 int launch_glds_vc(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
                    unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2, unsigned x2b) {
   static_assert(sizeof(TO) == 2, "LDS-DMA configs: 16-bit activations in and out (fp32-output heads have K <= 16)");
@@ -1182,8 +1220,12 @@ int launch_glds_vc(const void* x, const void* w, void* y, const ConvGeom& g, con
 template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS>
 int launch_glds(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb, unsigned wb,
                 hipStream_t s, float* ws, const PhaseTab* ph, const void* x2 = nullptr, unsigned x2b = 0) {
-  if (x2) return launch_glds_vc<TO, BM, BN, WM, WN, NW, NS, true>(x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
-  return launch_glds_vc<TO, BM, BN, WM, WN, NW, NS, false>(x, w, y, g, ep, xb, wb, s, ws, ph, nullptr, 0);
+  if (x2) return launch_glds_vc<TO, BM, BN, WM, WN, NW, NS, 1>(x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
+  if (g.C & 63) {   // general k: instantiated for the 64-wide n-tiles only (the C % 64 != 0 layers have K <= 98)
+    if constexpr (BN == 64) return launch_glds_vc<TO, BM, BN, WM, WN, NW, NS, 2>(x, w, y, g, ep, xb, wb, s, ws, ph, nullptr, 0);
+    return -1;
+  }
+  return launch_glds_vc<TO, BM, BN, WM, WN, NW, NS, 0>(x, w, y, g, ep, xb, wb, s, ws, ph, nullptr, 0);
 }
 
 

@@ -289,11 +289,16 @@ ALL_VARIANTS = [11] + list(range(1, 11)) + list(range(12, 24))
 @pytest.mark.parametrize('kind,cin,cout,k,H', [('conv', 64, 128, 3, 19), ('conv', 128, 64, 1, 17), ('conv', 192, 256, 3, 9),
                                                ('conv', 64, 256, 1, 21), ('convT', 128, 64, 4, 7),
                                                ('conv', 256, 200, 1, 23), ('conv', 192, 1024, 1, 11),
-                                               ('conv_s2', 128, 256, 1, 18), ('conv', 64, 64, 1, 64)])
+                                               ('conv_s2', 128, 256, 1, 18), ('conv', 64, 64, 1, 64),
+                                               # C % 64 != 0: the general-k LDS-DMA loader (64-wide n-tiles)
+                                               ('conv', 32, 32, 3, 33), ('conv', 16, 64, 3, 20), ('conv', 8, 48, 3, 17),
+                                               ('conv', 48, 50, 3, 15), ('conv', 96, 64, 3, 13), ('conv', 50, 28, 1, 19),
+                                               ('conv_s2', 32, 64, 3, 26), ('convT', 32, 32, 4, 9)])
 def test_conv_variants_bitwise(hip_device, kind, cin, cout, k, H):
     """Every bf16 engine variant (register-staged, LDS-DMA tile configs 1..10 and 12..23) accumulates the
     same MFMA k-sequence: forward and input-gradient outputs are bit-identical, so autotuning never changes
-    results."""
+    results.  C % 64 != 0 layers run the general-k loader on the 64-wide configs (the others fall back to the
+    register-staged kernel when forced), whose linear k order is the register-staged kernel's."""
     from ssseg import native as N
     from ssseg import nn as snn
     snn.set_compute_dtype(torch.bfloat16)
