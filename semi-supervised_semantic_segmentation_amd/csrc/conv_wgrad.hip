@@ -303,7 +303,10 @@ struct WSeg2 {
 // chunk lies before the seam from the first part and by the others from the second (EXEC-masked LDS-DMA: each
 // lane lands its 16 bytes in the same slot as in the unsplit issue), so the tile and its MFMA sequence are those of
 // the materialised concat.
-template <typename T16, int BMW, int BNW, int NS, int WM = 2, int WN = 2, int BKP = 64, bool ST = false>
+// GK (general k, C % 64 != 0: HRNet-W32's 32-channel branches, HarDNet's growth layers): a kk-tile holds several
+// taps, so every lane finds its own chunk's (tap, channel) once at the start (the kk-tile is fixed per block) and
+// gathers from that tap's offset; kk >= KK (the last tile's tail) loads zeros
+template <typename T16, int BMW, int BNW, int NS, int WM = 2, int WN = 2, int BKP = 64, bool ST = false, bool GK = false>
 __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const T16* __restrict__ x, const T16* __restrict__ dy,
                                                                    float* __restrict__ slab, ConvGeom g,
                                                                    long long pix_per_split, WDirect dd, unsigned xbytes,
@@ -352,11 +355,20 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const T16* __r
   // its pixel advances by BKP per k-tile (incremental decode, no per-tile division)
   long long xp[XI];
   int xoy[XI], xox[XI], ximg[XI], xcb[XI];
+  int gofy[GK ? XI : 1], gofx[GK ? XI : 1];   // GK: this lane's tap offsets per piece
   bool xin2[ST ? XI : 1];   // ST: this lane's chunk of piece ii lies past the seam (second part)
 #pragma unroll
   for (int ii = 0; ii < XI; ++ii) {
     const int row = (wave * XI + ii) * (64 / XCPR) + lane / XCPR;
     xcb[ii] = (cb0 + ((lane % XCPR) ^ wswz<ROWX>(row)) * 8) * 2;
+    if constexpr (GK) {
+      const int kk = kk0 + ((lane % XCPR) ^ wswz<ROWX>(row)) * 8;
+      const int tp = fdiv(kk, g.mC, g.sC), c = kk - tp * g.C;
+      const int r = fdiv(tp, g.mS, g.sS), s_ = tp - r * g.S;
+      xcb[ii] = c * 2;
+      gofy[ii] = tp < g.R * g.S ? r * g.dy + g.py : -0x40000000;   // padding tap: never in bounds
+      gofx[ii] = s_ * g.dx + g.px;
+    }
     if constexpr (ST) {
       xin2[ii] = strad && c0 + ((lane % XCPR) ^ wswz<ROWX>(row)) * 8 >= sg.c1;
       if (xin2[ii]) xcb[ii] -= sg.c1 * 2;   // channel offset inside the second part
@@ -396,7 +408,7 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const T16* __r
         }
       }
       if (xp[ii] < p_end) {
-        const int iy = xoy[ii] * g.sy + offy, ix = xox[ii] * g.sx + offx;
+        const int iy = xoy[ii] * g.sy + (GK ? gofy[ii] : offy), ix = xox[ii] * g.sx + (GK ? gofx[ii] : offx);
         if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
           off = (unsigned)(((ximg[ii] * g.H + iy) * g.W + ix) * ldx) * 2u + (unsigned)xcb[ii];
       }
@@ -635,10 +647,11 @@ void launch_wgrad(const void* x, const void* dy, float* slab, const ConvGeom& g,
     hipLaunchKernelGGL((wgrad_kernel<T, 128, 128>), grid, dim3(256), 0, s, (const T*)x, (const T*)dy, slab, g, p.pps, dd);
 }
 
-// LDS-DMA weight gradient: bf16, C % 64 == 0 (a 64- or 128-channel kk-tile inside one tap), operands < 2 GB
+// LDS-DMA weight gradient: bf16, C % 64 == 0 (a 64- or 128-channel kk-tile inside one tap) or any C % 8 == 0 (the
+// general-k tiles, 64 wide), operands < 2 GB
 static bool wgrad_glds_ok(const ConvGeom& g, int dt) {
   if ((dt != SSSEG_BF16 && dt != SSSEG_F16) || g_knobs[8] != 0) return false;
-  if (g.C % 64 || g.ldx % 8 || g.ldy % 8 || g.K % 8) return false;
+  if (g.C % 8 || g.ldx % 8 || g.ldy % 8 || g.K % 8) return false;
   const long long xb = (long long)g.N * g.H * g.W * g.ldx * 2, db = g.M * g.ldy * 2;
   return xb < 0x7fffffffLL && db < 0x7fffffffLL;
 }
@@ -657,7 +670,8 @@ static int static_wgrad_cfg(const ConvGeom& g) {
 // (st = true); other widths fall back to a 64-wide tile
 static int wgrad_cfg_for(const ConvGeom& g, int c1 = 0, bool* st = nullptr) {
   int c = g_knobs[9];
-  if (!(c > 0 && c < N_WGRAD_CFGS && g.C % WGRAD_CFGS[c].bmw == 0)) c = static_wgrad_cfg(g);
+  if (!(c > 0 && c < N_WGRAD_CFGS && (g.C % 64 ? WGRAD_CFGS[c].bmw == 64 : g.C % WGRAD_CFGS[c].bmw == 0)))
+    c = static_wgrad_cfg(g);
   if (st) *st = false;
   if (c1 > 0 && c1 % WGRAD_CFGS[c].bmw) {
     if (WGRAD_CFGS[c].bmw == 128 && c1 % 64 == 0 && st) *st = true;
@@ -679,10 +693,10 @@ static WgradPlan choose_wgrad(const ConvGeom& g, int dt) {
   return dt != SSSEG_F32 ? plan_wgrad<bf16_t>(g) : plan_wgrad<float>(g);
 }
 
-template <typename T16, int C, bool ST = false>
+template <typename T16, int C, bool ST = false, bool GK = false>
 constexpr auto wgrad_kernel_of() {
   return &wgrad_glds_kernel<T16, WGRAD_CFGS[C].bmw, WGRAD_CFGS[C].bnw, WGRAD_CFGS[C].ns, WGRAD_CFGS[C].wm,
-                            WGRAD_CFGS[C].wn, WGRAD_CFGS[C].bkp, ST>;
+                            WGRAD_CFGS[C].wn, WGRAD_CFGS[C].bkp, ST, GK>;
 }
 
 // resident blocks of an LDS-DMA wgrad config on the whole device (cached per config)
@@ -717,6 +731,14 @@ template <typename T16, int C>
 void launch_wgrad_glds_t(const void* x, const void* dy, float* slab, const ConvGeom& g, const WgradPlan& p, WDirect dd,
                          hipStream_t s, const WSeg2& sg) {
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.ldx * 2), db = (unsigned)(g.M * g.ldy * 2);
+  if constexpr (WGRAD_CFGS[C].bmw == 64) {
+    if (g.C % 64) {   // general k (wgrad_cfg_for picks 64-wide kk-tiles for these)
+      hipLaunchKernelGGL((wgrad_kernel_of<T16, C, false, true>()), dim3(p.mt * p.nt * p.splits),
+                         dim3(WGRAD_CFGS[C].wm * WGRAD_CFGS[C].wn * 64), 0, s, (const T16*)x, (const T16*)dy, slab, g,
+                         p.pps, dd, xb, db, sg);
+      return;
+    }
+  }
   if constexpr (WGRAD_CFGS[C].bmw == 128) {
     if (p.st) {   // kk-tiles straddling a virtual concat's seam
       hipLaunchKernelGGL((wgrad_kernel_of<T16, C, true>()), dim3(p.mt * p.nt * p.splits),

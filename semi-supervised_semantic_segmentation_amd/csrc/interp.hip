@@ -44,12 +44,13 @@ static Axis make_axis(int64_t in, int64_t out, bool align) {
   return a;
 }
 
-template <typename T>
-__global__ void bilinear_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t N, int64_t C, Axis ah, Axis aw,
+// I: index type of the element decode (int when N*C*Ho*Wo < 2^31: 64-bit divisions cost ~10x the 32-bit ones)
+template <typename T, typename I>
+__global__ void bilinear_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t N_, int64_t C_, Axis ah, Axis aw,
                                     Strides xs, Strides ys, int c_fastest) {
-  const int64_t Ho = ah.out, Wo = aw.out, total = N * C * Ho * Wo;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    int64_t n, c, oh, ow;
+  const I N = (I)N_, C = (I)C_, Ho = ah.out, Wo = aw.out, total = N * C * Ho * Wo;
+  for (I i = (I)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
+    I n, c, oh, ow;
     if (c_fastest) {
       c = i % C; ow = (i / C) % Wo; oh = (i / (C * Wo)) % Ho; n = i / (C * Wo * Ho);
     } else {
@@ -59,13 +60,13 @@ __global__ void bilinear_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, 
     float lh0, lh1, lw0, lw1;
     src_index(ah, (int)oh, h0, h1, lh0, lh1);
     src_index(aw, (int)ow, w0, w1, lw0, lw1);
-    const T* xb = x + n * xs.n + c * xs.c;
+    const T* xb = x + (int64_t)n * xs.n + (int64_t)c * xs.c;
     const float x00 = io<T>::ld(xb, h0 * xs.h + w0 * xs.w), x01 = io<T>::ld(xb, h0 * xs.h + w1 * xs.w);
     const float x10 = io<T>::ld(xb, h1 * xs.h + w0 * xs.w), x11 = io<T>::ld(xb, h1 * xs.h + w1 * xs.w);
     const float t0 = __fadd_rn(__fmul_rn(x00, lw0), __fmul_rn(x01, lw1));
     const float t1 = __fadd_rn(__fmul_rn(x10, lw0), __fmul_rn(x11, lw1));
     const float v = __fadd_rn(__fmul_rn(t0, lh0), __fmul_rn(t1, lh1));
-    io<T>::st(y, n * ys.n + c * ys.c + oh * ys.h + ow * ys.w, v);
+    io<T>::st(y, (int64_t)n * ys.n + (int64_t)c * ys.c + (int64_t)oh * ys.h + (int64_t)ow * ys.w, v);
   }
 }
 
@@ -89,12 +90,12 @@ __device__ __forceinline__ void out_window(const Axis& a, int i, int& lo, int& h
   hi = min((int)ceilf(c1) + 1, a.out - 1);
 }
 
-template <typename T>
-__global__ void bilinear_bwd_kernel(const T* __restrict__ gy, T* __restrict__ gx, int64_t N, int64_t C, Axis ah,
+template <typename T, typename I>
+__global__ void bilinear_bwd_kernel(const T* __restrict__ gy, T* __restrict__ gx, int64_t N_, int64_t C_, Axis ah,
                                     Axis aw, Strides gys, Strides gxs, int c_fastest) {
-  const int64_t H = ah.in, W = aw.in, total = N * C * H * W;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    int64_t n, c, h, w;
+  const I N = (I)N_, C = (I)C_, H = ah.in, W = aw.in, total = N * C * H * W;
+  for (I i = (I)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
+    I n, c, h, w;
     if (c_fastest) {
       c = i % C; w = (i / C) % W; h = (i / (C * W)) % H; n = i / (C * W * H);
     } else {
@@ -103,7 +104,7 @@ __global__ void bilinear_bwd_kernel(const T* __restrict__ gy, T* __restrict__ gx
     int ohlo, ohhi, owlo, owhi;
     out_window(ah, (int)h, ohlo, ohhi);
     out_window(aw, (int)w, owlo, owhi);
-    const T* gb = gy + n * gys.n + c * gys.c;
+    const T* gb = gy + (int64_t)n * gys.n + (int64_t)c * gys.c;
     float acc = 0.f;
     for (int oh = ohlo; oh <= ohhi; ++oh) {
       int h0, h1;
@@ -117,12 +118,105 @@ __global__ void bilinear_bwd_kernel(const T* __restrict__ gy, T* __restrict__ gx
         float m0, m1;
         src_index(aw, ow, w0, w1, m0, m1);
         const float ww = (w0 == w ? m0 : 0.f) + (w1 == w ? m1 : 0.f);
-        if (ww != 0.f) row = fmaf(io<T>::ld(gb, oh * gys.h + ow * gys.w), ww, row);
+        if (ww != 0.f) row = fmaf(io<T>::ld(gb, (int64_t)oh * gys.h + (int64_t)ow * gys.w), ww, row);
       }
       acc = fmaf(row, wh, acc);
     }
-    io<T>::st(gx, n * gxs.n + c * gxs.c + h * gxs.h + w * gxs.w, acc);
+    io<T>::st(gx, (int64_t)n * gxs.n + (int64_t)c * gxs.c + (int64_t)h * gxs.h + (int64_t)w * gxs.w, acc);
   }
+}
+
+// 16-bit NHWC activations (the HRNet / UNet feature maps: channels fastest, C % 8 == 0, 16-byte aligned rows): one
+// thread per (pixel, 8-channel chunk), blockIdx.y = output row, blockIdx.z = image -- no per-element index decode,
+// 16-byte loads and stores.  Per channel the arithmetic is the generic kernels' (same roundings, same order), so
+// the results are bit-identical to them.
+template <typename T>
+__device__ __forceinline__ uint4 pack8(const float (&v)[8]) {
+  T o[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) io<T>::st(o, e, v[e]);
+  return *(const uint4*)o;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bilinear_fwd_nhwc_kernel(const T* __restrict__ x, T* __restrict__ y, int C8,
+                                                                Axis ah, Axis aw, Strides xs, Strides ys) {
+  const int oh = blockIdx.y, n = blockIdx.z;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= aw.out * C8) return;
+  const int ow = idx / C8, c = (idx - ow * C8) * 8;
+  int h0, h1, w0, w1;
+  float lh0, lh1, lw0, lw1;
+  src_index(ah, oh, h0, h1, lh0, lh1);
+  src_index(aw, ow, w0, w1, lw0, lw1);
+  const T* xb = x + (int64_t)n * xs.n + c;
+  const typename Chunk<T, 8>::raw q00 = Chunk<T, 8>::ld(xb + (int64_t)h0 * xs.h + (int64_t)w0 * xs.w),
+                                  q01 = Chunk<T, 8>::ld(xb + (int64_t)h0 * xs.h + (int64_t)w1 * xs.w),
+                                  q10 = Chunk<T, 8>::ld(xb + (int64_t)h1 * xs.h + (int64_t)w0 * xs.w),
+                                  q11 = Chunk<T, 8>::ld(xb + (int64_t)h1 * xs.h + (int64_t)w1 * xs.w);
+  float a00[8], a01[8], a10[8], a11[8], v[8];
+  Chunk<T, 8>::cvt(q00, a00);
+  Chunk<T, 8>::cvt(q01, a01);
+  Chunk<T, 8>::cvt(q10, a10);
+  Chunk<T, 8>::cvt(q11, a11);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float t0 = __fadd_rn(__fmul_rn(a00[e], lw0), __fmul_rn(a01[e], lw1));
+    const float t1 = __fadd_rn(__fmul_rn(a10[e], lw0), __fmul_rn(a11[e], lw1));
+    v[e] = __fadd_rn(__fmul_rn(t0, lh0), __fmul_rn(t1, lh1));
+  }
+  *(uint4*)(y + (int64_t)n * ys.n + (int64_t)oh * ys.h + (int64_t)ow * ys.w + c) = pack8<T>(v);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bilinear_bwd_nhwc_kernel(const T* __restrict__ gy, T* __restrict__ gx, int C8,
+                                                                Axis ah, Axis aw, Strides gys, Strides gxs) {
+  const int h = blockIdx.y, n = blockIdx.z;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= aw.in * C8) return;
+  const int w = idx / C8, c = (idx - w * C8) * 8;
+  int ohlo, ohhi, owlo, owhi;
+  out_window(ah, h, ohlo, ohhi);
+  out_window(aw, w, owlo, owhi);
+  const T* gb = gy + (int64_t)n * gys.n + c;
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  for (int oh = ohlo; oh <= ohhi; ++oh) {
+    int h0, h1;
+    float l0, l1;
+    src_index(ah, oh, h0, h1, l0, l1);
+    const float wh = (h0 == h ? l0 : 0.f) + (h1 == h ? l1 : 0.f);
+    if (wh == 0.f) continue;
+    float row[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) row[e] = 0.f;
+    for (int ow = owlo; ow <= owhi; ++ow) {
+      int w0, w1;
+      float m0, m1;
+      src_index(aw, ow, w0, w1, m0, m1);
+      const float ww = (w0 == w ? m0 : 0.f) + (w1 == w ? m1 : 0.f);
+      if (ww != 0.f) {
+        float g[8];
+        Chunk<T, 8>::cvt(Chunk<T, 8>::ld(gb + (int64_t)oh * gys.h + (int64_t)ow * gys.w), g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) row[e] = fmaf(g[e], ww, row[e]);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = fmaf(row[e], wh, acc[e]);
+  }
+  *(uint4*)(gx + (int64_t)n * gxs.n + (int64_t)h * gxs.h + (int64_t)w * gxs.w + c) = pack8<T>(acc);
+}
+
+// the NHWC kernels apply: 16-bit, channels fastest in both tensors, 16-byte aligned chunks, grid dims in range
+static bool nhwc_ok(const void* a, const void* b, int64_t N, int64_t C, int64_t rows, int64_t cols, const Strides& as,
+                    const Strides& bs, int dt) {
+  if (dt != SSSEG_BF16 && dt != SSSEG_F16) return false;
+  if (as.c != 1 || bs.c != 1 || C % 8 || C < 8) return false;
+  if (((uintptr_t)a | (uintptr_t)b) % 16) return false;
+  if ((as.n | as.h | as.w | bs.n | bs.h | bs.w) % 8) return false;
+  return N <= 65535 && rows <= 65535 && cols * (C / 8) < 0x7fffffffLL;
 }
 
 static Strides to_strides(const int64_t* s) { return Strides{s[0], s[1], s[2], s[3]}; }
@@ -139,15 +233,33 @@ extern "C" int ssseg_bilinear_fwd(const void* x, void* y, int64_t N, int64_t C, 
   const Strides xs = to_strides(xs4), ys = to_strides(ys4);
   const int cf = ys.c == 1 && C > 1;
   hipStream_t s = (hipStream_t)stream;
+  if (nhwc_ok(x, y, N, C, Ho, Wo, xs, ys, dt)) {
+    const int C8 = (int)(C / 8);
+    const dim3 g((unsigned)((Wo * C8 + 255) / 256), (unsigned)Ho, (unsigned)N), b(256);
+    if (dt == SSSEG_BF16)
+      hipLaunchKernelGGL(bilinear_fwd_nhwc_kernel<bf16_t>, g, b, 0, s, (const bf16_t*)x, (bf16_t*)y, C8, ah, aw, xs, ys);
+    else
+      hipLaunchKernelGGL(bilinear_fwd_nhwc_kernel<f16_t>, g, b, 0, s, (const f16_t*)x, (f16_t*)y, C8, ah, aw, xs, ys);
+    SSSEG_LAUNCH_CHECK();
+    return 0;
+  }
   const dim3 g(ssseg_grid(total, 256, 256 * 32)), b(256);
-  if (dt == SSSEG_F32)
-    hipLaunchKernelGGL(bilinear_fwd_kernel<float>, g, b, 0, s, (const float*)x, (float*)y, N, C, ah, aw, xs, ys, cf);
-  else if (dt == SSSEG_BF16)
-    hipLaunchKernelGGL(bilinear_fwd_kernel<bf16_t>, g, b, 0, s, (const bf16_t*)x, (bf16_t*)y, N, C, ah, aw, xs, ys, cf);
-  else if (dt == SSSEG_F16)
-    hipLaunchKernelGGL(bilinear_fwd_kernel<f16_t>, g, b, 0, s, (const f16_t*)x, (f16_t*)y, N, C, ah, aw, xs, ys, cf);
-  else
+  const bool i32 = total < 0x7fffffffLL - (1LL << 24);   // i + grid stride stays in int range
+#define BIL_FWD(T)                                                                                                   \
+  if (i32)                                                                                                           \
+    hipLaunchKernelGGL((bilinear_fwd_kernel<T, int>), g, b, 0, s, (const T*)x, (T*)y, N, C, ah, aw, xs, ys, cf);     \
+  else                                                                                                               \
+    hipLaunchKernelGGL((bilinear_fwd_kernel<T, int64_t>), g, b, 0, s, (const T*)x, (T*)y, N, C, ah, aw, xs, ys, cf);
+  if (dt == SSSEG_F32) {
+    BIL_FWD(float)
+  } else if (dt == SSSEG_BF16) {
+    BIL_FWD(bf16_t)
+  } else if (dt == SSSEG_F16) {
+    BIL_FWD(f16_t)
+  } else {
     return SSSEG_EUNSUPPORTED;
+  }
+#undef BIL_FWD
   SSSEG_LAUNCH_CHECK();
   return 0;
 }
@@ -162,17 +274,35 @@ extern "C" int ssseg_bilinear_bwd(const void* gy, void* gx, int64_t N, int64_t C
   const Strides gys = to_strides(gys4), gxs = to_strides(gxs4);
   const int cf = gxs.c == 1 && C > 1;
   hipStream_t s = (hipStream_t)stream;
+  if (nhwc_ok(gy, gx, N, C, H, W, gys, gxs, dt)) {
+    const int C8 = (int)(C / 8);
+    const dim3 g((unsigned)((W * C8 + 255) / 256), (unsigned)H, (unsigned)N), b(256);
+    if (dt == SSSEG_BF16)
+      hipLaunchKernelGGL(bilinear_bwd_nhwc_kernel<bf16_t>, g, b, 0, s, (const bf16_t*)gy, (bf16_t*)gx, C8, ah, aw, gys,
+                         gxs);
+    else
+      hipLaunchKernelGGL(bilinear_bwd_nhwc_kernel<f16_t>, g, b, 0, s, (const f16_t*)gy, (f16_t*)gx, C8, ah, aw, gys,
+                         gxs);
+    SSSEG_LAUNCH_CHECK();
+    return 0;
+  }
   const dim3 g(ssseg_grid(total, 256, 256 * 32)), b(256);
-  if (dt == SSSEG_F32)
-    hipLaunchKernelGGL(bilinear_bwd_kernel<float>, g, b, 0, s, (const float*)gy, (float*)gx, N, C, ah, aw, gys, gxs, cf);
-  else if (dt == SSSEG_BF16)
-    hipLaunchKernelGGL(bilinear_bwd_kernel<bf16_t>, g, b, 0, s, (const bf16_t*)gy, (bf16_t*)gx, N, C, ah, aw, gys, gxs,
-                       cf);
-  else if (dt == SSSEG_F16)
-    hipLaunchKernelGGL(bilinear_bwd_kernel<f16_t>, g, b, 0, s, (const f16_t*)gy, (f16_t*)gx, N, C, ah, aw, gys, gxs,
-                       cf);
-  else
+  const bool i32 = total < 0x7fffffffLL - (1LL << 24);   // i + grid stride stays in int range
+#define BIL_BWD(T)                                                                                                     \
+  if (i32)                                                                                                             \
+    hipLaunchKernelGGL((bilinear_bwd_kernel<T, int>), g, b, 0, s, (const T*)gy, (T*)gx, N, C, ah, aw, gys, gxs, cf);   \
+  else                                                                                                                 \
+    hipLaunchKernelGGL((bilinear_bwd_kernel<T, int64_t>), g, b, 0, s, (const T*)gy, (T*)gx, N, C, ah, aw, gys, gxs, cf);
+  if (dt == SSSEG_F32) {
+    BIL_BWD(float)
+  } else if (dt == SSSEG_BF16) {
+    BIL_BWD(bf16_t)
+  } else if (dt == SSSEG_F16) {
+    BIL_BWD(f16_t)
+  } else {
     return SSSEG_EUNSUPPORTED;
+  }
+#undef BIL_BWD
   SSSEG_LAUNCH_CHECK();
   return 0;
 }

@@ -327,7 +327,7 @@ def test_conv_variants_bitwise(hip_device, kind, cin, cout, k, H):
 
 
 WGRAD_CASES = [
-    # cin, cout, k, stride, pad, dil, H, W, N   (C % 64 == 0: the LDS-DMA weight-gradient kernel)
+    # cin, cout, k, stride, pad, dil, H, W, N   (the LDS-DMA weight-gradient kernel)
     (64, 64, 3, 1, 1, 1, 37, 29, 2),      # 64-channel kk-tiles, 64-channel co tile, several pixel splits
     (128, 192, 3, 1, 1, 1, 21, 19, 2),    # 128-channel kk-tiles, ragged co tile
     (256, 64, 1, 1, 0, 1, 45, 43, 3),     # 1x1, ragged last split
@@ -335,6 +335,12 @@ WGRAD_CASES = [
     (64, 128, 3, 1, 2, 2, 23, 25, 2),     # dilation 2
     (512, 256, 1, 2, 0, 1, 18, 18, 2),    # strided 1x1 downsample
     (128, 64, 1, 1, 0, 1, 9, 11, 2),      # one split: dW written in its final layout directly
+    # C % 64 != 0: the general-k tiles (a 64-wide kk-tile holds several taps; per-lane tap offsets)
+    (32, 32, 3, 1, 1, 1, 37, 29, 2),      # HRNet-W32 branch
+    (16, 64, 3, 1, 1, 1, 33, 31, 2),      # four taps per kk-tile
+    (96, 64, 3, 2, 1, 1, 30, 28, 2),      # a tap boundary inside the second kk-tile, stride 2
+    (40, 24, 1, 1, 0, 1, 25, 27, 2),      # 1x1, ragged kk-tile
+    (32, 64, 3, 2, 1, 1, 34, 33, 2),      # HRNet-W32 transition (strided)
 ]
 
 

@@ -83,6 +83,28 @@ def test_bilinear_channels_last_bf16(hip_device):
     np.testing.assert_allclose(yb.float().cpu().numpy(), ref.numpy(), rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize('dt', [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize('shape,size,ac', [((2, 32, 16, 16), (64, 64), False), ((3, 24, 13, 11), (26, 22), True),
+                                           ((2, 16, 9, 7), (32, 29), False), ((1, 8, 40, 36), (20, 18), False)])
+def test_bilinear_nhwc_vector_path_bitwise(hip_device, dt, shape, size, ac):
+    """The 16-bit channels-last kernels (one thread per pixel and 8-channel chunk, HRNet / UNet feature maps) do the
+    generic kernels' per-channel arithmetic: forward and backward are bit-identical to the generic path on the
+    same values in NCHW layout (which the generic kernels handle)."""
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(shape, generator=g).to(dt).to(hip_device)
+    gy = torch.randn(shape[:2] + size, generator=g).to(dt).to(hip_device)
+    outs = []
+    for fmt in (torch.channels_last, torch.contiguous_format):
+        xt = x.contiguous(memory_format=fmt).clone().requires_grad_(True)
+        y = ops().interpolate_bilinear(xt, size, align_corners=ac)
+        y.backward(gy.contiguous(memory_format=fmt))
+        outs.append((y.detach().contiguous(), xt.grad.contiguous()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    ref = torch.nn.functional.interpolate(x.float().cpu(), size=size, mode='bilinear', align_corners=ac)
+    np.testing.assert_allclose(outs[0][0].float().cpu().numpy(), ref.numpy(), rtol=2e-2, atol=2e-2)
+
+
 def test_bce_fwd_bwd(hip_device):
     rng = np.random.default_rng(1)
     x = (rng.standard_normal((4, 2, 64, 64)) * 3).astype(np.float32)
