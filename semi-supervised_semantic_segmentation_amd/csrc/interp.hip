@@ -6,6 +6,10 @@
 // the CPU kernel.  Backward is a deterministic gather over the outputs that read each input pixel.
 #include "common.h"
 
+// Built with -ffp-contract=off (Makefile): HIP's __fadd_rn / __fmul_rn are plain operators, contractible into FMAs
+// differently per kernel; the vector and generic kernels must agree bitwise, and PyTorch's CPU kernel rounds every
+// product.
+
 namespace {
 
 struct Strides {
@@ -18,18 +22,20 @@ struct Axis {
   bool align;
 };
 
+// every operation rounded explicitly: no FMA contraction, whose choice may differ between kernels (the vector and
+// the generic kernels must agree bitwise) and which PyTorch's CPU kernel does not do
 __device__ __forceinline__ void src_index(const Axis& a, int d, int& i0, int& i1, float& l0, float& l1) {
   float src;
   if (a.align) {
-    src = a.scale * (float)d;
+    src = __fmul_rn(a.scale, (float)d);
   } else {
-    src = a.scale * ((float)d + 0.5f) - 0.5f;
+    src = __fsub_rn(__fmul_rn(a.scale, __fadd_rn((float)d, 0.5f)), 0.5f);
     src = src < 0.f ? 0.f : src;
   }
   i0 = min((int)src, a.in - 1);
-  l1 = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
+  l1 = fminf(fmaxf(__fsub_rn(src, (float)i0), 0.f), 1.f);
   i1 = i0 + (i0 < a.in - 1 ? 1 : 0);
-  l0 = 1.f - l1;
+  l0 = __fsub_rn(1.f, l1);
 }
 
 static Axis make_axis(int64_t in, int64_t out, bool align) {
