@@ -118,6 +118,7 @@ def run(name, path, dev, threshold=0.5, calibrate=True, layers=False):
         torch.cuda.synchronize()
         times.append(time.time() - t0)
         out.append((float(cls), float(unsup) if unsup is not None else None, float(cm) if cm is not None else None))
+    conv = None
     if layers:   # one more step with HIP events around every conv-engine launch (tools/layer_report.py format)
         sys.path.insert(0, os.path.join(ROOT, 'tools'))
         import layer_report
@@ -128,7 +129,7 @@ def run(name, path, dev, threshold=0.5, calibrate=True, layers=False):
         print(f'== {name} conv layers', file=sys.stderr)
         stdout, sys.stdout = sys.stdout, sys.stderr
         try:
-            layer_report.report(rows, 40)
+            conv = layer_report.report(rows, 40)
         finally:
             sys.stdout = stdout
     params_finite = all(bool(torch.isfinite(p).all()) for p in model.parameters())
@@ -142,6 +143,8 @@ def run(name, path, dev, threshold=0.5, calibrate=True, layers=False):
     tf = STEP_GFLOP_PER_IMAGE[name] * b / step_s / 1e3
     rec['conv_tflops'] = round(tf, 1)
     rec['frac_of_dense_peak'] = round(tf * 1e12 / PEAK[rec['dtype']], 4)
+    if conv:   # the conv engine of the extra probed step: MFMA and bytes rooflines (algorithmic flops / bytes)
+        rec['conv_engine'] = conv
     if 'adversarial' in tc:
         rec['loss_d'] = float(tc['adversarial']['last_loss_d'])
     print(json.dumps(rec), flush=True)

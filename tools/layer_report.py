@@ -95,6 +95,12 @@ def report(rows, top):
     for (kind, tag), (ms, fl, n, by) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:top]:
         print(f'{ms:8.3f} {100 * ms / tot_ms:6.2f} {n:5d} {fl / 1e9:8.1f} {fl / ms / 1e9:7.1f} {by / 1e6:8.1f} '
               f'{by / ms / 1e9:6.2f} {roof[(kind, tag)] / ms:5.2f}  {kind:6s} {tag}')
+    return {'conv_ms': round(tot_ms, 3), 'conv_gflop': round(tot_fl / 1e9, 1), 'conv_tflops': round(tot_fl / tot_ms / 1e9, 1),
+            'conv_alg_GB': round(tot_b / 1e9, 2), 'conv_alg_TBps': round(tot_b / tot_ms / 1e9, 3),
+            'conv_bytes_frac_of_8TBps': round(tot_b / tot_ms / 1e9 / 8.0, 4),
+            'conv_mfma_frac_of_2.5PF': round(tot_fl / tot_ms / 1e9 / 2500.0, 4),
+            'conv_roofline_floor_ms': round(tot_roof, 3), 'conv_floor_frac': round(tot_roof / tot_ms, 3),
+            'conv_calls': len(rows)}
 
 
 if __name__ == '__main__':
