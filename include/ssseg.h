@@ -105,6 +105,51 @@ int ssseg_rotate_bwd(const float* gy, float* gx, int64_t N, int64_t C, int64_t H
                      ssseg_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * Train-time augmentations on the device (reference configs/default_config.py:179-212: the albumentations
+ * ReplayCompose pipelines the reference datasets apply per sample, data/dataset.py:71-74,
+ * unsupervised_dataset.py:20-21).  The host (data/device_augment.py) draws each sample's parameters in the
+ * pipeline's order and uploads one record per sample; images are uint8 NHWC (3 channels) after the host's
+ * LongestMaxSize + PadIfNeeded, masks uint8 NHWC.  albumentations / cv2 are absent: parity with them is unpinned.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct ssseg_aug_warp_params {
+  float a[6];        /* input-image coords = A * q, q = the crop-grid pixel after the distortion (OpenCV centres) */
+  int32_t distort;   /* 0 none, 1 ElasticTransform, 2 GridDistortion, 3 OpticalDistortion */
+  int32_t field;     /* ElasticTransform: index of this sample's displacement field in `fields` */
+  float m[6];        /* ElasticTransform: inverse of its random affine (applied to (x + dx, y + dy)) */
+  float k, cx, cy, fx, fy;   /* OpticalDistortion: radial k (k1 = k2 = k), centre, focal lengths */
+  int32_t border;    /* image / mask border: 0 constant 0, 1 reflect-101 */
+} ssseg_aug_warp_params;
+
+typedef struct ssseg_aug_color_params {
+  int32_t bc;    float alpha, beta;      /* RandomBrightnessContrast: floor(clip(v * alpha + beta * 255)) */
+  int32_t gray;                          /* ToGray */
+  int32_t rgb;   float shift[3];         /* RGBShift: floor(clip(v + shift)) */
+  int32_t hsv;   float hsv_shift[3];     /* HueSaturationValue on 8-bit HSV (H in [0, 180)) */
+  int32_t iso;   float iso_color_std, iso_intensity;   /* ISONoise: hue N(0, color_std), luminance Poisson */
+} ssseg_aug_color_params;
+
+/* One resampling per sample: out pixel (x, y) -> distortion -> A -> bilinear image sample (rounded to the uint8
+ * grid), nearest mask sample.  gmaps: [N][Wo + Ho] GridDistortion axis maps; fields: [nf][Ho][Wo][2] elastic
+ * displacements.  out_nchw01 = 0: out_img NHWC [0, 255] (feeds ssseg_aug_color); 1: NCHW [0, 1] (ToFloat).
+ * out_mask: NCHW [0, 1]; mask may be NULL (unsupervised pipeline). */
+int ssseg_aug_warp(const uint8_t* img, const uint8_t* mask, int64_t mask_c, int64_t N, int64_t H, int64_t W,
+                   float* out_img, float* out_mask, int64_t Ho, int64_t Wo, const ssseg_aug_warp_params* params,
+                   const float* gmaps, const float* fields, int out_nchw01, ssseg_stream_t stream);
+/* Brightness / contrast, gray, RGB shift / HSV on an NHWC [0, 255] float batch, in place. */
+int ssseg_aug_color(float* img, int64_t N, int64_t H, int64_t W, const ssseg_aug_color_params* params,
+                    ssseg_stream_t stream);
+/* Separable Gaussian per sample, in place (tmp: same size): radius[n] (0 = untouched), weights [N][wmax];
+ * sym_border 0 = reflect-101 (cv2), 1 = symmetric (scipy 'reflect'); round_u8_out rounds to the uint8 grid. */
+int ssseg_aug_blur(float* x, float* tmp, int64_t N, int64_t H, int64_t W, int64_t C, const int32_t* radius,
+                   const float* weights, int64_t wmax, int sym_border, int round_u8_out, ssseg_stream_t stream);
+/* ISONoise on the samples with params[n].iso (per-image luminance std from fp64 sums in stats_ws [N][2]), then
+ * ToFloat: out = NCHW [0, 1]. */
+int ssseg_aug_iso_finish(const float* img, float* out, int64_t N, int64_t H, int64_t W,
+                         const ssseg_aug_color_params* params, double* stats_ws, uint64_t seed, ssseg_stream_t stream);
+/* uniform(-1, 1) noise (Philox, key = seed) for the ElasticTransform displacement fields. */
+int ssseg_aug_uniform_field(float* f, int64_t n, uint64_t seed, ssseg_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Losses.  Reductions are two-stage and deterministic; scalars live in device memory.
  * ------------------------------------------------------------------------------------------- */
 size_t ssseg_reduce_workspace_bytes(int64_t n);

@@ -34,6 +34,11 @@ SIGS = {
     'ssseg_cast': (i32, [vp, vp, i64, i32, i32, vp]),
     'ssseg_bilinear_fwd': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, I64P, I64P, i32, i32, vp]),
     'ssseg_bilinear_bwd': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, I64P, I64P, i32, i32, vp]),
+    'ssseg_aug_warp': (i32, [vp, vp, i64, i64, i64, i64, vp, vp, i64, i64, vp, vp, vp, i32, vp]),
+    'ssseg_aug_color': (i32, [vp, i64, i64, i64, vp, vp]),
+    'ssseg_aug_blur': (i32, [vp, vp, i64, i64, i64, i64, vp, vp, i64, i32, i32, vp]),
+    'ssseg_aug_iso_finish': (i32, [vp, vp, i64, i64, i64, vp, vp, u64, vp]),
+    'ssseg_aug_uniform_field': (i32, [vp, i64, u64, vp]),
     'ssseg_rotate_fwd': (i32, [vp, vp, i64, i64, i64, i64, f64, vp]),
     'ssseg_rotate_bwd': (i32, [vp, vp, i64, i64, i64, i64, f64, vp]),
     'ssseg_reduce_workspace_bytes': (sz, [i64]),
