@@ -499,7 +499,7 @@ __global__ void __launch_bounds__(256) bn_eval_bwd_kernel(const T* __restrict__ 
     red[0][t][e] = s1[e];
     red[1][t][e] = s2[e];
   }
-  __syncthreads();
+  lds_barrier();   // the dconv / dres stores keep draining
   for (int idx = t; idx < L.cpb * V; idx += 256) {
     const int ch = idx / V, e = idx % V;
     const int c = (blockIdx.y * L.cpb + ch) * V + e;

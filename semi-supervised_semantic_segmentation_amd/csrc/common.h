@@ -38,6 +38,12 @@ __device__ __forceinline__ bf16_t f32_to_bf16(float f) {
 typedef _Float16 f16_t;
 typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
 
+// workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its global stores.
+// __syncthreads() (release fence) also drains vmcnt, i.e. every store the wave issued before it: in an epilogue
+// that stores its tile and then reduces statistics through LDS that is ~2 us of HBM write latency per tile,
+// serialised (+60 % on the conv 1x1 expansions' fused-statistics launches).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 template <typename T> struct io;
 template <> struct io<float> {
   __device__ __forceinline__ static float ld(const float* p, int64_t i) { return p[i]; }

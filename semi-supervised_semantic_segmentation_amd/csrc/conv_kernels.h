@@ -218,7 +218,7 @@ __device__ __forceinline__ void tile_stats(SA (&s1)[V], SA (&s2)[V], int lstride
       s2[e] += __shfl_xor(s2[e], o, 64);
     }
   }
-  __syncthreads();   // LDS free (the caller's last LDS reads are done)
+  lds_barrier();   // LDS free (the caller's last LDS reads are done); the y stores keep draining
   double* red = (double*)smem;   // [NW][BN][2]
   const int w = threadIdx.x >> 6;
   if (holder)
@@ -227,7 +227,7 @@ __device__ __forceinline__ void tile_stats(SA (&s1)[V], SA (&s2)[V], int lstride
       red[(w * BN + cofs + e) * 2] = (double)s1[e];
       red[(w * BN + cofs + e) * 2 + 1] = (double)s2[e];
     }
-  __syncthreads();
+  lds_barrier();
   for (int c = threadIdx.x; c < BN; c += NW * 64) {
     const int n = n0 + c;
     if (n >= sld) continue;
@@ -562,10 +562,10 @@ __device__ __forceinline__ void frag_stats(double (&st1)[FN][4], double (&st2)[F
         st1[i][e] += __shfl_xor(st1[i][e], o, 64);
         st2[i][e] += __shfl_xor(st2[i][e], o, 64);
       }
-  __syncthreads();
+  lds_barrier();
   double* red = (double*)smem;   // [NW][BN][2], zero where a wave holds no channel
   for (int k = threadIdx.x; k < NW * BN * 2; k += NW * 64) red[k] = 0.0;
-  __syncthreads();
+  lds_barrier();
   const int w = threadIdx.x >> 6;
   if ((lane & 15) == 0)
 #pragma unroll
@@ -576,7 +576,7 @@ __device__ __forceinline__ void frag_stats(double (&st1)[FN][4], double (&st2)[F
         red[(w * BN + c) * 2] = st1[i][e];
         red[(w * BN + c) * 2 + 1] = st2[i][e];
       }
-  __syncthreads();
+  lds_barrier();
   for (int c = threadIdx.x; c < BN; c += NW * 64) {
     const int n = n0 + c;
     if (n >= sld) continue;

@@ -23,6 +23,9 @@ def main():
     ap.add_argument('layers', nargs='+', help='cin,cout,k,hw')
     ap.add_argument('--batch', type=int, default=16)
     ap.add_argument('--reps', type=int, default=20)
+    ap.add_argument('--tune', action='store_true',
+                    help='print the autotuner\'s own per-config event timings (SSSEG_TUNE_LOG=1 must be set) for the plain '
+                         'and the statistics launch of each layer instead of the Python-timed loop')
     a = ap.parse_args()
     dev = torch.device('cuda')
     snn.set_compute_dtype(torch.bfloat16)
@@ -31,6 +34,14 @@ def main():
         conv = snn.Conv2d(cin, cout, k, 1, k // 2, bias=False).to(dev)
         x = snn.to_act(torch.randn(a.batch, cin, hw, hw, device=dev))
         cap = conv.stat_rows_cap(a.batch, hw, hw)
+        if a.tune:
+            for st in (False, True):
+                N.lib().ssseg_set_knob(6, 1)   # clear the variant cache: the next launch tunes (and logs)
+                print(f'{cin}->{cout} k{k} @{a.batch}x{hw}^2 stats={st}', file=sys.stderr, flush=True)
+                with torch.no_grad():
+                    conv._ssseg_forward(x, False, stats=snn.StatRows(cout, cap, dev) if st else None)
+                torch.cuda.synchronize()
+            continue
         line = []
         for v in CFGS:
             N.lib().ssseg_set_knob(4, v)
