@@ -429,6 +429,15 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
   constexpr int RPP = NT / CPR, NP = (BM + RPP - 1) / RPP;   // rows per pass, passes
   const int ch = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
   const int n = n0 + ch * 8;
+  // STATS: the fused BatchNorm statistics are summed in the store pass itself, from the values it stores (the conv
+  // feeding a training BatchNorm has no scale / residual / activation in its epilogue -- host contract -- so that
+  // is acc + shift).  Per-thread sums over <= BM / RPP rows in the accumulator type SA (fp32 for bf16 outputs:
+  // exact products of 8-bit mantissas, <= 32 terms), fp64 across threads and tiles.  (A second pass over the staged
+  // tile after the stores cost ~1.9 us per tile: 50 -> 80 us on the 64->256 1x1 @16x128^2 forward.)
+  using SA = typename std::conditional<sizeof(TO) == 2, float, double>::type;
+  SA s1[STATS ? 8 : 1], s2[STATS ? 8 : 1];
+#pragma unroll
+  for (int e = 0; e < (STATS ? 8 : 1); ++e) s1[e] = s2[e] = (SA)0;
   if (n < g.K) {
     const bool vec = (g.ldy & 7) == 0 && (!ep.res || (ep.ldr & 7) == 0);
     const bool full = vec && n + 7 < g.K;
@@ -499,6 +508,14 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
         for (int e = 0; e < 8; ++e) v[e] = raw[e] * sc[e] + sh[e] + r[p][e];   // scale 1 / shift 0 when absent
         act8(v, ep.relu, ep.slope);
       }
+      if constexpr (STATS) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const SA q = n + e < g.K ? (SA)stored<TO>(v[e]) : (SA)0;
+          s1[e] += q;
+          s2[e] += q * q;
+        }
+      }
       const long long o = op[p] * g.ldy + n;
       TO* yp = out_at(ep, y, g.ldy, op[p], n);   // (a split output has no aux: host contract)
       if (full) {
@@ -514,36 +531,8 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
       }
     }
   }
-  if constexpr (STATS) {
-    // a second pass over the staged tile (registers of the store pass are dead by then): the conv feeding a
-    // training BatchNorm has no scale / residual / activation in its epilogue (host contract), so the stored
-    // value is acc + shift.  Per-thread sums over <= BM / RPP rows in the accumulator type SA (fp32 for bf16
-    // outputs: exact products of 8-bit mantissas, <= 32 terms), fp64 across threads and tiles.
-    using SA = typename std::conditional<sizeof(TO) == 2, float, double>::type;
-    SA s1[8], s2[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s1[e] = s2[e] = (SA)0;
-    if (n < g.K) {
-      float sh[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) sh[e] = (ep.shift && n + e < g.K) ? ep.shift[n + e] : 0.f;
-#pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        const int row = r0 + p * RPP;
-        if (row >= BM || m0 + row >= g.M) continue;
-        const float* a = (const float*)(smem + row * LDR + ch * 32);
-        const float4 a0 = *(const float4*)a, a1 = *(const float4*)(a + 4);
-        const float raw[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const SA q = n + e < g.K ? (SA)stored<TO>(raw[e] + sh[e]) : (SA)0;
-          s1[e] += q;
-          s2[e] += q * q;
-        }
-      }
-    }
+  if constexpr (STATS)
     tile_stats<8, BN, NT / 64, SA>(s1, s2, CPR, (threadIdx.x & 63) < CPR, ch * 8, smem, m0 / BM, n0, ep.stats, ep.sld);
-  }
 }
 
 // fused statistics after store_tile (register epilogue): lane holds fp64 sums of fragment column i's 4
