@@ -1,7 +1,82 @@
-"""ModelWrapper (reference ModelWrapper.py:5-53) is truncated at `result =` in the reference (a
-SyntaxError), so its intended output is unknown; inference wrappers are outside the training hot path
-(SURVEY §8f rank 4).  The class is kept as a named placeholder that fails loudly."""
+"""ResizeWrapper — drop-in for reference ModelWrapper.py:5-53, on the device kernels.
+
+The reference forward (ModelWrapper.py:12-51) resizes the image so its longer side is `larger_side_size`
+(bilinear, align_corners=False), then pads the shorter side with zeros up to the smallest size class of
+[256, 512, 1024, 2048] strictly larger than the resized shorter side, floor(diff / 2) before and ceil(diff / 2)
+after.  The reference file ends at `result =` (line 53, a SyntaxError); this build completes it as
+`return self.model(input)`, the only reading under which the wrapper is a model wrapper.
+
+Where the reference as written cannot run or contradicts its own plan, the evident intent is taken (each checked by
+tests/test_resize_wrapper.py against oracle/resize_ref.py, which restates the same plan in torch-CPU):
+  * `torch.max(input.size()[2:4])` (line 13) raises on a torch.Size: the Python max of (H, W) is used;
+  * F.interpolate rejects the float target size of line 16-23: the resized shorter side is int(smaller * ratio)
+    (truncation, as int() of a positive float);
+  * `diff` (line 31) is measured on dim 2 whatever the orientation, which for a portrait input (H > W) pads the
+    WIDTH by (class - H) -- a negative pad, i.e. a crop, whenever the class is below the long side: the pad is
+    measured on the resized shorter side, the dimension lines 39-48 actually pad.
+
+Device path: one ssseg_zero of the padded batch + one ssseg_bilinear_fwd written straight into its interior (the
+kernel takes output strides), then the wrapped model.  Differentiable (ssseg_bilinear_bwd from the interior view).
+"""
+import torch
 import torch.nn as nn
+
+from ssseg import native as N
+
+SIZES = (256, 512, 1024, 2048)   # ModelWrapper.py:10
+
+
+def resize_plan(H, W, larger_side_size=1024, sizes=SIZES):
+    """(resized H, resized W, pad_left, pad_right, pad_top, pad_bottom) of ModelWrapper.py:12-51 (see the module
+    docstring for the three readings taken where the reference cannot run)."""
+    H, W = int(H), int(W)
+    larger = max(H, W)                                   # :13
+    ratio = float(larger_side_size) / larger             # :14
+    smaller_tgt = min(H, W) * ratio                      # :15-16
+    if H > W:                                            # :20-23
+        th, tw = int(larger_side_size), int(smaller_tgt)
+    else:
+        th, tw = int(smaller_tgt), int(larger_side_size)
+    valid = [s for s in sizes if s > smaller_tgt]        # :27-29
+    if not valid:
+        raise ValueError(f'ResizeWrapper: resized shorter side {smaller_tgt} has no size class above it in {sizes}')
+    cls = min(valid)
+    if H > W:                                            # :39-48: pad the shorter (width) side
+        diff = cls - tw
+        return th, tw, diff // 2, diff - diff // 2, 0, 0
+    diff = cls - th
+    return th, tw, 0, 0, diff // 2, diff - diff // 2
+
+
+class _ResizePad(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, plan):
+        th, tw, pl, pr, pt, pb = plan
+        Nn, C, H, W = x.shape
+        xc = x if x.is_contiguous() else x.contiguous()
+        y = torch.empty((Nn, C, th + pt + pb, tw + pl + pr), device=x.device, dtype=x.dtype)
+        N.call('ssseg_zero', N.dev_ptr(y), y.numel() * y.element_size(), N.stream())
+        inner = y[:, :, pt:pt + th, pl:pl + tw]
+        N.call('ssseg_bilinear_fwd', N.dev_ptr(xc, 'x'), N.dev_ptr(inner), Nn, C, H, W, th, tw, N.strides4(xc),
+               N.strides4(inner), 0, N.dt_code(xc), N.stream())
+        ctx.meta = (Nn, C, H, W, plan)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        Nn, C, H, W, (th, tw, pl, pr, pt, pb) = ctx.meta
+        inner = gy[:, :, pt:pt + th, pl:pl + tw]
+        gx = torch.empty((Nn, C, H, W), device=gy.device, dtype=gy.dtype)
+        N.call('ssseg_bilinear_bwd', N.dev_ptr(inner, 'gy'), N.dev_ptr(gx), Nn, C, H, W, th, tw, N.strides4(inner),
+               N.strides4(gx), 0, N.dt_code(gy), N.stream())
+        return gx, None
+
+
+def resize_pad(x, larger_side_size=1024, sizes=SIZES):
+    """The resized + padded model input of ModelWrapper.py:12-51 (NCHW float image batch on the device)."""
+    if x.dim() != 4:
+        raise ValueError(f'ResizeWrapper: expects an NCHW batch, got {tuple(x.shape)}')
+    return _ResizePad.apply(x, resize_plan(x.shape[2], x.shape[3], larger_side_size, sizes))
 
 
 class ResizeWrapper(nn.Module):
@@ -9,6 +84,8 @@ class ResizeWrapper(nn.Module):
         super().__init__()
         self.model = model
         self.larger_side_size = larger_side_size
+        self.sizes = torch.tensor(SIZES)
 
-    def forward(self, input):
-        raise NotImplementedError('ResizeWrapper: the reference implementation is truncated (ModelWrapper.py:53)')
+    def forward(self, input: torch.Tensor):
+        sizes = tuple(int(s) for s in self.sizes.tolist())
+        return self.model(resize_pad(input, self.larger_side_size, sizes))

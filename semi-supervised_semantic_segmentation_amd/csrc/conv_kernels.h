@@ -817,6 +817,14 @@ __device__ __forceinline__ void vmcnt_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// wait until the ring's oldest tile landed when `ahead` (<= D - 1) later tiles of NL vmcnt units each may stay in flight
+template <int NL, int D>
+__device__ __forceinline__ void ring_wait(int ahead) {
+  if (D >= 3 && ahead >= 2) vmcnt_wait<2 * NL>();
+  else if (D >= 2 && ahead >= 1) vmcnt_wait<NL>();
+  else vmcnt_wait<0>();
+}
+
 constexpr unsigned OOB = 0x80000000u;   // > any num_records we build: the load returns zeros
 
 // KM (k mode): 0 = 64-channel k-tiles (C % 64 == 0, channel block major, tap minor: the tile's tap and channel block

@@ -481,11 +481,11 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const T16* __r
   for (int p = 0; p < D; ++p)
     if (p < nk) issue(p);
   for (int kt = 0; kt < nk; ++kt) {
-    // tile kt landed; the tiles issued after it (at most D - 1) may stay in flight
+    // tile kt landed; the tiles issued after it (at most D - 1) may stay in flight.  An ST block whose kk-tile lies
+    // wholly in one part of the concat (C > 128, e.g. [64 | 192]) issues each x piece once: XI + DI units per stage
     const int ahead = min(nk - 1, kt + D - 1) - kt;
-    if (D >= 3 && ahead >= 2) vmcnt_wait<2 * NL>();
-    else if (D >= 2 && ahead >= 1) vmcnt_wait<NL>();
-    else vmcnt_wait<0>();
+    if (ST && !strad) ring_wait<XI + DI, D>(ahead);
+    else ring_wait<NL, D>(ahead);
     __builtin_amdgcn_s_barrier();                  // every wave's tile kt landed; slot (kt+D)%NS is free
     if (kt + D < nk) issue((kt + D) % NS);
     compute(kt % NS);

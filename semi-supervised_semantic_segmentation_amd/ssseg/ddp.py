@@ -30,12 +30,26 @@ import torch.nn as nn
 
 from . import arena as _arena
 
+_FORCE = {'on': False}
+
+
+def force_collectives(on):
+    """TEST ONLY: run the reducer's bucketed all-reduces and SyncBN's statistic all-reduces even at world size 1, so a
+    one-GPU box executes the RCCL code path (ReduceOp.AVG, the side-stream launch and its event join, the fp64
+    SyncBN sums) whose results must then equal the non-distributed step bit for bit."""
+    _FORCE['on'] = bool(on)
+
+
+def forced():
+    return _FORCE['on'] and dist.is_available() and dist.is_initialized()
+
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module, device_ids=None, find_unused_parameters=False, bucket_cap_mb=25, broadcast_buffers=True):
         super().__init__()
         self.module = module
         self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self._active = self.world > 1 or forced()   # reduce at all (world 1 only under force_collectives)
         self.arena = _arena.attach(module)
         a = self.arena
         if self.world > 1:
@@ -57,9 +71,9 @@ class DistributedDataParallel(nn.Module):
         for i, (_, _, ps) in enumerate(self.buckets):
             for p in ps:
                 self._bucket_of[id(p)] = i
-                if self.world > 1:
+                if self._active:
                     p._ssseg_reducer = self
-        self._avg = self.world > 1 and dist.get_backend() == 'nccl'
+        self._avg = self._active and dist.get_backend() == 'nccl'
         self._expected = None         # per-param contributions of an armed backward (learned on the first)
         self._learning = True
         self._overlap = os.environ.get('SSSEG_DDP_OVERLAP', '1') != '0'   # 0: every bucket in finish() (A/B)
@@ -67,7 +81,7 @@ class DistributedDataParallel(nn.Module):
         self.last_early = 0
         self._launched = None
         self._works = []
-        self._stream = torch.cuda.Stream() if (self.world > 1 and a.data.is_cuda) else None
+        self._stream = torch.cuda.Stream() if (self._active and a.data.is_cuda) else None
 
     def forward(self, *args, **kwargs):
         return self.module(*args, **kwargs)
@@ -75,7 +89,7 @@ class DistributedDataParallel(nn.Module):
     # -- reducer protocol --------------------------------------------------------------------------
     def arm(self):
         """The next backward pass is the last one of this step: reduce buckets as they complete."""
-        self._armed = self.world > 1
+        self._armed = self._active
         self._launched = [False] * len(self.buckets)
         self._works = []
         self._seen = {}

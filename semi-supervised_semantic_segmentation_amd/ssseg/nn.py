@@ -1038,8 +1038,10 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
 # batch norm (+ReLU, +residual)
 # ------------------------------------------------------------------------------------------------
 def _sync_group(training):
-    return (training and _CFG['sync_bn'] and dist.is_available() and dist.is_initialized()
-            and dist.get_world_size() > 1)
+    if not (training and _CFG['sync_bn'] and dist.is_available() and dist.is_initialized()):
+        return False
+    from .ddp import forced
+    return dist.get_world_size() > 1 or forced()
 
 
 def _pad16(C, dtype):
@@ -1335,11 +1337,14 @@ class VirtualCat:
     """The two parts of a virtual channel concat (cat_crop(lazy=True)): the consuming conv's kernels read channels
     [0, ca) from a and [ca, ca + cb) from b where they lie (ssseg_vcat); the concat tensor itself is allocated but
     not written unless materialize() runs (a consumer that cannot read it part by part)."""
-    __slots__ = ('a', 'b', 'ca', 'cb', '_d2', 'grads', 'mask_a')
+    __slots__ = ('a', 'b', 'ca', 'cb', '_d2', 'grads', 'mask_a', 'versions')
 
     def __init__(self, a, b, ca, cb):
         self.a, self.b, self.ca, self.cb = a, b, ca, cb
         self._d2 = None
+        # the parts are held here, not by save_for_backward: autograd's version check cannot see an in-place change
+        # to them between the forward and the consumer's backward, so the backward checks these itself
+        self.versions = (a._version, b._version)
         self.grads = None   # (da, db) from the consumer's split-output dgrad, taken by the concat's backward
         # a is the output of a fused conv+ReLU (the UpBlock upsampler): da can be written with that ReLU's
         # backward already applied (ssseg_conv_igemm_epi_vsplit's mask), which removes its ssseg_act_bwd pass
@@ -1363,12 +1368,19 @@ class VirtualCat:
     def same_split(self, other):
         return self.ca == other.ca and self.b.shape[1] == other.b.shape[1]
 
+    def check_versions(self):
+        if (self.a._version, self.b._version) != self.versions:
+            raise RuntimeError('ssseg: a part of a virtual concat was modified in place between its consumer\'s '
+                               'forward and backward (the gradient would be computed from the modified values)')
+
 
 def _vcat_of(x):
     return x.__dict__.get('_ssseg_vcat') if isinstance(x, torch.Tensor) else None
 
 
 def _vcat_restore(x, vc):
+    if vc is not None:
+        vc.check_versions()
     if vc is not None and '_ssseg_vcat' not in x.__dict__ and not getattr(x, '_ssseg_materialized', False):
         x.__dict__['_ssseg_vcat'] = vc
 
@@ -1417,6 +1429,11 @@ class _CatFn(torch.autograd.Function):
         split = ctx.vc.grads if ctx.vc is not None else None   # the consumer wrote the parts' gradients itself
         if split is not None:
             ctx.vc.grads = None
+            if any(st != 0 for st in gy.stride()):
+                # the consumer returned the never-written placeholder (all strides 0) as its input gradient: any
+                # other gradient summed into it by autograd means a second consumer, whose contribution is lost
+                raise RuntimeError('ssseg: a virtual concat (cat_crop(lazy=True)) has more than one consumer; '
+                                   'use cat_crop(lazy=False) where the concat is read twice')
         for k, (sh, c, c0, (oy, ox), j) in enumerate(((ash, ca, 0, offs[0], ctx.joins[0]),
                                                         (bsh, cb, ca, offs[1], ctx.joins[1]))):
             if split is not None:

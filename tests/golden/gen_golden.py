@@ -22,8 +22,12 @@ Fixture index:
   G6b model2_*.npz      HarDNet / Discriminator / MultiscaleFeatureDiscriminator / MultiscaleAttention(HRNet)
                         forwards (eval + train), input + selected parameter gradients, BN buffers; weights are
                         seeded (tests/seeded.py) and pinned by a state_dict SHA-256 instead of stored
+  G11 msa_trainsteps.npz 2 steps of train.train on MultiscaleAttention(HigherHRNet-W32, 480, 2) at 128^2, bs 2 (config
+                        C4's model family; DDP gloo world 1), fp32 and fp64; parameters / BN buffers after the steps
+                        as seeded index samples                            (reference/train.py:41-130,
+                        models/multiscale_attention.py:38-58)
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py [all | models2 | metrics]
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py [all | models2 | metrics | msa_trainsteps]
 """
 import os
 import sys
@@ -440,6 +444,79 @@ def gen_models2():
 
 
 # ----------------------------------------------------------------------------------------------
+# G11: two reference train steps of config C4's model family (MultiscaleAttention over HigherHRNet-W32, 480 feature
+# channels, 2 scales) at 128x128, bs 2, DDP on gloo world 1, fp32 and fp64
+# ----------------------------------------------------------------------------------------------
+def _sample_idx(n, i, k=256):
+    g = torch.Generator().manual_seed(7000 + i)
+    return torch.sort(torch.randperm(n, generator=g)[:k]).values
+
+
+def gen_msa_trainsteps():
+    """The student's parameters and BN buffers after 2 steps are stored as seeded index samples (256 elements per
+    tensor, _sample_idx; the whole network is 29 M parameters); the fp64 run is the same reference code on a
+    .double() copy with the CowMix draws taken in fp32 (the noise draw otherwise consumes the generator differently
+    in fp64, giving a different mask) -- the fp32 rounding yardstick of tests/parity.py."""
+    ensure_pg()
+    sys.path.insert(0, os.path.dirname(OUT))      # tests/ (seeded.py)
+    import copy
+    import seeded
+    _yacs_shim()
+    from functools import partial
+    from models import higher_hrnet, multiscale_attention
+    seed = 64
+    torch.manual_seed(seed)
+    m = multiscale_attention.MultiscaleAttention(
+        partial(higher_hrnet.get_pose_net, cfg=higher_hrnet.POSE_HIGHER_RESOLUTION_NET), 480, 2)
+    seeded.perturb(m, seed + 1000, 'he')
+    sha = seeded.state_sha(m)
+    g = torch.Generator().manual_seed(seed + 3000)
+    B, H, steps = 2, 128, 2
+    imgs = torch.rand(steps, B, 3, H, H, generator=g)
+    fg = (torch.rand(steps, B, 1, H, H, generator=g) > 0.5).float()
+    masks = torch.cat([1 - fg, fg], dim=2)
+    unl = torch.rand(2 * steps, B, 3, H, H, generator=g)
+    cfg = {'train': dict(loss=losses.CalculateLoss([
+        {'loss_fn': losses.DenseBinaryCrossEntropyLossWithLogits(reduction='mean'), 'weight': [0.5]}]),
+        virtual_batch_size_multiplier=1, use_semi_supervised=True,
+        mask_proportion_range=(0.45, 0.55), sigma_range=(4, 8), confidence_threshold=0.5,
+        consistency_loss_weight=10, ema_model_alpha=0.99, print_freq=1, gradient_clip_value=5.0)}
+    init = m.state_dict()
+    d = dict(seed=seed, sha=np.asarray(sha), rng_seed=seed + 4000, lr=0.01, imgs_sha=np.asarray(sha_of(imgs)),
+             masks_sha=np.asarray(sha_of(masks)), unl_sha=np.asarray(sha_of(unl)))
+    orig_cm = cowmix.generate_cowmix_masks_like
+    for dt, suf in ((torch.float32, ''), (torch.float64, '64')):
+        student = copy.deepcopy(m).to(dt)
+        teacher = copy.deepcopy(m).to(dt)
+        ddp = torch.nn.parallel.DistributedDataParallel(student)
+        mean_teacher.detach_model_parameters(teacher)
+        teacher.eval()
+        opt = torch.optim.SGD(ddp.parameters(), lr=0.01, momentum=0.9, weight_decay=0.0005)
+        cowmix.generate_cowmix_masks_like = (lambda t, **kw: orig_cm(t.float(), **kw).to(t.dtype))
+        log = ScalarLog()
+        torch.manual_seed(seed + 4000)
+        try:
+            ref_train.train(ddp, teacher, opt, [{'image': imgs[i].to(dt), 'semantic_mask': masks[i].to(dt)}
+                                                for i in range(steps)],
+                            iter([{'image': unl[i].to(dt)} for i in range(2 * steps)]), 30, 0, log, cfg, 'cpu')
+        finally:
+            cowmix.generate_cowmix_masks_like = orig_cm
+        d['sup_loss' + suf] = np.array([v for n, v, _ in log.rows if n == 'train_classification_loss'][:steps])
+        d['unsup_loss' + suf] = np.array([v for n, v, _ in log.rows if n == 'train_unsupervised_loss'][:steps])
+        for i, (k, v) in enumerate(student.state_dict().items()):
+            if not torch.is_floating_point(v):
+                d[f'final{suf}.{k}'] = v
+                continue
+            idx = _sample_idx(v.numel(), i)
+            if not suf:
+                d['idx.' + k] = idx
+                d['init.' + k] = init[k].reshape(-1)[idx]
+            d[f'final{suf}.{k}'] = v.detach().reshape(-1)[idx].double()
+        print('msa trainsteps', suf or '32', d['sup_loss' + suf], d['unsup_loss' + suf])
+    save('msa_trainsteps.npz', **d)
+
+
+# ----------------------------------------------------------------------------------------------
 # G9: validation metrics (Dice + IoU)
 # ----------------------------------------------------------------------------------------------
 def gen_metrics():
@@ -492,6 +569,9 @@ if __name__ == '__main__':
     if len(sys.argv) > 1 and sys.argv[1] == 'models2':
         gen_models2()
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == 'msa_trainsteps':
+        gen_msa_trainsteps()
+        sys.exit(0)
     gen_cowmix()
     gen_mix()
     gen_consistency()
@@ -502,3 +582,4 @@ if __name__ == '__main__':
     gen_models2()
     gen_metrics()
     gen_inference()
+    gen_msa_trainsteps()

@@ -292,3 +292,107 @@ def _check_collectives(res, world):
             assert sum(f64) == 2 * sum(2 * c * 8 for c in bn_c), (r, k, sum(f64))
             assert len(f32) == out['nbuckets'], (r, k, len(f32), out['nbuckets'])
             assert sum(f32) == sum(out['bucket_bytes']), (r, k, sum(f32))
+
+
+def _worker_rccl(port, q):
+    """world-1 RCCL process group with the collectives forced on (ssseg.ddp.force_collectives): the bucketed
+    ReduceOp.AVG all-reduces on the side HIP stream, their event join and SyncBN's fp64 all-reduces all execute on
+    RCCL; the same steps without DDP / process group must give bit-identical gradients and parameters."""
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    import torch.distributed as dist
+    try:
+        import cowmix
+        import train
+        from ssseg import arena, ddp, optim
+        from ssseg import native as N
+        from ssseg import nn as snn
+        dev = torch.device('cuda:0')
+        torch.cuda.set_device(dev)
+        N.call('ssseg_set_knob', 5, 0)          # static variants: both runs launch the same kernels
+        snn.set_compute_dtype(torch.bfloat16)
+        cowmix.NOISE_SOURCE = 'cpu'
+        imgs, masks, unl = _data(1)
+
+        def run(distributed):
+            student, teacher = _model().to(dev), _model().to(dev)
+            for p in teacher.parameters():
+                p.detach_()
+            teacher.eval()
+            model = ddp.DistributedDataParallel(student, bucket_cap_mb=0.02) if distributed else student
+            if not distributed:
+                arena.attach(student)
+            arena.attach(teacher, with_grads=False)
+            opt = optim.SGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
+            grads, early, calls = [], [], []
+            orig_step = opt.step
+
+            def rec(*a, **k):
+                grads.append([p.grad.detach().clone() for p in student.parameters()])
+                return orig_step(*a, **k)
+            opt.step = rec
+            log = _CollectiveLog(dist) if distributed else None
+            torch.manual_seed(3)
+            model.train()
+            opt.zero_grad()
+            for step in range(STEPS):
+                train.train_step(model, teacher, opt, imgs[step, 0].to(dev), masks[step, 0].to(dev),
+                                 unl[step, 0, 0].to(dev), unl[step, 0, 1].to(dev), 30, step, {'train': _cfg(True)})
+                torch.cuda.synchronize()
+                if step == 0:
+                    grads.append([p.grad.detach().clone() for p in student.parameters()])
+                if distributed:
+                    early.append(model.last_early)
+                    calls.append(log.take())
+            if log is not None:
+                dist.all_reduce = log._orig
+            n_bn = sum(1 for m in student.modules() if isinstance(m, snn.BatchNorm2d))
+            return (grads, [v.detach().clone() for v in student.state_dict().values()],
+                    [v.detach().clone() for v in teacher.state_dict().values()], early, calls, n_bn,
+                    len(model.buckets) if distributed else 0)
+
+        dist.init_process_group('nccl', rank=0, world_size=1)
+        ddp.force_collectives(True)
+        got = run(True)
+        ddp.force_collectives(False)
+        ref = run(False)
+        out = {'backend': dist.get_backend(), 'early': got[3], 'nbuckets': got[6], 'n_bn': got[5],
+               'ncalls': [len(c) for c in got[4]], 'mismatch': []}
+        for k, (ga, gb) in enumerate(zip(got[0], ref[0])):
+            for i, (a, b) in enumerate(zip(ga, gb)):
+                if not torch.equal(a, b):
+                    out['mismatch'].append(('grad', k, i, float((a.float() - b.float()).abs().max())))
+        for name, xa, xb in (('student', got[1], ref[1]), ('teacher', got[2], ref[2])):
+            for i, (a, b) in enumerate(zip(xa, xb)):
+                if not torch.equal(a, b):
+                    out['mismatch'].append((name, i))
+        out['ngrads'] = len(got[0])
+        q.put(out)
+    except Exception as exc:
+        import traceback
+        q.put('ERROR ' + repr(exc) + '\n' + traceback.format_exc())
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_rccl_world1_forced_collectives_bitwise(hip_device):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_rccl, args=(_free_port(), q))
+    p.start()
+    try:
+        out = q.get(timeout=110)
+    finally:
+        p.join(30)
+        if p.is_alive():
+            p.kill()
+    assert not isinstance(out, str), out
+    assert out['backend'] == 'nccl'
+    assert out['ngrads'] == STEPS
+    # the learning backward launches every bucket in finish(); later armed backwards launch from inside the backward
+    assert out['early'][0] == 0 and all(e > 0 for e in out['early'][1:]), out['early']
+    # per step: one AVG all-reduce per bucket + (sum, sum^2) and (sum dy, sum dy*xhat) per training BatchNorm
+    assert all(n == out['nbuckets'] + 2 * out['n_bn'] for n in out['ncalls']), out['ncalls']
+    assert not out['mismatch'], out['mismatch'][:10]

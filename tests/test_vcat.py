@@ -65,6 +65,31 @@ def test_upblock_virtual_concat_bitwise(hip_device, cin, skip, cout, H, mode):
         assert torch.equal(a, b), f'{mode}: tensor {i} differs (max |d| {float((a.float() - b.float()).abs().max())})'
 
 
+@pytest.mark.parametrize('cin,skip,cout', [(128, 192, 64), (128, 64, 192)])
+@pytest.mark.parametrize('wcfg', [0, 2, 5, 10, 12])
+def test_vcat_mixed_straddle_wgrad_configs(hip_device, cin, skip, cout, wcfg):
+    """[64 | 192] and [192 | 64]: the seam sits inside one 128-wide kk-tile while the other lies wholly in one part,
+    so the ST weight-gradient kernel runs straddling and non-straddling blocks in one launch (their per-stage LDS-DMA
+    counts differ).  Forced 3- and 4-deep 128-wide configs (knob 9) must stay bitwise equal to the copy path."""
+    from ssseg import native as N
+    from ssseg import nn as snn
+    snn.set_compute_dtype(torch.bfloat16)
+    block = _upblock(hip_device, cin, skip, cout)
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, cin, 24, 24, generator=g).to(hip_device)
+    s = torch.randn(2, skip, 48, 48, generator=g).to(hip_device)
+    gy = snn.to_act(torch.randn(2, cout, 48, 48, generator=g).to(hip_device))
+    N.call('ssseg_set_knob', 9, wcfg)
+    try:
+        for mode in ('train', 'merged'):
+            ref = _run(block, x, s, mode, False, gy)
+            got = _run(block, x, s, mode, True, gy)
+            for i, (a, b) in enumerate(zip(got, ref)):
+                assert torch.equal(a, b), f'cfg {wcfg} {mode}: tensor {i} differs'
+    finally:
+        N.call('ssseg_set_knob', 9, 0)
+
+
 def test_virtual_concat_is_not_copied(hip_device):
     """The lazy concat of an eligible UpBlock carries its parts and its memory is never written by the forward."""
     from ssseg import nn as snn
@@ -115,3 +140,34 @@ def test_virtual_concat_backward_writes_parts(hip_device, monkeypatch, mode):
     assert 'ssseg_nhwc_copy' not in calls
     # the upsampler's ReLU backward runs inside the split launch (the up part's gradient arrives masked)
     assert 'ssseg_act_bwd' not in calls
+
+
+def test_virtual_concat_second_consumer_raises(hip_device):
+    """The split-output dgrad returns a never-written placeholder as the concat's input gradient: a second consumer of
+    the lazy concat would have its gradient summed into that placeholder and lost, so the concat's backward raises."""
+    from ssseg import nn as snn
+    snn.set_compute_dtype(torch.bfloat16)
+    block = _upblock(hip_device, 128, 64, 64)
+    x = snn.to_act(torch.randn(2, 128, 8, 8, device=hip_device)).requires_grad_(True)
+    s = snn.to_act(torch.randn(2, 64, 16, 16, device=hip_device)).requires_grad_(True)
+    up = block._upsample(x)
+    cat = snn.cat_crop(up, s, 64, 64, lazy=True)
+    assert snn._vcat_of(cat) is not None
+    y = block.conv3_0(cat)
+    loss = y.float().sum() + cat.float().sum()   # a second consumer of the lazy concat
+    with pytest.raises(RuntimeError, match='more than one consumer'):
+        loss.backward()
+
+
+def test_virtual_concat_part_modified_in_place_raises(hip_device):
+    from ssseg import nn as snn
+    snn.set_compute_dtype(torch.bfloat16)
+    block = _upblock(hip_device, 128, 64, 64)
+    x = snn.to_act(torch.randn(2, 128, 8, 8, device=hip_device)).requires_grad_(True)
+    s = snn.to_act(torch.randn(2, 64, 16, 16, device=hip_device))
+    up = block._upsample(x)
+    cat = snn.cat_crop(up, s, 64, 64, lazy=True)
+    y = block.conv3_0(cat)
+    s.mul_(2.0)
+    with pytest.raises(RuntimeError, match='modified in place'):
+        y.float().sum().backward()
