@@ -106,6 +106,56 @@ def wgrad_pending():
     return sum(1 for m in _WGRAD['pending'] if '_ssseg_wg_pending' in m.__dict__)
 
 
+_WSTREAM = {'on': os.environ.get('SSSEG_WGRAD_STREAM', '1') != '0', 'live': False, 'streams': {}, 'used': False}
+
+
+@contextlib.contextmanager
+def wgrad_side_stream():
+    """Inside: every conv weight-gradient launch runs on a second HIP stream (ordered after everything issued so far
+    on the compute stream, its operands kept alive for it by record_stream), so the weight gradients -- needed only by
+    the optimizer step and the DDP buckets -- fill the compute units the input-gradient chain of the backward leaves
+    idle.  On exit the compute stream waits for the side stream.  The training step wraps its last backward in this
+    (train.train_step); outside it every launch stays on the compute stream."""
+    if not _WSTREAM['on'] or _WSTREAM['live'] or not torch.cuda.is_available():
+        yield
+        return
+    _WSTREAM['live'] = True
+    try:
+        yield
+    finally:
+        _WSTREAM['live'] = False
+        join_wgrad_stream()
+
+
+def join_wgrad_stream():
+    if _WSTREAM['used']:
+        _WSTREAM['used'] = False
+        torch.cuda.current_stream().wait_stream(_WSTREAM['streams'][torch.cuda.current_device()])
+
+
+@contextlib.contextmanager
+def _on_wgrad_stream(*tensors):
+    """the launches inside go to the weight-gradient stream when wgrad_side_stream() is live"""
+    if not _WSTREAM['live']:
+        yield
+        return
+    dev = torch.cuda.current_device()
+    s = _WSTREAM['streams'].get(dev)
+    if s is None:
+        s = _WSTREAM['streams'][dev] = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    for t in tensors:
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            t.record_stream(s)
+            vc = _vcat_of(t)
+            if vc is not None:
+                vc.a.record_stream(s)
+                vc.b.record_stream(s)
+    _WSTREAM['used'] = True
+    with torch.cuda.stream(s):
+        yield
+
+
 def set_fused_bn_stats(flag):
     """Training BatchNorm statistics from the producing conv's epilogue (default) or a separate pass."""
     _CFG['fuse_stats'] = bool(flag)
@@ -756,6 +806,11 @@ class Conv2d(nn.Conv2d, _ConvBase):
         if self._wg_defer(x, gy):
             return
         pend = self._wg_take(x, gy)
+        with _on_wgrad_stream(x, gy, *(pend or ())):
+            self._wgrad_launch(x, gy, pend)
+
+    def _wgrad_launch(self, x, gy, pend):
+        n, _, H, W = x.shape
         R, S = self.kernel_size
         if pend is None:
             d = self._fwd_desc(n, H, W)
@@ -992,33 +1047,40 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
             if self._wg_defer(x, gy):
                 return
             pend = self._wg_take(x, gy)
-            cin, cout = self._dims()
-            n, _, H, W = x.shape
-            (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
-            OH, OW = gy.shape[2], gy.shape[3]
-            n1 = pend[0].shape[0] if pend is not None else n
-            # dW[ci][co][r][s] = sum_p x[p][ci] * gy[p*s - pad + r][co]: a conv over gy with x as its output grad
-            d = _desc(N=n1, H=OH, W=OW, C=cout, ldx=cout, OH=H, OW=W, K=cin, R=R, S=S, sy=sh, sx=sw, dy=1, dx=1,
-                      py=-ph, px=-pw, outH=H, outW=W, osy=1, osx=1, ooy=0, oox=0, ldy=cin, ldw=R * S * cout)
-            if pend is None:
-                nb = N.lib().ssseg_conv_wgrad_workspace_bytes(ctypes_ref(d), N.dt_code(x))
-                ws = N.workspace(nb, x.device)
-                with _Timed(_conv_flops(n, H, W, self.out_channels, self.in_channels, R, S), 'wgrad',
-                            _tag(self, n, H, W)):
-                    N.call('ssseg_conv_wgrad', N.dev_ptr(gy), N.dev_ptr(x), N.dev_ptr(_grad_of(self.weight)),
-                           ctypes_ref(d), N.dt_code(x), self.out_channels, self.in_channels, 1, 1, N.dev_ptr(ws), nb,
-                           N.stream())
-            else:   # the deferred pass and this one: one launch over both pixel sets (operands in (gy, x) order)
-                x1, gy1 = pend
-                nb = N.lib().ssseg_conv_wgrad2_workspace_bytes(ctypes_ref(d), n, N.dt_code(x))
-                ws = N.workspace(nb, x.device)
-                with _Timed(_conv_flops(n1 + n, H, W, self.out_channels, self.in_channels, R, S), 'wgrad',
-                            _tag(self, n1 + n, H, W)):
-                    N.call('ssseg_conv_wgrad2', N.dev_ptr(gy1), N.dev_ptr(x1), N.dev_ptr(gy), N.dev_ptr(x), n,
-                           N.dev_ptr(_grad_of(self.weight)), ctypes_ref(d), N.dt_code(x), self.out_channels,
-                           self.in_channels, 1, 1, N.dev_ptr(ws), nb, N.stream())
+            with _on_wgrad_stream(x, gy, *(pend or ())):
+                self._wgrad_launch(x, gy, pend, want)
+            return
         wb = self.bias is not None and (self.bias.requires_grad if want is None else want[1])
-        _ready(*[p for p, on in ((self.weight, ww), (self.bias, wb)) if on])
+        _ready(*[p for p, on in ((self.bias, wb),) if on])
+
+    def _wgrad_launch(self, x, gy, pend, want):
+        cin, cout = self._dims()
+        n, _, H, W = x.shape
+        (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
+        OH, OW = gy.shape[2], gy.shape[3]
+        n1 = pend[0].shape[0] if pend is not None else n
+        # dW[ci][co][r][s] = sum_p x[p][ci] * gy[p*s - pad + r][co]: a conv over gy with x as its output grad
+        d = _desc(N=n1, H=OH, W=OW, C=cout, ldx=cout, OH=H, OW=W, K=cin, R=R, S=S, sy=sh, sx=sw, dy=1, dx=1,
+                  py=-ph, px=-pw, outH=H, outW=W, osy=1, osx=1, ooy=0, oox=0, ldy=cin, ldw=R * S * cout)
+        if pend is None:
+            nb = N.lib().ssseg_conv_wgrad_workspace_bytes(ctypes_ref(d), N.dt_code(x))
+            ws = N.workspace(nb, x.device)
+            with _Timed(_conv_flops(n, H, W, self.out_channels, self.in_channels, R, S), 'wgrad',
+                        _tag(self, n, H, W)):
+                N.call('ssseg_conv_wgrad', N.dev_ptr(gy), N.dev_ptr(x), N.dev_ptr(_grad_of(self.weight)),
+                       ctypes_ref(d), N.dt_code(x), self.out_channels, self.in_channels, 1, 1, N.dev_ptr(ws), nb,
+                       N.stream())
+        else:   # the deferred pass and this one: one launch over both pixel sets (operands in (gy, x) order)
+            x1, gy1 = pend
+            nb = N.lib().ssseg_conv_wgrad2_workspace_bytes(ctypes_ref(d), n, N.dt_code(x))
+            ws = N.workspace(nb, x.device)
+            with _Timed(_conv_flops(n1 + n, H, W, self.out_channels, self.in_channels, R, S), 'wgrad',
+                        _tag(self, n1 + n, H, W)):
+                N.call('ssseg_conv_wgrad2', N.dev_ptr(gy1), N.dev_ptr(x1), N.dev_ptr(gy), N.dev_ptr(x), n,
+                       N.dev_ptr(_grad_of(self.weight)), ctypes_ref(d), N.dt_code(x), self.out_channels,
+                       self.in_channels, 1, 1, N.dev_ptr(ws), nb, N.stream())
+        wb = self.bias is not None and (self.bias.requires_grad if want is None else want[1])
+        _ready(*[p for p, on in ((self.weight, True), (self.bias, wb)) if on])
 
     def _ssseg_dgrad(self, gy, xshape):
         cin, cout = self._dims()

@@ -11,6 +11,7 @@ print steps (the reference syncs 4x per step for logging only); the DDP gradient
 per step, armed on the last backward pass (linear, so the averaged gradient is the same).
 """
 import contextlib
+import os
 import time
 
 import torch
@@ -110,10 +111,52 @@ def _scaled(loss, optimizer):
     return sc.scale(loss) if sc is not None else loss
 
 
+_OVERLAP = {'teacher': os.environ.get('SSSEG_OVERLAP_TEACHER', '1') != '0', 'streams': {}}
+
+
+def _teacher_targets(ema_model, unsup_a, unsup_b, tc):
+    """train.py:66-85: the teacher's predictions on both unlabelled batches (no grad, eval), resized to the image size,
+    the CowMix mask and the two mixes.  Returns (mixed teacher logits, mixed images)."""
+    size = unsup_a.shape[2:4]
+    with torch.no_grad(), snn.folded(_inner(ema_model)):   # one batched BN fold for both teacher passes
+        if _batched_eval_ok(ema_model, unsup_a, unsup_b):
+            # train.py:69-75 runs the teacher twice; in eval mode every output depends on its own sample
+            # only, so ONE forward over [unsup_a; unsup_b] gives the same logits (the conv variants
+            # accumulate the same k-sequence at any batch) with half the launches and twice the tiles on
+            # the small-map layers
+            b = unsup_a.shape[0]
+            ema_logits = ema_model(snn.to_act_cat([unsup_a, unsup_b]))[-1][-1]
+            ema_pred_a = ops.interpolate_bilinear(ema_logits[:b], size, align_corners=False)
+            ema_pred_b = ops.interpolate_bilinear(ema_logits[b:], size, align_corners=False)
+            del ema_logits
+        else:
+            ema_pred_a = ops.interpolate_bilinear(ema_model(unsup_a)[-1][-1], size, align_corners=False)
+            ema_pred_b = ops.interpolate_bilinear(ema_model(unsup_b)[-1][-1], size, align_corners=False)
+        cmask = cowmix.generate_cowmix_masks_like(unsup_a, mask_proportion_range=tc['mask_proportion_range'],
+                                                  sigma_range=tc['sigma_range'])
+        mixed_ema_pred = cowmix.mix_with_mask(ema_pred_a, ema_pred_b, cmask)
+        mixed_images = cowmix.mix_with_mask(unsup_a, unsup_b, cmask)
+    return mixed_ema_pred, mixed_images
+
+
+def _side_stream(device):
+    s = _OVERLAP['streams'].get(device)
+    if s is None:
+        s = _OVERLAP['streams'][device] = torch.cuda.Stream(device=device)
+    return s
+
+
 def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch, step, config):
     """One step of train.py:44-130.  Returns device scalars (classification loss, unsup loss, cm mean).
     With config['train']['adversarial'] = dict(discriminator=D, optimizer=opt_D, weight=w) the student's
-    supervised loss gets the adversarial term and D is updated after the supervised backward (C5)."""
+    supervised loss gets the adversarial term and D is updated after the supervised backward (C5).
+
+    Stream schedule (same arithmetic as the reference order): the teacher pass (train.py:66-85) depends on the
+    supervised forward only -- the running statistics its eval BatchNorms read are the ones that forward updated
+    (the teacher's BN buffers alias the student's, mean_teacher.py:13-18), and the supervised backward neither
+    changes them nor draws random numbers -- so it is issued on a side HIP stream right after the supervised forward
+    and runs concurrently with the supervised backward; the consistency forward waits for it.  The consistency
+    backward puts its (merged) weight gradients on a side stream too (ssseg.nn.wgrad_side_stream)."""
     tc = config['train']
     ddp = model if isinstance(model, _DDP) else None
     semi = tc['use_semi_supervised']
@@ -125,6 +168,18 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
     if adv is not None:
         adv_loss, prob = adversarial_terms(pred_maps, mask, adv)
         sup_loss = ops.add_scaled(sup_loss, adv_loss)
+    overlap = semi and adv is None and _OVERLAP['teacher'] and image.is_cuda and unsup_a.is_cuda
+    targets = None
+    if overlap:
+        main = torch.cuda.current_stream()
+        side = _side_stream(image.device)
+        side.wait_stream(main)                # the supervised forward (and its running statistics) first
+        for t in (unsup_a, unsup_b):
+            t.record_stream(side)
+        with torch.cuda.stream(side):
+            targets = _teacher_targets(ema_model, unsup_a, unsup_b, tc)
+        for t in targets:
+            t.record_stream(main)
     if ddp is not None and not semi:
         ddp.arm()
     # with a consistency backward to follow, each conv's supervised weight gradient is merged into that pass's
@@ -139,39 +194,26 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
         adv['last_loss_adv'] = adv_loss.detach()
         del prob
     unsup_loss = cm_mean = None
-    if semi:
-        size = unsup_a.shape[2:4]
-        with torch.no_grad(), snn.folded(_inner(ema_model)):   # one batched BN fold for both teacher passes
-            if _batched_eval_ok(ema_model, unsup_a, unsup_b):
-                # train.py:69-75 runs the teacher twice; in eval mode every output depends on its own sample
-                # only, so ONE forward over [unsup_a; unsup_b] gives the same logits (the conv variants
-                # accumulate the same k-sequence at any batch) with half the launches and twice the tiles on
-                # the small-map layers
-                b = unsup_a.shape[0]
-                ema_logits = ema_model(snn.to_act_cat([unsup_a, unsup_b]))[-1][-1]
-                ema_pred_a = ops.interpolate_bilinear(ema_logits[:b], size, align_corners=False)
-                ema_pred_b = ops.interpolate_bilinear(ema_logits[b:], size, align_corners=False)
-                del ema_logits
+    with snn.wgrad_side_stream():
+        if semi:
+            if overlap:
+                torch.cuda.current_stream().wait_stream(_side_stream(image.device))
+                mixed_ema_pred, mixed_images = targets
             else:
-                ema_pred_a = ops.interpolate_bilinear(ema_model(unsup_a)[-1][-1], size, align_corners=False)
-                ema_pred_b = ops.interpolate_bilinear(ema_model(unsup_b)[-1][-1], size, align_corners=False)
-            cmask = cowmix.generate_cowmix_masks_like(unsup_a, mask_proportion_range=tc['mask_proportion_range'],
-                                                      sigma_range=tc['sigma_range'])
-            mixed_ema_pred = cowmix.mix_with_mask(ema_pred_a, ema_pred_b, cmask)
-            mixed_images = cowmix.mix_with_mask(unsup_a, unsup_b, cmask)
-            del cmask, ema_pred_a, ema_pred_b
-        model.eval()
-        with snn.folded(_inner(model)):
-            student_pred = model(mixed_images)[-1][-1]
-        model.train()
-        student_pred = ops.interpolate_bilinear(student_pred, mixed_images.shape[2:4], align_corners=False)
-        consistency, cm_mean = ops.consistency_loss(student_pred, mixed_ema_pred, tc['confidence_threshold'])
-        # consistency * weight * float(epoch > 25) (train.py:112; a 0/0 NaN survives the 0.0 gate, as there)
-        unsup_loss = ops.scale(consistency, float(tc['consistency_loss_weight']) * float(epoch > 25))
-        if ddp is not None:
-            ddp.arm()
-        ops.backward(_scaled(unsup_loss, optimizer))
-    snn.flush_wgrad()
+                mixed_ema_pred, mixed_images = _teacher_targets(ema_model, unsup_a, unsup_b, tc)
+            del targets
+            model.eval()
+            with snn.folded(_inner(model)):
+                student_pred = model(mixed_images)[-1][-1]
+            model.train()
+            student_pred = ops.interpolate_bilinear(student_pred, mixed_images.shape[2:4], align_corners=False)
+            consistency, cm_mean = ops.consistency_loss(student_pred, mixed_ema_pred, tc['confidence_threshold'])
+            # consistency * weight * float(epoch > 25) (train.py:112; a 0/0 NaN survives the 0.0 gate, as there)
+            unsup_loss = ops.scale(consistency, float(tc['consistency_loss_weight']) * float(epoch > 25))
+            if ddp is not None:
+                ddp.arm()
+            ops.backward(_scaled(unsup_loss, optimizer))
+        snn.flush_wgrad()
     if ddp is not None:
         ddp.finish()
     if step % tc['virtual_batch_size_multiplier'] == 0 and step != 0:
