@@ -156,7 +156,8 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
     (the teacher's BN buffers alias the student's, mean_teacher.py:13-18), and the supervised backward neither
     changes them nor draws random numbers -- so it is issued on a side HIP stream right after the supervised forward
     and runs concurrently with the supervised backward; the consistency forward waits for it.  The consistency
-    backward puts its (merged) weight gradients on a side stream too (ssseg.nn.wgrad_side_stream)."""
+    backward can put its (merged) weight gradients on a side stream too (ssseg.nn.wgrad_side_stream; off by default,
+    measured neutral).  Measured on the C2 step (A/B in one call): 443.9 img/s serial, 452.9 with the teacher overlap."""
     tc = config['train']
     ddp = model if isinstance(model, _DDP) else None
     semi = tc['use_semi_supervised']
