@@ -599,7 +599,8 @@ extern int g_knobs[12];   // runtime variant switches (ssseg_set_knob), defined 
 // 7: LDS-staged coalesced epilogue in the LDS-DMA kernel (0 on, -1 off);
 // 8: bf16 weight gradient on the LDS-DMA kernel (0 on, -1 = register-staged wgrad_kernel);
 // 9: LDS-DMA weight-gradient tile variant (0 = the static plan, 1.. = a forced WGRAD_CFGS entry, conv_wgrad.hip);
-// 10: weight-gradient split count scale in percent (100 = the plan's); 11: reserved
+// 10: weight-gradient split count scale in percent (100 = the plan's); 11: halo-tiled 3x3 weight gradient
+// (conv_wgrad_halo.hip; 0 on, -1 = the split-K LDS-DMA kernel)
 
 // STATS: the epilogue also writes the fused BatchNorm statistics partials (a separate instantiation: the fp64
 // sums raise the register count, which must not cost the launches that do not need them)
@@ -1261,6 +1262,32 @@ inline int plan_splits(const ConvGeom& g) {
   return (int)std::max<long long>(1, std::min<long long>(sp, 64));
 }
 
+
+// halo-tiled 3x3 / stride-1 weight gradient (conv_wgrad_halo.hip)
+struct HaloSeg {
+  const void* x;    // input (pixel stride ldx), channels [0, c1) of a virtual concat (all C without one)
+  const void* x2;   // a virtual concat's second part (channels >= c1, pixel stride ldx2), else null
+  const void* dy;   // output gradient (pixel stride ldy)
+  unsigned xbytes, x2bytes, dbytes;
+};
+struct HaloArgs {
+  HaloSeg seg[2];
+  int H, W, C, K, ldx, ldx2, ldy, c1;
+  int ncb, nkb, nstrips;
+  long long steps[2], sps[2];   // row steps per segment, row steps per split
+  int splits, s1;               // total splits, splits of segment 0
+  float* slab;                  // [splits][K][9 * C] fp32 partials (splits > 1)
+  float* dw;                    // splits == 1: dW written directly in `layout` (0 = [K][3][3][C], 1 = OIHW)
+  int c_real, k_real, layout, accumulate;
+};
+struct HaloPlan {
+  int ncb, nkb, nstrips, splits, s1;
+  long long steps[2], sps[2];
+};
+bool halo3_eligible(const ConvGeom& g, int dt);
+HaloPlan halo3_plan(const ConvGeom& g, long long n1, long long n2);
+size_t halo3_ws_bytes(const ConvGeom& g, long long n1, long long n2);
+void launch_wgrad_halo3(int dt, const HaloArgs& a, hipStream_t s);
 
 // register-staged kernel launches (conv_reg_*.hip): returns the tile height BM
 template <typename T, typename TO>

@@ -785,6 +785,7 @@ bool wg_geom_ok(const ConvGeom& g, int dt) {
 static size_t wgrad_ws_bytes(const ConvGeom& g, int dt) {
   const WgradPlan p = choose_wgrad(g, dt);
   size_t b = (size_t)p.splits * g.K * g.KK * sizeof(float);
+  if (halo3_eligible(g, dt)) b = std::max(b, halo3_ws_bytes(g, g.N, 0));
   if (p.glds) {
     const WgradPlan q = plan_for_cfg(g, wgrad_cfg_for(g, 64));
     b = std::max(b, (size_t)q.splits * g.K * g.KK * sizeof(float));
@@ -819,6 +820,51 @@ bool vcat_ok(const ssseg_vcat* vc, const ConvGeom& g, int dt) {
          (long long)g.N * g.H * g.W * vc->ldx2 * 2 < 0x7fffffffLL;
 }
 
+// the halo-tiled 3x3 weight gradient over one or two pixel segments (x2 / dy2 / n2: the merged launch's second)
+void run_halo3(const ConvGeom& g, int dt, const void* x, const ssseg_vcat* vc, const void* dy, const void* x2,
+               const ssseg_vcat* vc2, const void* dy2, long long n2, float* dw, int64_t c_real, int64_t k_real,
+               int layout, int accumulate, float* slab, hipStream_t s) {
+  const HaloPlan p = halo3_plan(g, g.N, n2);
+  HaloArgs a{};
+  const long long pix1 = (long long)g.N * g.H * g.W, pix2 = n2 * g.H * g.W;
+  a.seg[0] = HaloSeg{x, vc ? vc->x2 : nullptr, dy, (unsigned)(pix1 * g.ldx * 2),
+                     vc ? (unsigned)(pix1 * vc->ldx2 * 2) : 0u, (unsigned)(pix1 * g.ldy * 2)};
+  if (n2 > 0)
+    a.seg[1] = HaloSeg{x2, vc2 ? vc2->x2 : nullptr, dy2, (unsigned)(pix2 * g.ldx * 2),
+                       vc2 ? (unsigned)(pix2 * vc2->ldx2 * 2) : 0u, (unsigned)(pix2 * g.ldy * 2)};
+  a.H = g.H;
+  a.W = g.W;
+  a.C = g.C;
+  a.K = g.K;
+  a.ldx = g.ldx;
+  a.ldx2 = vc ? (int)vc->ldx2 : 0;
+  a.ldy = g.ldy;
+  a.c1 = vc ? (int)vc->c1 : 0;
+  a.ncb = p.ncb;
+  a.nkb = p.nkb;
+  a.nstrips = p.nstrips;
+  a.steps[0] = p.steps[0];
+  a.steps[1] = p.steps[1];
+  a.sps[0] = p.sps[0];
+  a.sps[1] = p.sps[1];
+  a.splits = p.splits;
+  a.s1 = p.s1;
+  a.slab = slab;
+  a.dw = p.splits == 1 ? dw : nullptr;
+  a.c_real = (int)c_real;
+  a.k_real = (int)k_real;
+  a.layout = layout;
+  a.accumulate = accumulate;
+  launch_wgrad_halo3(dt, a, s);
+  if (p.splits > 1) launch_reduce(slab, g, p.splits, c_real, k_real, dw, layout, accumulate, s);
+}
+
+// operands addressable with 32-bit byte offsets (the LDS-DMA buffer resources)
+bool halo3_fits(const ConvGeom& g, long long n, const ssseg_vcat* vc) {
+  const long long pix = n * g.H * g.W;
+  return pix * g.ldx * 2 < 0x7fffffffLL && pix * g.ldy * 2 < 0x7fffffffLL && (!vc || pix * vc->ldx2 * 2 < 0x7fffffffLL);
+}
+
 int wgrad_one(const void* x, const ssseg_vcat* vc, const void* dy, float* dw, const ssseg_conv_desc* d, int dt,
               int64_t c_real, int64_t k_real, int layout, int accumulate, void* ws, size_t ws_bytes,
               ssseg_stream_t stream) {
@@ -832,6 +878,11 @@ int wgrad_one(const void* x, const ssseg_vcat* vc, const void* dy, float* dw, co
   if (dt != SSSEG_BF16 && dt != SSSEG_F16 && dt != SSSEG_F32) return SSSEG_EUNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   float* slab = (float*)ws;
+  if (halo3_eligible(g, dt) && halo3_fits(g, g.N, vc)) {
+    run_halo3(g, dt, x, vc, dy, nullptr, nullptr, nullptr, 0, dw, c_real, k_real, layout, accumulate, slab, s);
+    SSSEG_LAUNCH_CHECK();
+    return 0;
+  }
   WgradPlan p = choose_wgrad(g, dt);
   if (vc) {
     if (!p.glds) return SSSEG_EUNSUPPORTED;   // the register-staged kernel has no second source
@@ -896,6 +947,7 @@ size_t wgrad2_ws_bytes(const ConvGeom& g, int64_t n2, int dt) {
   size_t b = 0;
   for (int c1 : {0, 64})   // the static config and the 64-wide one a virtual concat may need
     if (merged_plan(g, n2, dt, p, s1, g2, c1)) b = std::max(b, (size_t)p.splits * g.K * g.KK * sizeof(float) + 256);
+  if (halo3_eligible(g, dt)) b = std::max(b, halo3_ws_bytes(g, g.N, n2));
   if (b) return b;
   ConvGeom gb = g;
   gb.N = (int)n2;
@@ -917,6 +969,12 @@ int wgrad_two(const void* x, const ssseg_vcat* vc, const void* dy, const void* x
   gb.M = n2 * (long long)g.OH * g.OW;
   if (!vcat_ok(vc, g, dt) || !vcat_ok(vc2, gb, dt)) return SSSEG_EINVAL;
   if (!ws || ws_bytes < wgrad2_ws_bytes(g, n2, dt)) return SSSEG_EWORKSPACE;
+  if (halo3_eligible(g, dt) && halo3_fits(g, g.N, vc) && halo3_fits(g, n2, vc2)) {
+    run_halo3(g, dt, x, vc, dy, x2, vc2, dy2, n2, dw, c_real, k_real, layout, accumulate, (float*)ws,
+              (hipStream_t)stream);
+    SSSEG_LAUNCH_CHECK();
+    return 0;
+  }
   WgradPlan p;
   int s1;
   if (!merged_plan(g, n2, dt, p, s1, g2, vc ? (int)vc->c1 : 0)) {   // the two contributions one after the other

@@ -381,6 +381,57 @@ def test_wgrad_lds_dma(hip_device, cin, cout, k, s, p, d, H, W, n):
         assert err < 1e-4, f'{name}: max rel err {err}'
 
 
+HALO_CASES = [
+    # cin, cout, H, W, n, n2 (second pixel segment of a merged launch: 0 = none)
+    (64, 64, 37, 64, 2, 0),       # one 64-channel block each way, column changes mid-split
+    (128, 64, 20, 128, 2, 3),     # two channel blocks, two strips, merged launch with a different batch
+    (384, 128, 9, 64, 3, 0),      # 6 x 2 channel blocks (the UNet decoder's 384 -> 128 shape)
+    (64, 128, 64, 192, 1, 1),     # three strips, merged
+    (64, 64, 1, 64, 1, 0),        # one row step: a single split writes dW directly
+]
+
+
+@pytest.mark.parametrize('cin,cout,H,W,n,n2', HALO_CASES)
+def test_wgrad_halo3(hip_device, cin, cout, H, W, n, n2):
+    """Halo-tiled 3x3 weight gradient (conv_wgrad_halo.hip, knob 11 = 0, the default for 3x3 / stride-1 / pad-1
+    layers with W % 64 == 0) and the split-K LDS-DMA kernel (knob 11 = -1) vs PyTorch fp32 on the same bf16-rounded
+    operands, single and merged (defer_wgrad: two backward passes, one launch over both pixel sets): fp32 summation
+    order only, 1e-4 of max|dW|."""
+    import contextlib
+    from ssseg import native as N
+    from ssseg import nn as snn
+    snn.set_compute_dtype(torch.bfloat16)
+    torch.manual_seed(5)
+    ref = torch.nn.Conv2d(cin, cout, 3, 1, 1, bias=False)
+    with torch.no_grad():
+        ref.weight.copy_(ref.weight.bfloat16().float())
+    mod = snn.Conv2d(cin, cout, 3, 1, 1, bias=False).to(hip_device)
+    mod.load_state_dict(ref.state_dict())
+    passes = [n] + ([n2] if n2 else [])
+    xs = [torch.randn(b, cin, H, W).bfloat16().float() for b in passes]
+    gys = [torch.randn(b, cout, H, W).bfloat16().float() for b in passes]
+    for x, gy in zip(xs, gys):
+        ref(x).backward(gy)
+    gref = ref.weight.grad
+    grads = []
+    try:
+        for knob in (0, -1):
+            N.call('ssseg_set_knob', 11, knob)
+            mod.weight.grad = None
+            for i, (x, gy) in enumerate(zip(xs, gys)):
+                with (snn.defer_wgrad() if i == 0 and len(passes) > 1 else contextlib.nullcontext()):
+                    mod(snn.to_act(x.to(hip_device))).backward(snn.to_act(gy.to(hip_device)))
+            snn.flush_wgrad()
+            torch.cuda.synchronize()
+            grads.append(mod.weight.grad.detach().float().cpu())
+    finally:
+        N.call('ssseg_set_knob', 11, 0)
+    scale = float(gref.abs().max())
+    for name, g in zip(('halo', 'split-K'), grads):
+        err = float((g - gref).abs().max()) / scale
+        assert err < 1e-4, f'{name}: max rel err {err}'
+
+
 @pytest.mark.parametrize('k,s,p,ceil', [(3, 2, 1, False), (2, 2, 0, True)])
 def test_maxpool(hip_device, mode, k, s, p, ceil):
     from ssseg import nn as snn

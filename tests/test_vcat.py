@@ -48,7 +48,9 @@ def _run(block, x, skip, mode, vcat, gy=None):
         block.train()
 
 
-@pytest.mark.parametrize('cin,skip,cout,H', [(256, 256, 128, 16), (128, 64, 64, 33), (512, 1024, 128, 9)])
+# (128, 64, 64, 32): conv3_0 at 64 x 64 runs the halo-tiled 3x3 weight gradient over the two parts
+@pytest.mark.parametrize('cin,skip,cout,H', [(256, 256, 128, 16), (128, 64, 64, 33), (512, 1024, 128, 9),
+                                            (128, 64, 64, 32)])
 @pytest.mark.parametrize('mode', ['train', 'eval', 'nograd', 'merged'])
 def test_upblock_virtual_concat_bitwise(hip_device, cin, skip, cout, H, mode):
     from ssseg import nn as snn
