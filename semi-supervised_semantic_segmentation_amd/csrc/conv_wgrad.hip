@@ -861,6 +861,7 @@ void run_halo3(const ConvGeom& g, int dt, const void* x, const ssseg_vcat* vc, c
 
 // operands addressable with 32-bit byte offsets (the LDS-DMA buffer resources)
 bool halo3_fits(const ConvGeom& g, long long n, const ssseg_vcat* vc) {
+  if (!vc && g.ldx < g.C) return false;
   const long long pix = n * g.H * g.W;
   return pix * g.ldx * 2 < 0x7fffffffLL && pix * g.ldy * 2 < 0x7fffffffLL && (!vc || pix * vc->ldx2 * 2 < 0x7fffffffLL);
 }

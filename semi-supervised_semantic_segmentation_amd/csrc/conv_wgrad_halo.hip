@@ -17,18 +17,26 @@
 // right.  Both operands are pixel-major in LDS and read with ds_read_b64_tr_b16 under the k-slot -> pixel map of the
 // split-K kernel (wkp), so the pixel contraction is permuted identically for A and B.
 //
+// The ring is HD = 2 row steps deep (5 input-row slots, 3 dY slots, 69 KB: two blocks per CU): while row y is
+// multiplied, the pieces of rows y + 1 and y + 2 are in flight (one block per CU and one step ahead measured latency-
+// bound: 1.9 us per step for 0.5 us of MFMA work).
 // A split is a contiguous range of row steps t = ((n * nstrips) + strip) * H + y of one pixel segment (the merged
-// supervised + consistency launch has two); a column change (new strip or image) reloads the three ring rows.  Every
+// supervised + consistency launch has two); a column change (new strip or image) drains the ring and reloads the
+// three rows of the first step's taps.  Every
 // split writes its fp32 partial of the whole dW into its own slab, which wgrad_reduce sums in split order
 // (deterministic), exactly like the split-K path.
 #include "conv_kernels.h"
 
 namespace {
 
-constexpr int HX_ROWS = 72;                 // ring row: 66 pixels (64 + halo) padded to whole 8-row wave-instructions
-constexpr int HX_SLOT = HX_ROWS * 128;      // one input row segment: 64 channels x 2 B per pixel
+constexpr int HX_ROWS = 66;                 // ring row: 64 pixels + the halo pixel on each side
+constexpr int HX_SLOT = 72 * 128;           // one input row segment (64 channels x 2 B per pixel), 8-row padded
 constexpr int HD_SLOT = 64 * 128;           // one dY row segment
-constexpr int H_SMEM = 4 * HX_SLOT + 2 * HD_SLOT;
+constexpr int HD = 2;                       // row steps in flight ahead of the one being multiplied
+constexpr int HXS = HD + 3;                 // input-row ring slots: rows y-1 .. y+1 in use, y+2 .. y+HD+1 landing
+constexpr int HDS = HD + 1;                 // dY ring slots
+constexpr int H_SMEM = HXS * HX_SLOT + HDS * HD_SLOT;
+constexpr int H_NL = 5;                     // vmcnt units of one row step per wave: 3 input pieces + 2 dY pieces
 
 __device__ __forceinline__ int hswz(int r) { return (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 1); }
 __device__ __forceinline__ int hkp(int g, int j) { return 16 * (g >> 1) + 8 * (g & 1) + 4 * (j >> 2) + (j & 3); }
@@ -54,30 +62,34 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo3_kernel(HaloArgs a) {
   const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc((void*)S.dy, (short)0, (int)S.dbytes, 0x00020000);
   const int H = a.H, W = a.W;
 
-  // this lane's fixed part of its LDS-DMA pieces: row-in-instruction and logical 16-byte chunk (bank swizzle applied
-  // on the source side: the DMA writes lane-linearly)
+  // LDS-DMA pieces (the DMA writes lane-linearly: 16-byte chunk (lane & 7) of row lane >> 3 of an 8-row piece; the
+  // bank swizzle is applied on the source side).  An input row segment is 66 pixel rows: every wave issues two full
+  // 8-row pieces (rows 16w .. 16w + 15) and a quarter piece (rows 64 + 2w, 65 + 2w: lanes 0-15, the rest masked off,
+  // rows 66+ never read), so every wave counts the same 3 + 2 vmcnt units per row step.
   const int lrow = lane >> 3;
-  auto x_chunk = [&](int row) { return ((lane & 7) ^ hswz(row)) * 16; };
-
-  auto issue_x = [&](int slot, int n, int yy, int strip) {   // input row yy of the strip (66 pixels) -> ring slot
+  auto chunk_of = [&](int row) { return ((lane & 7) ^ hswz(row)) * 16; };
+  auto x_off = [&](int n, int yy, int row, int strip) {
+    const int xx = strip * 64 - 1 + row;
+    if ((unsigned)yy >= (unsigned)H || row >= HX_ROWS || (unsigned)xx >= (unsigned)W) return OOB;
+    return (unsigned)(((n * H + yy) * W + xx) * ldx + c0) * 2u + (unsigned)chunk_of(row);
+  };
+  auto issue_x = [&](int slot, int n, int yy, int strip) {   // input row yy of the strip -> ring slot
     char* base = smem + slot * HX_SLOT;
-    const bool yok = (unsigned)yy < (unsigned)H;
-    for (int i = wave; i < HX_ROWS / 8; i += 4) {
-      const int row = 8 * i + lrow;
-      const int xx = strip * 64 - 1 + row;
-      unsigned off = OOB;
-      if (yok && row < 66 && (unsigned)xx < (unsigned)W)
-        off = (unsigned)(((n * H + yy) * W + xx) * ldx + c0) * 2u + (unsigned)x_chunk(row);
-      bldslds16(xr, base + i * 1024, off, 0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = 2 * wave + h;
+      bldslds16(xr, base + i * 1024, x_off(n, yy, 8 * i + lrow, strip), 0);
     }
+    if (lane < 16) bldslds16(xr, base + 8 * 1024 + wave * 256, x_off(n, yy, 64 + 2 * wave + lrow, strip), 0);
   };
   auto issue_dy = [&](int slot, int n, int y, int strip) {   // dY row y of the strip (64 pixels) -> dy slot
-    char* base = smem + 4 * HX_SLOT + slot * HD_SLOT;
+    char* base = smem + HXS * HX_SLOT + slot * HD_SLOT;
 #pragma unroll
-    for (int i = wave; i < 8; i += 4) {
+    for (int h = 0; h < 2; ++h) {
+      const int i = 2 * wave + h;
       const int row = 8 * i + lrow;
-      const int xx = strip * 64 + row;
-      const unsigned off = (unsigned)(((n * H + y) * W + xx) * a.ldy + kb * 64) * 2u + (unsigned)x_chunk(row);
+      const unsigned off =
+          (unsigned)(((n * H + y) * W + strip * 64 + row) * a.ldy + kb * 64) * 2u + (unsigned)chunk_of(row);
       bldslds16(dr, base + i * 1024, off, 0);
     }
   };
@@ -87,6 +99,9 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo3_kernel(HaloArgs a) {
     n = (int)(q / a.nstrips);
     strip = (int)(q - (long long)n * a.nstrips);
   };
+  // ring slots, rebased at every column start (the ring is drained there): input row yy in slot (yy + 1) % HXS,
+  // dY row y in slot y % HDS
+  auto xslot = [&](int yy) { return (yy + 1) % HXS; };
 
   f32x4 acc[9][4];
 #pragma unroll
@@ -98,8 +113,8 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo3_kernel(HaloArgs a) {
   // fragment addresses inside a slot: rows (pixel) of the lane's lo / hi transposed reads, column chunk + byte
   const int xcol = 2 * wave + (p4 >> 1), dsub = 8 * (p4 & 1);
 
-  auto compute = [&](int y, int dslot) {
-    const char* D = smem + 4 * HX_SLOT + dslot * HD_SLOT;
+  auto compute = [&](int y) {
+    const char* D = smem + HXS * HX_SLOT + (y % HDS) * HD_SLOT;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int r0 = ks * 32 + hkp(gq, q4), r1 = ks * 32 + hkp(gq, 4 + q4);
@@ -113,7 +128,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo3_kernel(HaloArgs a) {
       }
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
-        const char* X = smem + ((y + r) & 3) * HX_SLOT;   // input row y + r - 1 lives in slot (y + r) & 3
+        const char* X = smem + xslot(y + r - 1) * HX_SLOT;
 #pragma unroll
         for (int s = 0; s < 3; ++s) {
           const int x0 = r0 + s, x1 = r1 + s;
@@ -129,42 +144,39 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo3_kernel(HaloArgs a) {
     }
   };
 
-  // prologue / column change: the three ring rows of row y's taps and dY row y, then wait
-  auto load_column = [&](int n, int strip, int y, int dslot) {
-    issue_x((y) & 3, n, y - 1, strip);
-    issue_x((y + 1) & 3, n, y, strip);
-    issue_x((y + 2) & 3, n, y + 1, strip);
-    issue_dy(dslot, n, y, strip);
-  };
-
   if (t0 < t1) {
     int n, strip, y;
     decode(t0, n, strip, y);
-    load_column(n, strip, y, 0);
-    vmcnt_wait<0>();
-    __builtin_amdgcn_s_barrier();
-    int dslot = 0;
-    for (long long t = t0; t < t1; ++t) {
-      // prefetch the next step while this one is multiplied: within a column one new input row (y + 2) and the
-      // next dY row; the slot of row y + 2 held row y - 2, last read by the previous step (behind the barrier)
-      const bool more = t + 1 < t1;
-      const bool same_col = more && y + 1 < H;
-      if (same_col) {
-        issue_x((y + 3) & 3, n, y + 2, strip);
-        issue_dy(dslot ^ 1, n, y + 1, strip);
+    long long t = t0;
+    while (true) {
+      // column start (the ring is idle): the three input rows of row y's taps and dY row y, then the rows of the
+      // next HD - 1 steps of this column
+      const int last = (int)min((long long)(H - 1), y + (t1 - 1 - t));   // last row of this column in the range
+      issue_x(xslot(y - 1), n, y - 1, strip);
+      issue_x(xslot(y), n, y, strip);
+      issue_x(xslot(y + 1), n, y + 1, strip);
+      issue_dy(y % HDS, n, y, strip);
+#pragma unroll
+      for (int d = 1; d < HD; ++d)
+        if (y + d <= last) {
+          issue_x(xslot(y + d + 1), n, y + d + 1, strip);
+          issue_dy((y + d) % HDS, n, y + d, strip);
+        }
+      for (;; ++y, ++t) {
+        // row y's pieces landed: only the later steps already issued (at most HD - 1) may stay in flight
+        ring_wait<H_NL, HD + 1>(min(HD - 1, last - y));
+        __builtin_amdgcn_s_barrier();   // every wave's pieces of row y landed; the slots of row y - 2 are idle
+        if (y + HD <= last) {
+          issue_x(xslot(y + HD + 1), n, y + HD + 1, strip);
+          issue_dy((y + HD) % HDS, n, y + HD, strip);
+        }
+        compute(y);
+        if (y == last) break;
       }
-      compute(y, dslot);
-      if (!more) break;
-      if (same_col) {
-        ++y;
-      } else {   // next column: every ring slot may be rewritten once all waves are done with this step
-        __builtin_amdgcn_s_barrier();
-        decode(t + 1, n, strip, y);
-        load_column(n, strip, y, dslot ^ 1);
-      }
-      dslot ^= 1;
-      vmcnt_wait<0>();
-      __builtin_amdgcn_s_barrier();   // every wave's pieces of the next step landed; the ring slot it frees is idle
+      ++t;
+      if (t >= t1) break;
+      lds_barrier();   // every wave is done with the ring before the next column rewrites it
+      decode(t, n, strip, y);
     }
   }
 
@@ -199,10 +211,10 @@ bool halo3_eligible(const ConvGeom& g, int dt) {
   if (g_knobs[11] < 0 || (dt != SSSEG_BF16 && dt != SSSEG_F16)) return false;
   return g.R == 3 && g.S == 3 && g.sy == 1 && g.sx == 1 && g.dy == 1 && g.dx == 1 && g.py == -1 && g.px == -1 &&
          g.OH == g.H && g.OW == g.W && g.W % 64 == 0 && g.C % 64 == 0 && g.K % 64 == 0 && g.ldx % 8 == 0 &&
-         g.ldy % 8 == 0 && g.ldx >= g.C && g.ldy >= g.K;
+         g.ldy % 8 == 0 && g.ldy >= g.K;   // ldx >= C unless a virtual concat supplies channels >= c1 (caller)
 }
 
-// split plan: ~2 resident blocks per CU over the chip, slabs capped at 32 MiB (>= one block per CU), splits shared out
+// split plan: 2 resident blocks per CU over the chip, slabs capped at 64 MiB (>= one block per CU), splits shared out
 // between the two pixel segments in proportion to their row steps
 HaloPlan halo3_plan(const ConvGeom& g, long long n1, long long n2) {
   HaloPlan p;
@@ -213,8 +225,9 @@ HaloPlan halo3_plan(const ConvGeom& g, long long n1, long long n2) {
   const long long st1 = n1 * p.nstrips * g.H, st2 = n2 * p.nstrips * g.H;
   const long long slab1 = 4LL * g.K * 9 * g.C;
   long long want = std::max<long long>(1, (512 + tiles - 1) / tiles);
-  const long long cap = std::max<long long>((256 + tiles - 1) / tiles, (32LL << 20) / slab1);
+  const long long cap = std::max<long long>((256 + tiles - 1) / tiles, (64LL << 20) / slab1);
   want = std::min(want, cap);
+  if (g_knobs[10] != 100 && g_knobs[10] > 0) want = std::max<long long>(1, want * g_knobs[10] / 100);   // A/B
   want = std::min<long long>(want, st1 + st2);
   long long a1 = n2 > 0 ? std::max<long long>(1, std::min(want - 1, (long long)((double)want * st1 / (st1 + st2) + 0.5)))
                         : want;
