@@ -813,6 +813,24 @@ __device__ __forceinline__ void bldslds16(__amdgpu_buffer_rsrc_t rs, char* lds_w
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)lds_wave_base, 16, voff, soff, 0, 0);
 }
 
+// The same LDS-DMA issued from inline asm, i.e. invisible to hipcc's s_waitcnt bookkeeping.  Kernels whose LDS reads
+// are ds_read_b64_tr_b16 need it: the transposed-read builtin carries no LDS alias scope, so for every such read hipcc
+// inserts an s_waitcnt vmcnt(0) on ALL outstanding LDS-DMA -- including the ring's prefetch issued just before the
+// compute, which serialises the pipeline (seen in the .s of wgrad_glds_kernel and wgrad_halo3_kernel; the ds_read_b128
+// fragments of igemm_glds_kernel carry the scope and get no such wait).  Completion is then counted only by the kernel's
+// own vmcnt_wait<> ring waits.  M0 (the LDS destination) is compiler-reserved: set and restored inside the statement.
+__device__ __forceinline__ void bldslds16_nt(__amdgpu_buffer_rsrc_t rs, char* lds_wave_base, unsigned voff,
+                                             unsigned soff) {
+  const unsigned la = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds_wave_base);
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rs), "s"(la), "s"(soff)
+      : "memory");
+}
+
 template <int N>
 __device__ __forceinline__ void vmcnt_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");

@@ -403,8 +403,8 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const T16* __r
               o2 = pix * (unsigned)sg.ldx2 * 2u + (unsigned)xcb[ii];
             }
           }
-          if (!xin2[ii]) bldslds16(xr, Xs + (wave * XI + ii) * 1024, o1, 0);
-          if (xin2[ii]) bldslds16(xr2, Xs + (wave * XI + ii) * 1024, o2, 0);
+          if (!xin2[ii]) bldslds16_nt(xr, Xs + (wave * XI + ii) * 1024, o1, 0);
+          if (xin2[ii]) bldslds16_nt(xr2, Xs + (wave * XI + ii) * 1024, o2, 0);
         }
       }
       if (xp[ii] < p_end) {
@@ -412,7 +412,7 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const T16* __r
         if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
           off = (unsigned)(((ximg[ii] * g.H + iy) * g.W + ix) * ldx) * 2u + (unsigned)xcb[ii];
       }
-      if (!strad) bldslds16(xr, Xs + (wave * XI + ii) * 1024, off, 0);
+      if (!strad) bldslds16_nt(xr, Xs + (wave * XI + ii) * 1024, off, 0);
       xp[ii] += BKP;
       if (BKP < g.OW) {   // at most one row wrap (wave-uniform test)
         xox[ii] += BKP;
@@ -430,7 +430,7 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const T16* __r
 #pragma unroll
     for (int jj = 0; jj < DI; ++jj) {
       const unsigned off = (dp[jj] < p_end && dcb[jj] >= 0) ? (unsigned)(dp[jj] * g.ldy * 2 + dcb[jj]) : OOB;
-      bldslds16(dr, Ds + (wave * DI + jj) * 1024, off, 0);
+      bldslds16_nt(dr, Ds + (wave * DI + jj) * 1024, off, 0);
       dp[jj] += BKP;
     }
   };

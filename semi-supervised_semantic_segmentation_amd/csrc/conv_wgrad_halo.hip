@@ -78,9 +78,9 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo3_kernel(HaloArgs a) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int i = 2 * wave + h;
-      bldslds16(xr, base + i * 1024, x_off(n, yy, 8 * i + lrow, strip), 0);
+      bldslds16_nt(xr, base + i * 1024, x_off(n, yy, 8 * i + lrow, strip), 0);
     }
-    if (lane < 16) bldslds16(xr, base + 8 * 1024 + wave * 256, x_off(n, yy, 64 + 2 * wave + lrow, strip), 0);
+    if (lane < 16) bldslds16_nt(xr, base + 8 * 1024 + wave * 256, x_off(n, yy, 64 + 2 * wave + lrow, strip), 0);
   };
   auto issue_dy = [&](int slot, int n, int y, int strip) {   // dY row y of the strip (64 pixels) -> dy slot
     char* base = smem + HXS * HX_SLOT + slot * HD_SLOT;
@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo3_kernel(HaloArgs a) {
       const int row = 8 * i + lrow;
       const unsigned off =
           (unsigned)(((n * H + y) * W + strip * 64 + row) * a.ldy + kb * 64) * 2u + (unsigned)chunk_of(row);
-      bldslds16(dr, base + i * 1024, off, 0);
+      bldslds16_nt(dr, base + i * 1024, off, 0);
     }
   };
   auto decode = [&](long long t, int& n, int& strip, int& y) {
