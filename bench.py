@@ -235,10 +235,15 @@ def timed_run(args, world, rank, device, dtype, probe=True):
     torch.cuda.synchronize()
     rows = []
     if probe:   # instrumented step: HIP events around every conv-engine launch (dominant kernel family)
+        # serial schedule for this one step: with the teacher pass overlapping the supervised backward on a side
+        # stream (train.train_step), concurrent kernels would stretch each other's event intervals
+        overlap = train._OVERLAP['teacher']
+        train._OVERLAP['teacher'] = False
         rows = snn.probe(True)
         one_step()
         snn.probe(False)
         torch.cuda.synchronize()
+        train._OVERLAP['teacher'] = overlap
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

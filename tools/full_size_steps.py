@@ -122,10 +122,12 @@ def run(name, path, dev, threshold=0.5, calibrate=True, layers=False):
     if layers:   # one more step with HIP events around every conv-engine launch (tools/layer_report.py format)
         sys.path.insert(0, os.path.join(ROOT, 'tools'))
         import layer_report
+        overlap, train._OVERLAP['teacher'] = train._OVERLAP['teacher'], False   # serial schedule for the probe
         rows = snn.probe(True)
         train.train_step(model, ema, opt, img, mask, ua, ub, 30, 3, cfg)
         snn.probe(False)
         torch.cuda.synchronize()
+        train._OVERLAP['teacher'] = overlap
         print(f'== {name} conv layers', file=sys.stderr)
         stdout, sys.stdout = sys.stdout, sys.stderr
         try:

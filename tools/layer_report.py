@@ -59,6 +59,7 @@ def main():
         img, mask, ua, ub = data[s % 2]
         train.train_step(model, teacher, opt, img, mask, ua, ub, 30, s, cfg)
     torch.cuda.synchronize()
+    train._OVERLAP['teacher'] = False   # per-launch event timings of the serial schedule (no concurrent teacher)
     rows = snn.probe(True)
     img, mask, ua, ub = data[1]
     train.train_step(model, teacher, opt, img, mask, ua, ub, 30, 3, cfg)
