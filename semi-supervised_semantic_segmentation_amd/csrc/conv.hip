@@ -83,6 +83,7 @@ int launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvGe
     case 21:
     case 22:
     case 23: return launch_glds_grp_e<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
+    case 24: return launch_hconv3<TO>(x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);   // halo-tiled 3x3 (-1: n/a)
     case 5:
     case 7:
     case 8:
@@ -95,10 +96,11 @@ int launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvGe
 // ---- bf16 variant choice: per-geometry autotune cache ----------------------------------------
 // Every variant accumulates the same 32-deep MFMA k-sequence in the same order, so the choice changes
 // speed, never results (tests/test_hip_layers.py::test_conv_variants_bitwise).  Variant 0 is the
-// register-staged kernel, 1..10 and 12..23 the LDS-DMA configs.  With knob 5 on (default) an unseen geometry is
-// timed once over the candidates on the caller's stream (HIP events) and the fastest is cached.
+// register-staged kernel, 1..10 and 12..23 the LDS-DMA configs, 24 the halo-tiled 3x3 kernel (conv_hconv3.hip; only
+// where it applies).  With knob 5 on (default) an unseen geometry is timed once over the candidates on the caller's
+// stream (HIP events) and the fastest is cached.
 constexpr int kSplitBit = 256;   // cached choice flag: run the variant with its split-K plan
-constexpr int kCandidates[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23};
+constexpr int kCandidates[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24};
 std::unordered_map<unsigned long long, int> g_variant;
 std::mutex g_variant_mu;
 
@@ -234,6 +236,10 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
                                        ph ? nullptr : wsv, ph, x2, (unsigned)x2b);
       // a forced config without a general-k instantiation (128/256-wide n-tiles, C % 64 != 0): register-staged
       if (r == -1 && g_knobs[4] != 0 && !x2 && g.C % 64) return run_variant<T, TO>(0, x, w, y, g, ep, 0, 0, s, nullptr, ph);
+      if (r == -1 && g_knobs[4] == 24) {   // the forced halo kernel does not apply to this launch: the heuristic's
+        const int hv = x2 && heuristic_variant(g) == 0 ? 5 : heuristic_variant(g);
+        return run_variant<T, TO>(hv, x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, nullptr, ph, x2, (unsigned)x2b);
+      }
       return r;
     }
   }

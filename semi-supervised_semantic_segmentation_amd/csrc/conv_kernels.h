@@ -411,10 +411,18 @@ template <int NP> struct PreRes {   // residual chunks an epilogue thread loaded
   bool on;
 };
 
-template <typename TO, int BM, int BN, int FM, int FN, int NT, bool STATS, int NPRE = 1>
+// T2D (the halo-tiled 3x3 kernel, conv_hconv3.hip): the tile is t2.rows image rows x 64 columns of image t2.n starting
+// at (t2.y0, t2.x0) instead of BM consecutive GEMM rows; its statistics row is t2.tile (output grid == GEMM grid)
+struct Tile2D {
+  int n, y0, x0, rows;
+  long long tile;
+};
+
+template <typename TO, int BM, int BN, int FM, int FN, int NT, bool STATS, int NPRE = 1, bool T2D = false>
 __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char* smem, long long m0, int n0, int wmo,
                                                int wno, int lane, const ConvGeom& g, TO* __restrict__ y,
-                                               const Epi<TO>& ep, PreRes<NPRE> pre = PreRes<NPRE>{{}, false}) {
+                                               const Epi<TO>& ep, PreRes<NPRE> pre = PreRes<NPRE>{{}, false},
+                                               Tile2D t2 = Tile2D{0, 0, 0, 0, 0}) {
   // pre: this thread's residual chunks, already loaded by the caller (one per pass; used where `full`)
   constexpr int LDR = BN * 4 + 16;   // bytes per staged pixel row
   __syncthreads();                   // every wave is done with the LDS ring
@@ -463,10 +471,15 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
       const int row = r0 + p * RPP;
-      const long long m = m0 + row;
       op[p] = -1;
-      if (row < BM && m < g.M) {
-        op[p] = out_pixel(g, (int)m);   // M < 2^31 (geom_ok)
+      if constexpr (T2D) {
+        if (row < BM && (row >> 6) < t2.rows)
+          op[p] = ((long long)t2.n * g.outH + t2.y0 + (row >> 6)) * g.outW + t2.x0 + (row & 63);
+      } else {
+        const long long m = m0 + row;
+        if (row < BM && m < g.M) {
+          op[p] = out_pixel(g, (int)m);   // M < 2^31 (geom_ok)
+        }
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) r[p][e] = 0.f;
@@ -532,7 +545,8 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
     }
   }
   if constexpr (STATS)
-    tile_stats<8, BN, NT / 64, SA>(s1, s2, CPR, (threadIdx.x & 63) < CPR, ch * 8, smem, m0 / BM, n0, ep.stats, ep.sld);
+    tile_stats<8, BN, NT / 64, SA>(s1, s2, CPR, (threadIdx.x & 63) < CPR, ch * 8, smem, T2D ? t2.tile : m0 / BM, n0,
+                                   ep.stats, ep.sld);
 }
 
 // fused statistics after store_tile (register epilogue): lane holds fp64 sums of fragment column i's 4
@@ -594,13 +608,14 @@ constexpr int ROWB = 80;   // 64 data bytes + 16 pad per LDS row
 extern int g_knobs[12];   // runtime variant switches (ssseg_set_knob), defined in conv.hip
 // 0: reg-staged pipeline depth; 1: split-K cap (-1 off = default, 0 auto: the autotuner also times each variant with
 // its split plan, fp32-atomic partials + finalize, and keeps it where faster); 2: 64x64 small-M tiles (reg-staged path);
-// 3: bf16 LDS-DMA path (0 on, -1 off); 4: variant (0 auto, 1..10 / 12..23 LDS-DMA config, 11 register-staged);
+// 3: bf16 LDS-DMA path (0 on, -1 off); 4: variant (0 auto, 1..10 / 12..23 LDS-DMA config, 11 register-staged, 24 the
+// halo-tiled 3x3 kernel where it applies);
 // 5: autotune unseen geometries (1 on, 0 = static heuristic); knob 6 = 1 clears the variant cache;
 // 7: LDS-staged coalesced epilogue in the LDS-DMA kernel (0 on, -1 off);
 // 8: bf16 weight gradient on the LDS-DMA kernel (0 on, -1 = register-staged wgrad_kernel);
 // 9: LDS-DMA weight-gradient tile variant (0 = the static plan, 1.. = a forced WGRAD_CFGS entry, conv_wgrad.hip);
-// 10: weight-gradient split count scale in percent (100 = the plan's); 11: halo-tiled 3x3 weight gradient
-// (conv_wgrad_halo.hip; 0 on, -1 = the split-K LDS-DMA kernel)
+// 10: weight-gradient split count scale in percent (100 = the plan's); 11: halo-tiled 3x3 kernels (conv_wgrad_halo.hip,
+// conv_hconv3.hip; 0 on, -1 = the split-K weight gradient and no variant 24)
 
 // STATS: the epilogue also writes the fused BatchNorm statistics partials (a separate instantiation: the fp64
 // sums raise the register count, which must not cost the launches that do not need them)
@@ -1280,6 +1295,12 @@ inline int plan_splits(const ConvGeom& g) {
   return (int)std::max<long long>(1, std::min<long long>(sp, 64));
 }
 
+
+// halo-tiled 3x3 / stride-1 / pad-1 forward (and stride-1 input-gradient) contraction, LDS-DMA variant 24 of the
+// autotuner (conv_hconv3.hip); returns the tile height 256, or -1 where it cannot run the launch
+template <typename TO>
+int launch_hconv3(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
+                  unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2, unsigned x2b);
 
 // halo-tiled 3x3 / stride-1 weight gradient (conv_wgrad_halo.hip)
 struct HaloSeg {

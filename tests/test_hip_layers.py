@@ -283,7 +283,7 @@ def test_conv_bn_act_fused_eval_grad(hip_device, mode, monkeypatch, kind, cin, c
     _close(mb.bias.grad, rb.bias.grad, mode, 'dbeta')
 
 
-ALL_VARIANTS = [11] + list(range(1, 11)) + list(range(12, 24))
+ALL_VARIANTS = [11] + list(range(1, 11)) + list(range(12, 25))
 
 
 @pytest.mark.parametrize('kind,cin,cout,k,H', [('conv', 64, 128, 3, 19), ('conv', 128, 64, 1, 17), ('conv', 192, 256, 3, 9),
@@ -293,23 +293,30 @@ ALL_VARIANTS = [11] + list(range(1, 11)) + list(range(12, 24))
                                                # C % 64 != 0: the general-k LDS-DMA loader (64-wide n-tiles)
                                                ('conv', 32, 32, 3, 33), ('conv', 16, 64, 3, 20), ('conv', 8, 48, 3, 17),
                                                ('conv', 48, 50, 3, 15), ('conv', 96, 64, 3, 13), ('conv', 50, 28, 1, 19),
-                                               ('conv_s2', 32, 64, 3, 26), ('convT', 32, 32, 4, 9)])
+                                               ('conv_s2', 32, 64, 3, 26), ('convT', 32, 32, 4, 9),
+                                               # W % 64 == 0, H % 4 == 0: the halo-tiled 3x3 kernel (variant 24)
+                                               ('conv64', 64, 64, 3, 8), ('conv64', 128, 128, 3, 12),
+                                               ('conv64', 192, 64, 3, 4), ('conv64', 64, 192, 3, 20)])
 def test_conv_variants_bitwise(hip_device, kind, cin, cout, k, H):
     """Every bf16 engine variant (register-staged, LDS-DMA tile configs 1..10 and 12..23) accumulates the
     same MFMA k-sequence: forward and input-gradient outputs are bit-identical, so autotuning never changes
     results.  C % 64 != 0 layers run the general-k loader on the 64-wide configs (the others fall back to the
-    register-staged kernel when forced), whose linear k order is the register-staged kernel's."""
+    register-staged kernel when forced), whose linear k order is the register-staged kernel's.  'conv64' maps
+    (W = 64 or 128) run the halo-tiled 3x3 kernel (variant 24) in the forward and the input gradient."""
     from ssseg import native as N
     from ssseg import nn as snn
     snn.set_compute_dtype(torch.bfloat16)
     torch.manual_seed(11)
+    Wd = H + 3
+    if kind == 'conv64':
+        kind, Wd = 'conv', 64 if cin != 64 or cout != 192 else 128
     if kind == 'conv':
         mod = snn.Conv2d(cin, cout, k, 1, k // 2, bias=False).to(hip_device)
     elif kind == 'conv_s2':
         mod = snn.Conv2d(cin, cout, k, 2, 0, bias=False).to(hip_device)
     else:
         mod = snn.ConvTranspose2d(cin, cout, k, 2, 1).to(hip_device)
-    x = _act_in(torch.randn(2, cin, H, H + 3), hip_device).detach().requires_grad_(True)
+    x = _act_in(torch.randn(2, cin, H, Wd), hip_device).detach().requires_grad_(True)
     outs = []
     try:
         for v in ALL_VARIANTS:
