@@ -111,7 +111,11 @@ def _scaled(loss, optimizer):
     return sc.scale(loss) if sc is not None else loss
 
 
-_OVERLAP = {'teacher': os.environ.get('SSSEG_OVERLAP_TEACHER', '1') != '0', 'streams': {}}
+# the first SERIAL_STEPS steps of a process run serially: the engine autotunes every new conv geometry on first use
+# (HIP-event timings, conv.hip tune_variant), and a teacher pass running concurrently on the side stream would skew
+# those timings -- and with them the variant choices kept for the rest of the run
+_OVERLAP = {'teacher': os.environ.get('SSSEG_OVERLAP_TEACHER', '1') != '0', 'streams': {}, 'steps': 0,
+            'serial_steps': 2}
 
 
 def _teacher_targets(ema_model, unsup_a, unsup_b, tc):
@@ -169,7 +173,9 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
     if adv is not None:
         adv_loss, prob = adversarial_terms(pred_maps, mask, adv)
         sup_loss = ops.add_scaled(sup_loss, adv_loss)
-    overlap = semi and adv is None and _OVERLAP['teacher'] and image.is_cuda and unsup_a.is_cuda
+    overlap = (semi and adv is None and _OVERLAP['teacher'] and image.is_cuda and unsup_a.is_cuda
+               and _OVERLAP['steps'] >= _OVERLAP['serial_steps'])
+    _OVERLAP['steps'] += 1
     targets = None
     if overlap:
         main = torch.cuda.current_stream()
