@@ -246,6 +246,18 @@ def timed_run(args, world, rank, device, dtype, probe=True):
         train._OVERLAP['teacher'] = overlap
     if world > 1:
         dist.barrier()
+    graph = None
+    if args.graph and world == 1:
+        # the step captured once as a HIP graph (ssseg.graph.StepGraph) and replayed: each replay copies the next
+        # batch into the captured input buffers and runs the whole step (fresh CowMix draws from the device counter)
+        from ssseg.graph import StepGraph
+        graph = StepGraph(lambda img, mask, ua, ub: train.train_step(model, teacher, opt, img, mask, ua, ub, 30, 2, cfg),
+                          *data[0])
+
+        def one_step():
+            out = graph(*data[step_idx[0] % len(data)])
+            step_idx[0] += 1
+            return tuple(t.clone() for t in out)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     e0 = torch.cuda.Event(enable_timing=True)
@@ -265,7 +277,7 @@ def timed_run(args, world, rank, device, dtype, probe=True):
         elapsed = float(t)
     live = torch.stack([torch.stack([c.float(), u.float(), m.float()]) for c, u, m in recs]).cpu()
     snn.set_compute_dtype(torch.bfloat16)
-    return elapsed, rows, live, model
+    return elapsed, rows, live, model, graph is not None
 
 
 def main():
@@ -277,6 +289,8 @@ def main():
     ap.add_argument('--size', type=int, default=512)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-fp32', action='store_true', help='skip the secondary fp32 (parity-mode) record')
+    ap.add_argument('--no-graph', dest='graph', action='store_false',
+                    help='issue every launch from Python each step instead of replaying the captured HIP graph')
     args = ap.parse_args()
 
     if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
@@ -292,7 +306,7 @@ def main():
               f'{dist.get_backend()}, device cuda:{local}', file=sys.stderr, flush=True)
     device = torch.device('cuda', local)
 
-    elapsed, rows, live, model = timed_run(args, world, rank, device, torch.bfloat16)
+    elapsed, rows, live, model, graphed = timed_run(args, world, rank, device, torch.bfloat16)
     finite = bool(torch.isfinite(live).all())
     if not finite:
         raise RuntimeError(f'bench: non-finite loss in the timed steps (rank {rank}): {live.tolist()}')
@@ -316,6 +330,8 @@ def main():
                      'traffic_unit': 'HBM bytes per step, conv engine (rocprofv3 PMC, ' + os.path.relpath(PMC_PROFILE, ROOT) + ')',
                      'conv_ms_per_step': round(conv_ms, 3), 'conv_gflop_per_step': round(conv_flops / 1e9, 1),
                      'launches_per_step': len(rows)},
+        'execution': ('HIP graph replay of the captured step (ssseg.graph.StepGraph), one per step' if graphed
+                      else 'eager launches from Python'),
         'step_tflops': round(8 * FWD_GFLOP_PER_IMAGE * args.batch * world / (elapsed / args.steps) / 1e3, 2),
         'liveness': {'losses_finite': finite, 'sup_loss_last': round(float(live[-1, 0]), 6),
                      'unsup_loss_last': round(float(live[-1, 1]), 6),
@@ -323,7 +339,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_fp32:
         try:
-            f_el, _, f_live, _ = timed_run(argparse.Namespace(**dict(vars(args), steps=min(args.steps, 5), warmup=2)),
+            f_el, _, f_live, _, _ = timed_run(argparse.Namespace(**dict(vars(args), steps=min(args.steps, 5), warmup=2)),
                                         world, rank, device, torch.float32, probe=False)
             n = min(args.steps, 5)
             result['fp32_mode'] = {'value': round(args.batch * n / f_el, 3), 'unit': 'images/sec',

@@ -63,6 +63,11 @@ int ssseg_normal_f32(float* out, int64_t n, uint64_t seed, uint64_t offset, ssse
  * same quantities from the CPU torch generator in the reference's order and uploads them. */
 int ssseg_cowmix_draw(float* p, float* sigma, float* noise, int64_t B, int64_t HW, double prop_lo, double prop_hi,
                       double sigma_lo, double sigma_hi, uint64_t seed, uint64_t offset, ssseg_stream_t stream);
+/* as ssseg_cowmix_draw with the Philox counter offset read from device memory and advanced there by
+ * B + ceil(B*HW/4) + 1 after the draw (the host form's sequence): a captured HIP graph replays fresh draws. */
+int ssseg_cowmix_draw_dev(float* p, float* sigma, float* noise, int64_t B, int64_t HW, double prop_lo, double prop_hi,
+                          double sigma_lo, double sigma_hi, uint64_t seed, unsigned long long* offset_dev,
+                          ssseg_stream_t stream);
 
 /* mix_with_mask (cowmix.py:72-73): out = a*m + b*(1-m), m [B,1,HW] broadcast over C.
  * a, b, out: [B,C,HW] (NCHW) of dtype `dt`; mask f32. */

@@ -17,7 +17,7 @@ from ssseg import native as N
 from ssseg import ops
 
 NOISE_SOURCE = 'device'
-_DEVICE_RNG = {'seed': None, 'offset': 0}
+_DEVICE_RNG = {'seed': None, 'ctr': {}}
 
 
 def generate_gaussian(window_size, sigma):
@@ -66,10 +66,15 @@ def draw_inputs(example_tensor, mask_proportion_range, sigma_range, source=None)
     sig = torch.empty(B, device=dev)
     noise = torch.empty(B, 1, H, W, device=dev)
     seed = _device_seed(dev)
-    N.call('ssseg_cowmix_draw', N.dev_ptr(p), N.dev_ptr(sig), N.dev_ptr(noise), B, H * W,
+    # the Philox counter lives in device memory and the draw advances it there (ssseg_cowmix_draw_dev): the same
+    # sequence as a host counter, and a captured HIP graph of the step (ssseg.graph) replays fresh draws
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    ctr = _DEVICE_RNG['ctr'].get(key)
+    if ctr is None:
+        ctr = _DEVICE_RNG['ctr'][key] = torch.zeros(1, dtype=torch.int64, device=dev)
+    N.call('ssseg_cowmix_draw_dev', N.dev_ptr(p), N.dev_ptr(sig), N.dev_ptr(noise), B, H * W,
            float(mask_proportion_range[0]), float(mask_proportion_range[1]), float(sigma_range[0]),
-           float(sigma_range[1]), seed, _DEVICE_RNG['offset'], N.stream())
-    _DEVICE_RNG['offset'] += B + (B * H * W + 3) // 4 + 1
+           float(sigma_range[1]), seed, N.dev_ptr(ctr), N.stream())
     return p, sig, noise
 
 

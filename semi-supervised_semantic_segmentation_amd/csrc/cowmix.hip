@@ -207,7 +207,15 @@ __device__ __forceinline__ void philox_round(unsigned (&c)[4], unsigned k0, unsi
   c[0] = n0; c[1] = n1; c[2] = n2; c[3] = n3;
 }
 
-__global__ void normal_kernel(float* out, int64_t n, uint64_t seed, uint64_t offset) {
+// the Philox counter offset from device memory (graph-replayable draws: every replay reads the advanced counter) or
+// from the argument
+__device__ __forceinline__ uint64_t rng_offset(const unsigned long long* dev, uint64_t host, uint64_t add) {
+  return (dev ? (uint64_t)*dev : host) + add;
+}
+
+__global__ void normal_kernel(float* out, int64_t n, uint64_t seed, uint64_t offset,
+                              const unsigned long long* offset_dev = nullptr, uint64_t add = 0) {
+  offset = rng_offset(offset_dev, offset, add);
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q * 4 < n; q += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t ctr = offset + (uint64_t)q;
     unsigned c[4] = {(unsigned)ctr, (unsigned)(ctr >> 32), 0u, 0u};
@@ -237,9 +245,10 @@ __global__ void normal_kernel(float* out, int64_t n, uint64_t seed, uint64_t off
 
 // p_b = lo + u*(hi-lo), sigma_b = exp(llo + u'*(lhi-llo)) from Philox uniforms (stream 1 of the key)
 __global__ void cowmix_draw_kernel(float* p, float* sigma, int B, float lo, float hi, float llo, float lhi, uint64_t seed,
-                                   uint64_t offset) {
+                                   uint64_t offset, const unsigned long long* offset_dev = nullptr) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
+  offset = rng_offset(offset_dev, offset, 0);
   unsigned c[4] = {(unsigned)(offset + b), (unsigned)((offset + b) >> 32), 1u, 0u};
   unsigned k0 = (unsigned)seed, k1 = (unsigned)(seed >> 32);
 #pragma unroll
@@ -252,6 +261,8 @@ __global__ void cowmix_draw_kernel(float* p, float* sigma, int B, float lo, floa
   p[b] = lo + u1 * (hi - lo);
   sigma[b] = expf(llo + u2 * (lhi - llo));
 }
+
+__global__ void rng_advance_kernel(unsigned long long* offset_dev, unsigned long long inc) { *offset_dev += inc; }
 
 template <typename T>
 __global__ void mix_kernel(const T* a, const T* b, const float* m, T* out, int64_t C, int64_t HW, int64_t total) {
@@ -313,6 +324,24 @@ extern "C" int ssseg_cowmix_draw(float* p, float* sigma, float* noise, int64_t B
   const int64_t n = B * HW;
   hipLaunchKernelGGL(normal_kernel, dim3(ssseg_grid((n + 3) / 4, 256)), dim3(256), 0, s, noise, n, seed,
                      offset + (uint64_t)B);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_cowmix_draw_dev(float* p, float* sigma, float* noise, int64_t B, int64_t HW, double prop_lo,
+                                     double prop_hi, double sigma_lo, double sigma_hi, uint64_t seed,
+                                     unsigned long long* offset_dev, ssseg_stream_t stream) {
+  if (!p || !sigma || !noise || !offset_dev || B < 1 || HW < 1 || sigma_lo <= 0 || sigma_hi <= 0) return SSSEG_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(cowmix_draw_kernel, dim3((B + 63) / 64), dim3(64), 0, s, p, sigma, (int)B, (float)prop_lo,
+                     (float)prop_hi, (float)log(sigma_lo), (float)log(sigma_hi), seed, (uint64_t)0,
+                     (const unsigned long long*)offset_dev);
+  const int64_t n = B * HW;
+  hipLaunchKernelGGL(normal_kernel, dim3(ssseg_grid((n + 3) / 4, 256)), dim3(256), 0, s, noise, n, seed, (uint64_t)0,
+                     (const unsigned long long*)offset_dev, (uint64_t)B);
+  // the same advance as the host-counter form: B + ceil(B*HW / 4) + 1
+  hipLaunchKernelGGL(rng_advance_kernel, dim3(1), dim3(1), 0, s, offset_dev,
+                     (unsigned long long)(B + (n + 3) / 4 + 1));
   SSSEG_LAUNCH_CHECK();
   return 0;
 }

@@ -1,0 +1,37 @@
+"""One training step captured as a HIP graph and replayed (torch.cuda.CUDAGraph is hipGraph on ROCm).
+
+A C2 step is ~1,000 kernel launches, a C4 (MultiscaleAttention over HRNet-W32) step ~10,000 mostly small ones: issued
+from Python through ctypes, the host falls behind the device on the small-map layers and the GPU idles between
+launches.  Captured once, a step replays as one graph launch.
+
+Everything the step launches is capture-safe by construction: no call allocates outside the caching allocator or
+synchronises (include/ssseg.h), the conv autotuner falls back to its cached / heuristic choice while a stream is
+capturing (so run at least one eager step first: it tunes every geometry), and the CowMix draws read and advance a
+device-side Philox counter (ssseg_cowmix_draw_dev), so every replay draws fresh masks -- the same sequence the eager
+steps would.  Host-side values are baked in at capture: a replay repeats the captured step's Python decisions (the
+optimizer step taken or skipped, the epoch gate of the consistency weight, the learning rate), so capture a step with
+step != 0 and recapture when those change.  Single process only (the RCCL collectives of a DDP step are not captured).
+
+    step = StepGraph(lambda img, mask, ua, ub: train.train_step(model, teacher, opt, img, mask, ua, ub, epoch, 1, cfg),
+                     img, mask, ua, ub)
+    cls, unsup, cm = step(img2, mask2, ua2, ub2)    # copies the inputs into the captured buffers, replays
+"""
+import torch
+
+
+class StepGraph:
+    def __init__(self, fn, *example_inputs, warmup=0):
+        self.static_in = [t.detach().clone() for t in example_inputs]
+        for _ in range(warmup):   # eager steps first (they tune every conv geometry); callers usually ran them
+            fn(*self.static_in)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.static_out = fn(*self.static_in)
+
+    def __call__(self, *inputs):
+        for dst, src in zip(self.static_in, inputs):
+            if src is not dst:
+                dst.copy_(src, non_blocking=True)
+        self.graph.replay()
+        return self.static_out

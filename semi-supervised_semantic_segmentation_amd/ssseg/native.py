@@ -29,6 +29,7 @@ SIGS = {
     'ssseg_normal_f32': (i32, [vp, i64, u64, u64, vp]),
     'ssseg_mix': (i32, [vp, vp, vp, vp, i64, i64, i64, i32, vp]),
     'ssseg_cowmix_draw': (i32, [vp, vp, vp, i64, i64, f64, f64, f64, f64, u64, u64, vp]),
+    'ssseg_cowmix_draw_dev': (i32, [vp, vp, vp, i64, i64, f64, f64, f64, f64, u64, vp, vp]),
     'ssseg_nchw_to_nhwc': (i32, [vp, vp, i64, i64, i64, i64, i64, i32, i32, vp]),
     'ssseg_nhwc_to_nchw': (i32, [vp, vp, i64, i64, i64, i64, i64, i32, i32, vp]),
     'ssseg_cast': (i32, [vp, vp, i64, i32, i32, vp]),
