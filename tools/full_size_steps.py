@@ -64,15 +64,18 @@ def calibrate_bn(model, x):
         m.momentum = mo
 
 
-def run(name, path, dev, threshold=0.5, calibrate=True, layers=False):
+def build(name, path, dev, threshold=0.5, calibrate=True):
+    """model / teacher / optimizer / config / synthetic batch of config `name`, deterministic (seed 0)"""
     import config
+    import cowmix
     import mean_teacher
-    import train
     from ssseg import amp, arena
     from ssseg import nn as snn
     from ssseg import optim as soptim
     from ssseg.ddp import DistributedDataParallel
     torch.manual_seed(0)
+    for c in cowmix._DEVICE_RNG['ctr'].values():   # the CowMix Philox counter restarts with every build
+        c.zero_()
     cfg = config.fromfile(os.path.join(PKG, path))
     snn.set_compute_dtype({'fp32': torch.float32, 'fp16': torch.float16}.get(cfg['common'].get('compute_dtype'),
                                                                              torch.bfloat16))
@@ -109,9 +112,40 @@ def run(name, path, dev, threshold=0.5, calibrate=True, layers=False):
         calibrate_bn(model.module, ua)
     with torch.no_grad():   # after the calibration: the teacher's own BN buffers are used until the first EMA update
         ema.load_state_dict(model.module.state_dict())
+    return model, ema, opt, cfg, tc, (img, mask, ua, ub), b, s
+
+
+def graph_steps(name, path, dev, threshold, calibrate, eager_losses, n_eager=3, n_replay=5):
+    """Rebuild the config, run the same first n_eager eager steps, capture step n_eager as a HIP graph
+    (ssseg.graph.StepGraph) and replay it: the replayed steps' losses must equal the eager run's bit for bit; returns
+    (ms per replayed step, bitwise flag, replayed losses)."""
+    import train
+    from ssseg.graph import StepGraph
+    model, ema, opt, cfg, tc, data, _, _ = build(name, path, dev, threshold, calibrate)
+    for step in range(n_eager):
+        train.train_step(model, ema, opt, *data, 30, step, cfg)
+    g = StepGraph(lambda i, m, a, b: train.train_step(model, ema, opt, i, m, a, b, 30, n_eager, cfg), *data)
+    out = []
+    for _ in range(2):
+        out.append(tuple(None if t is None else float(t) for t in g(*data)))
+    same = out == [tuple(v for v in row) for row in eager_losses[n_eager:n_eager + 2]]
+    torch.cuda.synchronize()
+    t0 = time.time()
+    for _ in range(n_replay):
+        g(*data)
+    torch.cuda.synchronize()
+    ms = 1e3 * (time.time() - t0) / n_replay
+    del g, model, ema, opt
+    return ms, same, out
+
+
+def run(name, path, dev, threshold=0.5, calibrate=True, layers=False, graph=False):
+    import train
+    from ssseg import nn as snn
+    model, ema, opt, cfg, tc, (img, mask, ua, ub), b, s = build(name, path, dev, threshold, calibrate)
     torch.cuda.reset_peak_memory_stats(dev)
     times, out = [], []
-    for step in range(3):
+    for step in range(5 if graph else 3):
         torch.cuda.synchronize()
         t0 = time.time()
         cls, unsup, cm = train.train_step(model, ema, opt, img, mask, ua, ub, 30, step, cfg)
@@ -139,9 +173,9 @@ def run(name, path, dev, threshold=0.5, calibrate=True, layers=False):
     rec = {'config': name, 'image_size': s, 'batch': b, 'dtype': str(snn.compute_dtype()).replace('torch.', ''),
            'confidence_threshold': threshold, 'bn_calibrated': calibrate,
            'cm_mean': [row[2] for row in out], 'losses': out, 'losses_finite': losses_finite, 'params_finite': params_finite,
-           'ms_per_step_last2': round(1e3 * sum(times[1:]) / 2, 1), 'first_step_s': round(times[0], 1),
+           'ms_per_step_last2': round(1e3 * sum(times[-2:]) / 2, 1), 'first_step_s': round(times[0], 1),
            'peak_mem_GB': round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)}
-    step_s = sum(times[1:]) / 2
+    step_s = sum(times[-2:]) / 2
     tf = STEP_GFLOP_PER_IMAGE[name] * b / step_s / 1e3
     rec['conv_tflops'] = round(tf, 1)
     rec['frac_of_dense_peak'] = round(tf * 1e12 / PEAK[rec['dtype']], 4)
@@ -149,6 +183,13 @@ def run(name, path, dev, threshold=0.5, calibrate=True, layers=False):
         rec['conv_engine'] = conv
     if 'adversarial' in tc:
         rec['loss_d'] = float(tc['adversarial']['last_loss_d'])
+    if graph:   # the same steps replayed from a captured HIP graph (fresh build, same seeds)
+        del model, ema, opt
+        torch.cuda.empty_cache()
+        gms, same, gl = graph_steps(name, path, dev, threshold, calibrate, out)
+        rec['graph'] = {'ms_per_step': round(gms, 1), 'losses_bitwise_equal_eager': same, 'losses_steps_3_4': gl,
+                        'frac_of_dense_peak': round(STEP_GFLOP_PER_IMAGE[name] * b / (gms / 1e3) / 1e3 * 1e12 /
+                                                    PEAK[rec['dtype']], 4)}
     print(json.dumps(rec), flush=True)
     return rec['losses_finite'] and rec['params_finite']
 
@@ -159,13 +200,15 @@ def main():
     ap.add_argument('--threshold', type=float, default=0.5)
     ap.add_argument('--no-calibrate', action='store_true')
     ap.add_argument('--layers', action='store_true', help='per-layer conv report of one extra step (stderr)')
+    ap.add_argument('--graph', action='store_true', help='also replay a captured HIP graph of the step (5 eager steps '
+                    'first; graph losses checked bitwise against eager steps 3 and 4)')
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     dist.init_process_group('nccl', init_method='tcp://127.0.0.1:29533', rank=0, world_size=1)
     ok = True
     for name in a.configs.split(','):
-        ok &= run(name, CFGS[name], dev, a.threshold, not a.no_calibrate, a.layers)
+        ok &= run(name, CFGS[name], dev, a.threshold, not a.no_calibrate, a.layers, a.graph)
         torch.cuda.empty_cache()
     dist.destroy_process_group()
     sys.exit(0 if ok else 1)
