@@ -187,6 +187,24 @@ int ssseg_lovasz_fwd(const float* logits, const float* target, int64_t B, int64_
 int ssseg_lovasz_bwd(const float* logits, const float* target, int64_t B, int64_t C, int64_t HW,
                      const float* gout, float* grad_out, void* ws, size_t ws_bytes, ssseg_stream_t stream);
 
+/* RMILoss, sigmoid form (losses.RMILoss.forward -> forward_sigmoid -> rmi_lower_bound, losses.py:480-592; the
+ * default-config loss, configs/default_config.py:147).  logits, target [N,C,H,W] f32 contiguous.
+ * pool (k, s, pad): avg_pool2d(k, s, pad, count_include_pad) of losses.py:534-538 (k == s, pad = k/2; (1,1,0) for
+ * rmi_pool='none' or stride <= 1).  radius 1..3 (rmi_radius; D = radius^2 <= 9).  (N*C) % num_classes == 0.
+ * Forward: loss_out[0] = sum_k float(mean over rows of rmi.view(-1, num_classes)[:, k]) / D, rmi per (n, c) from
+ * fp64 centred covariances, inverse and Cholesky log-det.  want_grad != 0 also leaves the backward coefficients in
+ * ws; ssseg_rmi_bwd (same ws, same geometry) then writes grad_out [N,C,H,W] = gout[0] * d loss / d logits.
+ * A non-positive-definite matrix gives a NaN loss (the reference's torch.cholesky raises).  Workspace 0 = the
+ * geometry is not supported. */
+size_t ssseg_rmi_workspace_bytes(int64_t N, int64_t C, int64_t H, int64_t W, int64_t num_classes, int64_t radius,
+                                 int64_t pool_k, int64_t pool_s, int64_t pool_pad);
+int ssseg_rmi_fwd(const float* logits, const float* target, int64_t N, int64_t C, int64_t H, int64_t W,
+                  int64_t num_classes, int64_t radius, int64_t pool_k, int64_t pool_s, int64_t pool_pad, int want_grad,
+                  float* loss_out, void* ws, size_t ws_bytes, ssseg_stream_t stream);
+int ssseg_rmi_bwd(const float* logits, int64_t N, int64_t C, int64_t H, int64_t W, int64_t num_classes,
+                  int64_t radius, int64_t pool_k, int64_t pool_s, int64_t pool_pad, const float* gout,
+                  float* grad_out, void* ws, size_t ws_bytes, ssseg_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Teacher EMA and optimiser over flat parameter arenas
  * ------------------------------------------------------------------------------------------- */

@@ -304,6 +304,48 @@ def lovasz_binary(logits, target, valid_weighted=True):
 
 
 # ------------------------------------------------------------------------------------------------
+# RMILoss (losses.py:271-592, sigmoid form)
+# ------------------------------------------------------------------------------------------------
+class _RMI(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, geo):
+        logits, target = _c(logits.float()), _c(target.float())
+        Nn, C, H, W = logits.shape
+        nb = N.lib().ssseg_rmi_workspace_bytes(Nn, C, H, W, *geo)
+        if nb == 0:
+            raise ValueError(f'RMILoss: geometry {tuple(logits.shape)} / (num_classes, radius, k, s, pad) = {geo} '
+                             'is not supported')
+        # the workspace carries the pooled maps and the backward coefficients to backward: a tensor of its own
+        ws = torch.empty(nb, dtype=torch.uint8, device=logits.device)
+        out = torch.empty((), device=logits.device, dtype=torch.float32)
+        want = int(ctx.needs_input_grad[0])
+        N.call('ssseg_rmi_fwd', N.dev_ptr(logits, 'logits'), N.dev_ptr(target, 'target'), Nn, C, H, W, *geo, want,
+               N.dev_ptr(out), N.dev_ptr(ws), nb, N.stream())
+        if want:
+            ctx.save_for_backward(logits, ws)
+        ctx.geo = geo
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, ws = ctx.saved_tensors
+        Nn, C, H, W = logits.shape
+        gx = torch.empty_like(logits)
+        g = _c(g.float())
+        N.call('ssseg_rmi_bwd', N.dev_ptr(logits), Nn, C, H, W, *ctx.geo, N.dev_ptr(g), N.dev_ptr(gx), N.dev_ptr(ws),
+               ws.numel(), N.stream())
+        return gx, None, None
+
+
+def rmi_loss(logits, target, num_classes, radius, pool_k, pool_s, pool_pad):
+    """RMILoss.forward (losses.py:480-592) on the device: sigmoid probabilities, avg pool (k, s, pad; (1, 1, 0) =
+    none), fp64 region covariances and Cholesky log-det per (image, class), summed over classes."""
+    if logits.dim() != 4 or tuple(logits.shape) != tuple(target.shape):
+        raise ValueError(f'RMILoss: logits {tuple(logits.shape)} and target {tuple(target.shape)} must be the same NCHW shape')
+    return _RMI.apply(logits, target, (int(num_classes), int(radius), int(pool_k), int(pool_s), int(pool_pad)))
+
+
+# ------------------------------------------------------------------------------------------------
 # Multi-scale attention blend (multiscale_attention.py:52-54)
 # ------------------------------------------------------------------------------------------------
 class _AttBlend(torch.autograd.Function):

@@ -26,8 +26,10 @@ Fixture index:
                         C4's model family; DDP gloo world 1), fp32 and fp64; parameters / BN buffers after the steps
                         as seeded index samples                            (reference/train.py:41-130,
                         models/multiscale_attention.py:38-58)
+  G12 rmi_*.npz         RMILoss forward + input gradient: the default-config RMI (radius 3, avg pool 4/4) and two
+                        generic cases (3 classes / radius 2 / pool 3; radius 1 / no pooling)  (reference/losses.py:271-592)
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py [all | models2 | metrics | msa_trainsteps]
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py [all | models2 | metrics | msa_trainsteps | rmi]
 """
 import os
 import sys
@@ -45,6 +47,7 @@ sys.modules.setdefault('kornia', types.ModuleType('kornia'))
 
 import torch  # noqa: E402
 import torch.nn as nn  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
 
 import cowmix  # noqa: E402  (reference)
 import losses  # noqa: E402
@@ -561,7 +564,47 @@ def gen_inference():
     save('inference.npz', logits=logits, image_hw=np.asarray([75, 101]), mask=mask, prob=prob)
 
 
+# ----------------------------------------------------------------------------------------------
+# G12: RMILoss
+# ----------------------------------------------------------------------------------------------
+RMI_CASES = {
+    # name: (N, C, H, W, RMILoss kwargs, gout)
+    'rmi_a': (2, 2, 91, 70, dict(num_classes=2, rmi_radius=3, rmi_pool='avg', rmi_pool_size=4, rmi_pool_stride=4), 1.0),
+    'rmi_b': (2, 3, 50, 47, dict(num_classes=3, rmi_radius=2, rmi_pool='avg', rmi_pool_size=3, rmi_pool_stride=3), 0.5),
+    'rmi_c': (3, 2, 12, 9, dict(num_classes=2, rmi_radius=1, rmi_pool='none', rmi_pool_size=4, rmi_pool_stride=4), 2.0),
+}
+
+
+def gen_rmi():
+    """The reference's RMILoss on the CPU.  Its one device-specific line is `.type(torch.cuda.DoubleTensor)`
+    (losses.py:549-550); torch.cuda.DoubleTensor is mapped to torch.DoubleTensor for the call (the arithmetic is
+    the reference's own: fp32 pooling, fp64 covariances, torch.inverse, torch.cholesky).  Inputs: seeded logits with
+    saturated patches (the clamp at losses.py:515) and one-hot blob targets (configs/default_config.py:147 shape)."""
+    saved = torch.cuda.DoubleTensor
+    torch.cuda.DoubleTensor = torch.DoubleTensor
+    try:
+        for i, (name, (N, C, H, W, kw, gout)) in enumerate(RMI_CASES.items()):
+            g = torch.Generator().manual_seed(61 + i)
+            logits = torch.randn(N, C, H, W, generator=g) * 3.0
+            logits[0, 0, :5, :7] = 25.0                       # sigmoid == 1.0 in fp32 (clamp max, inclusive)
+            logits[-1, -1, -4:, -6:] = -30.0                  # sigmoid < 1e-6 (clamped, zero gradient)
+            blob = F.avg_pool2d(torch.rand(N, 1, H, W, generator=g), 5, 1, 2) > 0.5
+            lab = torch.randint(0, C, (N, 1, H, W), generator=g)
+            lab = torch.where(blob, lab, torch.zeros_like(lab))
+            target = torch.zeros(N, C, H, W).scatter_(1, lab, 1.0)
+            x = logits.clone().requires_grad_(True)
+            loss = losses.RMILoss(**kw)(x, target)
+            loss.backward(torch.tensor(gout))
+            save(f'{name}.npz', logits=logits, target=target, loss=loss.detach(), grad=x.grad, gout=np.float32(gout),
+                 **{k: np.asarray(v) for k, v in kw.items()})
+    finally:
+        torch.cuda.DoubleTensor = saved
+
+
 if __name__ == '__main__':
+    if len(sys.argv) > 1 and sys.argv[1] == 'rmi':
+        gen_rmi()
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == 'metrics':
         gen_metrics()
         gen_inference()

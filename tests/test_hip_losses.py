@@ -7,7 +7,7 @@ import pytest
 import torch
 
 from conftest import golden
-from oracle import cowmix_ref, losses_ref
+from oracle import cowmix_ref, losses_ref, rmi_ref
 
 pytestmark = pytest.mark.gpu
 
@@ -352,3 +352,77 @@ def test_reversible_augmentations_roundtrip(hip_device):
     assert small.shape[2] == int(64 * res.scale)
     back = res.reverse([small])[0]
     assert back.shape[2] in (63, 64)
+
+
+def _rmi_hip(x, t, dev, gout=1.0, **kw):
+    import losses as L
+    mod = L.RMILoss(num_classes=kw['num_classes'], rmi_radius=kw['radius'], rmi_pool=kw['pool'],
+                    rmi_pool_size=kw['pool_size'], rmi_pool_stride=kw['pool_stride'])
+    xd = torch.from_numpy(np.ascontiguousarray(x)).to(dev).requires_grad_(True)
+    loss = mod(xd, torch.from_numpy(np.ascontiguousarray(t)).to(dev))
+    loss.backward(torch.tensor(gout, device=dev))
+    return float(loss.detach().cpu()), xd.grad.cpu().numpy()
+
+
+def _rmi_kw(g):
+    return dict(num_classes=int(g['num_classes']), radius=int(g['rmi_radius']), pool=str(g['rmi_pool']),
+                pool_size=int(g['rmi_pool_size']), pool_stride=int(g['rmi_pool_stride']))
+
+
+@pytest.mark.parametrize('case', ['rmi_a', 'rmi_b', 'rmi_c'])
+def test_rmi_vs_reference_golden(hip_device, case):
+    """G12 (the reference's RMILoss: default config radius 3 / avg pool 4, 3 classes / radius 2 / pool 3, radius 1 /
+    no pooling; saturated logits on both clamp bounds).  fp64 algebra in a different order (Cholesky-based inverse vs
+    torch.inverse's LU): loss within 2e-6 relative, gradient within 1e-4 relative of the largest entry."""
+    g = golden(f'{case}.npz')
+    loss, grad = _rmi_hip(g['logits'], g['target'], hip_device, gout=float(g['gout']), **_rmi_kw(g))
+    np.testing.assert_allclose(loss, float(g['loss']), rtol=2e-6)
+    scale = float(np.abs(g['grad']).max())
+    np.testing.assert_allclose(grad, g['grad'], rtol=1e-3, atol=1e-4 * scale)
+    assert (grad[g['logits'] < -20] == 0).all()
+
+
+def _rmi_inputs(N, C, H, W, seed):
+    rng = np.random.default_rng(seed)
+    x = (rng.standard_normal((N, C, H, W)) * 2.5).astype(np.float32)
+    lab = rng.integers(0, C, size=(N, 1, H, W))
+    lab = np.where(rng.random((N, 1, H, W)) > 0.3, lab, 0)
+    t = (np.arange(C).reshape(1, C, 1, 1) == lab).astype(np.float32)
+    return x, t
+
+
+@pytest.mark.parametrize('N,C,H,W,kw', [
+    (16, 2, 512, 512, dict(num_classes=2, radius=3, pool='avg', pool_size=4, pool_stride=4)),   # C2 shape, default RMI
+    (2, 2, 91, 70, dict(num_classes=2, radius=3, pool='avg', pool_size=4, pool_stride=4)),      # uncovered last row
+    (4, 2, 37, 29, dict(num_classes=2, radius=2, pool='none', pool_size=2, pool_stride=2)),
+    (1, 4, 9, 9, dict(num_classes=2, radius=3, pool='avg', pool_size=2, pool_stride=2)),        # rows = N*C/ncls
+])
+def test_rmi_vs_oracle(hip_device, N, C, H, W, kw):
+    """Device RMILoss vs the pinned oracle (rmi_ref) at the bench shape (bs 16, 512^2: 16129 positions per series,
+    4 covariance chunks) and small / odd geometries; same tolerances as the golden test."""
+    x, t = _rmi_inputs(N, C, H, W, N * 100 + H)
+    loss, grad = _rmi_hip(x, t, hip_device, gout=0.75, **kw)
+    ref_l, ref_g = rmi_ref.rmi_loss_and_grad(x, t, gout=0.75, **kw)
+    np.testing.assert_allclose(loss, float(ref_l), rtol=2e-6)
+    np.testing.assert_allclose(grad, ref_g, rtol=1e-3, atol=1e-4 * float(np.abs(ref_g).max()))
+
+
+def test_rmi_deterministic_and_default_config_combo(hip_device):
+    """Two runs are bitwise equal; the default config's CalculateLoss (BCE 0.5 + RMI 0.5, configs/default_config.py:
+    141-148) on the device matches 0.5 * oracle BCE + 0.5 * oracle RMI."""
+    import losses as L
+    x, t = _rmi_inputs(4, 2, 128, 96, 5)
+    a = _rmi_hip(x, t, hip_device, **dict(num_classes=2, radius=3, pool='avg', pool_size=4, pool_stride=4))
+    b = _rmi_hip(x, t, hip_device, **dict(num_classes=2, radius=3, pool='avg', pool_size=4, pool_stride=4))
+    assert a[0] == b[0] and np.array_equal(a[1], b[1])
+    crit = L.CalculateLoss([
+        {'loss_fn': L.DenseBinaryCrossEntropyLossWithLogits(reduction='mean'), 'weight': [0.5]},
+        {'loss_fn': L.RMILoss(num_classes=2, rmi_radius=3, rmi_pool='avg', rmi_pool_size=4, rmi_pool_stride=4),
+         'weight': [0.5]}])
+    xd = torch.from_numpy(x).to(hip_device)
+    tot = float(crit([xd], torch.from_numpy(t).to(hip_device)).cpu())
+    ref_bce = losses_ref.bce_logits_mean(x, t)
+    ref_bce = ref_bce[0] if isinstance(ref_bce, tuple) else ref_bce
+    ref_rmi, _ = rmi_ref.rmi_loss_and_grad(x, t)
+    np.testing.assert_allclose(tot, 0.5 * float(ref_bce) + 0.5 * float(ref_rmi), rtol=1e-5)
+

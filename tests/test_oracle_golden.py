@@ -6,7 +6,7 @@ import pytest
 import torch
 
 from conftest import golden
-from oracle import cowmix_ref, losses_ref, models_ref, train_ref
+from oracle import cowmix_ref, losses_ref, models_ref, rmi_ref, train_ref
 
 COWMIX_CASES = ['a0', 'a1', 'a2', 'b3', 'c0']
 
@@ -55,6 +55,21 @@ def test_binary_lovasz():
     np.testing.assert_allclose(loss, g['loss'], rtol=1e-5)
     np.testing.assert_allclose(grad, g['grad'], rtol=1e-4, atol=1e-7)
     assert np.all(grad[:, 0] == 0)
+
+
+def rmi_kwargs(g):
+    return dict(num_classes=int(g['num_classes']), radius=int(g['rmi_radius']), pool=str(g['rmi_pool']),
+                pool_size=int(g['rmi_pool_size']), pool_stride=int(g['rmi_pool_stride']))
+
+
+@pytest.mark.parametrize('case', ['rmi_a', 'rmi_b', 'rmi_c'])
+def test_rmi(case):
+    """G12: the RMILoss restatement reproduces the reference's loss and input gradient (bitwise on this torch)."""
+    g = golden(f'{case}.npz')
+    loss, grad = rmi_ref.rmi_loss_and_grad(g['logits'], g['target'], gout=float(g['gout']), **rmi_kwargs(g))
+    np.testing.assert_allclose(loss, g['loss'], rtol=1e-6)
+    np.testing.assert_allclose(grad, g['grad'], rtol=1e-5, atol=1e-9)
+    assert (grad[g['logits'] < -20] == 0).all()          # sigmoid < 1e-6: clamped, no gradient
 
 
 def test_ema():
