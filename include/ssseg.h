@@ -176,7 +176,7 @@ int ssseg_consistency_bwd(const float* s, const float* t, int64_t B, int64_t C, 
                           const float* out3, const float* gout, float* gs, ssseg_stream_t stream);
 
 /* Binary Lovász (losses.binary_lovasz_loss_with_logits losses.py:239-250 -> lovasz_softmax
- * lovasz.py:155-201 with classes=[1], per_image=True).  logits, target [B,C,HW] f32.
+ * lovasz.py:155-201 with classes=[1], per_image=True).  logits, target [B,C,HW] f32, 1 <= B <= 4096.
  * Per image: labels = argmax_c target, e = |[label==1] - logit1|, sort e descending, Lovász gradient
  * (lovasz_grad lovasz.py:19-31) by a scan, loss_b = <e_sorted, grad>;
  * loss_out[0] = sum_b loss_b*valid_b / (sum valid + 0.001).  grad_out (nullable) [B,C,HW]:
@@ -574,6 +574,11 @@ int ssseg_add_n(const void* const* xs_host, int n, void* y, int64_t numel, int a
  * with the same (seed, offset).  n % 4 == 0. */
 int ssseg_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, uint64_t offset, int dt,
                   ssseg_stream_t stream);
+/* as ssseg_dropout with the Philox counter offset read from device memory (a captured HIP graph replays fresh masks) */
+int ssseg_dropout_dev(const void* x, void* y, int64_t n, float p, uint64_t seed, const unsigned long long* offset_dev,
+                      int dt, ssseg_stream_t stream);
+/* device-side counter reservation: snap[0] = counter[0]; counter[0] += inc (one thread, in stream order) */
+int ssseg_rng_take(unsigned long long* counter, unsigned long long* snap, uint64_t inc, ssseg_stream_t stream);
 /* MultiscaleAttention blend (multiscale_attention.py:52-54), fp32 [N][C][H][W] with arbitrary strides:
  * out = lo*s + hi*(1-s), s = sigmoid(att[n][0][h][w]); out contiguous NCHW. */
 int ssseg_att_blend_fwd(const float* lo, const int64_t* lo_strides4_host, const float* hi,

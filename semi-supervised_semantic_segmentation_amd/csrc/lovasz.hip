@@ -241,19 +241,34 @@ __global__ void __launch_bounds__(LT) lovasz_grad_kernel(const unsigned* __restr
   }
 }
 
-// loss and the per-image scale valid_b / denom (kept in ws for the gradient)
-__global__ void lovasz_final_kernel(const double* __restrict__ dots, const unsigned* __restrict__ tile_fg, int B, int T,
-                                    float* __restrict__ loss_out, float* __restrict__ wscale) {
+// loss and the per-image scale valid_b / denom (kept in ws for the gradient).  One wave per image sums its T tile
+// dots (lane-strided, then a fixed xor tree: deterministic); lane 0 of block thread 0 combines the B images in order.
+// (A single thread walking all B*T dots was a chain of dependent loads: 122 us at B=16, T=128.)
+constexpr int FIN_T = 1024;
+__global__ void __launch_bounds__(FIN_T) lovasz_final_kernel(const double* __restrict__ dots,
+                                                             const unsigned* __restrict__ tile_fg, int B, int T,
+                                                             float* __restrict__ loss_out, float* __restrict__ wscale) {
+  extern __shared__ double img_dot[];   // [B] dots, then [B] valid flags
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = FIN_T / 64;
+  for (int b = wv; b < B; b += nw) {
+    double s = 0.0;
+    for (int t = lane; t < T; t += 64) s += dots[(int64_t)b * T + t];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) {
+      img_dot[b] = s;
+      img_dot[B + b] = tile_fg[(int64_t)b * (T + 1) + T] > 0 ? 1.0 : 0.0;
+    }
+  }
+  __syncthreads();
   if (threadIdx.x != 0) return;
   float nvalid = 0.f;
-  for (int b = 0; b < B; ++b) nvalid += tile_fg[(int64_t)b * (T + 1) + T] > 0 ? 1.f : 0.f;
+  for (int b = 0; b < B; ++b) nvalid += (float)img_dot[B + b];
   const float denom = nvalid + 0.001f;
   float total = 0.f;
   for (int b = 0; b < B; ++b) {
-    double s = 0.0;
-    for (int t = 0; t < T; ++t) s += dots[(int64_t)b * T + t];
-    const float valid = tile_fg[(int64_t)b * (T + 1) + T] > 0 ? 1.f : 0.f;
-    total += (float)s * valid;   // losses.py:248: loss += lovasz_softmax(...) * mask_sample
+    const float valid = (float)img_dot[B + b];
+    total += (float)img_dot[b] * valid;   // losses.py:248: loss += lovasz_softmax(...) * mask_sample
     if (wscale) wscale[b] = valid / denom;
   }
   if (loss_out) loss_out[0] = total / denom;
@@ -338,7 +353,7 @@ int lovasz_core(const float* logits, const float* target, int64_t B, int64_t C, 
   hipLaunchKernelGGL(fg_scan_kernel, dim3((unsigned)B), dim3(64), 0, s, w.tile_fg, T);
   hipLaunchKernelGGL(lovasz_grad_kernel, dim3(T, (unsigned)B), dim3(LT), 0, s, w.ka, w.va, HW, T, w.tile_fg, w.gpix,
                      w.dots);
-  hipLaunchKernelGGL(lovasz_final_kernel, dim3(1), dim3(64), 0, s, w.dots, w.tile_fg, (int)B, T, loss_out, w.wscale);
+  hipLaunchKernelGGL(lovasz_final_kernel, dim3(1), dim3(FIN_T), 2 * B * sizeof(double), s, w.dots, w.tile_fg, (int)B, T, loss_out, w.wscale);
   return 0;
 }
 
@@ -351,7 +366,7 @@ extern "C" size_t ssseg_lovasz_workspace_bytes(int64_t B, int64_t HW) {
 
 extern "C" int ssseg_lovasz_fwd(const float* logits, const float* target, int64_t B, int64_t C, int64_t HW,
                                 float* loss_out, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
-  if (!logits || !target || !loss_out || B < 1 || C < 2 || HW < 1 || HW > 0x7fffffff) return SSSEG_EINVAL;
+  if (!logits || !target || !loss_out || B < 1 || B > 4096 || C < 2 || HW < 1 || HW > 0x7fffffff) return SSSEG_EINVAL;
   if (!ws || ws_bytes < ssseg_lovasz_workspace_bytes(B, HW)) return SSSEG_EWORKSPACE;
   Ws w;
   ws_layout(B, HW, (char*)ws, &w);
@@ -362,7 +377,7 @@ extern "C" int ssseg_lovasz_fwd(const float* logits, const float* target, int64_
 
 extern "C" int ssseg_lovasz_bwd(const float* logits, const float* target, int64_t B, int64_t C, int64_t HW,
                                 const float* gout, float* grad_out, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
-  if (!logits || !target || !grad_out || B < 1 || C < 2 || HW < 1 || HW > 0x7fffffff) return SSSEG_EINVAL;
+  if (!logits || !target || !grad_out || B < 1 || B > 4096 || C < 2 || HW < 1 || HW > 0x7fffffff) return SSSEG_EINVAL;
   if (!ws || ws_bytes < ssseg_lovasz_workspace_bytes(B, HW)) return SSSEG_EWORKSPACE;
   Ws w;
   ws_layout(B, HW, (char*)ws, &w);

@@ -235,7 +235,8 @@ __device__ __forceinline__ void philox4(unsigned (&c)[4], uint64_t seed) {
 
 template <typename T>
 __global__ void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n4, float p, float scale,
-                               uint64_t seed, uint64_t offset) {
+                               uint64_t seed, uint64_t offset, const unsigned long long* __restrict__ offset_dev) {
+  if (offset_dev) offset = (uint64_t)*offset_dev;
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t ctr = offset + (uint64_t)q;
     unsigned c[4] = {(unsigned)ctr, (unsigned)(ctr >> 32), 0x5eedu, 0u};
@@ -440,21 +441,54 @@ extern "C" int ssseg_add_n(const void* const* xs_host, int n, void* y, int64_t n
   return 0;
 }
 
-extern "C" int ssseg_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, uint64_t offset, int dt,
-                             ssseg_stream_t stream) {
+namespace {
+int dropout_launch(const void* x, void* y, int64_t n, float p, uint64_t seed, uint64_t offset,
+                   const unsigned long long* offset_dev, int dt, ssseg_stream_t stream) {
   if (!x || !y || n < 0 || n % 4 || !(p >= 0.f && p < 1.f)) return SSSEG_EINVAL;
   if (n == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   const float scale = 1.f / (1.f - p);
   const dim3 g(ssseg_grid(n / 4, 256, 1 << 20)), b(256);
   if (dt == SSSEG_BF16)
-    hipLaunchKernelGGL(dropout_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)x, (bf16_t*)y, n / 4, p, scale, seed, offset);
+    hipLaunchKernelGGL(dropout_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)x, (bf16_t*)y, n / 4, p, scale, seed, offset,
+                       offset_dev);
   else if (dt == SSSEG_F16)
-    hipLaunchKernelGGL(dropout_kernel<f16_t>, g, b, 0, st, (const f16_t*)x, (f16_t*)y, n / 4, p, scale, seed, offset);
+    hipLaunchKernelGGL(dropout_kernel<f16_t>, g, b, 0, st, (const f16_t*)x, (f16_t*)y, n / 4, p, scale, seed, offset,
+                       offset_dev);
   else if (dt == SSSEG_F32)
-    hipLaunchKernelGGL(dropout_kernel<float>, g, b, 0, st, (const float*)x, (float*)y, n / 4, p, scale, seed, offset);
+    hipLaunchKernelGGL(dropout_kernel<float>, g, b, 0, st, (const float*)x, (float*)y, n / 4, p, scale, seed, offset,
+                       offset_dev);
   else
     return SSSEG_EUNSUPPORTED;
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+__global__ void rng_take_kernel(unsigned long long* counter, unsigned long long* snap, unsigned long long inc) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const unsigned long long v = *counter;
+    snap[0] = v;
+    counter[0] = v + inc;
+  }
+}
+}  // namespace
+
+extern "C" int ssseg_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, uint64_t offset, int dt,
+                             ssseg_stream_t stream) {
+  return dropout_launch(x, y, n, p, seed, offset, nullptr, dt, stream);
+}
+
+extern "C" int ssseg_dropout_dev(const void* x, void* y, int64_t n, float p, uint64_t seed,
+                                 const unsigned long long* offset_dev, int dt, ssseg_stream_t stream) {
+  if (!offset_dev) return SSSEG_EINVAL;
+  return dropout_launch(x, y, n, p, seed, 0, offset_dev, dt, stream);
+}
+
+extern "C" int ssseg_rng_take(unsigned long long* counter, unsigned long long* snap, uint64_t inc,
+                              ssseg_stream_t stream) {
+  if (!counter || !snap) return SSSEG_EINVAL;
+  hipLaunchKernelGGL(rng_take_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, counter, snap,
+                     (unsigned long long)inc);
   SSSEG_LAUNCH_CHECK();
   return 0;
 }

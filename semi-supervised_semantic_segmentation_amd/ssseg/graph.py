@@ -6,7 +6,8 @@ launches.  Captured once, a step replays as one graph launch.
 
 Everything the step launches is capture-safe by construction: no call allocates outside the caching allocator or
 synchronises (include/ssseg.h), the conv autotuner falls back to its cached / heuristic choice while a stream is
-capturing (so run at least one eager step first: it tunes every geometry), and the CowMix draws read and advance a
+capturing (so run at least two eager steps first: the first tunes every geometry and registers the conv/BN
+pairs, the second builds the teacher's BN fold table, a host-to-device copy that cannot be captured), and the CowMix draws read and advance a
 device-side Philox counter (ssseg_cowmix_draw_dev), so every replay draws fresh masks -- the same sequence the eager
 steps would.  Host-side values are baked in at capture: a replay repeats the captured step's Python decisions (the
 optimizer step taken or skipped, the epoch gate of the consistency weight, the learning rate), so capture a step with

@@ -124,6 +124,8 @@ SIGS = {
     'ssseg_global_avgpool_bwd': (i32, [vp, vp, i64, i64, i64, i64, i32, vp]),
     'ssseg_add_n': (i32, [ctypes.POINTER(ctypes.c_void_p), i32, vp, i64, i32, f32, i32, vp]),
     'ssseg_dropout': (i32, [vp, vp, i64, f32, u64, u64, i32, vp]),
+    'ssseg_dropout_dev': (i32, [vp, vp, i64, f32, u64, vp, i32, vp]),
+    'ssseg_rng_take': (i32, [vp, vp, u64, vp]),
     'ssseg_att_blend_fwd': (i32, [vp, I64P, vp, I64P, vp, I64P, vp, i64, i64, i64, i64, vp]),
     'ssseg_att_blend_bwd': (i32, [vp, I64P, vp, I64P, vp, I64P, vp, I64P, vp, vp, vp, i64, i64, i64, i64, vp]),
 }

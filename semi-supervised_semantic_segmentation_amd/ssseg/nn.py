@@ -1555,6 +1555,9 @@ def folded(model):
         sig = tuple(r[3] + (float(r[0].eps),) for r in rows)
         cache = model.__dict__.setdefault('_ssseg_fold_table', [None, None])
         if cache[0] != sig:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError('ssseg.nn.folded: the BN fold table changed while a HIP graph is being captured; '
+                                   'run eager steps until every conv/BN pair has been seen (two steps) before capturing')
             import struct
             blob = b''.join(struct.pack('<6q2qd', *r[3], float(r[0].eps)) for r in rows)
             dev = rows[0][2].device
@@ -1802,7 +1805,17 @@ def add_act(tensors, act=False):
     return _AddNFn.apply(act, *tensors)
 
 
-_DROP = {'seed': None, 'offset': 0}
+# Philox key drawn once per process; the counter lives on the device (one int64 per device) and each dropout launch
+# reserves its range with ssseg_rng_take, so a captured HIP graph draws fresh masks on every replay.  Same counter
+# sequence as a host offset starting at 0: the forward of a call uses [ctr, ctr + ceil(n/4)], its backward the same.
+_DROP = {'seed': None, 'ctr': {}}
+
+
+def dropout_counter(device):
+    c = _DROP['ctr'].get(device)
+    if c is None:
+        c = _DROP['ctr'][device] = torch.zeros(1, dtype=torch.int64, device=device)
+    return c
 
 
 class _DropoutFn(torch.autograd.Function):
@@ -1810,19 +1823,25 @@ class _DropoutFn(torch.autograd.Function):
     def forward(ctx, x, p):
         if _DROP['seed'] is None:
             _DROP['seed'] = int(torch.randint(0, 2 ** 62, (1,)).item())
-        seed, off = _DROP['seed'], _DROP['offset']
-        _DROP['offset'] += (x.numel() + 3) // 4 + 1
+        seed = _DROP['seed']
+        snap = torch.empty(1, dtype=torch.int64, device=x.device)
+        N.call('ssseg_rng_take', N.dev_ptr(dropout_counter(x.device)), N.dev_ptr(snap), (x.numel() + 3) // 4 + 1,
+               N.stream())
         y = torch.empty_like(x)
-        N.call('ssseg_dropout', N.dev_ptr(x), N.dev_ptr(y), x.numel(), float(p), seed, off, N.dt_code(x), N.stream())
-        ctx.meta = (float(p), seed, off)
+        N.call('ssseg_dropout_dev', N.dev_ptr(x), N.dev_ptr(y), x.numel(), float(p), seed, N.dev_ptr(snap),
+               N.dt_code(x), N.stream())
+        ctx.meta = (float(p), seed)
+        ctx.save_for_backward(snap)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        p, seed, off = ctx.meta
+        p, seed = ctx.meta
+        snap, = ctx.saved_tensors
         gyc = gy if gy.is_contiguous(memory_format=torch.channels_last) else gy.contiguous(memory_format=torch.channels_last)
         gx = torch.empty_like(gyc)
-        N.call('ssseg_dropout', N.dev_ptr(gyc), N.dev_ptr(gx), gyc.numel(), p, seed, off, N.dt_code(gy), N.stream())
+        N.call('ssseg_dropout_dev', N.dev_ptr(gyc), N.dev_ptr(gx), gyc.numel(), p, seed, N.dev_ptr(snap),
+               N.dt_code(gy), N.stream())
         return gx, None
 
 

@@ -14,18 +14,20 @@ def _run(graphed, device, steps=3, size=64, batch=2):
     import train
     from ssseg.graph import StepGraph
     model, teacher, opt, cfg = bench.build(batch, size, device)
-    data = bench.synthetic_batches(steps + 1, batch, size, device, 0)
+    data = bench.synthetic_batches(steps + 2, batch, size, device, 0)
     for c in cowmix._DEVICE_RNG['ctr'].values():
         c.zero_()
     model.train()
     opt.zero_grad()
-    losses = [train.train_step(model, teacher, opt, *data[0], 30, 0, cfg)]   # eager step 0 (tunes every geometry)
+    # eager steps 0 and 1: step 0 tunes every conv geometry and registers the conv/BN pairs, step 1 builds the
+    # teacher's BN fold table (host -> device, not capturable)
+    losses = [train.train_step(model, teacher, opt, *data[k], 30, k, cfg) for k in range(2)]
     if graphed:
-        g = StepGraph(lambda i, m, a, b: train.train_step(model, teacher, opt, i, m, a, b, 30, 1, cfg), *data[1])
-        for k in range(1, steps + 1):
+        g = StepGraph(lambda i, m, a, b: train.train_step(model, teacher, opt, i, m, a, b, 30, 2, cfg), *data[2])
+        for k in range(2, steps + 2):
             losses.append(tuple(t.clone() for t in g(*data[k])))
     else:
-        for k in range(1, steps + 1):
+        for k in range(2, steps + 2):
             losses.append(train.train_step(model, teacher, opt, *data[k], 30, k, cfg))
     torch.cuda.synchronize()
     state = {**{'s.' + k: v.detach().clone() for k, v in model.state_dict().items()},

@@ -73,8 +73,12 @@ def build(name, path, dev, threshold=0.5, calibrate=True):
     from ssseg import nn as snn
     from ssseg import optim as soptim
     from ssseg.ddp import DistributedDataParallel
+    import train
     torch.manual_seed(0)
     for c in cowmix._DEVICE_RNG['ctr'].values():   # the CowMix Philox counter restarts with every build
+        c.zero_()
+    train._OVERLAP['steps'] = 0   # and so does the step schedule (the first serial_steps steps run without overlap)
+    for c in snn._DROP['ctr'].values():   # and the dropout Philox counter
         c.zero_()
     cfg = config.fromfile(os.path.join(PKG, path))
     snn.set_compute_dtype({'fp32': torch.float32, 'fp16': torch.float16}.get(cfg['common'].get('compute_dtype'),
@@ -122,13 +126,16 @@ def graph_steps(name, path, dev, threshold, calibrate, eager_losses, n_eager=3, 
     import train
     from ssseg.graph import StepGraph
     model, ema, opt, cfg, tc, data, _, _ = build(name, path, dev, threshold, calibrate)
+    rerun = []
     for step in range(n_eager):
-        train.train_step(model, ema, opt, *data, 30, step, cfg)
+        r = train.train_step(model, ema, opt, *data, 30, step, cfg)
+        rerun.append(tuple(None if t is None else float(t) for t in r))
     g = StepGraph(lambda i, m, a, b: train.train_step(model, ema, opt, i, m, a, b, 30, n_eager, cfg), *data)
     out = []
     for _ in range(2):
         out.append(tuple(None if t is None else float(t) for t in g(*data)))
     same = out == [tuple(v for v in row) for row in eager_losses[n_eager:n_eager + 2]]
+    same_eager = rerun == [tuple(v for v in row) for row in eager_losses[:n_eager]]   # the rebuild's eager steps
     torch.cuda.synchronize()
     t0 = time.time()
     for _ in range(n_replay):
@@ -136,7 +143,7 @@ def graph_steps(name, path, dev, threshold, calibrate, eager_losses, n_eager=3, 
     torch.cuda.synchronize()
     ms = 1e3 * (time.time() - t0) / n_replay
     del g, model, ema, opt
-    return ms, same, out
+    return ms, same, out, same_eager
 
 
 def run(name, path, dev, threshold=0.5, calibrate=True, layers=False, graph=False):
@@ -186,8 +193,9 @@ def run(name, path, dev, threshold=0.5, calibrate=True, layers=False, graph=Fals
     if graph:   # the same steps replayed from a captured HIP graph (fresh build, same seeds)
         del model, ema, opt
         torch.cuda.empty_cache()
-        gms, same, gl = graph_steps(name, path, dev, threshold, calibrate, out)
+        gms, same, gl, same_eager = graph_steps(name, path, dev, threshold, calibrate, out)
         rec['graph'] = {'ms_per_step': round(gms, 1), 'losses_bitwise_equal_eager': same, 'losses_steps_3_4': gl,
+                        'rebuild_eager_steps_bitwise_equal': same_eager,
                         'frac_of_dense_peak': round(STEP_GFLOP_PER_IMAGE[name] * b / (gms / 1e3) / 1e3 * 1e12 /
                                                     PEAK[rec['dtype']], 4)}
     print(json.dumps(rec), flush=True)
