@@ -5,7 +5,7 @@
 
 #include "conv_kernels.h"
 
-int g_knobs[12] = {0, -1, 0, 0, 0, 1, 0, 0, 0, 0, 100, 0};   // split-K off: measured a net loss on the C2 step (r2u)   // runtime variant switches (ssseg_set_knob)
+int g_knobs[16] = {0, -1, 0, 0, 0, 1, 0, 0, 0, 0, 100, 0, 0, 0, 0, 0};   // split-K off: measured a net loss on the C2 step (r2u)   // runtime variant switches (ssseg_set_knob)
 
 // ------------------------------------------------------------------------------------------------
 // weight packing: dst[k][rr][ss][c] (c < Cp; zero for c >= Cd) from an fp32 source
@@ -68,9 +68,11 @@ namespace {
 
 // returns the tile height BM of the launched config (the fused BN statistics write ceil(M / BM) partial rows)
 template <typename TO>
-int launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep,
+int launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep_in,
                     unsigned xb, unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2 = nullptr,
                     unsigned x2b = 0) {
+  Epi<TO> ep = ep_in;
+  ep.sdbg = g_knobs[12];
   switch (cfg) {
     case 1:
     case 2:
@@ -174,6 +176,8 @@ int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const
   for (int split = 0; split < (ws ? 2 : 1); ++split) {
     float* wsv = split ? ws : nullptr;
     for (int v : kCandidates) {
+      // a virtually padded contraction (C > ldx: the host's vpad) runs on the bounded LDS-DMA loads only
+      if (g.C > g.ldx && (v == 0 || v == 24)) continue;
       // warm (code load, caches); a variant that cannot run this launch (-1) is skipped
       if (run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, ph ? nullptr : wsv, ph, x2, x2b) <= 0) continue;
       float ms = 1e30f;
@@ -223,11 +227,14 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
                                                (unsigned)x2b)
                          : heuristic_variant(g);
           if (x2 && (v & ~kSplitBit) == 0) v = 5;   // the register-staged kernel has no second source
+          if (g.C > g.ldx && ((v & ~kSplitBit) == 0 || (v & ~kSplitBit) == 24)) v = 14;   // (vpad: LDS-DMA only)
           g_variant[key] = v;
         }
       } else if (g_knobs[4] == 11) {
         v = 0;   // forced register-staged
-        if (x2) return -1;
+        if (x2 || g.C > g.ldx) return -1;
+      } else if (g.C > g.ldx && g_knobs[4] == 24) {
+        v = 14;
       }
       // split-K only where the autotuner measured it faster (its fp32 atomics reorder the sums); a variant
       // forced by knob 4 runs unsplit, so forced variants stay bit-comparable
@@ -235,7 +242,8 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
       const int r = run_variant<T, TO>(v & ~kSplitBit, x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s,
                                        ph ? nullptr : wsv, ph, x2, (unsigned)x2b);
       // a forced config without a general-k instantiation (128/256-wide n-tiles, C % 64 != 0): register-staged
-      if (r == -1 && g_knobs[4] != 0 && !x2 && g.C % 64) return run_variant<T, TO>(0, x, w, y, g, ep, 0, 0, s, nullptr, ph);
+      if (r == -1 && g_knobs[4] != 0 && !x2 && g.C % 64 && g.C <= g.ldx)
+        return run_variant<T, TO>(0, x, w, y, g, ep, 0, 0, s, nullptr, ph);
       if (r == -1 && g_knobs[4] == 24) {   // the forced halo kernel does not apply to this launch: the heuristic's
         const int hv = x2 && heuristic_variant(g) == 0 ? 5 : heuristic_variant(g);
         return run_variant<T, TO>(hv, x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, nullptr, ph, x2, (unsigned)x2b);
@@ -244,6 +252,7 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
     }
   }
   if (x2) return -1;
+  if (g.C > g.ldx) return SSSEG_EUNSUPPORTED;   // a virtually padded contraction needs the bounded LDS-DMA loads
   return run_variant<T, TO>(0, x, w, y, g, ep, 0, 0, s, ph ? nullptr : ws, ph);
 }
 
@@ -259,7 +268,7 @@ bool geom_ok(const ConvGeom& g, int dt) {
 }  // namespace
 
 extern "C" int ssseg_set_knob(int id, int value) {
-  if (id < 0 || id >= 12) return SSSEG_EINVAL;
+  if (id < 0 || id >= 16) return SSSEG_EINVAL;
   if (id == 6 && value) {
     std::lock_guard<std::mutex> lk(g_variant_mu);
     g_variant.clear();

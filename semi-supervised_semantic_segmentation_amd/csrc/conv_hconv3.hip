@@ -144,7 +144,7 @@ bool hconv3_ok(const ConvGeom& g, const PhaseTab* ph, const float* ws) {
   return g_knobs[11] >= 0 && !ws && !(ph && ph->n > 1) && g.R == 3 && g.S == 3 && g.sy == 1 && g.sx == 1 &&
          g.dy == 1 && g.dx == 1 && g.py == -1 && g.px == -1 && g.oident && g.H == g.OH && g.W == g.OW &&
          g.W % 64 == 0 && g.H % 4 == 0 && g.C % 64 == 0 && g.K % 64 == 0 && g.ldw == 9 * g.C && g.ldx % 8 == 0 &&
-         g.ldy % 8 == 0 && g.M < 0x7fffffffLL;
+         g.ldy % 8 == 0 && g.ldx >= g.C && g.M < 0x7fffffffLL;
 }
 
 template <typename TO>

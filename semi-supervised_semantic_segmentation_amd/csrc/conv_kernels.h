@@ -186,6 +186,8 @@ struct Epi {
   // rmask (split outputs only): res is not added but is the forward output of the first part's producer, whose
   // ReLU backward is applied in place: channels [0, oc1) are stored as (res > 0 ? v : 0), channels >= oc1 read no res
   int rmask = 0;
+  int sdbg = 0;   // experiment switch for the fused statistics (knob 12): 1 no sums, 2 no tile_stats, 4 no row write,
+                  // 8 no cross-lane shuffles
 };
 
 // where output channel n of pixel op is stored (y, or the second part of a split output)
@@ -200,6 +202,16 @@ template <> __device__ __forceinline__ float stored<float>(float v) { return v; 
 template <> __device__ __forceinline__ float stored<bf16_t>(float v) { return bf16_to_f32(f32_to_bf16(v)); }
 template <> __device__ __forceinline__ float stored<f16_t>(float v) { return (float)(f16_t)v; }
 
+// sum over a 16-lane DPP row (quad_perm xor 1, xor 2, row_half_mirror, row_mirror): every lane of the row ends with
+// the same value, in a fixed order, without LDS traffic
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
 // Per-tile BatchNorm statistics partials from the epilogue (fused training BN statistics, replaces a separate
 // read of the conv output).  Each thread holds fp64 (sum, sumsq) of V consecutive channels starting at
 // channel offset cofs within the tile, over some of the tile's rows; lanes holding the same channels are those
@@ -208,10 +220,11 @@ template <> __device__ __forceinline__ float stored<f16_t>(float v) { return (fl
 // written for channels [n0, n0 + BN).  Every thread of the block must call this (two barriers).
 template <int V, int BN, int NW, typename SA>
 __device__ __forceinline__ void tile_stats(SA (&s1)[V], SA (&s2)[V], int lstride, bool holder, int cofs,
-                                           char* smem, long long mtile, int n0, double* __restrict__ stats, int sld) {
+                                           char* smem, long long mtile, int n0, double* __restrict__ stats, int sld,
+                                           int dbg = 0) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
-    if (o < lstride) break;
+    if (o < lstride || (dbg & 8)) break;
 #pragma unroll
     for (int e = 0; e < V; ++e) {
       s1[e] += __shfl_xor(s1[e], o, 64);
@@ -230,7 +243,7 @@ __device__ __forceinline__ void tile_stats(SA (&s1)[V], SA (&s2)[V], int lstride
   lds_barrier();
   for (int c = threadIdx.x; c < BN; c += NW * 64) {
     const int n = n0 + c;
-    if (n >= sld) continue;
+    if (n >= sld || (dbg & 4)) continue;
     double a = 0.0, b = 0.0;
 #pragma unroll
     for (int k = 0; k < NW; ++k) {
@@ -425,13 +438,84 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
                                                Tile2D t2 = Tile2D{0, 0, 0, 0, 0}) {
   // pre: this thread's residual chunks, already loaded by the caller (one per pass; used where `full`)
   constexpr int LDR = BN * 4 + 16;   // bytes per staged pixel row
+  // REGST: the fused BatchNorm statistics come from the accumulators, before the staging: per lane fp32 sums of the
+  // stored value over its FM fragment rows (acc + shift: a conv feeding a training BN has no scale / residual /
+  // activation -- host contract), a 16-lane DPP row sum, and each wave's (sum, sumsq) of its WTN channels goes into
+  // the 16 pad bytes of the staged rows: slot (wm * BN + channel) * 2, 4 floats per row.  No extra barrier, no LDS
+  // shuffles and nothing live across the store pass (the store-pass summation it replaces kept 16 sums live there
+  // and reduced them with 48 LDS permutes + 2 barriers per tile).  ep.sdbg & 16 = that older path (A/B).
+  constexpr int WTM = FM * 16, WM_ = BM / WTM;
+  constexpr bool REGST = STATS && BN <= 32 * FM;
+  const bool regst = REGST && !(ep.sdbg & 16);
+  float rs1[REGST ? FN : 1][4], rs2[REGST ? FN : 1][4];
+  if constexpr (REGST) {
+    if (regst) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        const int nb = n0 + wno + i * 16 + (lane >> 4) * 4;
+        float sh[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          sh[e] = (ep.shift && nb + e < g.K) ? ep.shift[nb + e] : 0.f;
+          rs1[i][e] = rs2[i][e] = 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+          const int row = wmo + j * 16 + (lane & 15);
+          const bool rv = T2D ? (row >> 6) < t2.rows : m0 + row < g.M;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float q = (rv && nb + e < g.K) ? stored<TO>(acc[i][j][e] + sh[e]) : 0.f;
+            rs1[i][e] += q;
+            rs2[i][e] += q * q;
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          rs1[i][e] = row16_sum(rs1[i][e]);
+          rs2[i][e] = row16_sum(rs2[i][e]);
+        }
+      }
+    }
+  }
   __syncthreads();                   // every wave is done with the LDS ring
 #pragma unroll
   for (int j = 0; j < FM; ++j)
 #pragma unroll
     for (int i = 0; i < FN; ++i)
       *(f32x4*)(smem + (wmo + j * 16 + (lane & 15)) * LDR + (wno + i * 16 + (lane >> 4) * 4) * 4) = acc[i][j];
+  if constexpr (REGST) {
+    if (regst && (lane & 15) == 0) {
+      const int wmi = wmo / WTM;
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int slot = (wmi * BN + wno + i * 16 + (lane >> 4) * 4 + e) * 2;
+          *(float2*)(smem + (slot >> 2) * LDR + BN * 4 + (slot & 3) * 4) = make_float2(rs1[i][e], rs2[i][e]);
+        }
+    }
+  }
   __syncthreads();
+  if constexpr (REGST) {
+    if (regst) {
+      for (int c = threadIdx.x; c < BN; c += NT) {
+        const int n = n0 + c;
+        if (n >= ep.sld || (ep.sdbg & 4)) continue;
+        double a = 0.0, b = 0.0;
+#pragma unroll
+        for (int w = 0; w < WM_; ++w) {
+          const int slot = (w * BN + c) * 2;
+          const float2 v = *(const float2*)(smem + (slot >> 2) * LDR + BN * 4 + (slot & 3) * 4);
+          a += (double)v.x;
+          b += (double)v.y;
+        }
+        const long long mt = T2D ? t2.tile : m0 / BM;
+        ep.stats[(mt * 2) * ep.sld + n] = a;
+        ep.stats[(mt * 2 + 1) * ep.sld + n] = b;
+      }
+    }
+  }
   constexpr int CPR = BN / 8;                 // 8-channel chunks per row
   static_assert(NT % CPR == 0 && 64 % CPR == 0, "epilogue: one fixed channel chunk per thread");
   constexpr int RPP = NT / CPR, NP = (BM + RPP - 1) / RPP;   // rows per pass, passes
@@ -522,6 +606,7 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
         act8(v, ep.relu, ep.slope);
       }
       if constexpr (STATS) {
+        if (!regst && !(ep.sdbg & 1))
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const SA q = n + e < g.K ? (SA)stored<TO>(v[e]) : (SA)0;
@@ -545,8 +630,9 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
     }
   }
   if constexpr (STATS)
-    tile_stats<8, BN, NT / 64, SA>(s1, s2, CPR, (threadIdx.x & 63) < CPR, ch * 8, smem, T2D ? t2.tile : m0 / BM, n0,
-                                   ep.stats, ep.sld);
+    if (!regst && !(ep.sdbg & 2))
+      tile_stats<8, BN, NT / 64, SA>(s1, s2, CPR, (threadIdx.x & 63) < CPR, ch * 8, smem, T2D ? t2.tile : m0 / BM, n0,
+                                     ep.stats, ep.sld, ep.sdbg);
 }
 
 // fused statistics after store_tile (register epilogue): lane holds fp64 sums of fragment column i's 4
@@ -605,7 +691,7 @@ constexpr int ROWB = 80;   // 64 data bytes + 16 pad per LDS row
 // ------------------------------------------------------------------------------------------------
 // forward / dgrad / transposed-conv gather GEMM
 // ------------------------------------------------------------------------------------------------
-extern int g_knobs[12];   // runtime variant switches (ssseg_set_knob), defined in conv.hip
+extern int g_knobs[16];   // runtime variant switches (ssseg_set_knob), defined in conv.hip
 // 0: reg-staged pipeline depth; 1: split-K cap (-1 off = default, 0 auto: the autotuner also times each variant with
 // its split plan, fp32-atomic partials + finalize, and keeps it where faster); 2: 64x64 small-M tiles (reg-staged path);
 // 3: bf16 LDS-DMA path (0 on, -1 off); 4: variant (0 auto, 1..10 / 12..23 LDS-DMA config, 11 register-staged, 24 the
@@ -615,7 +701,8 @@ extern int g_knobs[12];   // runtime variant switches (ssseg_set_knob), defined 
 // 8: bf16 weight gradient on the LDS-DMA kernel (0 on, -1 = register-staged wgrad_kernel);
 // 9: LDS-DMA weight-gradient tile variant (0 = the static plan, 1.. = a forced WGRAD_CFGS entry, conv_wgrad.hip);
 // 10: weight-gradient split count scale in percent (100 = the plan's); 11: halo-tiled 3x3 kernels (conv_wgrad_halo.hip,
-// conv_hconv3.hip; 0 on, -1 = the split-K weight gradient and no variant 24)
+// conv_hconv3.hip; 0 on, -1 = the split-K weight gradient and no variant 24); 12: fused-statistics experiment switch
+// (Epi::sdbg, LDS-DMA configs; 0 = normal)
 
 // STATS: the epilogue also writes the fused BatchNorm statistics partials (a separate instantiation: the fp64
 // sums raise the register count, which must not cost the launches that do not need them)

@@ -885,8 +885,11 @@ int wgrad_one(const void* x, const ssseg_vcat* vc, const void* dy, float* dw, co
     return 0;
   }
   WgradPlan p = choose_wgrad(g, dt);
+  // the register-staged kernel has no second source, and its plain loads cannot read a virtually padded
+  // contraction (C > ldx: the host's vpad; the LDS-DMA reads are bounded by the buffer size)
+  if (!p.glds && g.C > g.ldx) return SSSEG_EUNSUPPORTED;
   if (vc) {
-    if (!p.glds) return SSSEG_EUNSUPPORTED;   // the register-staged kernel has no second source
+    if (!p.glds) return SSSEG_EUNSUPPORTED;
     bool st = false;
     p = plan_for_cfg(g, wgrad_cfg_for(g, (int)vc->c1, &st));
     p.st = st;

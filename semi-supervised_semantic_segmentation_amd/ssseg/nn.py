@@ -20,7 +20,8 @@ import torch.nn as nn
 from . import native as N
 
 _CFG = {'grad_join': True, 'stem': True, 'phases': True, 'eval_bwd_y': True, 'dtype': torch.bfloat16, 'sync_bn': True,
-        'fuse_stats': True, 'vcat': os.environ.get('SSSEG_VCAT', '1') != '0'}
+        'fuse_stats': True, 'vcat': os.environ.get('SSSEG_VCAT', '1') != '0',
+        'vpad': os.environ.get('SSSEG_VPAD', '0') != '0'}
 
 
 def set_virtual_concat(on):
@@ -168,6 +169,26 @@ def vec(dtype=None):
 
 def rup(c, v):
     return (c + v - 1) // v * v
+
+
+def set_virtual_pad(on):
+    """Virtual channel padding of the 16-bit conv engine's contraction (default on; SSSEG_VPAD=0 turns it off)."""
+    _CFG['vpad'] = bool(on)
+
+
+def vpad(c):
+    """Contraction width the 16-bit conv engine runs for an input of c physical channels (c % 8 == 0).  A width that
+    is not a multiple of 64 runs the general-k loader (per-lane tap / channel split of every 16-byte chunk); within
+    12.5 % of the next multiple of 64 (HRNet-W32's 480- and 240-channel fuse / head layers) the GEMM instead runs the
+    64-aligned path over rup(c, 64) "virtual" channels: the packed weights are zero for channels >= c and the
+    activation keeps its physical pixel stride c, so a 16-byte chunk past channel c reads the next pixel's first
+    channels (finite data times zero weights; past the end of the buffer the bounded LDS-DMA reads return 0).
+    The engine then refuses its register-staged kernels (plain loads) for such a launch.  Measured (tools/conv_ab.py,
+    16x256^2): 480->240 3x3 fwd 3.13 -> 2.2 ms, fwd+bwd 12.1 -> 6.7-8.3 ms."""
+    if not _CFG['vpad'] or _CFG['dtype'] == torch.float32 or c % 64 == 0:
+        return c
+    p = rup(c, 64)
+    return p if (p - c) * 8 <= c else c
 
 
 def _zero_(t):
@@ -563,7 +584,7 @@ class _ConvBase:
         _PACK_EPOCH[0] += 1
 
     def _pack(self, key, Kd, Kr, Cd, Cp, layout, r0, rstep, Rn, s0, sstep, Sn):
-        key = (key, _CFG['dtype'])
+        key = (key, _CFG['dtype'], Cp)
         t = self._ssseg_packs.get(key)
         if t is None:
             w = self.weight.detach()
@@ -658,12 +679,16 @@ class Conv2d(nn.Conv2d, _ConvBase):
         (R, S), (sh, sw), (ph, pw), (dh, dw) = self.kernel_size, self.stride, self.padding, self.dilation
         return (H + 2 * ph - dh * (R - 1) - 1) // sh + 1, (W + 2 * pw - dw * (S - 1) - 1) // sw + 1
 
+    def _vpad_ok(self):
+        return not (self._ssseg_dw or self._ssseg_head)
+
     def _fwd_desc(self, n, H, W):
         cin, cout = self._dims()
         (R, S), (sh, sw), (ph, pw), (dh, dw) = self.kernel_size, self.stride, self.padding, self.dilation
         OH, OW = self._out_hw(H, W)
-        return _desc(N=n, H=H, W=W, C=cin, ldx=cin, OH=OH, OW=OW, K=cout, R=R, S=S, sy=sh, sx=sw, dy=dh, dx=dw,
-                     py=-ph, px=-pw, outH=OH, outW=OW, osy=1, osx=1, ooy=0, oox=0, ldy=cout, ldw=R * S * cin)
+        ce = vpad(cin) if self._vpad_ok() else cin
+        return _desc(N=n, H=H, W=W, C=ce, ldx=cin, OH=OH, OW=OW, K=cout, R=R, S=S, sy=sh, sx=sw, dy=dh, dx=dw,
+                     py=-ph, px=-pw, outH=OH, outW=OW, osy=1, osx=1, ooy=0, oox=0, ldy=cout, ldw=R * S * ce)
 
     def _ssseg_res_dgrad(self):
         return not self._ssseg_dw
@@ -740,7 +765,7 @@ class Conv2d(nn.Conv2d, _ConvBase):
         if stem:   # image-input kernel: weights [K][R][S][4]
             w = self._pack('stem', cout, self.out_channels, self.in_channels, 4, 0, 0, 1, R, 0, 1, S)
         else:
-            w = self._pack('fwd', cout, self.out_channels, self.in_channels, cin, 0, 0, 1, R, 0, 1, S)
+            w = self._pack('fwd', cout, self.out_channels, self.in_channels, d.C, 0, 0, 1, R, 0, 1, S)
         fl = _conv_flops(n, d.OH, d.OW, self.out_channels, self.in_channels, R, S)
         tg = _tag(self, n, H, W)
         if bn is not None:
@@ -873,11 +898,12 @@ class Conv2d(nn.Conv2d, _ConvBase):
                        N.dt_code(gy), N.stream())
             return dx
         timer = _Timed(_conv_flops(n, OH, OW, self.out_channels, self.in_channels, R, S), 'dgrad', _tag(self, n, H, W))
+        ce = vpad(cout) if self._vpad_ok() else cout   # the dgrad contracts over the output channels
         if sh == 1 and sw == 1:
-            w = self._pack('dgrad', cin, self.in_channels, self.out_channels, cout, 1, R - 1, -1, R, S - 1, -1, S)
-            d = _desc(N=n, H=OH, W=OW, C=cout, ldx=cout, OH=H, OW=W, K=cin, R=R, S=S, sy=1, sx=1, dy=dh, dx=dw,
+            w = self._pack('dgrad', cin, self.in_channels, self.out_channels, ce, 1, R - 1, -1, R, S - 1, -1, S)
+            d = _desc(N=n, H=OH, W=OW, C=ce, ldx=cout, OH=H, OW=W, K=cin, R=R, S=S, sy=1, sx=1, dy=dh, dx=dw,
                       py=ph - (R - 1) * dh, px=pw - (S - 1) * dw, outH=H, outW=W, osy=1, osx=1, ooy=0, oox=0,
-                      ldy=cin, ldw=R * S * cout)
+                      ldy=cin, ldw=R * S * ce)
             with timer:
                 self._igemm(gy, w, dx, d, N.dt_code(dx),
                             fold=(None, None, residual, None) if residual is not None else None)
@@ -888,11 +914,11 @@ class Conv2d(nn.Conv2d, _ConvBase):
                 if qy == 0 or qx == 0:
                     continue
                 rr, ss = (rny, rnx) if rny * rnx > 0 else (0, 0)
-                w = self._pack(('dgrad', phy, phx), cin, self.in_channels, self.out_channels, cout, 1, ry0, sh,
+                w = self._pack(('dgrad', phy, phx), cin, self.in_channels, self.out_channels, ce, 1, ry0, sh,
                                rny, rx0, sw, rnx) if rr else None
-                d = _desc(N=n, H=OH, W=OW, C=cout, ldx=cout, OH=qy, OW=qx, K=cin, R=rr, S=ss, sy=1, sx=1, dy=-1,
+                d = _desc(N=n, H=OH, W=OW, C=ce, ldx=cout, OH=qy, OW=qx, K=cin, R=rr, S=ss, sy=1, sx=1, dy=-1,
                           dx=-1, py=dly, px=dlx, outH=H, outW=W, osy=sh, osx=sw, ooy=phy, oox=phx, ldy=cin,
-                          ldw=max(rr * ss * cout, cout))
+                          ldw=max(rr * ss * ce, ce))
                 # each phase adds the pending gradient at its own output pixels (the residual is indexed by
                 # the output pixel, so the phases together cover it exactly once)
                 self._igemm(gy, w, dx, d, N.dt_code(dx),

@@ -23,6 +23,8 @@ def main():
     ap.add_argument('layers', nargs='+', help='cin,cout,k,hw')
     ap.add_argument('--batch', type=int, default=16)
     ap.add_argument('--reps', type=int, default=20)
+    ap.add_argument('--sdbg', default='0', help='comma list of knob-12 values (fused-statistics experiment switch: '
+                    '1 no sums, 2 no tile_stats, 4 no row write, 8 no shuffles); --tune runs the stats launch per value')
     ap.add_argument('--tune', action='store_true',
                     help='print the autotuner\'s own per-config event timings (SSSEG_TUNE_LOG=1 must be set) for the plain '
                          'and the statistics launch of each layer instead of the Python-timed loop')
@@ -35,12 +37,14 @@ def main():
         x = snn.to_act(torch.randn(a.batch, cin, hw, hw, device=dev))
         cap = conv.stat_rows_cap(a.batch, hw, hw)
         if a.tune:
-            for st in (False, True):
+            for st, dbg in [(False, 0)] + [(True, int(v)) for v in a.sdbg.split(',')]:
                 N.lib().ssseg_set_knob(6, 1)   # clear the variant cache: the next launch tunes (and logs)
-                print(f'{cin}->{cout} k{k} @{a.batch}x{hw}^2 stats={st}', file=sys.stderr, flush=True)
+                N.lib().ssseg_set_knob(12, dbg)
+                print(f'{cin}->{cout} k{k} @{a.batch}x{hw}^2 stats={st} sdbg={dbg}', file=sys.stderr, flush=True)
                 with torch.no_grad():
                     conv._ssseg_forward(x, False, stats=snn.StatRows(cout, cap, dev) if st else None)
                 torch.cuda.synchronize()
+            N.lib().ssseg_set_knob(12, 0)
             continue
         line = []
         for v in CFGS:
