@@ -65,6 +65,16 @@ def conv3x3(in_planes, out_planes, stride=1):
     return snn.Conv2d(in_planes, out_planes, kernel_size=3, stride=stride, padding=1, bias=False)
 
 
+def _shortcut_grad(downsample, x):
+    """The residual block's shortcut gradient route (as models/encoders/resnet.py): identity -> a GradHandoff the
+    block's last BN backward fills and its first conv's dgrad adds in its epilogue; a projection (a module of ssseg
+    convs) -> x's consumers joined (snn.mark_join), returns None."""
+    if isinstance(downsample, nn.Identity):
+        return snn.GradHandoff()
+    snn.mark_join(x)
+    return None
+
+
 class BasicBlock(nn.Module):
     expansion = 1
 
@@ -79,9 +89,13 @@ class BasicBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x):
+        # x feeds conv1 and the shortcut: an identity shortcut's gradient is added in conv1's dgrad epilogue
+        # (snn.GradHandoff), a projection shortcut's meets conv1's through a join -- no separate autograd add
+        h = _shortcut_grad(self.downsample, x)
         residual = self.downsample(x)
-        out = snn.conv_bn_act(self.conv1, x, self.bn1, relu=True)
-        return snn.conv_bn_act(self.conv2, out, self.bn2, relu=True, residual=residual)   # skip_add.add_relu
+        out = snn.conv_bn_act(self.conv1, x, self.bn1, relu=True, grad_in=h)
+        return snn.conv_bn_act(self.conv2, out, self.bn2, relu=True, residual=residual,
+                               grad_out=h)   # skip_add.add_relu
 
 
 class BottleneckBlock(nn.Module):
@@ -101,10 +115,11 @@ class BottleneckBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x):
+        h = _shortcut_grad(self.downsample, x)
         residual = self.downsample(x)
-        out = snn.conv_bn_act(self.conv1, x, self.bn1, relu=True)
+        out = snn.conv_bn_act(self.conv1, x, self.bn1, relu=True, grad_in=h)
         out = snn.conv_bn_act(self.conv2, out, self.bn2, relu=True)
-        return snn.conv_bn_act(self.conv3, out, self.bn3, relu=True, residual=residual)
+        return snn.conv_bn_act(self.conv3, out, self.bn3, relu=True, residual=residual, grad_out=h)
 
 
 class ConvBNRelu(nn.Module):

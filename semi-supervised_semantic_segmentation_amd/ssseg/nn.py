@@ -21,7 +21,7 @@ from . import native as N
 
 _CFG = {'grad_join': True, 'stem': True, 'phases': True, 'eval_bwd_y': True, 'dtype': torch.bfloat16, 'sync_bn': True,
         'fuse_stats': True, 'vcat': os.environ.get('SSSEG_VCAT', '1') != '0',
-        'vpad': os.environ.get('SSSEG_VPAD', '0') != '0'}
+        'vpad': os.environ.get('SSSEG_VPAD', '1') != '0'}
 
 
 def set_virtual_concat(on):
