@@ -39,7 +39,7 @@ FWD_GFLOP_PER_IMAGE = 95.94     # UNet-R50 mw128 ConvT @512 (verifie
 # MI355X_MICROARCH.md gfx950 correction).  PMC cannot run inside the timed process, so the committed
 # measurement of the same workload is reported next to the live flop rate.
 THRESHOLD = 0.5                 # see the module docstring (liveness)
-PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r3f_pmc_traffic.json')
+PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r4_pmc_traffic.json')
 
 
 def pmc_traffic():
