@@ -86,6 +86,7 @@ int launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvGe
     case 22:
     case 23: return launch_glds_grp_e<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
     case 24: return launch_hconv3<TO>(x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);   // halo-tiled 3x3 (-1: n/a)
+    case 25: return launch_hconv3s<TO>(x, w, y, g, ep, xb, s, ws, ph, x2);   // its 32 -> 32-channel form
     case 5:
     case 7:
     case 8:
@@ -102,7 +103,7 @@ int launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvGe
 // where it applies).  With knob 5 on (default) an unseen geometry is timed once over the candidates on the caller's
 // stream (HIP events) and the fastest is cached.
 constexpr int kSplitBit = 256;   // cached choice flag: run the variant with its split-K plan
-constexpr int kCandidates[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24};
+constexpr int kCandidates[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25};
 std::unordered_map<unsigned long long, int> g_variant;
 std::mutex g_variant_mu;
 
@@ -231,8 +232,8 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
           g_variant[key] = v;
         }
       } else if (g_knobs[4] == 11) {
-        v = 0;   // forced register-staged
-        if (x2 || g.C > g.ldx) return -1;
+        v = g.C > g.ldx ? 14 : 0;   // forced register-staged (a vpad contraction runs LDS-DMA config 14 instead)
+        if (x2) return -1;
       } else if (g.C > g.ldx && g_knobs[4] == 24) {
         v = 14;
       }
@@ -244,7 +245,7 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
       // a forced config without a general-k instantiation (128/256-wide n-tiles, C % 64 != 0): register-staged
       if (r == -1 && g_knobs[4] != 0 && !x2 && g.C % 64 && g.C <= g.ldx)
         return run_variant<T, TO>(0, x, w, y, g, ep, 0, 0, s, nullptr, ph);
-      if (r == -1 && g_knobs[4] == 24) {   // the forced halo kernel does not apply to this launch: the heuristic's
+      if (r == -1 && (g_knobs[4] == 24 || g_knobs[4] == 25)) {   // a forced halo kernel does not apply: the heuristic's
         const int hv = x2 && heuristic_variant(g) == 0 ? 5 : heuristic_variant(g);
         return run_variant<T, TO>(hv, x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, nullptr, ph, x2, (unsigned)x2b);
       }

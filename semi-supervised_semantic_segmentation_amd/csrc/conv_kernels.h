@@ -1389,6 +1389,11 @@ template <typename TO>
 int launch_hconv3(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
                   unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2, unsigned x2b);
 
+// the same for 32 input and 32 output channels (conv_hconv3s.hip), variant 25; 256 or -1
+template <typename TO>
+int launch_hconv3s(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
+                   hipStream_t s, float* ws, const PhaseTab* ph, const void* x2);
+
 // halo-tiled 3x3 / stride-1 weight gradient (conv_wgrad_halo.hip)
 struct HaloSeg {
   const void* x;    // input (pixel stride ldx), channels [0, c1) of a virtual concat (all C without one)

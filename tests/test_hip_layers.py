@@ -283,7 +283,7 @@ def test_conv_bn_act_fused_eval_grad(hip_device, mode, monkeypatch, kind, cin, c
     _close(mb.bias.grad, rb.bias.grad, mode, 'dbeta')
 
 
-ALL_VARIANTS = [11] + list(range(1, 11)) + list(range(12, 25))
+ALL_VARIANTS = [11] + list(range(1, 11)) + list(range(12, 26))
 
 
 @pytest.mark.parametrize('kind,cin,cout,k,H', [('conv', 64, 128, 3, 19), ('conv', 128, 64, 1, 17), ('conv', 192, 256, 3, 9),
@@ -296,13 +296,18 @@ ALL_VARIANTS = [11] + list(range(1, 11)) + list(range(12, 25))
                                                ('conv_s2', 32, 64, 3, 26), ('convT', 32, 32, 4, 9),
                                                # W % 64 == 0, H % 4 == 0: the halo-tiled 3x3 kernel (variant 24)
                                                ('conv64', 64, 64, 3, 8), ('conv64', 128, 128, 3, 12),
-                                               ('conv64', 192, 64, 3, 4), ('conv64', 64, 192, 3, 20)])
+                                               ('conv64', 192, 64, 3, 4), ('conv64', 64, 192, 3, 20),
+                                               # 32 -> 32 channels: its halo form (variant 25)
+                                               ('conv64', 32, 32, 3, 8), ('conv64', 32, 32, 3, 12),
+                                               # vpad: 240 / 120 channels run the 64-aligned path over 256 / 128
+                                               ('conv', 240, 120, 3, 11), ('conv64', 240, 120, 3, 4)])
 def test_conv_variants_bitwise(hip_device, kind, cin, cout, k, H):
     """Every bf16 engine variant (register-staged, LDS-DMA tile configs 1..10 and 12..23) accumulates the
     same MFMA k-sequence: forward and input-gradient outputs are bit-identical, so autotuning never changes
     results.  C % 64 != 0 layers run the general-k loader on the 64-wide configs (the others fall back to the
     register-staged kernel when forced), whose linear k order is the register-staged kernel's.  'conv64' maps
-    (W = 64 or 128) run the halo-tiled 3x3 kernel (variant 24) in the forward and the input gradient."""
+    (W = 64 or 128) run the halo-tiled 3x3 kernel (variant 24; variant 25 for 32 -> 32 channels) in the forward and the
+    input gradient; 240 -> 120 runs every variant on the virtually padded contraction (ssseg.nn.vpad)."""
     from ssseg import native as N
     from ssseg import nn as snn
     snn.set_compute_dtype(torch.bfloat16)
