@@ -17,44 +17,56 @@
 // 4 waves; wave w owns output row w of the tile: 4 pixel fragments x 2 channel fragments (32 accumulator VGPRs), its
 // weights are 18 bf16x8 fragments (72 VGPRs).  Halo pixel p keeps its four 16-byte channel chunks at slots c ^ ((p >> 2)
 // & 3): the 16 lanes of a fragment read 16 consecutive pixels' chunk c from four different bank groups.  The LDS-staged
-// epilogue (store_tile_lds, T2D row map, fused BN statistics) reuses the halo buffer.
+// epilogue (store_tile_lds, T2D row map, fused BN statistics) reuses the tile's halo buffer.  Measured: a one-tile-per-
+// block form (4096 blocks at 16x256^2) ran 32->32 @16x256^2 in 60 us (the gather kernel: 89 us); persistent below.
 #include "conv_kernels.h"
+
+#include <algorithm>
 
 namespace {
 
 constexpr int HS_PX = 400;                    // halo pixels: 6 rows x 66 (+4 padding pixels)
 constexpr int HS_XBUF = HS_PX * 64;           // 32 channels x 2 B per pixel
 constexpr int HS_EPI = 256 * (32 * 4 + 16);   // the staged 256 x 32 fp32 output tile
-constexpr int HS_SMEM = HS_EPI > HS_XBUF ? HS_EPI : HS_XBUF;
+constexpr int HS_BUF = HS_EPI > HS_XBUF ? HS_EPI : HS_XBUF;
+constexpr int HS_SMEM = 2 * HS_BUF;           // two buffers: 73,728 B, two blocks per CU
 
 __device__ __forceinline__ int hs_swz(int p) { return (p >> 2) & 3; }
 
+// Persistent: block b runs tiles b, b + G, b + 2G, ... (G = grid size).  Buffer (it & 1) holds tile it's halo, and
+// after its MFMAs the same buffer stages its output for the epilogue; tile it + 1's halo streams into the other
+// buffer meanwhile.  The halo DMA is issued from inline asm (invisible to the compiler's waitcnt bookkeeping) and
+// waited for with an explicit count: at the top of iteration it, the only VM operations younger than tile it's halo
+// are tile it - 1's epilogue stores -- at least 4 per thread (4 row passes x one 16-byte store; more with an aux copy,
+// residual loads or the statistics row) -- so vmcnt(4) guarantees the halo landed (in-order retirement).
 template <typename TO, bool STATS>
-__global__ void __launch_bounds__(256) hconv3s_kernel(const TO* __restrict__ x, const TO* __restrict__ w,
-                                                      TO* __restrict__ y, ConvGeom g, Epi<TO> ep, unsigned xbytes) {
+__global__ void __launch_bounds__(256, 2) hconv3s_kernel(const TO* __restrict__ x, const TO* __restrict__ w,
+                                                         TO* __restrict__ y, ConvGeom g, Epi<TO> ep, unsigned xbytes,
+                                                         int ntiles) {
   __shared__ __attribute__((aligned(1024))) char smem[HS_SMEM];
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int nstrips = g.W >> 6, nrg = g.H >> 2;
-  const int pt = xcd_tile(blockIdx.x, gridDim.x);
-  const int strip = pt % nstrips, q = pt / nstrips;
-  const int rg = q % nrg, n = q / nrg;
-  const int y0 = rg * 4, x0 = strip * 64;
   const int H = g.H, W = g.W;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)xbytes, 0x00020000);
 
-  // halo: 25 wave-instructions of 64 chunks, chunk q = 64 i + lane -> pixel p = q / 4 at slot q % 4, which holds the
-  // global chunk (q % 4) ^ swz(p); padding / out-of-image pixels read zeros (out-of-range offset)
-  for (int i = wave; i < HS_PX * 4 / 64; i += 4) {
-    const int qq = 64 * i + lane, p = qq >> 2, slot = qq & 3;
-    const int row = p / 66, col = p - row * 66;
-    const int yy = y0 - 1 + row, xx = x0 - 1 + col;
-    unsigned off = OOB;
-    if (p < 396 && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
-      off = (unsigned)(((n * H + yy) * W + xx) * g.ldx + 8 * (slot ^ hs_swz(p))) * 2u;
-    bldslds16(xr, smem + i * 1024, off, 0u);
-  }
+  // halo of tile pt into buffer b: 25 wave-instructions of 64 chunks, chunk q = 64 i + lane -> pixel p = q / 4 at
+  // slot q % 4, which holds the global chunk (q % 4) ^ swz(p); padding / out-of-image pixels read zeros
+  auto issue_halo = [&](int b, int pt) {
+    const int strip = pt % nstrips, q = pt / nstrips;
+    const int rg = q % nrg, n = q / nrg;
+    const int y0 = rg * 4, x0 = strip * 64;
+    for (int i = wave; i < HS_PX * 4 / 64; i += 4) {
+      const int qq = 64 * i + lane, p = qq >> 2, slot = qq & 3;
+      const int row = p / 66, col = p - row * 66;
+      const int yy = y0 - 1 + row, xx = x0 - 1 + col;
+      unsigned off = OOB;
+      if (p < 396 && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
+        off = (unsigned)(((n * H + yy) * W + xx) * g.ldx + 8 * (slot ^ hs_swz(p))) * 2u;
+      bldslds16_nt(xr, smem + b * HS_BUF + i * 1024, off, 0u);
+    }
+  };
 
-  // weights into registers: tap t, fragment i -> output channel 16 i + (lane & 15), channels 8 (lane >> 4) .. + 7
+  // weights into registers once: tap t, fragment i -> output channel 16 i + (lane & 15), channels 8 (lane >> 4) .. + 7
   const int li = lane & 15, lg = lane >> 4;
   bf16x8 wf[9][2];
 #pragma unroll
@@ -62,33 +74,43 @@ __global__ void __launch_bounds__(256) hconv3s_kernel(const TO* __restrict__ x, 
 #pragma unroll
     for (int i = 0; i < 2; ++i) wf[tp][i] = *(const bf16x8*)(w + (long long)(i * 16 + li) * g.ldw + tp * 32 + lg * 8);
 
-  f32x4 acc[2][4];   // [channel fragment][pixel fragment]
+  const int G = gridDim.x;
+  int pt = blockIdx.x;
+  if (pt < ntiles) issue_halo(0, pt);
+  for (int it = 0; pt < ntiles; ++it, pt += G) {
+    const int b = it & 1;
+    if (it == 0) vmcnt_wait<0>();
+    else vmcnt_wait<4>();
+    __syncthreads();   // tile pt's halo landed for every wave; buffer b ^ 1 (the last epilogue's) is free
+    if (pt + G < ntiles) issue_halo(b ^ 1, pt + G);
+    const char* X = smem + b * HS_BUF;
+    f32x4 acc[2][4];   // [channel fragment][pixel fragment]
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  vmcnt_wait<0>();
-  __syncthreads();
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int r = 0; r < 3; ++r)
+    for (int r = 0; r < 3; ++r)
 #pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      bf16x8 bfr[4];
+      for (int s = 0; s < 3; ++s) {
+        bf16x8 bfr[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int p = (wave + r) * 66 + j * 16 + li + s;
-        bfr[j] = *(const bf16x8*)(smem + p * 64 + ((lg ^ hs_swz(p)) << 4));
+        for (int j = 0; j < 4; ++j) {
+          const int p = (wave + r) * 66 + j * 16 + li + s;
+          bfr[j] = *(const bf16x8*)(X + p * 64 + ((lg ^ hs_swz(p)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = M16<TO>::mma(wf[r * 3 + s][i], bfr[j], acc[i][j]);
       }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = M16<TO>::mma(wf[r * 3 + s][i], bfr[j], acc[i][j]);
-    }
-
-  const Tile2D t2{n, y0, x0, min(4, H - y0), (long long)pt};
-  store_tile_lds<TO, 256, 32, 4, 2, 256, STATS, 1, true>(acc, smem, 0, 0, wave * 64, 0, lane, g, y, ep,
-                                                        PreRes<1>{{}, false}, t2);
+    const int strip = pt % nstrips, q = pt / nstrips;
+    const int rg = q % nrg, n = q / nrg;
+    const Tile2D t2{n, rg * 4, strip * 64, min(4, H - rg * 4), (long long)pt};
+    // staged in this tile's own buffer (store_tile_lds opens with a barrier: every wave's MFMAs are done with it)
+    store_tile_lds<TO, 256, 32, 4, 2, 256, STATS, 1, true>(acc, smem + b * HS_BUF, 0, 0, wave * 64, 0, lane, g, y, ep,
+                                                          PreRes<1>{{}, false}, t2);
+  }
 }
 
 }  // namespace
@@ -104,14 +126,18 @@ template <typename TO>
 int launch_hconv3s(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
                    hipStream_t s, float* ws, const PhaseTab* ph, const void* x2) {
   if (x2 || !hconv3s_ok(g, ph, ws)) return -1;
-  const long long blocks = (long long)g.N * (g.H / 4) * (g.W / 64);
-  if (blocks > 0x7fffffffLL) return -1;
+  const long long tiles = (long long)g.N * (g.H / 4) * (g.W / 64);
+  if (tiles > 0x7fffffffLL) return -1;
+  // two resident blocks per CU (73.7 KB of LDS each): a grid of 2 x 256 covers the chip once, every block then
+  // loops over its tiles (the epilogue's stores must leave >= 4 VM operations per thread behind the next halo's DMA:
+  // 4 row passes of the 256 x 32 tile, guaranteed by H % 4 == 0, W % 64 == 0, K == 32)
+  const unsigned grid = (unsigned)std::min<long long>(tiles, 512);
   if (ep.stats)
-    hipLaunchKernelGGL((hconv3s_kernel<TO, true>), dim3((unsigned)blocks), dim3(256), 0, s, (const TO*)x,
-                       (const TO*)w, (TO*)y, g, ep, xb);
+    hipLaunchKernelGGL((hconv3s_kernel<TO, true>), dim3(grid), dim3(256), 0, s, (const TO*)x, (const TO*)w, (TO*)y, g,
+                       ep, xb, (int)tiles);
   else
-    hipLaunchKernelGGL((hconv3s_kernel<TO, false>), dim3((unsigned)blocks), dim3(256), 0, s, (const TO*)x,
-                       (const TO*)w, (TO*)y, g, ep, xb);
+    hipLaunchKernelGGL((hconv3s_kernel<TO, false>), dim3(grid), dim3(256), 0, s, (const TO*)x, (const TO*)w, (TO*)y,
+                       g, ep, xb, (int)tiles);
   return 256;
 }
 

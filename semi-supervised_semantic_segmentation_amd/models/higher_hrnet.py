@@ -188,6 +188,12 @@ class TransitionFuse(nn.Module):
         self.fuse_layers = nn.ModuleList(fuse_layers)
 
     def forward(self, input: List[torch.Tensor]):
+        if len(self.fuse_layers) > 1:
+            # input j feeds every output branch: its conv consumers' input gradients meet in one join (the last one
+            # adds the others' in its dgrad epilogue) instead of one autograd add per extra consumer; an identity
+            # consumer (j == i) still reaches x_j through autograd's own accumulation
+            for t in input:
+                snn.mark_join(t)
         output = []
         for i, scale_fuse_layers in enumerate(self.fuse_layers):
             tensors = []

@@ -338,6 +338,38 @@ def test_conv_variants_bitwise(hip_device, kind, cin, cout, k, H):
         assert torch.equal(gx, outs[0][2]), f'variant {v}: input gradient differs'
 
 
+@pytest.mark.parametrize('n,H,W', [(4, 256, 256), (3, 20, 192)])
+def test_hconv3s_persistent_bitwise(hip_device, n, H, W):
+    """The 32 -> 32-channel halo kernel (variant 25) is persistent (<= 512 blocks looping over 4 x 64 tiles with the
+    next halo in flight): more tiles than blocks (1024 at 4 x 256^2) and a ragged last round must give the gather
+    kernel's outputs bit for bit, forward and input gradient, with and without the fused BN statistics."""
+    from ssseg import native as N
+    from ssseg import nn as snn
+    snn.set_compute_dtype(torch.bfloat16)
+    torch.manual_seed(3)
+    conv = snn.Conv2d(32, 32, 3, 1, 1, bias=False).to(hip_device)
+    bn = snn.BatchNorm2d(32).to(hip_device)
+    x = _act_in(torch.randn(n, 32, H, W), hip_device).detach().requires_grad_(True)
+    outs = []
+    try:
+        for v in (14, 25):
+            N.call('ssseg_set_knob', 4, v)
+            y = conv(x)
+            (gx,) = torch.autograd.grad(y, x, torch.ones_like(y))
+            bn.reset_running_stats()
+            with torch.no_grad():
+                z = snn.conv_bn_act(conv, x, bn, relu=True)
+            torch.cuda.synchronize()
+            outs.append((y.detach().clone(), gx.clone(), z.clone(), bn.running_mean.clone(), bn.running_var.clone()))
+    finally:
+        N.call('ssseg_set_knob', 4, 0)
+    a, b = outs
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    assert torch.equal(a[2], b[2])
+    torch.testing.assert_close(a[3], b[3], rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(a[4], b[4], rtol=1e-6, atol=1e-7)
+
+
 WGRAD_CASES = [
     # cin, cout, k, stride, pad, dil, H, W, N   (the LDS-DMA weight-gradient kernel)
     (64, 64, 3, 1, 1, 1, 37, 29, 2),      # 64-channel kk-tiles, 64-channel co tile, several pixel splits
