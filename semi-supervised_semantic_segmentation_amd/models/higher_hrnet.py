@@ -255,8 +255,8 @@ class HighResolutionMultiscaleAggregator(nn.Module):
 
     def forward(self, input: List[torch.Tensor]):
         tgt = (input[0].shape[2], input[0].shape[3])
-        resized = [snn.resize_act(t, tgt, align_corners=False) for t in input]
-        return snn.cat_n(resized, [t.shape[1] for t in input])
+        # the resizes write straight into their channel slices of the concat (snn.resize_cat)
+        return snn.resize_cat(input, [t.shape[1] for t in input], tgt, align_corners=False)
 
 
 class Stem(nn.Module):

@@ -1684,6 +1684,71 @@ class _CatNFn(torch.autograd.Function):
         return tuple(out)
 
 
+class _ResizeCatFn(torch.autograd.Function):
+    """cat_n([resize_act(t, size) for t in ts], chans) with every resize written straight into its channel slice of the
+    concat (the NHWC bilinear kernels take output strides), and in the backward read straight from the slice of the
+    concat's gradient: the resized maps are never materialised (HRNet's multi-resolution aggregation,
+    higher_hrnet.py:1020-1034).  Same-size inputs are copied, like cat_n.  Results are bitwise those of
+    resize_act + cat_n (the same kernels on the same values)."""
+
+    @staticmethod
+    def forward(ctx, size, align_corners, chans, *ts):
+        n = ts[0].shape[0]
+        H, W = size
+        total = sum(chans)
+        cp = rup(total, vec())
+        y = new_act(n, cp, H, W, ts[0].dtype, ts[0].device, zero=cp != total)
+        ys = y.stride()
+        c0 = 0
+        for t, c in zip(ts, chans):
+            _, pc, h, w = t.shape
+            if (h, w) == (H, W):
+                N.call('ssseg_nhwc_copy', N.dev_ptr(t), N.dev_ptr(y) + c0 * y.element_size(), n, H, W, c, H, W, pc,
+                       0, 0, H, W, cp, 0, 0, N.dt_code(t), N.stream())
+            else:
+                N.call('ssseg_bilinear_fwd', N.dev_ptr(t), N.dev_ptr(y) + c0 * y.element_size(), n, c, h, w, H, W,
+                       N.strides4(t), _strides4(ys), int(align_corners), N.dt_code(t), N.stream())
+            c0 += c
+        ctx.meta = (tuple(tuple(t.shape) for t in ts), tuple(chans), cp, bool(align_corners), ts[0].dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        shapes, chans, cp, ac, dt = ctx.meta
+        n, _, H, W = gy.shape
+        gs = gy.stride()
+        out, c0 = [None, None, None], 0
+        for (_, pc, h, w), c in zip(shapes, chans):
+            g = new_act(n, pc, h, w, dt, gy.device, zero=pc != c)
+            if (h, w) == (H, W):
+                N.call('ssseg_nhwc_copy', N.dev_ptr(gy) + c0 * gy.element_size(), N.dev_ptr(g), n, H, W, c, H, W, cp,
+                       0, 0, H, W, pc, 0, 0, N.dt_code(gy), N.stream())
+            else:
+                N.call('ssseg_bilinear_bwd', N.dev_ptr(gy) + c0 * gy.element_size(), N.dev_ptr(g), n, c, h, w, H, W,
+                       _strides4(gs), N.strides4(g), int(ac), N.dt_code(gy), N.stream())
+            out.append(g)
+            c0 += c
+        return tuple(out)
+
+
+def _strides4(st):
+    import ctypes
+    return (ctypes.c_int64 * 4)(*st)
+
+
+def resize_cat(tensors, chans, size, align_corners=False):
+    """cat_n of the bilinear resizes of `tensors` to `size` (NHWC activations, real channel counts `chans`) without
+    materialising the resized maps.  Falls back to resize_act + cat_n where the slice writes cannot be 16-byte
+    vectors (a channel offset not a multiple of 8)."""
+    for t in tensors:
+        _need_act(t, None, 'resize_cat')
+    offs = [sum(chans[:i]) for i in range(len(chans))]
+    if len(tensors) == 1 or any(o % 8 for o in offs) or any(c % 8 for c in chans):
+        return cat_n([resize_act(t, size, align_corners) for t in tensors], chans)
+    return _ResizeCatFn.apply((int(size[0]), int(size[1])), bool(align_corners), tuple(int(c) for c in chans),
+                              *tensors)
+
+
 def cat_n(tensors, chans):
     """Concatenate NHWC activations along channels; chans[i] = real channel count of tensors[i]."""
     for t in tensors:
