@@ -171,6 +171,11 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x
       if (MODE == 1 && res && relu)
 #pragma unroll
         for (int u = 0; u < U; ++u) qr[u] = CK::ld(res + clampp(p0 + u * stride, P) * ldr + c0);
+      // the U pixels of this batch are summed in fp32 (in u order: 4 terms; bf16 squares are exact in fp32), then one
+      // fp64 add per chunk and batch -- the per-element fp64 converts and adds made this pass VALU-bound (3.1 TB/s)
+      float f1[V], f2[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) f1[e] = f2[e] = 0.f;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (p0 + u * stride >= P) continue;
@@ -181,16 +186,21 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x
 #pragma unroll
         for (int e = 0; e < V; ++e) {
           if (MODE == 0) {
-            s1[e] += (double)v[u][e];
-            s2[e] += (double)v[u][e] * (double)v[u][e];
+            f1[e] += v[u][e];
+            f2[e] = fmaf(v[u][e], v[u][e], f2[e]);
           } else {
             const float xh = (v[u][e] - mu[e]) * is[e];
             float gr = g[u][e];
             if (relu) gr = act_bwd(gr, fmaf(ga[e], xh, be[e]) + r[u][e], relu, 0.f);
-            s1[e] += (double)gr;
-            s2[e] += (double)gr * (double)xh;
+            f1[e] += gr;
+            f2[e] = fmaf(gr, xh, f2[e]);
           }
         }
+      }
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        s1[e] += (double)f1[e];
+        s2[e] += (double)f2[e];
       }
     }
   }
@@ -466,6 +476,9 @@ __global__ void __launch_bounds__(256) bn_eval_bwd_kernel(const T* __restrict__ 
       if (relu && !ymode)
 #pragma unroll
         for (int u = 0; u < U; ++u) qy[u] = CK::ld(y + clampp(p0 + u * stride, P) * ld + c0);
+      float f1[V], f2[V];   // this batch's U pixels summed in fp32 (in u order), then one fp64 add per chunk
+#pragma unroll
+      for (int e = 0; e < V; ++e) f1[e] = f2[e] = 0.f;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t p = p0 + u * stride;
@@ -486,11 +499,16 @@ __global__ void __launch_bounds__(256) bn_eval_bwd_kernel(const T* __restrict__ 
           gr = live[e] ? gr : 0.f;
           od[e] = gr;
           oc[e] = sc[e] * gr;
-          s1[e] += (double)gr;
-          s2[e] += (double)gr * (double)((a[u][e] - me[e]) * is[e]);
+          f1[e] += gr;
+          f2[e] = fmaf(gr, (a[u][e] - me[e]) * is[e], f2[e]);
         }
         Vec<T, V>::st(dconv + p * ld + c0, oc);
         if (dres) Vec<T, V>::st(dres + p * ld + c0, od);
+      }
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        s1[e] += (double)f1[e];
+        s2[e] += (double)f2[e];
       }
     }
   }
