@@ -954,8 +954,23 @@ constexpr unsigned OOB = 0x80000000u;   // > any num_records we build: the load 
 // 64-channel blocks); 2 = general k (any C % 8 == 0: HRNet-W32's 32-channel branches, HarDNet's growth layers):
 // k runs linearly, k = tap * C + c, exactly like the register-staged kernel, so a 64-deep k-tile may hold several
 // taps -- every lane splits its own 16-byte chunk's k into (tap, channel) and gathers from that tap's pixel
+// minimum waves per SIMD the register allocator must leave room for, where registers (not LDS) bound the occupancy:
+// the single-slot 128x64 tile (the 1x1 expansions' choice, a load -> 8 MFMA -> store chain per tile) fits four blocks
+// per CU in LDS (34.8 KB each) but its 140 registers allowed three -- capped at 128 it runs four (64->256 1x1
+// @16x128^2: 56 -> 48 us, with fused statistics 78 -> 69 us); the 8-wave 256x64 two-slot tile fits two blocks in LDS
+// (80 KB each) but its statistics instantiation's 132 registers allowed one; the 8-wave 128x64 two-slot tile fits
+// three blocks (48 KB) but its 88-92 registers allowed two
+#ifndef SSSEG_GLDS_OCC_MODE
+#define SSSEG_GLDS_OCC_MODE 1   // 0: no caps, 2: also the 8-wave 128x64 tile at 6 waves (spills; A/B builds)
+#endif
+#define GLDS_OCC(BM, BN, NW, NS)                                                                                   \
+  (SSSEG_GLDS_OCC_MODE == 0 ? 1                                                                                  \
+   : (((BM) == 128 && (BN) == 64 && (NW) == 4 && (NS) == 1) ||                                                   \
+      ((BM) == 256 && (BN) == 64 && (NW) == 8 && (NS) == 2))                                                     \
+       ? 4                                                                                                       \
+       : ((SSSEG_GLDS_OCC_MODE >= 2 && (BM) == 128 && (BN) == 64 && (NW) == 8 && (NS) == 2) ? 6 : 1))
 template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS, bool STATS, int KM = 0>
-__global__ void __launch_bounds__(NW * 64, 1) igemm_glds_kernel(const TO* __restrict__ x,
+__global__ void __launch_bounds__(NW * 64, GLDS_OCC(BM, BN, NW, NS)) igemm_glds_kernel(const TO* __restrict__ x,
                                                                 const TO* __restrict__ w, TO* __restrict__ y,
                                                                 ConvGeom g, Epi<TO> ep, unsigned xbytes,
                                                                 unsigned wbytes, int g_epi_lds, int splits,

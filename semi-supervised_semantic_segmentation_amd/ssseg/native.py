@@ -11,7 +11,7 @@ import re
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libssseg.so')
+LIB_PATH = os.environ.get('SSSEG_LIB_PATH') or os.path.join(_HERE, 'libssseg.so')   # override: A/B builds only
 HEADER = os.path.join(_HERE, '..', '..', 'include', 'ssseg.h')
 
 F32, BF16, F16 = 0, 1, 2
