@@ -100,6 +100,14 @@ int ssseg_bilinear_bwd(const void* gy, void* gx, int64_t N, int64_t C, int64_t H
                        int64_t Wo, const int64_t* gy_strides4_host, const int64_t* gx_strides4_host,
                        int align_corners, int dt, ssseg_stream_t stream);
 
+/* ssseg_bilinear_bwd for 16-bit NHWC tensors in two separable passes (output rows summed over their columns into an
+ * fp32 workspace, then combined over the rows): bitwise the same gx, parallel over Ho x W chunks instead of walking the
+ * whole output window per input chunk.  Falls back to ssseg_bilinear_bwd where the NHWC kernels do not apply. */
+size_t ssseg_bilinear_bwd_workspace_bytes(int64_t N, int64_t C, int64_t W, int64_t Ho);
+int ssseg_bilinear_bwd_ws(const void* gy, void* gx, int64_t N, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
+                          const int64_t* gy_strides4_host, const int64_t* gx_strides4_host, int align_corners, int dt,
+                          void* ws, size_t ws_bytes, ssseg_stream_t stream);
+
 /* Rotation about the image centre by angle_deg (counter-clockwise, OpenCV / kornia get_rotation_matrix2d),
  * bilinear with zero padding, NCHW contiguous fp32: reversible_augmentations.Rotate.apply / reverse
  * (reference reversible_augmentations.py:5-23, kornia.rotate; kornia is unpinned and absent, parity with it is

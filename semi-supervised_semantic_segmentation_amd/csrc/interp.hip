@@ -215,6 +215,69 @@ __global__ void __launch_bounds__(256) bilinear_bwd_nhwc_kernel(const T* __restr
   *(uint4*)(gx + (int64_t)n * gxs.n + (int64_t)h * gxs.h + (int64_t)w * gxs.w + c) = pack8<T>(acc);
 }
 
+// The same input gradient in two separable passes (bitwise the one-pass kernel: that kernel already sums each output
+// row over its columns first, row[] = sum_ow g * ww in ow order, then acc = sum_oh row * wh in oh order, skipping rows
+// with wh == 0; here pass 1 stores those row sums in fp32 for every (oh, w), pass 2 combines them).  The one-pass kernel
+// has one thread per INPUT chunk walking a (2^k + 1)^2 output window with dependent loads -- 81 of them per thread for
+// HRNet's 8x fuse upsampling, over a grid of only N x h x w x C/8 threads (43 us average in C4's step); each pass here
+// walks one axis (<= 2^k + 1 loads) over a grid of N x Ho x w (resp. N x h x w) chunks.
+template <typename T>
+__global__ void __launch_bounds__(256) bilinear_bwd_rows_nhwc_kernel(const T* __restrict__ gy, float* __restrict__ rs,
+                                                                     int C8, int Ho, Axis aw, Strides gys) {
+  const int oh = blockIdx.y, n = blockIdx.z;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= aw.in * C8) return;
+  const int w = idx / C8, c = (idx - w * C8) * 8;
+  int owlo, owhi;
+  out_window(aw, w, owlo, owhi);
+  const T* gb = gy + (int64_t)n * gys.n + (int64_t)oh * gys.h + c;
+  float row[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) row[e] = 0.f;
+  for (int ow = owlo; ow <= owhi; ++ow) {
+    int w0, w1;
+    float m0, m1;
+    src_index(aw, ow, w0, w1, m0, m1);
+    const float ww = (w0 == w ? m0 : 0.f) + (w1 == w ? m1 : 0.f);
+    if (ww != 0.f) {
+      float g[8];
+      Chunk<T, 8>::cvt(Chunk<T, 8>::ld(gb + (int64_t)ow * gys.w), g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) row[e] = fmaf(g[e], ww, row[e]);
+    }
+  }
+  float* r = rs + (((int64_t)n * Ho + oh) * aw.in + w) * (C8 * 8) + c;
+  *(float4*)r = make_float4(row[0], row[1], row[2], row[3]);
+  *(float4*)(r + 4) = make_float4(row[4], row[5], row[6], row[7]);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bilinear_bwd_cols_nhwc_kernel(const float* __restrict__ rs, T* __restrict__ gx,
+                                                                     int C8, int Ho, Axis ah, int Wi, Strides gxs) {
+  const int h = blockIdx.y, n = blockIdx.z;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= Wi * C8) return;
+  const int w = idx / C8, c = (idx - w * C8) * 8;
+  int ohlo, ohhi;
+  out_window(ah, h, ohlo, ohhi);
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  for (int oh = ohlo; oh <= ohhi; ++oh) {
+    int h0, h1;
+    float l0, l1;
+    src_index(ah, oh, h0, h1, l0, l1);
+    const float wh = (h0 == h ? l0 : 0.f) + (h1 == h ? l1 : 0.f);
+    if (wh == 0.f) continue;
+    const float* r = rs + (((int64_t)n * Ho + oh) * Wi + w) * (C8 * 8) + c;
+    const float4 a = *(const float4*)r, b = *(const float4*)(r + 4);
+    const float row[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = fmaf(row[e], wh, acc[e]);
+  }
+  *(uint4*)(gx + (int64_t)n * gxs.n + (int64_t)h * gxs.h + (int64_t)w * gxs.w + c) = pack8<T>(acc);
+}
+
 // the NHWC kernels apply: 16-bit, channels fastest in both tensors, 16-byte aligned chunks, grid dims in range
 static bool nhwc_ok(const void* a, const void* b, int64_t N, int64_t C, int64_t rows, int64_t cols, const Strides& as,
                     const Strides& bs, int dt) {
@@ -266,6 +329,40 @@ extern "C" int ssseg_bilinear_fwd(const void* x, void* y, int64_t N, int64_t C, 
     return SSSEG_EUNSUPPORTED;
   }
 #undef BIL_FWD
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" size_t ssseg_bilinear_bwd_workspace_bytes(int64_t N, int64_t C, int64_t W, int64_t Ho) {
+  if (N < 1 || C < 1 || W < 1 || Ho < 1) return 0;
+  return (size_t)N * Ho * W * ((C + 7) / 8 * 8) * sizeof(float) + 256;
+}
+
+extern "C" int ssseg_bilinear_bwd_ws(const void* gy, void* gx, int64_t N, int64_t C, int64_t H, int64_t W, int64_t Ho,
+                                     int64_t Wo, const int64_t* gys4, const int64_t* gxs4, int align_corners, int dt,
+                                     void* ws, size_t ws_bytes, ssseg_stream_t stream) {
+  if (!gy || !gx || !gys4 || !gxs4 || N < 0 || C < 0 || H < 1 || W < 1 || Ho < 1 || Wo < 1) return SSSEG_EINVAL;
+  if (N * C * H * W == 0) return 0;
+  const Strides gys = to_strides(gys4), gxs = to_strides(gxs4);
+  if (!ws || !nhwc_ok(gy, gx, N, C, H, W, gys, gxs, dt) || !nhwc_ok(gy, gx, N, C, Ho, W, gys, gxs, dt))
+    return ssseg_bilinear_bwd(gy, gx, N, C, H, W, Ho, Wo, gys4, gxs4, align_corners, dt, stream);
+  if (ws_bytes < ssseg_bilinear_bwd_workspace_bytes(N, C, W, Ho) || ((uintptr_t)ws & 15)) return SSSEG_EWORKSPACE;
+  const Axis ah = make_axis(H, Ho, align_corners), aw = make_axis(W, Wo, align_corners);
+  const int C8 = (int)(C / 8);
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g1((unsigned)((W * C8 + 255) / 256), (unsigned)Ho, (unsigned)N), b(256);
+  const dim3 g2((unsigned)((W * C8 + 255) / 256), (unsigned)H, (unsigned)N);
+  if (dt == SSSEG_BF16) {
+    hipLaunchKernelGGL(bilinear_bwd_rows_nhwc_kernel<bf16_t>, g1, b, 0, s, (const bf16_t*)gy, (float*)ws, C8, (int)Ho,
+                       aw, gys);
+    hipLaunchKernelGGL(bilinear_bwd_cols_nhwc_kernel<bf16_t>, g2, b, 0, s, (const float*)ws, (bf16_t*)gx, C8, (int)Ho,
+                       ah, (int)W, gxs);
+  } else {
+    hipLaunchKernelGGL(bilinear_bwd_rows_nhwc_kernel<f16_t>, g1, b, 0, s, (const f16_t*)gy, (float*)ws, C8, (int)Ho,
+                       aw, gys);
+    hipLaunchKernelGGL(bilinear_bwd_cols_nhwc_kernel<f16_t>, g2, b, 0, s, (const float*)ws, (f16_t*)gx, C8, (int)Ho,
+                       ah, (int)W, gxs);
+  }
   SSSEG_LAUNCH_CHECK();
   return 0;
 }

@@ -35,6 +35,8 @@ SIGS = {
     'ssseg_cast': (i32, [vp, vp, i64, i32, i32, vp]),
     'ssseg_bilinear_fwd': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, I64P, I64P, i32, i32, vp]),
     'ssseg_bilinear_bwd': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, I64P, I64P, i32, i32, vp]),
+    'ssseg_bilinear_bwd_workspace_bytes': (sz, [i64, i64, i64, i64]),
+    'ssseg_bilinear_bwd_ws': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, I64P, I64P, i32, i32, vp, sz, vp]),
     'ssseg_aug_warp': (i32, [vp, vp, i64, i64, i64, i64, vp, vp, i64, i64, vp, vp, vp, i32, vp]),
     'ssseg_aug_color': (i32, [vp, i64, i64, i64, vp, vp]),
     'ssseg_aug_blur': (i32, [vp, vp, i64, i64, i64, i64, vp, vp, i64, i32, i32, vp]),

@@ -1724,8 +1724,8 @@ class _ResizeCatFn(torch.autograd.Function):
                 N.call('ssseg_nhwc_copy', N.dev_ptr(gy) + c0 * gy.element_size(), N.dev_ptr(g), n, H, W, c, H, W, cp,
                        0, 0, H, W, pc, 0, 0, N.dt_code(gy), N.stream())
             else:
-                N.call('ssseg_bilinear_bwd', N.dev_ptr(gy) + c0 * gy.element_size(), N.dev_ptr(g), n, c, h, w, H, W,
-                       _strides4(gs), N.strides4(g), int(ac), N.dt_code(gy), N.stream())
+                _bilinear_bwd(gy, g, n, c, h, w, H, W, _strides4(gs), N.strides4(g), ac,
+                              gy_ptr=N.dev_ptr(gy) + c0 * gy.element_size())
             out.append(g)
             c0 += c
         return tuple(out)
@@ -1828,6 +1828,14 @@ class AdaptiveAvgPool2d(nn.AdaptiveAvgPool2d):
         return global_avgpool(x)
 
 
+def _bilinear_bwd(gy, gx, n, c, h, w, oh, ow, gys4, gxs4, ac, gy_ptr=None):
+    """gx = bilinear backward of gy (ssseg_bilinear_bwd_ws: two separable passes through an fp32 workspace)."""
+    nb = N.lib().ssseg_bilinear_bwd_workspace_bytes(n, c, w, oh)
+    ws = N.workspace(nb, gy.device)
+    N.call('ssseg_bilinear_bwd_ws', gy_ptr if gy_ptr is not None else N.dev_ptr(gy), N.dev_ptr(gx), n, c, h, w, oh, ow,
+           gys4, gxs4, int(ac), N.dt_code(gy), N.dev_ptr(ws), nb, N.stream())
+
+
 class _ActBilinear(torch.autograd.Function):
     """F.interpolate(mode='bilinear') between NHWC activations (always channels_last in and out, including
     1x1 maps): HarDNet TransitionUp (hardnet.py:88), HRNet fuse / aggregation (higher_hrnet.py:454,1030),
@@ -1847,8 +1855,7 @@ class _ActBilinear(torch.autograd.Function):
     def backward(ctx, gy):
         n, c, h, w, oh, ow, ac, dt = ctx.meta
         gx = new_act(n, c, h, w, dt, gy.device)
-        N.call('ssseg_bilinear_bwd', N.dev_ptr(gy), N.dev_ptr(gx), n, c, h, w, oh, ow, N.strides4(gy), N.strides4(gx),
-               int(ac), N.dt_code(gy), N.stream())
+        _bilinear_bwd(gy, gx, n, c, h, w, oh, ow, N.strides4(gy), N.strides4(gx), ac)
         return gx, None, None
 
 

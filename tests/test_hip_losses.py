@@ -107,6 +107,33 @@ def test_bilinear_nhwc_vector_path_bitwise(hip_device, dt, shape, size, ac):
     np.testing.assert_allclose(outs[0][0].float().cpu().numpy(), ref.numpy(), rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize('shape,size,ac', [((2, 32, 32, 32), (256, 256), False), ((2, 64, 17, 13), (34, 26), True),
+                                           ((3, 16, 40, 36), (20, 18), False), ((1, 256, 8, 8), (64, 64), False)])
+def test_bilinear_bwd_two_pass_bitwise(hip_device, shape, size, ac):
+    """ssseg_bilinear_bwd_ws (separable rows / columns passes through an fp32 workspace, the activation resizes'
+    backward) is bitwise the one-pass NHWC kernel (ssseg_bilinear_bwd), incl. 8x upsampling (HRNet fuse) and a
+    downsampling resize."""
+    from ssseg import native as N
+    from ssseg import nn as snn
+    n, c, h, w = shape
+    oh, ow = size
+    g = torch.Generator().manual_seed(7)
+    gy = torch.randn(n, c, oh, ow, generator=g).to(torch.bfloat16).to(hip_device).contiguous(
+        memory_format=torch.channels_last)
+    outs = []
+    for two in (False, True):
+        gx = torch.empty(n, c, h, w, dtype=torch.bfloat16, device=hip_device).contiguous(
+            memory_format=torch.channels_last)
+        if two:
+            snn._bilinear_bwd(gy, gx, n, c, h, w, oh, ow, N.strides4(gy), N.strides4(gx), ac)
+        else:
+            N.call('ssseg_bilinear_bwd', N.dev_ptr(gy), N.dev_ptr(gx), n, c, h, w, oh, ow, N.strides4(gy),
+                   N.strides4(gx), int(ac), N.dt_code(gy), N.stream())
+        torch.cuda.synchronize()
+        outs.append(gx)
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_bce_fwd_bwd(hip_device):
     rng = np.random.default_rng(1)
     x = (rng.standard_normal((4, 2, 64, 64)) * 3).astype(np.float32)
