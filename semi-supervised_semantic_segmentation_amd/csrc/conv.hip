@@ -87,6 +87,8 @@ int launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvGe
     case 23: return launch_glds_grp_e<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
     case 24: return launch_hconv3<TO>(x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);   // halo-tiled 3x3 (-1: n/a)
     case 25: return launch_hconv3s<TO>(x, w, y, g, ep, xb, s, ws, ph, x2);   // its 32 -> 32-channel form
+    case 26: return launch_pw<TO>(4, x, w, y, g, ep, s, ws, ph, x2);   // pointwise, 64-pixel wave tiles
+    case 27: return launch_pw<TO>(2, x, w, y, g, ep, s, ws, ph, x2);   // pointwise, 32-pixel wave tiles
     case 5:
     case 7:
     case 8:
@@ -103,7 +105,8 @@ int launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvGe
 // where it applies).  With knob 5 on (default) an unseen geometry is timed once over the candidates on the caller's
 // stream (HIP events) and the fastest is cached.
 constexpr int kSplitBit = 256;   // cached choice flag: run the variant with its split-K plan
-constexpr int kCandidates[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25};
+constexpr int kCandidates[] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  10, 12, 13, 14,
+                                15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27};
 std::unordered_map<unsigned long long, int> g_variant;
 std::mutex g_variant_mu;
 
@@ -128,6 +131,7 @@ template <typename T, typename TO>
 int run_variant(int v, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
                 unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph = nullptr, const void* x2 = nullptr,
                 unsigned x2b = 0) {
+  t_pw_rows = -1;
   if constexpr (sizeof(TO) == 2) {
     if (v != 0) return launch_glds_cfg<TO>(v, x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
   }
@@ -245,7 +249,7 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
       // a forced config without a general-k instantiation (128/256-wide n-tiles, C % 64 != 0): register-staged
       if (r == -1 && g_knobs[4] != 0 && !x2 && g.C % 64 && g.C <= g.ldx)
         return run_variant<T, TO>(0, x, w, y, g, ep, 0, 0, s, nullptr, ph);
-      if (r == -1 && (g_knobs[4] == 24 || g_knobs[4] == 25)) {   // a forced halo kernel does not apply: the heuristic's
+      if (r == -1 && g_knobs[4] >= 24 && g_knobs[4] <= 27) {   // a forced halo / pointwise kernel does not apply: the heuristic's
         const int hv = x2 && heuristic_variant(g) == 0 ? 5 : heuristic_variant(g);
         return run_variant<T, TO>(hv, x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, nullptr, ph, x2, (unsigned)x2b);
       }
@@ -384,7 +388,7 @@ static int conv_igemm_epi(const void* x, const void* x2, int64_t c1, int64_t ldx
   else
     return SSSEG_EUNSUPPORTED;
   if (bm <= 0) return SSSEG_EUNSUPPORTED;
-  if (e.stats_rows_host && e.stats) *e.stats_rows_host = (g.M + bm - 1) / bm;
+  if (e.stats_rows_host && e.stats) *e.stats_rows_host = t_pw_rows >= 0 ? t_pw_rows : (g.M + bm - 1) / bm;
   SSSEG_LAUNCH_CHECK();
   return 0;
 }

@@ -695,14 +695,14 @@ extern int g_knobs[16];   // runtime variant switches (ssseg_set_knob), defined 
 // 0: reg-staged pipeline depth; 1: split-K cap (-1 off = default, 0 auto: the autotuner also times each variant with
 // its split plan, fp32-atomic partials + finalize, and keeps it where faster); 2: 64x64 small-M tiles (reg-staged path);
 // 3: bf16 LDS-DMA path (0 on, -1 off); 4: variant (0 auto, 1..10 / 12..23 LDS-DMA config, 11 register-staged, 24 the
-// halo-tiled 3x3 kernel where it applies);
+// halo-tiled 3x3 kernel where it applies, 25 its 32-channel form, 26 / 27 the pointwise kernels);
 // 5: autotune unseen geometries (1 on, 0 = static heuristic); knob 6 = 1 clears the variant cache;
 // 7: LDS-staged coalesced epilogue in the LDS-DMA kernel (0 on, -1 off);
 // 8: bf16 weight gradient on the LDS-DMA kernel (0 on, -1 = register-staged wgrad_kernel);
 // 9: LDS-DMA weight-gradient tile variant (0 = the static plan, 1.. = a forced WGRAD_CFGS entry, conv_wgrad.hip);
 // 10: weight-gradient split count scale in percent (100 = the plan's); 11: halo-tiled 3x3 kernels (conv_wgrad_halo.hip,
 // conv_hconv3.hip; 0 on, -1 = the split-K weight gradient and no variant 24); 12: fused-statistics experiment switch
-// (Epi::sdbg, LDS-DMA configs; 0 = normal)
+// (Epi::sdbg, LDS-DMA configs; 0 = normal); 13: pointwise kernels (conv_pw.hip, variants 26 / 27; 0 on, -1 off)
 
 // STATS: the epilogue also writes the fused BatchNorm statistics partials (a separate instantiation: the fp64
 // sums raise the register count, which must not cost the launches that do not need them)
@@ -1408,6 +1408,14 @@ int launch_hconv3(const void* x, const void* w, void* y, const ConvGeom& g, cons
 template <typename TO>
 int launch_hconv3s(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
                    hipStream_t s, float* ws, const PhaseTab* ph, const void* x2);
+
+// pointwise 1x1 / stride-1 contraction over 64 or 128 channels (conv_pw.hip), variants 26 (fj = 4: 64-pixel wave
+// tiles) and 27 (fj = 2: 32-pixel tiles); returns 64 or -1.  With fused statistics it writes t_pw_rows partial rows
+// (set by every launch of it; run_variant resets it to -1 before each launch)
+template <typename TO>
+int launch_pw(int fj, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, hipStream_t s,
+              float* ws, const PhaseTab* ph, const void* x2);
+extern thread_local long long t_pw_rows;
 
 // halo-tiled 3x3 / stride-1 weight gradient (conv_wgrad_halo.hip)
 struct HaloSeg {

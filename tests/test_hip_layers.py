@@ -283,7 +283,7 @@ def test_conv_bn_act_fused_eval_grad(hip_device, mode, monkeypatch, kind, cin, c
     _close(mb.bias.grad, rb.bias.grad, mode, 'dbeta')
 
 
-ALL_VARIANTS = [11] + list(range(1, 11)) + list(range(12, 26))
+ALL_VARIANTS = [11] + list(range(1, 11)) + list(range(12, 28))
 
 
 @pytest.mark.parametrize('kind,cin,cout,k,H', [('conv', 64, 128, 3, 19), ('conv', 128, 64, 1, 17), ('conv', 192, 256, 3, 9),
@@ -300,7 +300,10 @@ ALL_VARIANTS = [11] + list(range(1, 11)) + list(range(12, 26))
                                                # 32 -> 32 channels: its halo form (variant 25)
                                                ('conv64', 32, 32, 3, 8), ('conv64', 32, 32, 3, 12),
                                                # vpad: 240 / 120 channels run the 64-aligned path over 256 / 128
-                                               ('conv', 240, 120, 3, 11), ('conv64', 240, 120, 3, 4)])
+                                               ('conv', 240, 120, 3, 11), ('conv64', 240, 120, 3, 4),
+                                               # 1x1 over 64 / 128 channels: the pointwise kernel (variants 26, 27),
+                                               # several tiles per wave, ragged last tile
+                                               ('conv', 64, 256, 1, 150), ('conv', 128, 512, 1, 96)])
 def test_conv_variants_bitwise(hip_device, kind, cin, cout, k, H):
     """Every bf16 engine variant (register-staged, LDS-DMA tile configs 1..10 and 12..23) accumulates the
     same MFMA k-sequence: forward and input-gradient outputs are bit-identical, so autotuning never changes
@@ -368,6 +371,59 @@ def test_hconv3s_persistent_bitwise(hip_device, n, H, W):
     assert torch.equal(a[2], b[2])
     torch.testing.assert_close(a[3], b[3], rtol=1e-6, atol=1e-7)
     torch.testing.assert_close(a[4], b[4], rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize('cin,cout,n,H,W', [(64, 256, 4, 64, 64), (128, 512, 3, 33, 40), (64, 64, 2, 9, 13),
+                                            (128, 128, 2, 50, 31)])
+def test_pointwise_kernel_bitwise(hip_device, cin, cout, n, H, W):
+    """The register-direct pointwise kernel (variants 26 / 27, conv_pw.hip) vs the gather kernel (config 14): the
+    folded eval-BN epilogue with ReLU, with and without a residual (+ the raw-accumulator copy: the differentiated
+    consistency pass, output and every gradient), bit for bit, and a training BatchNorm fed by its fused statistics
+    (per-wave rows instead of per-tile rows: fp32 summation order only) within 1e-6 of the gather kernel's.  (The
+    64-pixel form, 26, takes no residual: forced there it falls back to the heuristic's kernel, so the residual pass
+    is compared for 27 only.)"""
+    from ssseg import native as N
+    from ssseg import nn as snn
+    snn.set_compute_dtype(torch.bfloat16)
+    torch.manual_seed(8)
+    conv = snn.Conv2d(cin, cout, 1, 1, 0, bias=False).to(hip_device)
+    bn = snn.BatchNorm2d(cout).to(hip_device)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.3, 0.3)
+    x = _act_in(torch.randn(n, cin, H, W) + 0.2, hip_device).detach().requires_grad_(True)
+    res = _act_in(torch.randn(n, cout, H, W), hip_device).detach().requires_grad_(True)
+    gy = _act_in(torch.randn(n, cout, H, W), hip_device)
+    outs = {}
+    try:
+        for v in (14, 26, 27):
+            N.call('ssseg_set_knob', 4, v)
+            bn.train()
+            bn.reset_running_stats()
+            with torch.no_grad():
+                z = snn.conv_bn_act(conv, x, bn, relu=True)
+            o = {'train': (z.clone(), bn.running_mean.clone(), bn.running_var.clone())}
+            bn.eval()
+            for key, r in (('plain', None), ('res', res)):
+                for t in (x, res, conv.weight):
+                    t.grad = None
+                y = snn.conv_bn_act(conv, x, bn, relu=True, residual=r)
+                y.backward(gy)
+                torch.cuda.synchronize()
+                o[key] = [y.detach().clone(), x.grad.clone(), conv.weight.grad.clone()] + (
+                    [res.grad.clone()] if r is not None else [])
+            outs[v] = o
+    finally:
+        N.call('ssseg_set_knob', 4, 0)
+    ref = outs[14]
+    for v in (26, 27) if cin == 64 else (27,):   # 26: 64 channels only
+        for key in ('plain', 'res') if v == 27 else ('plain',):
+            for a, b, name in zip(outs[v][key], ref[key], ('y', 'dx', 'dW', 'dres')):
+                assert torch.equal(a, b), (v, key, name)
+        (z, rm, rv), (z0, rm0, rv0) = outs[v]['train'], ref['train']
+        torch.testing.assert_close(rm, rm0, rtol=1e-6, atol=1e-7)
+        torch.testing.assert_close(rv, rv0, rtol=1e-6, atol=1e-7)
+        assert float((z.float() - z0.float()).abs().max()) <= 1e-2 * float(z0.float().abs().max())
 
 
 WGRAD_CASES = [

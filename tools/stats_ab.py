@@ -15,7 +15,7 @@ import torch  # noqa: E402
 from ssseg import native as N  # noqa: E402
 from ssseg import nn as snn  # noqa: E402
 
-CFGS = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23]
+CFGS = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 26, 27]
 
 
 def main():
