@@ -83,10 +83,25 @@ struct Layout {
   int cblocks;    // blocks along channels
 };
 
-static Layout layout_for(int64_t C, int V) {
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+// Small maps (P < 64K pixels: ResNet layers 3-4, 1024-2048 channels) put at most 32 chunks (256 bf16 channels) in a
+// block row: 8 pixel rows per block and the channels spread over cblocks >= 4 blocks, so the grid is filled with
+// few pixel blocks -- and a reduction's partial table (one row of 2C doubles per pixel block) stays small.  With
+// whole 256-chunk rows a 4096 x 2048 reduction wrote a 16.8 MB table for 16.8 MB of input.  SSSEG_BN_CPB overrides
+// the cap (256 = one block row spans every channel, the earlier layout).
+static Layout layout_for(int64_t C, int V, int64_t P) {
+  static const int small_cap = [] {
+    const int v = env_int("SSSEG_BN_CPB", 32);
+    return v == 8 || v == 16 || v == 32 || v == 64 || v == 128 || v == 256 ? v : 32;
+  }();
+  const int cap = P < 65536 ? small_cap : 256;
   Layout l;
   const int nch = (int)((C + V - 1) / V);
-  l.cpb = nch < 256 ? nch : 256;
+  l.cpb = nch < cap ? nch : cap;
   l.ppb = 256 / l.cpb;
   l.cblocks = (nch + l.cpb - 1) / l.cpb;
   return l;
@@ -103,6 +118,7 @@ static int64_t pixel_blocks(int64_t P, const Layout& L, int64_t cap) {
     const long v = e ? atol(e) : 512;
     return (int64_t)(v > 0 ? v : 512);
   }();
+  // (one batch of U pixels per thread on small maps, up to 2048 workgroups, measured no faster in the step)
   const int64_t want = (target + L.cblocks - 1) / L.cblocks;
   gx = gx > want ? want : gx;
   gx = gx > cap ? cap : gx;
@@ -113,10 +129,46 @@ struct ChanParams {
   const float *mean, *invstd, *gamma, *beta;
 };
 
+// V per-channel values from c0 (clamped index past C): 16-byte loads when the whole group is in range and the vector
+// is 16-byte aligned (the small maps' kernels are a few round trips long, and 4-byte gathers made the parameter
+// fetch one of them: 4096 x 2048 apply 14.5 -> 7.7 us)
+template <int V, typename F>
+__device__ __forceinline__ void ld_chan(const F* __restrict__ p, int c0, int C, F (&v)[V]) {
+  constexpr int W = 16 / sizeof(F);
+  if (V % W == 0 && c0 + V <= C && ((uintptr_t)p & 15) == 0) {
+    typedef F F4 __attribute__((ext_vector_type(W)));
+#pragma unroll
+    for (int e = 0; e < V; e += W) {
+      const F4 q = *(const F4*)(p + c0 + e);
+#pragma unroll
+      for (int k = 0; k < W; ++k) v[e + k] = q[k];
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < V; ++e) v[e] = p[min(c0 + e, C - 1)];
+  }
+}
+
 template <int V>
 __device__ __forceinline__ void load_params(const ChanParams& cp, int c0, int C, float (&mu)[V], float (&is)[V],
                                             float (&ga)[V], float (&be)[V], bool (&live)[V]) {
   // clamped channel indices: every load unconditional (none waits for another), dead channels zeroed after
+  const uintptr_t al = (uintptr_t)cp.mean | (uintptr_t)cp.invstd | (uintptr_t)cp.gamma | (uintptr_t)cp.beta;
+  if (c0 + V <= C && V % 4 == 0 && (al & 15) == 0) {   // 16-byte loads (c0 is a multiple of V)
+#pragma unroll
+    for (int e = 0; e < V; e += 4) {
+      const float4 m = *(const float4*)(cp.mean + c0 + e), i = *(const float4*)(cp.invstd + c0 + e);
+      const float4 g = cp.gamma ? *(const float4*)(cp.gamma + c0 + e) : make_float4(1.f, 1.f, 1.f, 1.f);
+      const float4 b = cp.beta ? *(const float4*)(cp.beta + c0 + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+      mu[e] = m.x; mu[e + 1] = m.y; mu[e + 2] = m.z; mu[e + 3] = m.w;
+      is[e] = i.x; is[e + 1] = i.y; is[e + 2] = i.z; is[e + 3] = i.w;
+      ga[e] = g.x; ga[e + 1] = g.y; ga[e + 2] = g.z; ga[e + 3] = g.w;
+      be[e] = b.x; be[e + 1] = b.y; be[e + 2] = b.z; be[e + 3] = b.w;
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) live[e] = true;
+    return;
+  }
 #pragma unroll
   for (int e = 0; e < V; ++e) {
     const int c = min(c0 + e, C - 1);
@@ -138,6 +190,17 @@ __device__ __forceinline__ void load_params(const ChanParams& cp, int c0, int C,
 __device__ __forceinline__ int64_t clampp(int64_t p, int64_t P) { return p < P ? p : P - 1; }
 
 constexpr int MAXG = 1024;   // partial blocks along pixels (several per CU: the partial passes are HBM-bound)
+
+// partial blocks along pixels of a reduction: each walks >= SSSEG_BN_PMIN (64) pixels, so the fp64 partial table
+// (16 C bytes per block) is <= 1/8 of the 16-bit input it summarises
+static int64_t partial_cap(int64_t P) {
+  static const int pmin = [] {
+    const int v = env_int("SSSEG_BN_PMIN", 64);
+    return v >= 0 ? v : 64;
+  }();
+  const int64_t c = pmin > 0 ? P / pmin : MAXG;
+  return c < 1 ? 1 : (c > MAXG ? MAXG : c);
+}
 
 // per-block partial sums of 2 per-channel quantities; mode 0: (x, x^2); mode 1: (dyr, dyr*xhat)
 template <typename T, int V, int MODE>
@@ -436,14 +499,11 @@ __global__ void __launch_bounds__(256) bn_eval_bwd_kernel(const T* __restrict__ 
   if (active) {
     float sc[V], me[V], is[V];
     bool live[V];
+    ld_chan<V>(scale, c0, C, sc);
+    ld_chan<V>(mean_eff, c0, C, me);
+    ld_chan<V>(invstd, c0, C, is);
 #pragma unroll
-    for (int e = 0; e < V; ++e) {
-      const int c = min(c0 + e, C - 1);
-      live[e] = c0 + e < C;
-      sc[e] = scale[c];
-      me[e] = mean_eff[c];
-      is[e] = invstd[c];
-    }
+    for (int e = 0; e < V; ++e) live[e] = c0 + e < C;
 #pragma unroll
     for (int e = 0; e < V; ++e) {
       sc[e] = live[e] ? sc[e] : 0.f;
@@ -453,8 +513,7 @@ __global__ void __launch_bounds__(256) bn_eval_bwd_kernel(const T* __restrict__ 
     const bool ymode = shift != nullptr;
     if (ymode) {
       float sh[V];
-#pragma unroll
-      for (int e = 0; e < V; ++e) sh[e] = shift[min(c0 + e, C - 1)];
+      ld_chan<V>(shift, c0, C, sh);
 #pragma unroll
       for (int e = 0; e < V; ++e) {
         me[e] = live[e] ? fmaf(me[e], sc[e], sh[e]) : 0.f;
@@ -605,12 +664,8 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
   }
   if (train) {
     double q1[V], q2[V];   // every load issued before the first division
-#pragma unroll
-    for (int e = 0; e < V; ++e) {
-      const int c = min(c0 + e, C - 1);
-      q1[e] = sums[c];
-      q2[e] = sums[C + c];
-    }
+    ld_chan<V>(sums, c0, C, q1);
+    ld_chan<V>(sums + C, c0, C, q2);
 #pragma unroll
     for (int e = 0; e < V; ++e) {
       const float a = (float)(q1[e] / count), b = (float)(q2[e] / count);
@@ -677,8 +732,8 @@ static bool wide_ok(int64_t C, std::initializer_list<int64_t> lds) {
 template <typename T, int V, int MODE>
 void run_partials(const T* x, const T* dy, const T* res, int64_t P, int64_t C, int64_t ldx, int64_t lddy, int64_t ldr,
                   ChanParams prm, int relu, double* sums, void* ws, hipStream_t s, FinalEpi fe) {
-  const Layout L = layout_for(C, V);
-  const int64_t gx = pixel_blocks(P, L, MAXG);
+  const Layout L = layout_for(C, V, P);
+  const int64_t gx = pixel_blocks(P, L, partial_cap(P));
   hipLaunchKernelGGL((bn_partial_kernel<T, V, MODE>), dim3((unsigned)gx, L.cblocks), dim3(256), 0, s, x, dy, res, P,
                      (int)C, ldx, lddy, ldr, L, prm, relu, (double*)ws);
   launch_partial_final((const double*)ws, gx, C, sums, s, fe);
@@ -699,11 +754,11 @@ void apply(const T* x, const T* res, T* y, int64_t P, int64_t C, int64_t ldx, in
            ChanParams prm, int relu, hipStream_t s) {
   constexpr int V16 = 16 / sizeof(T);
   if (wide_ok<T>(C, {ldx, ldy, res ? ldr : ldx})) {
-    const Layout L = layout_for(C, V16);
+    const Layout L = layout_for(C, V16, P);
     hipLaunchKernelGGL((bn_apply_kernel<T, V16>), dim3((unsigned)pixel_blocks(P, L, 1 << 20), L.cblocks), dim3(256),
                        0, s, x, res, y, P, (int)C, ldx, ldr, ldy, L, prm, relu);
   } else {
-    const Layout L = layout_for(C, V16 / 2);
+    const Layout L = layout_for(C, V16 / 2, P);
     hipLaunchKernelGGL((bn_apply_kernel<T, V16 / 2>), dim3((unsigned)pixel_blocks(P, L, 1 << 20), L.cblocks),
                        dim3(256), 0, s, x, res, y, P, (int)C, ldx, ldr, ldy, L, prm, relu);
   }
@@ -715,12 +770,12 @@ void bwd_apply(const T* dy, const T* x, const T* res, T* dx, T* dres, int64_t P,
                hipStream_t s) {
   constexpr int V16 = 16 / sizeof(T);
   if (wide_ok<T>(C, {ldx, lddy, lddx, (res && relu) ? ldr : ldx})) {
-    const Layout L = layout_for(C, V16);
+    const Layout L = layout_for(C, V16, P);
     hipLaunchKernelGGL((bn_bwd_apply_kernel<T, V16>), dim3((unsigned)pixel_blocks(P, L, 1 << 20), L.cblocks),
                        dim3(256), 0, s, dy, x, res, dx, dres, P, (int)C, ldx, ldr, lddy, lddx, L, prm, relu, train,
                        sums, count);
   } else {
-    const Layout L = layout_for(C, V16 / 2);
+    const Layout L = layout_for(C, V16 / 2, P);
     hipLaunchKernelGGL((bn_bwd_apply_kernel<T, V16 / 2>), dim3((unsigned)pixel_blocks(P, L, 1 << 20), L.cblocks),
                        dim3(256), 0, s, dy, x, res, dx, dres, P, (int)C, ldx, ldr, lddy, lddx, L, prm, relu, train,
                        sums, count);
@@ -847,8 +902,8 @@ static void eval_bwd(const T* dy, const T* y, const T* aux, T* dconv, T* dres, i
                      hipStream_t s, FinalEpi fe, const float* shift) {
   constexpr int V16 = 16 / sizeof(T);
   const bool wide = wide_ok<T>(C, {ld});
-  const Layout L = layout_for(C, wide ? V16 : V16 / 2);
-  const int64_t gx = pixel_blocks(P, L, MAXG);
+  const Layout L = layout_for(C, wide ? V16 : V16 / 2, P);
+  const int64_t gx = pixel_blocks(P, L, partial_cap(P));
   if (wide)
     hipLaunchKernelGGL((bn_eval_bwd_kernel<T, V16>), dim3((unsigned)gx, L.cblocks), dim3(256), 0, s, dy, y, aux, dconv,
                        dres, P, (int)C, ld, L, scale, mean_eff, invstd, relu, (double*)ws, shift);

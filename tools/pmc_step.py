@@ -28,7 +28,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CONV_KERNELS = ('igemm_kernel', 'igemm_glds_kernel', 'hconv3_kernel', 'wgrad_halo3_kernel', 'wgrad_kernel',
+CONV_KERNELS = ('igemm_kernel', 'igemm_glds_kernel', 'hconv3_kernel', 'hconv3s_kernel', 'pw_kernel', 'wgrad_halo3_kernel', 'wgrad_kernel',
                 'wgrad_glds_kernel', 'wgrad_reduce_kernel',
                 'wgrad_reduce_wide_kernel', 'splitk_finalize_kernel', 'slab_finalize_kernel', 'phase_zero_kernel')
 
