@@ -279,7 +279,8 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x
     const int c = (blockIdx.y * L.cpb + ch) * V + e;
     if (c >= C) continue;
     double a = 0, b = 0;
-    for (int k = 0; k < L.ppb; ++k) {
+#pragma unroll 8
+    for (int k = 0; k < L.ppb; ++k) {   // (unrolled: the LDS reads of 8 rows in flight, the adds in row order)
       a += red[0][k * L.cpb + ch][e];
       b += red[1][k * L.cpb + ch][e];
     }
@@ -371,12 +372,25 @@ __global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* par
     }
   }
   const double a0 = a[0] + a[2], a1 = a[1] + a[3], b0 = b[0] + b[2], b1 = b[1] + b[3];
-  red[0][pl][cl] = a0 + a1;
-  red[1][pl][cl] = b0 + b1;
+  // the LN lanes of a channel: a butterfly over the lane bits above log2(CH) inside each wave (fixed order), then the
+  // four waves' sums in order.  (One thread summing LN = 32..128 LDS slots in sequence was most of this launch's
+  // ~5 us: a chain of dependent LDS reads.)
+  double sa = a0 + a1, sb = b0 + b1;
+#pragma unroll
+  for (int o = 32; o >= CH; o >>= 1) {
+    sa += __shfl_xor(sa, o, 64);
+    sb += __shfl_xor(sb, o, 64);
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane < CH) {
+    red[0][wv][cl] = sa;
+    red[1][wv][cl] = sb;
+  }
   __syncthreads();
   if (pl == 0 && c < C) {
     double a = 0, b = 0;
-    for (int k = 0; k < LN; ++k) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
       a += red[0][k][cl];
       b += red[1][k][cl];
     }
@@ -582,7 +596,8 @@ __global__ void __launch_bounds__(256) bn_eval_bwd_kernel(const T* __restrict__ 
     const int c = (blockIdx.y * L.cpb + ch) * V + e;
     if (c >= C) continue;
     double a = 0, b = 0;
-    for (int k = 0; k < L.ppb; ++k) {
+#pragma unroll 8
+    for (int k = 0; k < L.ppb; ++k) {   // (unrolled: the LDS reads of 8 rows in flight, the adds in row order)
       a += red[0][k * L.cpb + ch][e];
       b += red[1][k * L.cpb + ch][e];
     }
