@@ -153,6 +153,37 @@ __global__ void maxpool_fwd_vec_kernel(const T* __restrict__ x, T* __restrict__ 
       m[e] = -INFINITY;
       best[e] = -1;
     }
+    if (k == 3) {   // the ResNet stem's 3x3 pool: all nine taps' loads in flight together (clamped addresses), then
+                    // the same first-valid-tap / greater-or-NaN scan in tap order as the general loop below
+      using CK = Chunk<T, V>;
+      typename CK::raw qv[9];
+      bool ok[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int ih = oh * s - p + t / 3, iw = ow * s - p + t % 3;
+        ok[t] = ih >= 0 && ih < H && iw >= 0 && iw < W;
+        const int ch = min(max(ih, 0), H - 1), cw = min(max(iw, 0), W - 1);
+        qv[t] = CK::ld(x + ((int64_t)(n * H + ch) * W + cw) * C + cv * V);
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (!ok[t]) continue;
+        float v[V];
+        CK::cvt(qv[t], v);
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          if (best[e] < 0) best[e] = t;
+          if (v[e] > m[e] || v[e] != v[e]) {
+            m[e] = v[e];
+            best[e] = t;
+          }
+        }
+      }
+      const int64_t o = (int64_t)i * V;
+      VC<T>::st(y + o, m);
+      IdxVec<V>::st(idx + o, best);
+      continue;
+    }
     for (int kh = 0; kh < k; ++kh) {
       const int ih = oh * s - p + kh;
       if (ih < 0 || ih >= H) continue;
@@ -199,6 +230,37 @@ __global__ void maxpool_bwd_vec_kernel(const T* __restrict__ gy, const uint8_t* 
     else
 #pragma unroll
       for (int e = 0; e < V; ++e) acc[e] = 0.f;
+    if (V == 8 && k == 3 && s == 2) {   // <= 2 x 2 windows reach a pixel: their index and gradient loads in flight together
+                              // (clamped), then the general loop's additions in its (oh, ow) order
+      using CK = Chunk<T, V>;
+      typename CK::raw qg[4];
+      uint2 qi[4];
+      bool ok[4];
+      int tap[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int oh = oh0 + (c >> 1), ow = ow0 + (c & 1);
+        const int kh = ih - (oh * s - p), kw = iw - (ow * s - p);
+        ok[c] = oh <= oh1 && ow <= ow1 && kh >= 0 && kh < k && kw >= 0 && kw < k;
+        tap[c] = kh * k + kw;
+        const int64_t o = ((int64_t)(n * OH + min(oh, OH - 1)) * OW + min(ow, OW - 1)) * C + cv * V;
+        qi[c] = *(const uint2*)(idx + o);
+        qg[c] = CK::ld(gy + o);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (!ok[c]) continue;
+        float g[V];
+        CK::cvt(qg[c], g);
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          const int b = (int)((e < 4 ? qi[c].x >> (8 * e) : qi[c].y >> (8 * (e - 4))) & 255u);
+          acc[e] += b == tap[c] ? g[e] : 0.f;
+        }
+      }
+      VC<T>::st(gx + (int64_t)i * V, acc);
+      continue;
+    }
     for (int oh = oh0; oh <= oh1; ++oh) {
       const int kh = ih - (oh * s - p);
       if (kh < 0 || kh >= k) continue;

@@ -548,6 +548,24 @@ def test_maxpool(hip_device, mode, k, s, p, ceil):
     _close(xa.grad, xr.grad, mode, 'dx')
 
 
+@pytest.mark.parametrize('H,W', [(12, 10), (13, 16)])
+def test_maxpool_ties(hip_device, mode, H, W):
+    """3x3 / stride-2 pool (the ResNet stem's: batched-load paths in misc.hip) on values with many ties: the
+    forward keeps PyTorch's first-maximal-tap index, so the input gradient lands where PyTorch's does, exactly."""
+    from ssseg import nn as snn
+    torch.manual_seed(5)
+    x = torch.randint(0, 3, (2, 16, H, W)).float()
+    xr = x.clone().requires_grad_(True)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    gy = torch.randint(-4, 5, yr.shape).float()
+    yr.backward(gy)
+    xa = _act_in(x, hip_device).detach().requires_grad_(True)
+    y = snn.MaxPool2d(3, 2, 1)(xa)
+    y.backward(_act_in(gy, hip_device))
+    assert torch.equal(y.detach().float().cpu(), yr.detach())
+    assert torch.equal(xa.grad.float().cpu(), xr.grad)
+
+
 def test_cat_crop(hip_device, mode):
     from ssseg import nn as snn
     torch.manual_seed(4)
