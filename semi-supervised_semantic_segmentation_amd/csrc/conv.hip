@@ -186,7 +186,7 @@ int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const
       // warm (code load, caches); a variant that cannot run this launch (-1) is skipped
       if (run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, ph ? nullptr : wsv, ph, x2, x2b) <= 0) continue;
       float ms = 1e30f;
-      for (int rep = 0; rep < 3; ++rep) {
+      for (int rep = 0; rep < 5; ++rep) {
         (void)hipEventRecord(e0, s);
         run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, ph ? nullptr : wsv, ph, x2, x2b);
         (void)hipEventRecord(e1, s);
