@@ -362,12 +362,15 @@ size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* desc_host, int dt
 /* Runtime variant switches for A/B measurement.  knob 0: register-staged pipeline depth (0 = one k-tile in
  * flight, default; 1 = two); knob 1: split-K cap (0 = heuristic, -1 = off (default), n = at most n);
  * knob 2: 64x64 small-M tiles of the register-staged kernel (0 = auto); knob 3: bf16 LDS-DMA kernel
- * (0 = on, -1 = off); knob 4: bf16 variant (0 = auto, 1..10 = an LDS-DMA tile config, 11 = register-staged);
+ * (0 = on, -1 = off); knob 4: bf16 variant (0 = auto, 1..10 / 12..23 = an LDS-DMA tile config, 11 = register-staged,
+ * 24 / 25 = the halo-tiled 3x3 kernels, 26 / 27 = the pointwise kernels, each where it applies);
  * knob 5: autotune unseen geometries once on the caller's stream (1 = on, default; 0 = static rule);
  * knob 6 (write 1): clear the per-geometry variant cache; knob 7: LDS-staged coalesced epilogue of the LDS-DMA
  * kernel (0 = on, default; -1 = off); knob 8: LDS-DMA weight gradient (0 = on, -1 = register-staged);
  * knob 9: LDS-DMA weight-gradient tile config (0 = the static plan, n = config n); knob 10: weight-gradient
- * split count in percent of the plan's (100 = default).  Forward variants never change results; the
+ * split count in percent of the plan's (100 = default); knob 11: halo-tiled 3x3 kernels (0 = on, -1 = off);
+ * knob 12: fused-statistics experiment switch (0 = normal); knob 13: pointwise kernels (0 = on, -1 = off).
+ * Forward variants never change results; the
  * weight-gradient knobs change the fp32 summation order of dW.  Not thread-safe. */
 int ssseg_set_knob(int id, int value);
 
