@@ -212,7 +212,7 @@ def _spawn_ranks(n):
     return subprocess.call(cmd, env=env)
 
 
-def timed_run(args, world, rank, device, dtype, probe=True):
+def timed_run(args, world, rank, device, dtype, probe=True, eager_n1=False):
     """Build, warm up, time args.steps steps; returns (elapsed_s, conv probe rows, per-step loss records)."""
     import train
     from ssseg import nn as snn
@@ -244,13 +244,18 @@ def timed_run(args, world, rank, device, dtype, probe=True):
         snn.probe(False)
         torch.cuda.synchronize()
         train._OVERLAP['teacher'] = overlap
-    if world > 1:
-        dist.barrier()
     graph = None
+    # N = 1: the step captured as a HIP graph and replayed; N > 1: eager launches (the host reducer issues the RCCL bucket
+    # all-reduces and SyncBN reductions each step: a captured DDP step -- RCCL collectives inside a HIP graph -- hung at
+    # world 1 on this image's RCCL 2.26.6).  The N = 1 record also carries the eager rate ('eager_n1'),
+    # the like-for-like base of the N > 1 lines.
     if args.graph and world == 1:
         # the step captured once as a HIP graph (ssseg.graph.StepGraph) and replayed: each replay copies the next
         # batch into the captured input buffers and runs the whole step (fresh CowMix draws from the device counter)
         from ssseg.graph import StepGraph
+        # the replay repeats the captured step's host decisions: the optimizer step (step 2 % 1 == 0) and the epoch gate
+        # (epoch 30 > 25) are the same for every timed step only with no gradient accumulation
+        assert cfg['train']['virtual_batch_size_multiplier'] == 1, 'graph replay needs an optimizer step every step'
         graph = StepGraph(lambda img, mask, ua, ub: train.train_step(model, teacher, opt, img, mask, ua, ub, 30, 2, cfg),
                           *data[0])
 
@@ -258,26 +263,44 @@ def timed_run(args, world, rank, device, dtype, probe=True):
             out = graph(*data[step_idx[0] % len(data)])
             step_idx[0] += 1
             return tuple(t.clone() for t in out)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(args.steps):
-        recs.append(one_step())
-    e1.record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    wall = time.perf_counter() - t0
-    elapsed = max(wall, e0.elapsed_time(e1) / 1e3)
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+
+    def timed_steps(step_fn, n):
+        # the timed region: barrier + device sync on both sides, MAX of the elapsed time over ranks
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(n):
+            recs.append(step_fn())
+        e1.record()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        wall = time.perf_counter() - t0
+        el = max(wall, e0.elapsed_time(e1) / 1e3)
+        if world > 1:
+            t = torch.tensor([el], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t)
+        return el
+
+    elapsed = timed_steps(one_step, args.steps)
+    eager = None
+    if graph is not None and world == 1 and eager_n1:
+        # the same model continued for the same number of steps with every launch issued from Python
+        def eager_step():
+            img, mask, ua, ub = data[step_idx[0] % len(data)]
+            rec = train.train_step(model, teacher, opt, img, mask, ua, ub, 30, 2, cfg)
+            step_idx[0] += 1
+            return tuple(t.clone() for t in rec)
+        eager = timed_steps(eager_step, args.steps)
     live = torch.stack([torch.stack([c.float(), u.float(), m.float()]) for c, u, m in recs]).cpu()
     snn.set_compute_dtype(torch.bfloat16)
-    return elapsed, rows, live, model, graph is not None
+    return elapsed, rows, live, model, graph is not None, eager
 
 
 def main():
@@ -298,15 +321,21 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # one rank per GPU (LOCAL_RANK); SSSEG_BENCH_BACKEND=gloo and more ranks than GPUs are for the one-GPU test of this
+    # branch (tests/test_bench_ddp.py): RCCL needs one GPU per rank
+    dev_idx = local % max(1, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', rank=rank, world_size=world, device_id=torch.device('cuda', local))
-        print(f'[bench rank {rank}] RCCL process group: world {dist.get_world_size()}, backend '
-              f'{dist.get_backend()}, device cuda:{local}', file=sys.stderr, flush=True)
-    device = torch.device('cuda', local)
+        backend = os.environ.get('SSSEG_BENCH_BACKEND', 'nccl')
+        torch.cuda.set_device(dev_idx)
+        kw = {'device_id': torch.device('cuda', dev_idx)} if backend == 'nccl' else {}
+        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+        print(f'[bench rank {rank}] process group: world {dist.get_world_size()}, backend '
+              f'{dist.get_backend()}, device cuda:{dev_idx}', file=sys.stderr, flush=True)
+    device = torch.device('cuda', dev_idx)
 
-    elapsed, rows, live, model, graphed = timed_run(args, world, rank, device, torch.bfloat16)
+    elapsed, rows, live, model, graphed, eager = timed_run(args, world, rank, device, torch.bfloat16,
+                                                           eager_n1=(world == 1))
     finite = bool(torch.isfinite(live).all())
     if not finite:
         raise RuntimeError(f'bench: non-finite loss in the timed steps (rank {rank}): {live.tolist()}')
@@ -331,15 +360,20 @@ def main():
                      'conv_ms_per_step': round(conv_ms, 3), 'conv_gflop_per_step': round(conv_flops / 1e9, 1),
                      'launches_per_step': len(rows)},
         'execution': ('HIP graph replay of the captured step (ssseg.graph.StepGraph), one per step' if graphed
-                      else 'eager launches from Python'),
+                      else 'eager launches from Python (the host reducer issues the RCCL bucket all-reduces)'),
         'step_tflops': round(8 * FWD_GFLOP_PER_IMAGE * args.batch * world / (elapsed / args.steps) / 1e3, 2),
         'liveness': {'losses_finite': finite, 'sup_loss_last': round(float(live[-1, 0]), 6),
                      'unsup_loss_last': round(float(live[-1, 1]), 6),
                      'cm_mean_avg': round(float(live[:, 2].mean()), 4)},
     }
+    if eager is not None:
+        result['eager_n1'] = {'value': round(world * args.batch * args.steps / eager, 3), 'unit': 'images/sec',
+                              'ms_per_step': round(eager / args.steps * 1e3, 3), 'steps': args.steps,
+                              'note': 'the same N=1 workload, every launch issued from Python (the execution mode '
+                                      'of the N>1 lines)'}
     if rank == 0 and world == 1 and not args.no_fp32:
         try:
-            f_el, _, f_live, _, _ = timed_run(argparse.Namespace(**dict(vars(args), steps=min(args.steps, 5), warmup=2)),
+            f_el, _, f_live, _, _, _ = timed_run(argparse.Namespace(**dict(vars(args), steps=min(args.steps, 5), warmup=2)),
                                         world, rank, device, torch.float32, probe=False)
             n = min(args.steps, 5)
             result['fp32_mode'] = {'value': round(args.batch * n / f_el, 3), 'unit': 'images/sec',

@@ -346,6 +346,13 @@ int ssseg_conv_igemm_epi_vsplit(const void* x, const void* w, void* y, const sss
 int ssseg_conv_igemm_phases(const void* x, void* y, const ssseg_conv_desc* desc_host, int dt, int dt_out,
                             const ssseg_conv_epilogue* epi, int64_t nphase, const int64_t* phase_geom,
                             const void* const* w, ssseg_stream_t stream);
+/* ssseg_conv_igemm_phases with a workspace (ssseg_conv_igemm_phases_workspace_bytes; 0 = the launch does not split):
+ * the phases of a tile-starved transposed conv (e.g. ConvTranspose2d 2048 -> 128 over 16x16 maps) run the
+ * deterministic split-K described at ssseg_conv_igemm_workspace_bytes. */
+size_t ssseg_conv_igemm_phases_workspace_bytes(const ssseg_conv_desc* desc_host, int64_t nphase, int dt);
+int ssseg_conv_igemm_phases_ws(const void* x, void* y, const ssseg_conv_desc* desc_host, int dt, int dt_out,
+                               const ssseg_conv_epilogue* epi, int64_t nphase, const int64_t* phase_geom,
+                               const void* const* w, void* ws, size_t ws_bytes, ssseg_stream_t stream);
 
 /* First conv of an encoder on a 3-channel image (<= 4 real input channels, S <= 8 taps per filter row, R in {3, 7},
  * dilation 1, stride x <= 2, OW % 128 == 0; e.g. the ResNet-50 stem 7x7/s2/p3): k = (s, c) of one filter row per
@@ -355,12 +362,17 @@ int ssseg_conv_igemm_phases(const void* x, void* y, const ssseg_conv_desc* desc_
  * engine launch of the stem in Conv2d forward (reference: the encoders' first conv, e.g. SURVEY §0.4 ResNet-50). */
 int ssseg_conv_stem_epi(const void* x, const void* w4, void* y, const ssseg_conv_desc* desc_host, int dt,
                         const ssseg_conv_epilogue* epi, ssseg_stream_t stream);
-/* Workspace for ssseg_conv_igemm: non-zero when the launch splits K across workgroups (few output tiles,
- * long contraction: fp32 partials [M][K] + a finalize pass).  Passing no workspace disables the split. */
+/* Workspace for ssseg_conv_igemm(_epi / _vcat / _vsplit): non-zero when the 16-bit launch splits K across workgroups
+ * (deterministic split-K: fewer than 512 nominal 128 x 64 output tiles and >= 32 64-deep k-tiles -- ResNet layer3/4
+ * at 32x32 / 16x16; S = 2, 4 or 8 k-slices chosen from the geometry alone, knob 14).  Each slice writes fp32 partials,
+ * the last-arriving slice of a tile (an agent-scope ticket) sums the S partials in slice order and runs the full fused
+ * epilogue (affine, residual, activation, raw copy, BN statistics): the result is bitwise reproducible and identical
+ * for every tile config.  The workspace is caller-owned scratch (no contents carried between calls); passing none
+ * (or a smaller one) runs the launch unsplit. */
 size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* desc_host, int dt);
 
 /* Runtime variant switches for A/B measurement.  knob 0: register-staged pipeline depth (0 = one k-tile in
- * flight, default; 1 = two); knob 1: split-K cap (0 = heuristic, -1 = off (default), n = at most n);
+ * flight, default; 1 = two); knob 1: fp32-atomic split-K of the register-staged kernel (-1 = off, default; order-dependent sums);
  * knob 2: 64x64 small-M tiles of the register-staged kernel (0 = auto); knob 3: bf16 LDS-DMA kernel
  * (0 = on, -1 = off); knob 4: bf16 variant (0 = auto, 1..10 / 12..23 = an LDS-DMA tile config, 11 = register-staged,
  * 24 / 25 = the halo-tiled 3x3 kernels, 26 / 27 = the pointwise kernels, each where it applies);
@@ -369,7 +381,8 @@ size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* desc_host, int dt
  * kernel (0 = on, default; -1 = off); knob 8: LDS-DMA weight gradient (0 = on, -1 = register-staged);
  * knob 9: LDS-DMA weight-gradient tile config (0 = the static plan, n = config n); knob 10: weight-gradient
  * split count in percent of the plan's (100 = default); knob 11: halo-tiled 3x3 kernels (0 = on, -1 = off);
- * knob 12: fused-statistics experiment switch (0 = normal); knob 13: pointwise kernels (0 = on, -1 = off).
+ * knob 12: fused-statistics experiment switch (0 = normal); knob 13: pointwise kernels (0 = on, -1 = off);
+ * knob 14: deterministic split-K of the LDS-DMA configs (0 = the geometry rule, default; -1 = off; 2 / 4 / 8 = forced S).
  * Forward variants never change results; the
  * weight-gradient knobs change the fp32 summation order of dW.  Not thread-safe. */
 int ssseg_set_knob(int id, int value);

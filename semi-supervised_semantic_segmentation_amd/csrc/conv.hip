@@ -5,7 +5,10 @@
 
 #include "conv_kernels.h"
 
-int g_knobs[16] = {0, -1, 0, 0, 0, 1, 0, 0, 0, 0, 100, 0, 0, 0, 0, 0};   // split-K off: measured a net loss on the C2 step (r2u)   // runtime variant switches (ssseg_set_knob)
+int g_knobs[16] = {0, -1, 0, 0, 0, 1, 0, 0, 0, 0, 100, 0, 0, 0, 0, 0};   // runtime variant switches (ssseg_set_knob)
+// (knob 1, the register-staged kernel's fp32-atomic split-K, stays off: measured a net loss on the C2 step (r2u) and its
+// sums are order-dependent; knob 14 is the deterministic split-K of the LDS-DMA configs)
+thread_local int t_dsplit = 1;
 
 // ------------------------------------------------------------------------------------------------
 // weight packing: dst[k][rr][ss][c] (c < Cp; zero for c >= Cd) from an fp32 source
@@ -104,7 +107,6 @@ int launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvGe
 // register-staged kernel, 1..10 and 12..23 the LDS-DMA configs, 24 the halo-tiled 3x3 kernel (conv_hconv3.hip; only
 // where it applies).  With knob 5 on (default) an unseen geometry is timed once over the candidates on the caller's
 // stream (HIP events) and the fastest is cached.
-constexpr int kSplitBit = 256;   // cached choice flag: run the variant with its split-K plan
 constexpr int kCandidates[] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  10, 12, 13, 14,
                                 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27};
 std::unordered_map<unsigned long long, int> g_variant;
@@ -126,16 +128,37 @@ static int heuristic_variant(const ConvGeom& g) {
   return tiles(64, 64) < 512 ? 10 : 0;
 }
 
+// Deterministic split-K plan (knob 14: 0 = this rule, -1 = off, 2 / 4 / 8 = forced S): a static function of the
+// contraction, never of timings, so the summation order -- and with it every output bit -- is the same in every run and
+// for every tile config the autotuner may pick.  Tile-starved launches with long k-loops: fewer than 512 nominal
+// 128 x 64 output tiles (over all phases) and >= 64 k-tiles of 64.  Measured (tools/split_ab.py, bs 16, device time
+// of graph-replayed launches): 1152->128 3x3 @32^2 78.5 -> 56.5 us (S = 2; S = 4 no better), 512->512 3x3 @16^2
+// 37.9 -> 33.2, 512->512 3x3/s2 @32^2 36.9 -> 33.0, ConvTranspose2d 2048->128 @16^2 (4 phases) 63.9 -> 49.2; slower
+// with S = 2 where the k-loop is short or the tiles already fill the chip (2048->512 1x1 @16^2, nk = 32: 16.7 -> 21.1;
+// 256->256 3x3 @32^2, 512 tiles: 28.3 -> 35.2), and S = 4 / 8 lose everywhere but the longest contractions.
+static int dsplit_plan(const ConvGeom& g, int nph) {
+  const int kn = g_knobs[14];
+  if (kn < 0 || g.KK == 0) return 1;
+  const int nk = (g.C % 64 == 0) ? g.R * g.S * (g.C / 64) : (g.KK + 63) / 64;
+  if (kn > 0) return (kn == 2 || kn == 4 || kn == 8) && nk >= kn ? kn : 1;
+  const long long t = (long long)nph * ((g.M + 127) / 128) * ((g.K + 63) / 64);
+  if (t >= 512 || nk < 64) return 1;
+  return (t < 128 && nk >= 128) ? 4 : 2;
+}
+
 // x2: second source of a virtual concat input (LDS-DMA configs only: the register-staged kernel returns -1)
 template <typename T, typename TO>
 int run_variant(int v, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
                 unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph = nullptr, const void* x2 = nullptr,
                 unsigned x2b = 0) {
   t_pw_rows = -1;
+  // a split launch runs on the LDS-DMA configs only (the register-staged, halo and pointwise kernels do not split)
+  if (t_dsplit > 1 && (v == 0 || v >= 24)) return -1;
   if constexpr (sizeof(TO) == 2) {
     if (v != 0) return launch_glds_cfg<TO>(v, x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
   }
   if (x2) return -1;
+  ws = nullptr;   // (the register-staged kernel's fp32-atomic split-K stays off, knob 1)
   if (ph && ph->n > 1) {   // register-staged kernel: one launch per phase
     int bm = 0;
     long long rows = 0;
@@ -156,13 +179,19 @@ int run_variant(int v, const void* x, const void* w, void* y, const ConvGeom& g,
   return dispatch_regstaged<T, TO>(x, w, y, g, ep, ws, s);
 }
 
+// *cache_it = false when the choice is only the heuristic's stand-in (the stream is being captured: nothing may be
+// timed, and the geometry is tuned at its next eager launch)
 template <typename T, typename TO>
 int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                 unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2 = nullptr,
-                 unsigned x2b = 0) {
+                 unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2, unsigned x2b,
+                 bool* cache_it) {
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   const int heur = x2 && heuristic_variant(g) == 0 ? 5 : heuristic_variant(g);
-  if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return heur;
+  *cache_it = true;
+  if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) {
+    *cache_it = false;
+    return heur;
+  }
   hipEvent_t e0, e1;
   if (hipEventCreate(&e0) != hipSuccess) return heuristic_variant(g);
   if (hipEventCreate(&e1) != hipSuccess) {
@@ -176,19 +205,19 @@ int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const
   int len = log ? snprintf(line, sizeof line, "tune N%d %dx%d C%d -> %dx%d K%d %dx%d s%d d%d out%dx%d/%d ep%d%d:",
                            g.N, g.H, g.W, g.C, g.OH, g.OW, g.K, g.R, g.S, g.sy, g.dy, g.outH, g.outW, g.osy,
                            ep.scale ? 1 : 0, ep.aux ? 1 : 0) : 0;
-  // every variant without split-K and, when a workspace allows it, with the split-K plan of its tile
-  // (choice encoded as variant | kSplitBit)
-  for (int split = 0; split < (ws ? 2 : 1); ++split) {
-    float* wsv = split ? ws : nullptr;
+  // every variant (with the launch's split-K plan t_dsplit, where there is one: configs that cannot split are skipped)
+  {
+    const int split = t_dsplit > 1;
+    float* wsv = ws;
     for (int v : kCandidates) {
       // a virtually padded contraction (C > ldx: the host's vpad) runs on the bounded LDS-DMA loads only
       if (g.C > g.ldx && (v == 0 || v == 24)) continue;
       // warm (code load, caches); a variant that cannot run this launch (-1) is skipped
-      if (run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, ph ? nullptr : wsv, ph, x2, x2b) <= 0) continue;
+      if (run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, wsv, ph, x2, x2b) <= 0) continue;
       float ms = 1e30f;
       for (int rep = 0; rep < 5; ++rep) {
         (void)hipEventRecord(e0, s);
-        run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, ph ? nullptr : wsv, ph, x2, x2b);
+        run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, wsv, ph, x2, x2b);
         (void)hipEventRecord(e1, s);
         float t = 1e30f;
         if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&t, e0, e1) == hipSuccess) ms = std::min(ms, t);
@@ -197,7 +226,7 @@ int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const
         len += snprintf(line + len, sizeof line - len, " %d%s:%.0f", v, split ? "s" : "", ms * 1e3f);
       if (ms < best_ms) {
         best_ms = ms;
-        best = v | (split ? kSplitBit : 0);
+        best = v;
       }
     }
   }
@@ -207,7 +236,13 @@ int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const
   return best;
 }
 
-// x2 (virtual concat, g.c1b / g.ldx2 set): LDS-DMA configs only; returns -1 where they cannot run the launch
+// x2 (virtual concat, g.c1b / g.ldx2 set): LDS-DMA configs only; returns -1 where they cannot run the launch.
+// ws (sized by ssseg_conv_igemm_workspace_bytes) enables the deterministic split-K plan of the contraction.
+struct DsplitScope {   // t_dsplit for the duration of one dispatch
+  explicit DsplitScope(int S) { t_dsplit = S; }
+  ~DsplitScope() { t_dsplit = 1; }
+};
+
 template <typename T, typename TO>
 int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, float* ws,
                    hipStream_t s, const PhaseTab* ph = nullptr, const void* x2 = nullptr) {
@@ -217,35 +252,41 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
     // C % 64 != 0 (general-k loader, 64-wide n-tiles): any C % 8 == 0 (geom_ok), no virtual concat
     if (sizeof(TO) == 2 && g_knobs[3] == 0 && (g.C % 64 == 0 || !x2) && g.ldx % 8 == 0 && g.ldw % 8 == 0 && g.ldw == g.KK &&
         g.K > 16 && xb < 0x7fffffffLL && wb < 0x7fffffffLL && x2b < 0x7fffffffLL && (!x2 || g.ldx2 % 8 == 0)) {
+      const int nph = ph ? ph->n : 1;
+      const int S = ws ? dsplit_plan(g, nph) : 1;
+      DsplitScope scope(S);
+      float* wsv = S > 1 ? ws : nullptr;
       int v = g_knobs[4];
       if (v < 0) v = 0;
       if (v == 0) {
         const unsigned long long key =
-            geom_key(g, (int)sizeof(TO) * 8 + (ws ? 8 : 0) + (ep.stats ? 4 : 0) + (ep.res ? 2 : 0) + (ep.scale ? 1 : 0) +
-                        64 * (ph ? ph->n : 1) + (x2 ? 4096 * (g.c1b + 1) : 0) + (ep.y2 ? (1 << 24) : 0));
+            geom_key(g, (int)sizeof(TO) * 8 + (ep.stats ? 4 : 0) + (ep.res ? 2 : 0) + (ep.scale ? 1 : 0) + 16 * S +
+                        256 * nph + (x2 ? 4096 * (g.c1b + 1) : 0) + (ep.y2 ? (1 << 24) : 0));
         std::lock_guard<std::mutex> lk(g_variant_mu);
         auto it = g_variant.find(key);
         if (it != g_variant.end()) {
           v = it->second;
         } else {
-          v = g_knobs[5] ? tune_variant<T, TO>(x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, ws, ph, x2,
-                                               (unsigned)x2b)
+          bool cache_it = true;
+          v = g_knobs[5] ? tune_variant<T, TO>(x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, wsv, ph, x2,
+                                               (unsigned)x2b, &cache_it)
                          : heuristic_variant(g);
-          if (x2 && (v & ~kSplitBit) == 0) v = 5;   // the register-staged kernel has no second source
-          if (g.C > g.ldx && ((v & ~kSplitBit) == 0 || (v & ~kSplitBit) == 24)) v = 14;   // (vpad: LDS-DMA only)
-          g_variant[key] = v;
+          if (x2 && v == 0) v = 5;   // the register-staged kernel has no second source
+          if (g.C > g.ldx && (v == 0 || v == 24)) v = 14;   // (vpad: LDS-DMA only)
+          if (S > 1 && (v == 0 || v >= 24)) v = 14;         // a split launch: LDS-DMA configs only
+          if (cache_it) g_variant[key] = v;
         }
       } else if (g_knobs[4] == 11) {
-        v = g.C > g.ldx ? 14 : 0;   // forced register-staged (a vpad contraction runs LDS-DMA config 14 instead)
-        if (x2) return -1;
-      } else if (g.C > g.ldx && g_knobs[4] == 24) {
+        v = (g.C > g.ldx || S > 1) ? 14 : 0;   // forced register-staged (a vpad / split contraction runs config 14)
+        if (x2 && v == 0) return -1;
+      } else if ((g.C > g.ldx || S > 1) && g_knobs[4] == 24) {
         v = 14;
       }
-      // split-K only where the autotuner measured it faster (its fp32 atomics reorder the sums); a variant
-      // forced by knob 4 runs unsplit, so forced variants stay bit-comparable
-      float* wsv = (g_knobs[4] == 0 && (v & kSplitBit)) ? ws : nullptr;
-      const int r = run_variant<T, TO>(v & ~kSplitBit, x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s,
-                                       ph ? nullptr : wsv, ph, x2, (unsigned)x2b);
+      // every variant of a split launch sums the same k-slices in the same order: forced variants stay bit-comparable
+      int r = run_variant<T, TO>(v, x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, wsv, ph, x2, (unsigned)x2b);
+      // a forced config that cannot run the split launch (too many fragments per wave): config 14
+      if (r == -1 && S > 1 && g_knobs[4] != 0)
+        return run_variant<T, TO>(14, x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, wsv, ph, x2, (unsigned)x2b);
       // a forced config without a general-k instantiation (128/256-wide n-tiles, C % 64 != 0): register-staged
       if (r == -1 && g_knobs[4] != 0 && !x2 && g.C % 64 && g.C <= g.ldx)
         return run_variant<T, TO>(0, x, w, y, g, ep, 0, 0, s, nullptr, ph);
@@ -258,7 +299,7 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
   }
   if (x2) return -1;
   if (g.C > g.ldx) return SSSEG_EUNSUPPORTED;   // a virtually padded contraction needs the bounded LDS-DMA loads
-  return run_variant<T, TO>(0, x, w, y, g, ep, 0, 0, s, ph ? nullptr : ws, ph);
+  return run_variant<T, TO>(0, x, w, y, g, ep, 0, 0, s, nullptr, ph);
 }
 
 bool geom_ok(const ConvGeom& g, int dt) {
@@ -283,17 +324,16 @@ extern "C" int ssseg_set_knob(int id, int value) {
   return 0;
 }
 
+// deterministic split-K workspace of the 16-bit LDS-DMA path (0: the contraction does not split)
+static size_t igemm_ws_bytes(const ConvGeom& g, int dt, int nph) {
+  if (dt != SSSEG_BF16 && dt != SSSEG_F16) return 0;
+  return dsplit_ws_bytes(g, nph, dsplit_plan(g, nph));
+}
+
 extern "C" size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* d, int dt) {
   ConvGeom g;
   if (!make_geom(d, g)) return 0;
-  int sp;
-  const long long t128 = ((g.M + 127) / 128) * ((g.K + 127) / 128);
-  const bool small = g_knobs[2] == 0 ? (t128 < 512) : (g_knobs[2] > 0);
-  if (g.K <= 16) sp = dt != SSSEG_F32 ? plan_splits<bf16_t, 256, 16>(g) : plan_splits<float, 256, 16>(g);
-  else if (g.K <= 64 && !small) sp = dt != SSSEG_F32 ? plan_splits<bf16_t, 256, 64>(g) : plan_splits<float, 256, 64>(g);
-  else if (small) sp = dt != SSSEG_F32 ? plan_splits<bf16_t, 64, 64>(g) : plan_splits<float, 64, 64>(g);
-  else sp = dt != SSSEG_F32 ? plan_splits<bf16_t, 128, 128>(g) : plan_splits<float, 128, 128>(g);
-  return sp > 1 ? (size_t)g.M * g.K * sizeof(float) : 0;
+  return igemm_ws_bytes(g, dt, 1);
 }
 
 static int conv_igemm_epi(const void* x, const void* x2, int64_t c1, int64_t ldx2, const void* w, void* y,
@@ -367,9 +407,9 @@ static int conv_igemm_epi(const void* x, const void* x2, int64_t c1, int64_t ldx
     return 0;
   }
   if (!x || !w) return SSSEG_EINVAL;
-  const size_t need = ssseg_conv_igemm_workspace_bytes(d, dt);
-  // no workspace: no split-K (and never with fused statistics: the split partials are summed after the tiles)
-  float* wsf = (need > 0 && ws && ws_bytes >= need && !e.stats) ? (float*)ws : nullptr;
+  const size_t need = igemm_ws_bytes(g, dt, 1);
+  // no (or a too small) workspace: no split-K
+  float* wsf = (need > 0 && ws && ws_bytes >= need) ? (float*)ws : nullptr;
   int bm;
   if (x2 && dt == SSSEG_BF16)
     bm = dispatch_igemm<bf16_t, bf16_t>(x, w, y, g, eb, wsf, s, nullptr, x2);
@@ -462,9 +502,15 @@ extern "C" int ssseg_weight_pack(const float* src, void* dst, int64_t Kd, int64_
   return 0;
 }
 
-extern "C" int ssseg_conv_igemm_phases(const void* x, void* y, const ssseg_conv_desc* d, int dt, int dt_out,
-                                       const ssseg_conv_epilogue* epi, int64_t nphase, const int64_t* phase_geom,
-                                       const void* const* w, ssseg_stream_t stream) {
+extern "C" size_t ssseg_conv_igemm_phases_workspace_bytes(const ssseg_conv_desc* d, int64_t nphase, int dt) {
+  ConvGeom g;
+  if (!make_geom(d, g) || nphase < 1 || nphase > 4) return 0;
+  return igemm_ws_bytes(g, dt, (int)nphase);
+}
+
+extern "C" int ssseg_conv_igemm_phases_ws(const void* x, void* y, const ssseg_conv_desc* d, int dt, int dt_out,
+                                          const ssseg_conv_epilogue* epi, int64_t nphase, const int64_t* phase_geom,
+                                          const void* const* w, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
   ConvGeom g;
   if (!make_geom(d, g) || !x || !y || !w || !phase_geom || nphase < 1 || nphase > 4) return SSSEG_EINVAL;
   if (!geom_ok(g, dt) || g.KK == 0 || dt != dt_out || (dt != SSSEG_BF16 && dt != SSSEG_F16)) return SSSEG_EINVAL;
@@ -492,18 +538,26 @@ extern "C" int ssseg_conv_igemm_phases(const void* x, void* y, const ssseg_conv_
   g.ooy = ph.ooy[0];
   g.oox = ph.oox[0];
   hipStream_t s = (hipStream_t)stream;
+  const size_t need = igemm_ws_bytes(g, dt, (int)nphase);
+  float* wsf = (need > 0 && ws && ws_bytes >= need) ? (float*)ws : nullptr;
   int bm;
   if (dt == SSSEG_BF16) {
     const Epi<bf16_t> eb{e.scale, e.shift, (const bf16_t*)e.residual, (int)e.ldr, e.relu, (bf16_t*)e.aux, e.slope,
                          e.stats, (int)e.stats_ld};
-    bm = dispatch_igemm<bf16_t, bf16_t>(x, w[0], y, g, eb, nullptr, s, &ph);
+    bm = dispatch_igemm<bf16_t, bf16_t>(x, w[0], y, g, eb, wsf, s, &ph);
   } else {
     const Epi<f16_t> eh{e.scale, e.shift, (const f16_t*)e.residual, (int)e.ldr, e.relu, (f16_t*)e.aux, e.slope,
                         e.stats, (int)e.stats_ld};
-    bm = dispatch_igemm<f16_t, f16_t>(x, w[0], y, g, eh, nullptr, s, &ph);
+    bm = dispatch_igemm<f16_t, f16_t>(x, w[0], y, g, eh, wsf, s, &ph);
   }
   if (bm <= 0) return SSSEG_EUNSUPPORTED;
   if (e.stats_rows_host && e.stats) *e.stats_rows_host = nphase * ((g.M + bm - 1) / bm);
   SSSEG_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int ssseg_conv_igemm_phases(const void* x, void* y, const ssseg_conv_desc* d, int dt, int dt_out,
+                                       const ssseg_conv_epilogue* epi, int64_t nphase, const int64_t* phase_geom,
+                                       const void* const* w, ssseg_stream_t stream) {
+  return ssseg_conv_igemm_phases_ws(x, y, d, dt, dt_out, epi, nphase, phase_geom, w, nullptr, 0, stream);
 }

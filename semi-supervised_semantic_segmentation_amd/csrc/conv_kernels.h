@@ -948,6 +948,63 @@ __device__ __forceinline__ void ring_wait(int ahead) {
 
 constexpr unsigned OOB = 0x80000000u;   // > any num_records we build: the load returns zeros
 
+// ---- deterministic split-K (S k-slices per output tile, combined inside the launch) ---------------------------------
+// Workspace: [tickets: one u32 per (phase, tile), zeroed by the host before every launch, region padded to 256 B]
+// [slabs: per (phase, tile) S slices x NW waves x FN*FM fragments x 64 lanes x 16 B of fp32 partials].
+// Every slice block writes its partial accumulators with write-through (sc1) 16-byte stores, every wave drains its
+// stores, then one lane adds to the tile's ticket (agent scope); the block that draws S-1 is the last one and sums the
+// S partials with sc1 loads (they bypass this CU's L1, which may hold stale lines of an earlier launch's slabs) in
+// slice order 0, 1, ..., S-1 -- a fixed order, whichever block arrives last: the result is bitwise reproducible and the
+// same for every tile config (cdna_hip_programming.md §5 'In-launch split-K reduction', §6 Guideline 16, R1 form).
+constexpr int DSPLIT_MAX_FRAGS = 8;   // per wave: the combine keeps 2-3 accumulator sets live
+
+__host__ __device__ inline long long dsplit_ticket_bytes(long long ntiles) { return (ntiles * 4 + 255) / 256 * 256; }
+
+template <int FN, int FM, int NW>
+__device__ __forceinline__ bool dsplit_combine(f32x4 (&acc)[FN][FM], float* ws, int tg, int slice, int splits,
+                                               int ntiles, char* smem) {
+  constexpr int F = FN * FM;
+  constexpr unsigned TILE_BYTES = NW * F * 1024;   // one slice's partial tile
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  unsigned* tick = (unsigned*)ws;
+  char* base = (char*)ws + dsplit_ticket_bytes(ntiles) + (long long)tg * splits * TILE_BYTES;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(splits * TILE_BYTES), 0x00020000);
+  const unsigned vo = (unsigned)((wave * F * 64 + lane) * 16);
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, vo + (i * FM + j) * 1024,
+                                             slice * TILE_BYTES, 16);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its partial left the CU
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(tick + tg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *(volatile int*)smem = old == (unsigned)(splits - 1);
+  }
+  __syncthreads();
+  const bool last = *(volatile int*)smem != 0;
+  if (!last) return false;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below the ticket
+  for (int s = 0; s < splits; ++s) {
+    u32x4 v[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+        v[i][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo + (i * FM + j) * 1024, s * TILE_BYTES, 16);
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const f32x4 p = __builtin_bit_cast(f32x4, v[i][j]);
+        acc[i][j] = s ? acc[i][j] + p : p;
+      }
+  }
+  return true;
+}
+
 // KM (k mode): 0 = 64-channel k-tiles (C % 64 == 0, channel block major, tap minor: the tile's tap and channel block
 // are scalars); 1 = the same over a virtual concat input (ConvGeom.c1b / ldx2): k-tiles of channel block >= c1b
 // gather from x2 (a scalar choice per k-tile: the block never straddles the seam because both parts are whole
@@ -994,7 +1051,11 @@ __global__ void __launch_bounds__(NW * 64, GLDS_OCC(BM, BN, NW, NS)) igemm_glds_
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int nnt = (g.K + BN - 1) / BN;
-  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  // deterministic split-K (splits = S > 1, a power of two): block id -> (output tile, k-slice); the S slices of a tile
+  // are consecutive in the XCD-remapped order (one XCD, next to the n-tiles of the same pixel tile)
+  const int lsp = 31 - __builtin_clz((unsigned)splits);
+  const int bid = xcd_tile(blockIdx.x, gridDim.x);
+  const int tile = bid >> lsp, slice = bid & (splits - 1);
   static_assert(BN == 64 || BN == 128 || BN == 256, "n-tile divisor magic");
   const int mt_ = fdiv(tile, BN == 64 ? g.mn64 : (BN == 128 ? g.mn128 : g.mn256),
                        BN == 64 ? g.sn64 : (BN == 128 ? g.sn128 : g.sn256));   // tile / nnt
@@ -1011,12 +1072,13 @@ __global__ void __launch_bounds__(NW * 64, GLDS_OCC(BM, BN, NW, NS)) igemm_glds_
   }
   const int RS = g.R * g.S;
   const int cpt = g.C >> 6;                      // k-tiles per tap
-  // split-K (low-tile layers, blockIdx.y = split): this block reduces k-tiles [kt0, kt1) in order
+  // split-K (low-tile layers): this block reduces k-tiles [kt0, kt0 + nk) in order; the partition depends on the
+  // contraction and S only (never on the tile config), so every config sums the same slices
   const int nk_all = GK ? (g.KK + 63) >> 6 : RS * cpt;
   int kt0 = 0, nk = nk_all;   // the common unsplit launch: no divisions
   if (splits > 1) {
     const int kper = (nk_all + splits - 1) / splits;
-    kt0 = min(nk_all, (ph.n > 1 ? 0 : (int)blockIdx.y) * kper);
+    kt0 = min(nk_all, slice * kper);
     nk = min(nk_all, kt0 + kper) - kt0;
   }
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)xbytes, 0x00020000);
@@ -1209,20 +1271,13 @@ __global__ void __launch_bounds__(NW * 64, GLDS_OCC(BM, BN, NW, NS)) igemm_glds_
       compute(kt % NS);
     }
   }
-  if (splits > 1) {   // fp32 partials into ws[m][K] (zeroed by the host); splitk_finalize applies the epilogue
-#pragma unroll
-    for (int j = 0; j < FM; ++j) {
-      const long long m = m0 + wm * WTM + j * 16 + (lane & 15);
-      if (m >= g.M) continue;
-#pragma unroll
-      for (int i = 0; i < FN; ++i) {
-        const int n = n0 + wn * WTN + i * 16 + (lane >> 4) * 4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (n + e < g.K) atomicAdd(ws + m * g.K + n + e, acc[i][j][e]);
-      }
+  if constexpr (FN * FM <= DSPLIT_MAX_FRAGS) {
+    if (splits > 1) {   // the last-arriving slice of the tile sums all S partials in slice order, then the epilogue
+      const int tpp = (int)(gridDim.x >> lsp);   // tiles per phase
+      if (!dsplit_combine<FN, FM, NW>(acc, ws, (ph.n > 1 ? (int)blockIdx.y : 0) * tpp + tile, slice, splits,
+                                      tpp * (int)gridDim.y, smem))
+        return;
     }
-    return;
   }
   if constexpr (EPI <= SMEM) {
     // the LDS-staged epilogue whenever the staged tile fits the ring (the register epilogue is not even compiled
@@ -1310,43 +1365,42 @@ inline int plan_splits(const ConvGeom& g);
 template <typename TO>
 __global__ void splitk_finalize_kernel(const float* __restrict__ ws, TO* __restrict__ y, ConvGeom g, Epi<TO> ep);
 
+// S of the deterministic split-K for the launch being dispatched (conv.hip dispatch_igemm sets it: 1 = unsplit); a
+// config whose per-wave fragment count exceeds DSPLIT_MAX_FRAGS cannot run a split launch (-1)
+extern thread_local int t_dsplit;
+
 template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS, int VC>
 int launch_glds_vc(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
                    unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2, unsigned x2b) {
   static_assert(sizeof(TO) == 2, "LDS-DMA configs: 16-bit activations in and out (fp32-output heads have K <= 16)");
+  constexpr int FRAGS = (BM / WM / 16) * (BN / WN / 16);
   const long long tiles = ((g.M + BM - 1) / BM) * ((g.K + BN - 1) / BN);
   const int epi = (int)(g_knobs[7] == 0);
   const TO* xa = (const TO*)x2;
-  if (ph && ph->n > 1) {   // all phases in one launch (no split-K)
-    if (ep.stats)
-      hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, true, VC>),
-                         dim3((unsigned)tiles, (unsigned)ph->n), dim3(NW * 64), 0, s, (const TO*)x, (const TO*)w,
-                         (TO*)y, g, ep, xb, wb, epi, 1, nullptr, *ph, xa, x2b);
-    else
-      hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, false, VC>),
-                         dim3((unsigned)tiles, (unsigned)ph->n), dim3(NW * 64), 0, s, (const TO*)x, (const TO*)w,
-                         (TO*)y, g, ep, xb, wb, epi, 1, nullptr, *ph, xa, x2b);
-    return BM;
-  }
   const PhaseTab one{1, {0}, {0}, {0}, {0}, {nullptr}};
-  // split-K only with a workspace (never with fused statistics: the host passes none then)
-  const int sp = (ws && !ep.stats) ? plan_splits<TO, BM, BN>(g) : 1;
-  if (sp > 1) {
-    (void)hipMemsetAsync(ws, 0, sizeof(float) * g.M * g.K, s);
-    hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, false, VC>), dim3((unsigned)tiles, (unsigned)sp),
-                       dim3(NW * 64), 0, s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, 0, sp, ws, one, xa,
-                       x2b);
-    hipLaunchKernelGGL(splitk_finalize_kernel<TO>, dim3(ssseg_grid(g.M * g.K, 256)), dim3(256), 0, s, ws, (TO*)y, g,
-                       ep);
-  } else if (ep.stats) {
-    hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, true, VC>), dim3((unsigned)tiles), dim3(NW * 64),
-                       0, s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, epi, 1, nullptr, one, xa, x2b);
-  } else {
-    hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, false, VC>), dim3((unsigned)tiles),
-                       dim3(NW * 64), 0, s, (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, epi, 1, nullptr, one,
-                       xa, x2b);
-  }
+  const bool phased = ph && ph->n > 1;   // all output phases in one launch (blockIdx.y = phase)
+  const PhaseTab& pt = phased ? *ph : one;
+  const unsigned nph = phased ? (unsigned)ph->n : 1u;
+  const int sp = ws ? t_dsplit : 1;
+  if (sp > 1 && (FRAGS > DSPLIT_MAX_FRAGS || tiles * sp > 0x7fffffffLL)) return -1;
+  if (sp > 1) (void)hipMemsetAsync(ws, 0, dsplit_ticket_bytes(tiles * nph), s);
+  const dim3 grid((unsigned)(tiles * sp), nph);
+  if (ep.stats)
+    hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, true, VC>), grid, dim3(NW * 64), 0, s,
+                       (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, epi, sp, ws, pt, xa, x2b);
+  else
+    hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, false, VC>), grid, dim3(NW * 64), 0, s,
+                       (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, epi, sp, ws, pt, xa, x2b);
   return BM;
+}
+
+// bytes of the deterministic split-K workspace of S slices over any LDS-DMA config (tiles of BM <= 256, BN <= 128 with
+// at most DSPLIT_MAX_FRAGS fragments per wave: a slice tile holds at most BM x BN fp32 partials, and the tile grid
+// covers at most (M + 255) x (K + 127) outputs per phase); tickets for the smallest tile (64 x 64)
+static inline size_t dsplit_ws_bytes(const ConvGeom& g, int nph, int S) {
+  if (S <= 1) return 0;
+  const long long t64 = (long long)nph * ((g.M + 63) / 64) * ((g.K + 63) / 64);
+  return (size_t)(dsplit_ticket_bytes(t64) + (long long)S * nph * (g.M + 255) * (g.K + 127) * 4);
 }
 
 // x2 != nullptr: the virtual-concat instantiation (second input source, ConvGeom.c1b / ldx2)

@@ -11,13 +11,24 @@ pairs, the second builds the teacher's BN fold table, a host-to-device copy that
 device-side Philox counter (ssseg_cowmix_draw_dev), so every replay draws fresh masks -- the same sequence the eager
 steps would.  Host-side values are baked in at capture: a replay repeats the captured step's Python decisions (the
 optimizer step taken or skipped, the epoch gate of the consistency weight, the learning rate), so capture a step with
-step != 0 and recapture when those change.  Single process only (the RCCL collectives of a DDP step are not captured).
+step != 0 and recapture when those change.  Steps without collectives only: a DDP step with its RCCL collectives
+captured (gradient buckets on the side stream, SyncBN sums) hung on replay at world 1 on this image's RCCL 2.26.6, and
+gloo collectives run on the host.
 
     step = StepGraph(lambda img, mask, ua, ub: train.train_step(model, teacher, opt, img, mask, ua, ub, epoch, 1, cfg),
                      img, mask, ua, ub)
     cls, unsup, cm = step(img2, mask2, ua2, ub2)    # copies the inputs into the captured buffers, replays
 """
 import torch
+
+
+def _capture_mode():
+    """'thread_local' while an RCCL process group is live: its watchdog thread polls the events of earlier collectives
+    during the capture, which the default 'global' mode refuses (hipErrorStreamCaptureUnsupported in the watchdog)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_backend() == 'nccl':
+        return 'thread_local'
+    return 'global'
 
 
 class StepGraph:
@@ -27,7 +38,7 @@ class StepGraph:
             fn(*self.static_in)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph, capture_error_mode=_capture_mode()):
             self.static_out = fn(*self.static_in)
 
     def __call__(self, *inputs):

@@ -69,6 +69,8 @@ SIGS = {
     # convolution engine
     'ssseg_conv_igemm': (i32, [vp, vp, vp, vp, i32, i32, vp, i32, vp, sz, vp]),
     'ssseg_conv_igemm_phases': (i32, [vp, vp, vp, i32, i32, vp, i64, vp, vp, vp]),
+    'ssseg_conv_igemm_phases_ws': (i32, [vp, vp, vp, i32, i32, vp, i64, vp, vp, vp, sz, vp]),
+    'ssseg_conv_igemm_phases_workspace_bytes': (sz, [vp, i64, i32]),
     'ssseg_conv_stem_epi': (i32, [vp, vp, vp, vp, i32, vp, vp]),
     'ssseg_conv_igemm_epi': (i32, [vp, vp, vp, vp, i32, i32, vp, vp, sz, vp]),
     'ssseg_weight_pack_batch': (i32, [vp, i64, i32, vp]),

@@ -1057,8 +1057,12 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
                             N.dev_ptr(aux) if aux is not None else None, *_act(relu), *sf)
         geo = (ctypes.c_int64 * (4 * len(geoms)))(*[v for g4 in geoms for v in g4])
         wp = (ctypes.c_void_p * len(ws))(*[N.dev_ptr(w) for w in ws])
-        N.call('ssseg_conv_igemm_phases', N.dev_ptr(x), N.dev_ptr(y), ctypes_ref(desc), N.dt_code(x), N.dt_code(y),
-               ctypes_ref(ep), len(ws), ctypes.addressof(geo), ctypes.addressof(wp), N.stream())
+        # deterministic split-K scratch where the phases are tile-starved (16x16 inputs)
+        nb = N.lib().ssseg_conv_igemm_phases_workspace_bytes(ctypes_ref(desc), len(ws), N.dt_code(x))
+        scratch = N.workspace(nb, x.device) if nb else None
+        N.call('ssseg_conv_igemm_phases_ws', N.dev_ptr(x), N.dev_ptr(y), ctypes_ref(desc), N.dt_code(x), N.dt_code(y),
+               ctypes_ref(ep), len(ws), ctypes.addressof(geo), ctypes.addressof(wp),
+               N.dev_ptr(scratch) if scratch is not None else None, nb, N.stream())
         if stats is not None:
             stats.commit()
 

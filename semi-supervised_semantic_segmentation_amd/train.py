@@ -111,11 +111,17 @@ def _scaled(loss, optimizer):
     return sc.scale(loss) if sc is not None else loss
 
 
-# the first SERIAL_STEPS steps of a process run serially: the engine autotunes every new conv geometry on first use
-# (HIP-event timings, conv.hip tune_variant), and a teacher pass running concurrently on the side stream would skew
-# those timings -- and with them the variant choices kept for the rest of the run
+# the first `serial_steps` steps of every (student, teacher, input geometry, compute dtype) run serially: the engine
+# autotunes every new conv geometry on first use (HIP-event timings, conv.hip tune_variant), and a teacher pass running
+# concurrently on the side stream would skew those timings -- and with them the variant choices kept for the rest of
+# the run.  Counted per step key (a second model, a new batch size or dtype in the same process tunes serially too).
 _OVERLAP = {'teacher': os.environ.get('SSSEG_OVERLAP_TEACHER', '1') != '0', 'streams': {}, 'steps': 0,
-            'serial_steps': 2}
+            'serial_steps': 2, 'seen': {}}
+
+
+def _step_key(model, ema_model, image, unsup_a):
+    return (id(_inner(model)), id(_inner(ema_model)) if ema_model is not None else None, tuple(image.shape),
+            image.dtype, tuple(unsup_a.shape) if unsup_a is not None else None, snn.compute_dtype())
 
 
 def _teacher_targets(ema_model, unsup_a, unsup_b, tc):
@@ -173,8 +179,11 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
     if adv is not None:
         adv_loss, prob = adversarial_terms(pred_maps, mask, adv)
         sup_loss = ops.add_scaled(sup_loss, adv_loss)
+    key = _step_key(model, ema_model, image, unsup_a)
+    seen = _OVERLAP['seen'].get(key, 0)
     overlap = (semi and adv is None and _OVERLAP['teacher'] and image.is_cuda and unsup_a.is_cuda
-               and _OVERLAP['steps'] >= _OVERLAP['serial_steps'])
+               and seen >= _OVERLAP['serial_steps'])
+    _OVERLAP['seen'][key] = seen + 1
     _OVERLAP['steps'] += 1
     targets = None
     if overlap:
@@ -238,6 +247,91 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
         (cm_mean.detach() if cm_mean is not None else None)
 
 
+# ---- captured-step execution of train.train --------------------------------------------------------------------------
+# After the eager steps that tune every conv geometry and build the teacher's BN fold table, train() captures one step
+# of each kind as a HIP graph (ssseg.graph.StepGraph) and replays it for the following steps, the way bench.py runs
+# the benchmark: C5 (HarDNet + discriminator, ~660 small launches) 63.6 -> 33.5 ms/step, C4 213 -> 195 ms.  A replay
+# repeats the Python decisions of its capture, so the graph is keyed on every one of them: the optimizer step taken
+# or skipped (train.py:121, step % virtual_batch_size_multiplier), the epoch gate of the consistency weight
+# (train.py:112), every learning rate, the input geometry and compute dtype -- a new key captures a new graph (the two
+# most recent are kept).  Not captured (eager steps instead): CowMix drawn from the CPU generator (parity mode), steps
+# with collectives (world > 1: DDP buckets and SyncBN), the first optimizer step (SGD's momentum buffer starts from it),
+# and SSSEG_TRAIN_GRAPH=0.
+_GRAPH = {'on': os.environ.get('SSSEG_TRAIN_GRAPH', '1') != '0', 'cache': {}, 'eager_steps': 2, 'max_graphs': 2,
+          'captures': 0, 'replays': 0}
+
+
+def _optimizers(optimizer, config):
+    adv = config['train'].get('adversarial')
+    return [optimizer] + ([adv['optimizer']] if adv is not None else [])
+
+
+def _graph_key(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch, step, config):
+    """None where the step must run eagerly, else the key of its captured graph."""
+    tc = config['train']
+    if not (_GRAPH['on'] and image.is_cuda and torch.cuda.is_available()):
+        return None
+    if tc['use_semi_supervised'] and cowmix.NOISE_SOURCE != 'device':
+        return None
+    if torch.distributed.is_initialized() and (_world() > 1 or getattr(model, '_active', False)):
+        return None   # collectives in the step (DDP buckets, SyncBN): RCCL inside a captured graph hung (DESIGN.md §6)
+    opts = _optimizers(optimizer, config)
+    opt_step = step % tc['virtual_batch_size_multiplier'] == 0 and step != 0
+    # the first SGD step initialises the momentum buffer (a different kernel argument): run it eagerly (the
+    # discriminator of C5 steps every step)
+    if (opt_step and getattr(optimizer, '_first', False)) or any(getattr(o, '_first', False) for o in opts[1:]):
+        return None
+    step_key = _step_key(model, ema_model, image, unsup_a)
+    if _OVERLAP['seen'].get(step_key, 0) < _GRAPH['eager_steps']:
+        return None
+    lrs = tuple(float(g['lr']) for o in opts for g in o.param_groups)
+    shapes = tuple((tuple(t.shape), t.dtype) if t is not None else None for t in (image, mask, unsup_a, unsup_b))
+    return step_key + (id(optimizer), opt_step, float(epoch > 25), lrs, shapes, id(config))
+
+
+def _graph_step(key, model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch, step, config):
+    """One step replayed from the captured graph of `key` (captured from this step's inputs on first use)."""
+    from ssseg.graph import StepGraph
+    g = _GRAPH['cache'].pop(key, None)
+    if g is None:
+        while len(_GRAPH['cache']) >= _GRAPH['max_graphs']:
+            _GRAPH['cache'].pop(next(iter(_GRAPH['cache'])))
+        ins = (image, mask, unsup_a, unsup_b)
+        live = [i for i, t in enumerate(ins) if t is not None]
+
+        def fn(*xs):
+            full = [None] * 4
+            for i, t in zip(live, xs):
+                full[i] = t
+            out = train_step(model, ema_model, optimizer, *full, epoch, step, config)
+            return tuple(t for t in out if t is not None)
+        g = StepGraph(fn, *[ins[i] for i in live])
+        g.live = live
+        _GRAPH['captures'] += 1
+    _GRAPH['cache'][key] = g   # most recent last
+    ins = (image, mask, unsup_a, unsup_b)
+    outs = iter(t.clone() for t in g(*[ins[i] for i in g.live]))
+    _GRAPH['replays'] += 1
+    semi = config['train']['use_semi_supervised']
+    cls = next(outs)
+    unsup = next(outs) if semi else None
+    cm = next(outs) if semi else None
+    return cls, unsup, cm
+
+
+def run_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch, step, config):
+    """train_step, replayed from a captured HIP graph where the step's key allows it (see _GRAPH)."""
+    key = _graph_key(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch, step, config)
+    if key is None:
+        return train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch, step, config)
+    return _graph_step(key, model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch, step, config)
+
+
+def release_graphs():
+    """Drop the captured steps (their private memory pools) -- e.g. before the parameters are reallocated."""
+    _GRAPH['cache'].clear()
+
+
 def _reduce_meters(meters, keys, world):
     """Epoch-end average of the loss meters over ranks (the reference logs rank-reduced losses divided by
     world, train.py:53-59,109-114): one all-reduce of the stacked sums instead of one per step."""
@@ -271,7 +365,7 @@ def train(model, ema_model, optimizer, dataloader, unsupervised_dataloader, epoc
         if tc['use_semi_supervised']:
             ua = next(unsupervised_dataloader)['image'].to(device, non_blocking=True)
             ub = next(unsupervised_dataloader)['image'].to(device, non_blocking=True)
-        cls, unsup, cm = train_step(model, ema_model, optimizer, image, mask, ua, ub, epoch, step, config)
+        cls, unsup, cm = run_step(model, ema_model, optimizer, image, mask, ua, ub, epoch, step, config)
         meters['cls'].update(cls)
         meters['sup'].update(cls)
         meters['unsup'].update(unsup if unsup is not None else 0.)

@@ -396,3 +396,4 @@ def test_rccl_world1_forced_collectives_bitwise(hip_device):
     # per step: one AVG all-reduce per bucket + (sum, sum^2) and (sum dy, sum dy*xhat) per training BatchNorm
     assert all(n == out['nbuckets'] + 2 * out['n_bn'] for n in out['ncalls']), out['ncalls']
     assert not out['mismatch'], out['mismatch'][:10]
+

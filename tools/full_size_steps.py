@@ -77,7 +77,7 @@ def build(name, path, dev, threshold=0.5, calibrate=True):
     torch.manual_seed(0)
     for c in cowmix._DEVICE_RNG['ctr'].values():   # the CowMix Philox counter restarts with every build
         c.zero_()
-    train._OVERLAP['steps'] = 0   # and so does the step schedule (the first serial_steps steps run without overlap)
+    train._OVERLAP['seen'].clear()   # and so does the step schedule (the first serial_steps steps run without overlap)
     for c in snn._DROP['ctr'].values():   # and the dropout Philox counter
         c.zero_()
     cfg = config.fromfile(os.path.join(PKG, path))
