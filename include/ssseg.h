@@ -520,6 +520,27 @@ int ssseg_bn_eval_bwd_grad_y(const void* dy, const void* y, void* dconv, void* d
                              const float* scale, const float* shift, const float* mean_eff, const float* invstd,
                              int relu, int dt, double* sums, void* ws, size_t ws_bytes, float* dgamma, float* dbeta,
                              float* dconv_bias, ssseg_stream_t stream);
+/* Deferred parameter gradients of the differentiated eval BN (the student's consistency pass, train.py:90-92, whose
+ * BN/conv-bias gradients nothing reads before the optimizer step): ssseg_bn_eval_bwd(_grad_y) with the per-block
+ * partial rows (sum dyr, sum dyr*xhat) left in part (>= ssseg_bn_workspace_bytes(C) bytes, caller-owned, kept until
+ * ssseg_bn_param_grad_batch has run; *nparts_host = rows, < 1024) and no reduction launch.  shift != NULL: x_hat from y
+ * (the _grad_y form, aux unused); shift == NULL: x_hat from aux. */
+int ssseg_bn_eval_bwd_part(const void* dy, const void* y, const void* aux, void* dconv, void* dres, int64_t P, int64_t C,
+                           int64_t ld, const float* scale, const float* shift, const float* mean_eff,
+                           const float* invstd, int relu, int dt, double* part, size_t part_bytes, int64_t* nparts_host,
+                           ssseg_stream_t stream);
+/* ONE launch for many deferred reductions: per descriptor, dbeta[c] += sum of part rows 2r, dgamma[c] += sum of rows
+ * 2r + 1, dconv_bias[c] += scale[c] * (the first sum) (NULL pointers skipped); fixed-order fp64 column sums.  descs
+ * points to DEVICE memory; max_c >= every descriptor's C. */
+typedef struct ssseg_pgrad_desc {
+  const double* part;
+  int64_t nparts, C;
+  const float* scale;
+  float* dgamma;
+  float* dbeta;
+  float* dconv_bias;
+} ssseg_pgrad_desc;
+int ssseg_bn_param_grad_batch(const ssseg_pgrad_desc* descs, int64_t n, int64_t max_c, ssseg_stream_t stream);
 /* y = act(gamma*(x-mean)*invstd + beta [+ residual]); channels [C, rup(C, 16 bytes)) of y are written 0; relu = 1 for ReLU (unet.py:10, Bottleneck add+relu) */
 int ssseg_bn_apply(const void* x, const void* residual, void* y, int64_t P, int64_t C, int64_t ldx, int64_t ldr,
                    int64_t ldy, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu,

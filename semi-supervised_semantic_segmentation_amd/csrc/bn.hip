@@ -341,14 +341,17 @@ __global__ void __launch_bounds__(256) bn_partial_rows_kernel(double* part, int 
   }
 }
 
+// column sums of a partial table (rows 2r = first quantity, 2r + 1 = second) for channel c = blockIdx.x * CH + lane
+// group: block = CH channels x (256/CH) partial lanes, four independent chains per lane, a fixed-order in-wave butterfly
+// and the four waves in order (deterministic).  Every thread of the block must call it; the totals are valid on the
+// threads with threadIdx.x < CH.
 template <int CH>
-__global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* part, int nparts, int C, double* sums,
-                                                               FinalEpi fe, int rs = 1) {
+__device__ __forceinline__ void partial_col_sums(const double* part, int nparts, int C, int rs, int cblk, double& ta,
+                                                 double& tb) {
   constexpr int LN = 256 / CH;
-  if (fe.mode == 1 && fe.nbt && blockIdx.x == 0 && threadIdx.x == 0) *fe.nbt += 1;
   __shared__ double red[2][LN][CH];
   const int cl = threadIdx.x % CH, pl = threadIdx.x / CH;
-  const int c = blockIdx.x * CH + cl;
+  const int c = cblk * CH + cl;
   // four row pairs per iteration, all eight loads issued before the adds (independent chains)
   double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
   if (c < C) {
@@ -387,13 +390,24 @@ __global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* par
     red[1][wv][cl] = sb;
   }
   __syncthreads();
-  if (pl == 0 && c < C) {
-    double a = 0, b = 0;
+  ta = tb = 0;
+  if (pl == 0) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      a += red[0][k][cl];
-      b += red[1][k][cl];
+      ta += red[0][k][cl];
+      tb += red[1][k][cl];
     }
+  }
+}
+
+template <int CH>
+__global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* part, int nparts, int C, double* sums,
+                                                               FinalEpi fe, int rs = 1) {
+  if (fe.mode == 1 && fe.nbt && blockIdx.x == 0 && threadIdx.x == 0) *fe.nbt += 1;
+  double a, b;
+  partial_col_sums<CH>(part, nparts, C, rs, blockIdx.x, a, b);
+  const int c = blockIdx.x * CH + threadIdx.x;
+  if (threadIdx.x < CH && c < C) {
     sums[c] = a;
     sums[C + c] = b;
     if (fe.mode == 1) {
@@ -403,6 +417,22 @@ __global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* par
       if (fe.dgamma) fe.dgamma[c] += (float)b;
       if (fe.dbias) fe.dbias[c] += fe.scale[c] * (float)a;
     }
+  }
+}
+
+// the deferred parameter gradients of many eval BNs in one launch (blockIdx.y = descriptor): the same column sums and
+// the same mode-2 tail as bn_partial_final_kernel<8>
+__global__ void __launch_bounds__(256) bn_pgrad_batch_kernel(const ssseg_pgrad_desc* __restrict__ descs) {
+  const ssseg_pgrad_desc& d = descs[blockIdx.y];
+  const int C = (int)d.C;
+  if ((int)blockIdx.x * 8 >= C) return;   // uniform per block
+  double a, b;
+  partial_col_sums<8>(d.part, (int)d.nparts, C, 1, blockIdx.x, a, b);
+  const int c = blockIdx.x * 8 + threadIdx.x;
+  if (threadIdx.x < 8 && c < C) {
+    if (d.dbeta) d.dbeta[c] += (float)a;
+    if (d.dgamma) d.dgamma[c] += (float)b;
+    if (d.dconv_bias) d.dconv_bias[c] += d.scale[c] * (float)a;
   }
 }
 
@@ -911,10 +941,11 @@ extern "C" int ssseg_bn_fold_batch(const ssseg_fold_desc* descs, int64_t n, ssse
   return 0;
 }
 
+// sums == NULL: the partial rows stay in ws (the deferred parameter gradients, ssseg_bn_eval_bwd_part); returns their count
 template <typename T>
-static void eval_bwd(const T* dy, const T* y, const T* aux, T* dconv, T* dres, int64_t P, int64_t C, int64_t ld,
-                     const float* scale, const float* mean_eff, const float* invstd, int relu, double* sums, void* ws,
-                     hipStream_t s, FinalEpi fe, const float* shift) {
+static int64_t eval_bwd(const T* dy, const T* y, const T* aux, T* dconv, T* dres, int64_t P, int64_t C, int64_t ld,
+                        const float* scale, const float* mean_eff, const float* invstd, int relu, double* sums, void* ws,
+                        hipStream_t s, FinalEpi fe, const float* shift) {
   constexpr int V16 = 16 / sizeof(T);
   const bool wide = wide_ok<T>(C, {ld});
   const Layout L = layout_for(C, wide ? V16 : V16 / 2, P);
@@ -925,13 +956,14 @@ static void eval_bwd(const T* dy, const T* y, const T* aux, T* dconv, T* dres, i
   else
     hipLaunchKernelGGL((bn_eval_bwd_kernel<T, V16 / 2>), dim3((unsigned)gx, L.cblocks), dim3(256), 0, s, dy, y, aux,
                        dconv, dres, P, (int)C, ld, L, scale, mean_eff, invstd, relu, (double*)ws, shift);
-  launch_partial_final((const double*)ws, gx, C, sums, s, fe);
+  if (sums) launch_partial_final((const double*)ws, gx, C, sums, s, fe);
+  return gx;
 }
 
 static int eval_bwd_entry(const void* dy, const void* y, const void* aux, void* dconv, void* dres, int64_t P, int64_t C,
                           int64_t ld, const float* scale, const float* mean_eff, const float* invstd, int relu, int dt,
                           double* sums, void* ws, size_t ws_bytes, ssseg_stream_t stream, FinalEpi fe,
-                          const float* shift = nullptr);
+                          const float* shift = nullptr, int64_t* nparts = nullptr);
 
 extern "C" int ssseg_bn_eval_bwd(const void* dy, const void* y, const void* aux, void* dconv, void* dres, int64_t P,
                                  int64_t C, int64_t ld, const float* scale, const float* mean_eff, const float* invstd,
@@ -972,23 +1004,45 @@ extern "C" int ssseg_bn_eval_bwd_grad_y(const void* dy, const void* y, void* dco
 static int eval_bwd_entry(const void* dy, const void* y, const void* aux, void* dconv, void* dres, int64_t P, int64_t C,
                           int64_t ld, const float* scale, const float* mean_eff, const float* invstd, int relu, int dt,
                           double* sums, void* ws, size_t ws_bytes, ssseg_stream_t stream, FinalEpi fe,
-                          const float* shift) {
-  if (!dy || !aux || !dconv || !sums || !scale || !mean_eff || !invstd || (relu && !y) || P < 1 || C < 1 ||
+                          const float* shift, int64_t* nparts) {
+  if (!dy || !aux || !dconv || (!sums && !nparts) || !scale || !mean_eff || !invstd || (relu && !y) || P < 1 || C < 1 ||
       ld_bad(C, ld))
     return SSSEG_EINVAL;
   if (!ws || ws_bytes < ssseg_bn_workspace_bytes(C)) return SSSEG_EWORKSPACE;
   hipStream_t s = (hipStream_t)stream;
+  int64_t gx = 0;
   if (dt == SSSEG_BF16)
-    eval_bwd<bf16_t>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)aux, (bf16_t*)dconv, (bf16_t*)dres, P, C, ld,
+    gx = eval_bwd<bf16_t>((const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)aux, (bf16_t*)dconv, (bf16_t*)dres, P, C, ld,
                      scale, mean_eff, invstd, relu, sums, ws, s, fe, shift);
   else if (dt == SSSEG_F16)
-    eval_bwd<f16_t>((const f16_t*)dy, (const f16_t*)y, (const f16_t*)aux, (f16_t*)dconv, (f16_t*)dres, P, C, ld,
-                     scale, mean_eff, invstd, relu, sums, ws, s, fe, shift);
+    gx = eval_bwd<f16_t>((const f16_t*)dy, (const f16_t*)y, (const f16_t*)aux, (f16_t*)dconv, (f16_t*)dres, P, C, ld,
+                         scale, mean_eff, invstd, relu, sums, ws, s, fe, shift);
   else if (dt == SSSEG_F32)
-    eval_bwd<float>((const float*)dy, (const float*)y, (const float*)aux, (float*)dconv, (float*)dres, P, C, ld, scale,
+    gx = eval_bwd<float>((const float*)dy, (const float*)y, (const float*)aux, (float*)dconv, (float*)dres, P, C, ld, scale,
                     mean_eff, invstd, relu, sums, ws, s, fe, shift);
   else
     return SSSEG_EUNSUPPORTED;
+  if (nparts) *nparts = gx;
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_bn_eval_bwd_part(const void* dy, const void* y, const void* aux, void* dconv, void* dres, int64_t P,
+                                      int64_t C, int64_t ld, const float* scale, const float* shift,
+                                      const float* mean_eff, const float* invstd, int relu, int dt, double* part,
+                                      size_t part_bytes, int64_t* nparts_host, ssseg_stream_t stream) {
+  if (!nparts_host || (!aux && !shift) || (shift && !y)) return SSSEG_EINVAL;
+  *nparts_host = 0;
+  return eval_bwd_entry(dy, y, shift ? y : aux, dconv, dres, P, C, ld, scale, mean_eff, invstd, relu, dt, nullptr, part,
+                        part_bytes, stream, FinalEpi{}, shift, nparts_host);
+}
+
+extern "C" int ssseg_bn_param_grad_batch(const ssseg_pgrad_desc* descs, int64_t n, int64_t max_c,
+                                         ssseg_stream_t stream) {
+  if (n < 0 || n > 65535 || (n > 0 && !descs) || max_c < 0 || max_c > 0x7fffffff) return SSSEG_EINVAL;
+  if (n == 0 || max_c == 0) return 0;
+  hipLaunchKernelGGL(bn_pgrad_batch_kernel, dim3((unsigned)((max_c + 7) / 8), (unsigned)n), dim3(256), 0,
+                     (hipStream_t)stream, descs);
   SSSEG_LAUNCH_CHECK();
   return 0;
 }

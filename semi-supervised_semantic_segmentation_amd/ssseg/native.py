@@ -104,6 +104,8 @@ SIGS = {
     'ssseg_bn_eval_bwd_grad': (i32, [vp, vp, vp, vp, vp, i64, i64, i64, vp, vp, vp, i32, i32, vp, vp, sz, vp, vp,
                                       vp, vp]),
     'ssseg_bn_eval_param_grad': (i32, [vp, i64, vp, vp, vp, vp, vp]),
+    'ssseg_bn_eval_bwd_part': (i32, [vp, vp, vp, vp, vp, i64, i64, i64, vp, vp, vp, vp, i32, i32, vp, sz, I64P, vp]),
+    'ssseg_bn_param_grad_batch': (i32, [vp, i64, i64, vp]),
     'ssseg_bn_apply': (i32, [vp, vp, vp, i64, i64, i64, i64, i64, vp, vp, vp, vp, i32, i32, vp]),
     'ssseg_bn_bwd_reduce': (i32, [vp, vp, vp, i64, i64, i64, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp, sz, vp]),
     'ssseg_bn_param_grad': (i32, [vp, i64, vp, vp, vp]),

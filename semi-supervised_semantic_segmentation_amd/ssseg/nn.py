@@ -103,6 +103,53 @@ def flush_wgrad():
             mod._ssseg_wgrad(*pair, bias_grad=False, want=(True, False))
 
 
+# ---- deferred BN parameter gradients of the differentiated eval pass ---------------------------------------------------
+_PGRAD = {'on': os.environ.get('SSSEG_DEFER_BN_PGRAD', '1') != '0', 'live': False, 'pending': [], 'table': None}
+
+
+@contextlib.contextmanager
+def defer_param_grads():
+    """Inside: the differentiated eval BatchNorms (the student's consistency pass, train.py:90-92) leave their
+    parameter-gradient partial rows in per-layer buffers instead of reducing them right away; on exit ONE launch
+    (ssseg_bn_param_grad_batch) turns all of them into the BN weight / bias (and conv bias) gradients.  Those gradients
+    are read only by the optimizer step, so the ~60 small reduction launches per step (one per BN layer, ~4-5 us each,
+    a launch floor) become one.  Layers whose parameters a DDP reducer watches (world > 1: their gradient marks a bucket
+    ready) are reduced at once as before."""
+    if not _PGRAD['on'] or _PGRAD['live'] or not torch.cuda.is_available():
+        yield
+        return
+    _PGRAD['live'] = True
+    try:
+        yield
+    finally:
+        _PGRAD['live'] = False
+        flush_param_grads()
+
+
+def flush_param_grads():
+    import struct
+    pend, _PGRAD['pending'] = _PGRAD['pending'], []
+    if not pend:
+        return
+    rows = tuple((e['part'].data_ptr(), e['nparts'], e['C'], e['scale'].data_ptr(), e['dg'], e['db'], e['dbias'])
+                 for e in pend)
+    ent = _PGRAD['table']
+    if ent is None or ent[0] != rows:
+        if torch.cuda.is_current_stream_capturing():
+            # (a new descriptor table needs a host-to-device copy): reduce each layer on its own
+            for e in pend:
+                sums = torch.empty(2 * e['C'], dtype=torch.float64, device=e['part'].device)
+                N.call('ssseg_bn_partials_finalize', N.dev_ptr(e['part']), e['nparts'], e['C'], N.dev_ptr(sums), 0.0,
+                       0.0, 0.0, None, None, None, None, None, N.stream())
+                N.call('ssseg_bn_eval_param_grad', N.dev_ptr(sums), e['C'], N.dev_ptr(e['scale']), e['dg'] or None,
+                       e['db'] or None, e['dbias'] or None, N.stream())
+            return
+        blob = b''.join(struct.pack('<7q', *r) for r in rows)
+        ent = (rows, torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(pend[0]['part'].device))
+        _PGRAD['table'] = ent
+    N.call('ssseg_bn_param_grad_batch', N.dev_ptr(ent[1]), len(rows), max(e['C'] for e in pend), N.stream())
+
+
 def wgrad_pending():
     return sum(1 for m in _WGRAD['pending'] if '_ssseg_wg_pending' in m.__dict__)
 
@@ -1300,7 +1347,28 @@ class _ConvBNEvalFn(torch.autograd.Function):
         grads = (N.dev_ptr(_grad_of(bn.weight)) if want(bn.weight) else None,
                  N.dev_ptr(_grad_of(bn.bias)) if want(bn.bias) else None,
                  N.dev_ptr(_grad_of(conv.bias)) if want(conv.bias) else None)
-        if aux is None:   # x_hat from y (no residual): ssseg_bn_eval_bwd_grad_y
+        defer = (_PGRAD['live'] and any(g is not None for g in grads)
+                 and not any(getattr(p, '_ssseg_reducer', None) is not None for p in (bn.weight, bn.bias, conv.bias)
+                             if want(p)))
+        if defer:   # partial rows only; defer_param_grads() reduces every layer's in one launch
+            import ctypes
+            parts = bn.__dict__.setdefault('_ssseg_pg_parts', [])
+            k = sum(1 for e in _PGRAD['pending'] if e['bn'] is bn)   # a module run twice in the pass (MSA)
+            if k >= len(parts) or parts[k].numel() < nb or parts[k].device != dev:
+                buf = torch.empty(nb, dtype=torch.uint8, device=dev)
+                if k >= len(parts):
+                    parts.append(buf)
+                else:
+                    parts[k] = buf
+            part = parts[k]
+            rows = ctypes.c_int64(0)
+            N.call('ssseg_bn_eval_bwd_part', N.dev_ptr(gy), N.dev_ptr(y), N.dev_ptr(aux) if aux is not None else None,
+                   N.dev_ptr(dconv), N.dev_ptr(dres) if dres is not None else None, n * h * w, C, cp, N.dev_ptr(scale),
+                   N.dev_ptr(shift) if aux is None else None, N.dev_ptr(mean_eff), N.dev_ptr(invstd),
+                   _act(ctx.relu)[0], N.dt_code(y), N.dev_ptr(part), nb, ctypes.byref(rows), N.stream())
+            _PGRAD['pending'].append({'bn': bn, 'part': part, 'nparts': rows.value, 'C': C, 'scale': scale,
+                                      'dg': grads[0] or 0, 'db': grads[1] or 0, 'dbias': grads[2] or 0})
+        elif aux is None:   # x_hat from y (no residual): ssseg_bn_eval_bwd_grad_y
             N.call('ssseg_bn_eval_bwd_grad_y', N.dev_ptr(gy), N.dev_ptr(y), N.dev_ptr(dconv),
                    N.dev_ptr(dres) if dres is not None else None, n * h * w, C, cp, N.dev_ptr(scale), N.dev_ptr(shift),
                    N.dev_ptr(mean_eff), N.dev_ptr(invstd), _act(ctx.relu)[0], N.dt_code(y), N.dev_ptr(sums),

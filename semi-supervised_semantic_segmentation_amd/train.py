@@ -228,7 +228,8 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
             unsup_loss = ops.scale(consistency, float(tc['consistency_loss_weight']) * float(epoch > 25))
             if ddp is not None:
                 ddp.arm()
-            ops.backward(_scaled(unsup_loss, optimizer))
+            with snn.defer_param_grads():   # the eval BNs' parameter gradients: one batched reduction at the end
+                ops.backward(_scaled(unsup_loss, optimizer))
         snn.flush_wgrad()
     if ddp is not None:
         ddp.finish()
