@@ -39,7 +39,11 @@ FWD_GFLOP_PER_IMAGE = 95.94     # UNet-R50 mw128 ConvT @512 (verifie
 # MI355X_MICROARCH.md gfx950 correction).  PMC cannot run inside the timed process, so the committed
 # measurement of the same workload is reported next to the live flop rate.
 THRESHOLD = 0.5                 # see the module docstring (liveness)
-PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r4_pmc_traffic.json')
+PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r5_pmc_traffic.json')
+# MFMA utilisation of the same workload from rocprofv3 PMC (tools/pmc_step.py --mfma: SQ_VALU_MFMA_BUSY_CYCLES over
+# 1024 SIMDs x GRBM_GUI_ACTIVE / 8), committed next to the traffic; like the traffic it cannot be collected inside
+# the timed process
+PMC_MFMA = os.path.join(ROOT, 'profiles', 'r5_pmc_mfma.json')
 
 
 def pmc_traffic():
@@ -47,6 +51,20 @@ def pmc_traffic():
         with open(PMC_PROFILE) as fh:
             return int(json.load(fh)['traffic_bytes'])
     except (OSError, KeyError, ValueError):
+        return None
+
+
+def pmc_mfma():
+    try:
+        with open(PMC_MFMA) as fh:
+            d = json.load(fh)
+        return {'conv_engine_mfma_util': d['conv_engine']['mfma_util'],
+                'conv_engine_counted_gflop': d['conv_engine']['implied_gflop'],
+                'whole_step_mfma_util': d['whole_step']['mfma_util'],
+                'source': os.path.relpath(PMC_MFMA, ROOT) + ' (rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES '
+                                                          'GRBM_GUI_ACTIVE; util = busy SIMD-cycles / (1024 x active '
+                                                          'cycles))'}
+    except (OSError, KeyError, ValueError, TypeError):
         return None
 
 
@@ -358,7 +376,7 @@ def main():
                      'frac': round(achieved / BF16_DENSE_PEAK, 4), 'traffic': pmc_traffic(),
                      'traffic_unit': 'HBM bytes per step, conv engine (rocprofv3 PMC, ' + os.path.relpath(PMC_PROFILE, ROOT) + ')',
                      'conv_ms_per_step': round(conv_ms, 3), 'conv_gflop_per_step': round(conv_flops / 1e9, 1),
-                     'launches_per_step': len(rows)},
+                     'launches_per_step': len(rows), 'mfma_pmc': pmc_mfma()},
         'execution': ('HIP graph replay of the captured step (ssseg.graph.StepGraph), one per step' if graphed
                       else 'eager launches from Python (the host reducer issues the RCCL bucket all-reduces)'),
         'step_tflops': round(8 * FWD_GFLOP_PER_IMAGE * args.batch * world / (elapsed / args.steps) / 1e3, 2),

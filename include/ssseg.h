@@ -425,7 +425,8 @@ int ssseg_weight_pack(const float* src, void* dst, int64_t Kd, int64_t Kr, int64
 
 /* Batched repack: every conv's packed layouts refreshed by ONE launch after the master weights change
  * (optimizer step, EMA; train.py:122-124, mean_teacher.py:10-11).  descs points to DEVICE memory
- * holding n descriptors with the ssseg_weight_pack arguments. */
+ * holding n descriptors with the ssseg_weight_pack arguments; every filter has Rs * Ss <= 135 taps
+ * (larger ones: ssseg_weight_pack). */
 typedef struct ssseg_pack_desc {
   const float* src;
   void* dst;

@@ -38,29 +38,129 @@ __global__ void weight_pack_kernel(const float* __restrict__ src, T* __restrict_
   }
 }
 
-// one launch repacks many convs: blockIdx.y = descriptor, blocks along x grid-stride over its elements
+// one launch repacks many convs: blockIdx.y = descriptor, blocks along x grid-stride over its tiles.  A tile is KG
+// consecutive output rows k x CC input channels x every tap: the fp32 source sub-block is read in source order
+// (coalesced: [k][c][taps] runs for layout 0, [c][k][taps] runs for layout 1) into LDS, then written in packed order
+// [k][rr][ss][c] with 8 channels per thread (16-byte stores for the 16-bit packs).  (The per-element gather of the
+// earlier kernel -- three integer divisions and one strided 4-byte read per packed element -- took 156 us per
+// C2 repack of the student's two layouts; 2 per step.)  32-bit index math: the host checks every pack < 2^31 elements.
+constexpr int PK_KG = 4;
+constexpr int PK_MAXD = 2048;   // descriptors per launch (the host splits larger batches)
+// a / d for 0 <= a < 8192 and d >= 1 by a float reciprocal (3 VALU instead of an integer division's ~40): (a + 0.5) / d
+// lies >= 0.5 / d away from every integer and the two roundings err by < 1.2e-7 relative, i.e. < (a + 0.5) * 1.2e-7 / d
+// < 0.5 / d while a < 4e6: the truncation is exact
+__device__ __forceinline__ int pk_div(int a, float inv_d) { return (int)(((float)a + 0.5f) * inv_d); }
+// channels per tile: the largest power of two (8 .. 1024) whose PK_KG x CC x (RS | 1) floats fit the LDS tile, so a 1x1
+// conv's tile holds 4096 weights (with 64 channels per tile the ResNet's 1x1 layers made ~150K tiny tiles per repack)
+__device__ __forceinline__ int pk_cc(int RS) {
+  int cc = 1024;
+  while (cc > 8 && PK_KG * cc * (RS | 1) > PK_KG * 64 * 17) cc >>= 1;
+  return cc;
+}
+__device__ __forceinline__ int pk_tiles(const ssseg_pack_desc& d) {
+  const int RS = (int)(d.Rs * d.Ss);
+  if (RS > 135) return 0;   // (host contract: filters of <= 135 taps, ssseg.h)
+  return (int)((d.Kd + PK_KG - 1) / PK_KG) * (int)((d.Cp + pk_cc(RS) - 1) / pk_cc(RS));
+}
+
 template <typename T>
-__global__ void __launch_bounds__(256) weight_pack_batch_kernel(const ssseg_pack_desc* __restrict__ descs) {
-  // 32-bit index math (the host checks every pack < 2^31 elements)
-  const ssseg_pack_desc& d = descs[blockIdx.y];
-  const int Cp = (int)d.Cp, Sn = (int)d.Sn, Rn = (int)d.Rn, Cd = (int)d.Cd, Kr = (int)d.Kr, Rs = (int)d.Rs,
-            Ss = (int)d.Ss, r0 = (int)d.r0, rstep = (int)d.rstep, s0 = (int)d.s0, sstep = (int)d.sstep;
-  const int total = (int)d.Kd * Rn * Sn * Cp;
-  const bool l0 = d.layout == 0;
-  const float* src = d.src;
-  T* dst = (T*)d.dst;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    const int c = i % Cp;
-    int q = i / Cp;
-    const int ss = q % Sn;
-    q /= Sn;
-    const int rr = q % Rn, k = q / Rn;
-    float v = 0.f;
-    if (c < Cd && k < Kr) {
-      const int r = r0 + rr * rstep, s = s0 + ss * sstep;
-      v = src[l0 ? ((k * Cd + c) * Rs + r) * Ss + s : ((c * Kr + k) * Rs + r) * Ss + s];
+__global__ void __launch_bounds__(256) weight_pack_batch_kernel(const ssseg_pack_desc* __restrict__ descs, int n) {
+  __shared__ float lds[PK_KG * 64 * 17];
+  __shared__ int pre[PK_MAXD + 1];   // tile-count prefix sums of the descriptors (the flat tile space of the launch)
+  if (threadIdx.x < 64) {
+    int carry = 0;
+    const int lane = threadIdx.x;
+    for (int base = 0; base < n; base += 64) {
+      const int d = base + lane;
+      int v = d < n ? pk_tiles(descs[d]) : 0;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+      }
+      if (d < n) pre[d + 1] = carry + v;
+      carry += __shfl(v, 63, 64);
     }
-    io<T>::st(dst, i, v);
+    if (lane == 0) pre[0] = 0;
+  }
+  __syncthreads();
+  const int total = pre[n];
+  for (int g = blockIdx.x; g < total; g += gridDim.x) {
+    int lo = 0, hi = n - 1;   // the descriptor d with pre[d] <= g < pre[d + 1]
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pre[mid] <= g) lo = mid;
+      else hi = mid - 1;
+    }
+    const ssseg_pack_desc& d = descs[lo];
+    const int tile = g - pre[lo];
+    const int Cp = (int)d.Cp, Sn = (int)d.Sn, Rn = (int)d.Rn, Cd = (int)d.Cd, Kr = (int)d.Kr, Kd = (int)d.Kd,
+              Ss = (int)d.Ss, r0 = (int)d.r0, rstep = (int)d.rstep, s0 = (int)d.s0, sstep = (int)d.sstep;
+    const int RS = (int)d.Rs * Ss, RSP = RS | 1;   // odd LDS row stride: the 8-channel reads are conflict-free
+    const int CC = pk_cc(RS);
+    const bool l0 = d.layout == 0;
+    const float* src = d.src;
+    T* dst = (T*)d.dst;
+    const int ncc = (Cp + CC - 1) / CC, taps = Rn * Sn;
+    const int k0 = (tile / ncc) * PK_KG, c0 = (tile % ncc) * CC;
+    const float iRS = 1.f / (float)RS, iCRS = 1.f / (float)(CC * RS), iKRS = 1.f / (float)(PK_KG * RS);
+    // phase 1: the source sub-block in source order; every thread's loads are issued before the first LDS write (one
+    // memory round trip per tile instead of one per element row: n1 / 256 <= 17)
+    const int n1 = PK_KG * CC * RS;
+    constexpr int PK_IT = 17;
+    float v1[PK_IT];
+    int o1[PK_IT];
+#pragma unroll
+    for (int it = 0; it < PK_IT; ++it) {
+      const int i = threadIdx.x + it * 256;
+      o1[it] = -1;
+      v1[it] = 0.f;
+      if (i >= n1) continue;
+      int kk, c, t;
+      if (l0) {   // [k][c][t]: contiguous over (c, t) per k
+        kk = pk_div(i, iCRS);
+        const int rem = i - kk * CC * RS;
+        c = pk_div(rem, iRS);
+        t = rem - c * RS;
+      } else {    // [c][k][t]: contiguous over (k, t) per c
+        c = pk_div(i, iKRS);
+        const int rem = i - c * PK_KG * RS;
+        kk = pk_div(rem, iRS);
+        t = rem - kk * RS;
+      }
+      const int k = k0 + kk, cc = c0 + c;
+      o1[it] = (kk * CC + c) * RSP + t;
+      if (k < Kr && cc < Cd) v1[it] = src[l0 ? (k * Cd + cc) * RS + t : (cc * Kr + k) * RS + t];
+    }
+#pragma unroll
+    for (int it = 0; it < PK_IT; ++it)
+      if (o1[it] >= 0) lds[o1[it]] = v1[it];
+    __syncthreads();
+    // phase 2: packed order [k][rr][ss][c], 8 channels per thread
+    const int c8n = CC / 8, lc8 = __builtin_ctz((unsigned)c8n);
+    const int n2 = PK_KG * taps * c8n;
+    const float iTC = 1.f / (float)(taps * c8n), iSn = 1.f / (float)Sn;
+    for (int j = threadIdx.x; j < n2; j += 256) {
+      const int kk = pk_div(j, iTC);
+      const int rem = j - kk * taps * c8n;
+      const int tt = rem >> lc8, c8 = rem & (c8n - 1);
+      const int k = k0 + kk, c = c0 + c8 * 8;
+      if (k >= Kd || c >= Cp) continue;
+      const int rr = pk_div(tt, iSn), ss = tt - rr * Sn;
+      const int t = (r0 + rr * rstep) * Ss + s0 + ss * sstep;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = lds[(kk * CC + c8 * 8 + e) * RSP + t];
+      const int o = (k * taps + tt) * Cp + c;
+      if (c + 8 <= Cp && (Cp & 7) == 0) {
+        Out8<T>::st(dst + o, v);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (c + e < Cp) io<T>::st(dst, o + e, v[e]);
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -460,16 +560,18 @@ extern "C" int ssseg_conv_igemm(const void* x, const void* w, void* y, const sss
 
 extern "C" int ssseg_weight_pack_batch(const ssseg_pack_desc* descs, int64_t n, int dt, ssseg_stream_t stream) {
   if (n < 0 || n > 65535 || (n > 0 && !descs)) return SSSEG_EINVAL;
-  if (n == 0) return 0;
-  const dim3 grid(256, (unsigned)n);
-  if (dt == SSSEG_BF16)
-    hipLaunchKernelGGL(weight_pack_batch_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, descs);
-  else if (dt == SSSEG_F16)
-    hipLaunchKernelGGL(weight_pack_batch_kernel<f16_t>, grid, dim3(256), 0, (hipStream_t)stream, descs);
-  else if (dt == SSSEG_F32)
-    hipLaunchKernelGGL(weight_pack_batch_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, descs);
-  else
-    return SSSEG_EUNSUPPORTED;
+  if (dt != SSSEG_BF16 && dt != SSSEG_F16 && dt != SSSEG_F32) return SSSEG_EUNSUPPORTED;
+  // one block per CU slot over the launch's flat tile space; PK_MAXD descriptors per launch
+  for (int64_t b = 0; b < n; b += PK_MAXD) {
+    const int m = (int)std::min<int64_t>(PK_MAXD, n - b);
+    const dim3 grid(2048);
+    if (dt == SSSEG_BF16)
+      hipLaunchKernelGGL(weight_pack_batch_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, descs + b, m);
+    else if (dt == SSSEG_F16)
+      hipLaunchKernelGGL(weight_pack_batch_kernel<f16_t>, grid, dim3(256), 0, (hipStream_t)stream, descs + b, m);
+    else
+      hipLaunchKernelGGL(weight_pack_batch_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, descs + b, m);
+  }
   SSSEG_LAUNCH_CHECK();
   return 0;
 }

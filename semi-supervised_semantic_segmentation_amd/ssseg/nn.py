@@ -1697,6 +1697,9 @@ def invalidate_packed(model):
         if w.numel() >= 2 ** 31:
             m.invalidate_packed()
             continue
+        if w.shape[2] * w.shape[3] > 135:   # the batched repack's tile holds filters of <= 135 taps
+            m.invalidate_packed()
+            continue
         for key, t in m._ssseg_packs.items():
             if t.numel() >= 2 ** 31:
                 raise RuntimeError('ssseg: packed weight too large for the batched repack')

@@ -622,6 +622,45 @@ def test_batched_repack_after_weight_update(hip_device):
     assert torch.equal(ya, yb)
 
 
+@pytest.mark.parametrize('dt', [torch.bfloat16, torch.float32])
+def test_batched_repack_matches_single_pack(hip_device, dt):
+    """ssseg_weight_pack_batch (the LDS-tiled repack after an optimizer / EMA step) writes every packed layout --
+    forward [K][R][S][C], flipped dgrad, ConvTranspose2d phases, strided-dgrad phases, 7x7 stem, channel padding --
+    bit-identical to the one-pack-per-launch kernel ssseg_weight_pack."""
+    from ssseg import native as N
+    from ssseg import nn as snn
+    snn.set_compute_dtype(dt)
+    torch.manual_seed(5)
+    mods = [snn.Conv2d(3, 64, 7, 2, 3, bias=False), snn.Conv2d(64, 40, 3, 1, 1), snn.Conv2d(40, 256, 1),
+            snn.Conv2d(256, 72, 3, 2, 1), snn.ConvTranspose2d(72, 24, 4, 2, 1), snn.Conv2d(24, 24, 5, 1, 2)]
+    model = torch.nn.Sequential(*mods).to(hip_device)
+    try:
+        x = snn.to_act(torch.randn(2, 3, 32, 32, device=hip_device)).requires_grad_(True)
+        y = x
+        for m in mods:
+            y = m(y)
+        torch.autograd.backward(y, snn.to_act(torch.ones(y.shape, device=hip_device)))   # fwd + dgrad packs
+        with torch.no_grad():
+            for p in model.parameters():
+                p.mul_(-0.7).add_(0.01)
+        snn.invalidate_packed(model)                     # batched repack into the cached pack tensors
+        torch.cuda.synchronize()
+        npacks = 0
+        for m in mods:
+            w = m.weight.detach().contiguous()
+            for key, t in m._ssseg_packs.items():
+                Kd, Kr, Cd, Rs, Ss, Cp, layout, r0, rstep, Rn, s0, sstep, Sn = m._ssseg_specs[key]
+                ref = torch.empty_like(t)
+                N.call('ssseg_weight_pack', N.dev_ptr(w), N.dev_ptr(ref), Kd, Kr, Cd, Rs, Ss, Cp, layout, r0, rstep,
+                       Rn, s0, sstep, Sn, N.dt_code(ref), N.stream())
+                torch.cuda.synchronize()
+                assert torch.equal(t, ref), (type(m).__name__, key)
+                npacks += 1
+        assert npacks >= 10
+    finally:
+        snn.set_compute_dtype(torch.bfloat16)
+
+
 def test_folded_context_bitwise(hip_device):
     """snn.folded(model): one batched BN fold for the whole eval forward, bit-identical to per-layer folds,
     with and without autograd (teacher pass / consistency pass)."""

@@ -172,12 +172,78 @@ def parse(fetch_dir, write_dir, trace_dir=None):
     print(json.dumps(out, indent=1))
 
 
+# MFMA 16x16x32 (bf16 / f16): 16 x 16 x 32 multiply-adds = 16384 flop per instruction, 16 cycles of one SIMD
+# (MI355X_MICROARCH.md, instruction table); SQ_VALU_MFMA_BUSY_CYCLES counts MFMA-busy cycles summed over the SIMDs,
+# GRBM_GUI_ACTIVE the GPU-busy cycles summed over the 8 XCDs (so / 8 = elapsed cycles), 256 CUs x 4 SIMDs
+SIMDS = 1024
+
+
+def parse_mfma(mfma_dir, trace_dir, flops_json=None):
+    """MFMA utilisation per kernel family of one C2 step: SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8),
+    i.e. the fraction of SIMD-cycles the matrix cores were busy while the family's kernels ran, next to the
+    family's device time; with flops_json (tools/layer_report.py --json) the conv families' flop-derived fraction of
+    the 2.5 PF dense peak too."""
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    rows = _rows(mfma_dir)
+    key = 'Dispatch_Id' if 'Dispatch_Id' in rows[0] else 'Correlation_Id'
+    # several counters per dispatch (one row each): the step lies between the last two marker DISPATCHES
+    marks = sorted({int(r[key]) for r in rows if 'cast_kernel' in r['Kernel_Name']
+                    and int(r.get('Grid_Size', r.get('Grid_Size_X', 0)) or 0) <= 256})
+    if len(marks) < 2:
+        raise SystemExit('markers not found')
+    lo, hi = marks[-2], marks[-1]
+    for r in (r for r in rows if lo < int(r[key]) < hi):
+        fam = _family(r['Kernel_Name'])
+        per[fam][r['Counter_Name']] += float(r['Counter_Value'])
+    ta = _trace_sums(trace_dir) if trace_dir else {}
+    fams = []
+    tot = collections.defaultdict(float)
+    conv = collections.defaultdict(float)
+    for k in sorted(per, key=lambda k: -per[k].get('GRBM_GUI_ACTIVE', 0)):
+        c = per[k]
+        busy, act = c.get('SQ_VALU_MFMA_BUSY_CYCLES', 0.0), c.get('GRBM_GUI_ACTIVE', 0.0)
+        row = {'kernel': k, 'mfma_busy_cycles': busy, 'gpu_active_cycles_sum8': act,
+               'sq_busy_cycles': c.get('SQ_BUSY_CYCLES', 0.0),
+               'mfma_util': round(busy / (SIMDS * act / 8), 4) if act else None,
+               'implied_mfma_instructions': round(busy / 16)}
+        if k in ta:
+            row['time_us'] = round(ta[k][0], 1)
+            row['launches'] = ta[k][1]
+            row['implied_clock_GHz'] = round(act / 8 / (ta[k][0] * 1e3), 3) if ta[k][0] else None
+        fams.append(row)
+        for key in ('mfma_busy_cycles', 'gpu_active_cycles_sum8'):
+            tot[key] += row[key]
+            if k in CONV_KERNELS:
+                conv[key] += row[key]
+    out = {
+        'what': 'MFMA utilisation per kernel family of one C2 training step (UNet-R50 512x512 bs16 bf16), rocprofv3 '
+                '--pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE (one pass)',
+        'definition': 'mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs); '
+                      'implied_mfma_instructions = busy cycles / 16 (16x16x32 bf16: 16 cycles per SIMD)',
+        'conv_engine': {'mfma_util': round(conv['mfma_busy_cycles'] / (SIMDS * conv['gpu_active_cycles_sum8'] / 8), 4)
+                        if conv['gpu_active_cycles_sum8'] else None,
+                        'implied_gflop': round(conv['mfma_busy_cycles'] / 16 * 16384 / 1e9, 1),
+                        'time_us': round(sum(ta[k][0] for k in ta if k in CONV_KERNELS), 1) if ta else None},
+        'whole_step': {'mfma_util': round(tot['mfma_busy_cycles'] / (SIMDS * tot['gpu_active_cycles_sum8'] / 8), 4)
+                       if tot['gpu_active_cycles_sum8'] else None},
+        'families': fams,
+    }
+    ce = out['conv_engine']
+    if ce['time_us']:
+        ce['implied_TFLOPs'] = round(ce['implied_gflop'] * 1e9 / (ce['time_us'] * 1e-6) / 1e12, 1)
+        ce['implied_frac_of_2p5PF'] = round(ce['implied_TFLOPs'] / 2500.0, 4)
+    print(json.dumps(out, indent=1))
+
+
 if __name__ == '__main__':
     ap = argparse.ArgumentParser()
     ap.add_argument('--parse', nargs=2, metavar=('FETCH_DIR', 'WRITE_DIR'))
+    ap.add_argument('--mfma', default=None, metavar='MFMA_DIR')
     ap.add_argument('--trace', default=None)
     a = ap.parse_args()
-    if a.parse:
+    if a.mfma:
+        parse_mfma(a.mfma, a.trace)
+    elif a.parse:
         parse(*a.parse, trace_dir=a.trace)
     else:
         run()
