@@ -189,6 +189,7 @@ int launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvGe
     case 22:
     case 23: return launch_glds_grp_e<TO>(cfg, x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);
     case 24: return launch_hconv3<TO>(x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b);   // halo-tiled 3x3 (-1: n/a)
+    case 28: return launch_hconv3<TO>(x, w, y, g, ep, xb, wb, s, ws, ph, x2, x2b, 1);   // its two-blocks-per-CU form
     case 25: return launch_hconv3s<TO>(x, w, y, g, ep, xb, s, ws, ph, x2);   // its 32 -> 32-channel form
     case 26: return launch_pw<TO>(4, x, w, y, g, ep, s, ws, ph, x2);   // pointwise, 64-pixel wave tiles
     case 27: return launch_pw<TO>(2, x, w, y, g, ep, s, ws, ph, x2);   // pointwise, 32-pixel wave tiles
@@ -208,7 +209,7 @@ int launch_glds_cfg(int cfg, const void* x, const void* w, void* y, const ConvGe
 // where it applies).  With knob 5 on (default) an unseen geometry is timed once over the candidates on the caller's
 // stream (HIP events) and the fastest is cached.
 constexpr int kCandidates[] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  10, 12, 13, 14,
-                                15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27};
+                                15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28};
 std::unordered_map<unsigned long long, int> g_variant;
 std::mutex g_variant_mu;
 
@@ -311,7 +312,7 @@ int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const
     float* wsv = ws;
     for (int v : kCandidates) {
       // a virtually padded contraction (C > ldx: the host's vpad) runs on the bounded LDS-DMA loads only
-      if (g.C > g.ldx && (v == 0 || v == 24)) continue;
+      if (g.C > g.ldx && (v == 0 || v == 24 || v == 28)) continue;
       // warm (code load, caches); a variant that cannot run this launch (-1) is skipped
       if (run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, wsv, ph, x2, x2b) <= 0) continue;
       float ms = 1e30f;
@@ -372,14 +373,14 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
                                                (unsigned)x2b, &cache_it)
                          : heuristic_variant(g);
           if (x2 && v == 0) v = 5;   // the register-staged kernel has no second source
-          if (g.C > g.ldx && (v == 0 || v == 24)) v = 14;   // (vpad: LDS-DMA only)
+          if (g.C > g.ldx && (v == 0 || v == 24 || v == 28)) v = 14;   // (vpad: LDS-DMA only)
           if (S > 1 && (v == 0 || v >= 24)) v = 14;         // a split launch: LDS-DMA configs only
           if (cache_it) g_variant[key] = v;
         }
       } else if (g_knobs[4] == 11) {
         v = (g.C > g.ldx || S > 1) ? 14 : 0;   // forced register-staged (a vpad / split contraction runs config 14)
         if (x2 && v == 0) return -1;
-      } else if ((g.C > g.ldx || S > 1) && g_knobs[4] == 24) {
+      } else if ((g.C > g.ldx || S > 1) && (g_knobs[4] == 24 || g_knobs[4] == 28)) {
         v = 14;
       }
       // every variant of a split launch sums the same k-slices in the same order: forced variants stay bit-comparable
@@ -390,7 +391,7 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
       // a forced config without a general-k instantiation (128/256-wide n-tiles, C % 64 != 0): register-staged
       if (r == -1 && g_knobs[4] != 0 && !x2 && g.C % 64 && g.C <= g.ldx)
         return run_variant<T, TO>(0, x, w, y, g, ep, 0, 0, s, nullptr, ph);
-      if (r == -1 && g_knobs[4] >= 24 && g_knobs[4] <= 27) {   // a forced halo / pointwise kernel does not apply: the heuristic's
+      if (r == -1 && g_knobs[4] >= 24 && g_knobs[4] <= 28) {   // a forced halo / pointwise kernel does not apply: the heuristic's
         const int hv = x2 && heuristic_variant(g) == 0 ? 5 : heuristic_variant(g);
         return run_variant<T, TO>(hv, x, w, y, g, ep, (unsigned)xb, (unsigned)wb, s, nullptr, ph, x2, (unsigned)x2b);
       }

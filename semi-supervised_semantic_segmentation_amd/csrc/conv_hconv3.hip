@@ -27,14 +27,21 @@ constexpr int HC_PX = 400;                    // halo pixels per buffer: 6 rows 
 constexpr int HC_XBUF = HC_PX * 128;          // 64 channels x 2 B per pixel
 constexpr int HC_WBUF = 3 * 64 * 128;         // one tap row: 3 taps x 64 output channels x 64 input channels
 constexpr int HC_SMEM = 2 * HC_XBUF + 2 * HC_WBUF;
+constexpr int HC_SMEM1 = HC_XBUF + HC_WBUF;   // single-buffered form: two blocks per CU (75,776 B each)
+static_assert(256 * (64 * 4 + 16) <= HC_SMEM1, "the staged epilogue tile fits the single-buffered LDS");
 
 __device__ __forceinline__ int hc_swz(int r) { return (r >> 1) & 7; }   // 16-byte chunk swizzle of a 128-byte row
 
-template <typename TO, bool STATS, bool VC>
-__global__ void __launch_bounds__(256, 1) hconv3_kernel(const TO* __restrict__ x, const TO* __restrict__ w,
-                                                        TO* __restrict__ y, ConvGeom g, Epi<TO> ep, unsigned xbytes,
-                                                        unsigned wbytes, const TO* __restrict__ x2, unsigned x2bytes) {
-  __shared__ __attribute__((aligned(1024))) char smem[HC_SMEM];
+// TWO (autotuner variant 28): one halo and one weight buffer (75.8 KB), two blocks per CU -- each block loads a stage
+// while the other multiplies (2 waves per SIMD); the double-buffered form (variant 24) has one 151.5 KB block per CU,
+// one wave per SIMD, whose MFMA and LDS latencies do not overlap and whose prologue / epilogue latency is exposed on
+// every tile
+template <typename TO, bool STATS, bool VC, bool TWO>
+__global__ void __launch_bounds__(256, TWO ? 2 : 1) hconv3_kernel(const TO* __restrict__ x, const TO* __restrict__ w,
+                                                                  TO* __restrict__ y, ConvGeom g, Epi<TO> ep,
+                                                                  unsigned xbytes, unsigned wbytes,
+                                                                  const TO* __restrict__ x2, unsigned x2bytes) {
+  __shared__ __attribute__((aligned(1024))) char smem[TWO ? HC_SMEM1 : HC_SMEM];
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int nkb = g.K >> 6, nstrips = g.W >> 6, nrg = g.H >> 2;
   const int tile = xcd_tile(blockIdx.x, gridDim.x);   // consecutive ids (the k-blocks of one pixel tile) share an XCD
@@ -48,7 +55,7 @@ __global__ void __launch_bounds__(256, 1) hconv3_kernel(const TO* __restrict__ x
   __amdgpu_buffer_rsrc_t xr2 = xr;
   if constexpr (VC) xr2 = __builtin_amdgcn_make_buffer_rsrc((void*)x2, (short)0, (int)x2bytes, 0x00020000);
   char* const XB = smem;
-  char* const WB = smem + 2 * HC_XBUF;
+  char* const WB = smem + (TWO ? 1 : 2) * HC_XBUF;
 
   // halo of channel block cb into buffer b: pixel p = 8i + lane/8 of 50 wave-instructions (row p / 66, column p % 66
   // of the 6 x 66 window whose top-left input pixel is (y0 - 1, x0 - 1)); padding / out-of-image pixels read zeros
@@ -113,23 +120,37 @@ __global__ void __launch_bounds__(256, 1) hconv3_kernel(const TO* __restrict__ x
     }
   };
 
-  // stages (cb, r) in order; the halo of cb + 1 is issued with stage (cb, 0) (its buffer was last read by cb - 1),
-  // the weights of the next stage with every stage: one stage of prefetch, vmcnt(0) + barrier per stage
-  issue_x(0, 0);
-  issue_w(0, 0, 0);
-  vmcnt_wait<0>();
-  __builtin_amdgcn_s_barrier();
   const int nst = ncb * 3;
-  for (int st = 0; st < nst; ++st) {
-    const int cb = st / 3, r = st - cb * 3;
-    if (st + 1 < nst) {
-      const int cb1 = (st + 1) / 3, r1 = (st + 1) - cb1 * 3;
-      if (r == 0 && cb + 1 < ncb) issue_x((cb + 1) & 1, cb + 1);
-      issue_w((st + 1) & 1, cb1, r1);
+  if constexpr (TWO) {
+    // stages (cb, r) in order, each loaded into the single buffers after the previous stage's reads (the other block
+    // on the CU multiplies meanwhile)
+    for (int st = 0; st < nst; ++st) {
+      const int cb = st / 3, r = st - cb * 3;
+      if (r == 0) issue_x(0, cb);
+      issue_w(0, cb, r);
+      vmcnt_wait<0>();
+      __builtin_amdgcn_s_barrier();   // the stage landed for every wave
+      compute(0, 0, r);
+      __builtin_amdgcn_s_barrier();   // every wave is done reading it
     }
-    compute(cb & 1, st & 1, r);
+  } else {
+    // stages (cb, r) in order; the halo of cb + 1 is issued with stage (cb, 0) (its buffer was last read by cb - 1),
+    // the weights of the next stage with every stage: one stage of prefetch, vmcnt(0) + barrier per stage
+    issue_x(0, 0);
+    issue_w(0, 0, 0);
     vmcnt_wait<0>();
-    __builtin_amdgcn_s_barrier();   // this stage's buffers are free, the next stage's landed for every wave
+    __builtin_amdgcn_s_barrier();
+    for (int st = 0; st < nst; ++st) {
+      const int cb = st / 3, r = st - cb * 3;
+      if (st + 1 < nst) {
+        const int cb1 = (st + 1) / 3, r1 = (st + 1) - cb1 * 3;
+        if (r == 0 && cb + 1 < ncb) issue_x((cb + 1) & 1, cb + 1);
+        issue_w((st + 1) & 1, cb1, r1);
+      }
+      compute(cb & 1, st & 1, r);
+      vmcnt_wait<0>();
+      __builtin_amdgcn_s_barrier();   // this stage's buffers are free, the next stage's landed for every wave
+    }
   }
 
   // LDS-staged epilogue over the 4 x 64 pixel tile (the ring is idle: the loop ended on a barrier)
@@ -147,31 +168,42 @@ bool hconv3_ok(const ConvGeom& g, const PhaseTab* ph, const float* ws) {
          g.ldy % 8 == 0 && g.ldx >= g.C && g.M < 0x7fffffffLL;
 }
 
-template <typename TO>
-int launch_hconv3(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                  unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2, unsigned x2b) {
-  if (!hconv3_ok(g, ph, ws) || (x2 && (g.ldx2 % 8 || g.c1b < 1 || g.c1b >= g.C / 64))) return -1;
-  const long long blocks = (long long)g.N * (g.H / 4) * (g.W / 64) * (g.K / 64);
-  if (blocks > 0x7fffffffLL) return -1;
+template <typename TO, bool TWO>
+static void launch_hconv3_t(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
+                            unsigned wb, hipStream_t s, const void* x2, unsigned x2b, long long blocks) {
   const TO* xa = (const TO*)x2;
   if (x2) {
     if (ep.stats)
-      hipLaunchKernelGGL((hconv3_kernel<TO, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, (const TO*)x,
+      hipLaunchKernelGGL((hconv3_kernel<TO, true, true, TWO>), dim3((unsigned)blocks), dim3(256), 0, s, (const TO*)x,
                          (const TO*)w, (TO*)y, g, ep, xb, wb, xa, x2b);
     else
-      hipLaunchKernelGGL((hconv3_kernel<TO, false, true>), dim3((unsigned)blocks), dim3(256), 0, s, (const TO*)x,
+      hipLaunchKernelGGL((hconv3_kernel<TO, false, true, TWO>), dim3((unsigned)blocks), dim3(256), 0, s, (const TO*)x,
                          (const TO*)w, (TO*)y, g, ep, xb, wb, xa, x2b);
   } else if (ep.stats) {
-    hipLaunchKernelGGL((hconv3_kernel<TO, true, false>), dim3((unsigned)blocks), dim3(256), 0, s, (const TO*)x,
+    hipLaunchKernelGGL((hconv3_kernel<TO, true, false, TWO>), dim3((unsigned)blocks), dim3(256), 0, s, (const TO*)x,
                        (const TO*)w, (TO*)y, g, ep, xb, wb, xa, x2b);
   } else {
-    hipLaunchKernelGGL((hconv3_kernel<TO, false, false>), dim3((unsigned)blocks), dim3(256), 0, s, (const TO*)x,
+    hipLaunchKernelGGL((hconv3_kernel<TO, false, false, TWO>), dim3((unsigned)blocks), dim3(256), 0, s, (const TO*)x,
                        (const TO*)w, (TO*)y, g, ep, xb, wb, xa, x2b);
   }
+}
+
+// mode 0: the double-buffered kernel (variant 24), 1: the single-buffered two-blocks-per-CU kernel (variant 28)
+template <typename TO>
+int launch_hconv3(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
+                  unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2, unsigned x2b, int mode) {
+  if (!hconv3_ok(g, ph, ws) || (x2 && (g.ldx2 % 8 || g.c1b < 1 || g.c1b >= g.C / 64))) return -1;
+  if (mode == 1 && g_knobs[15] < 0) return -1;   // knob 15 = -1: no variant 28 (A/B)
+  const long long blocks = (long long)g.N * (g.H / 4) * (g.W / 64) * (g.K / 64);
+  if (blocks > 0x7fffffffLL) return -1;
+  if (mode == 1)
+    launch_hconv3_t<TO, true>(x, w, y, g, ep, xb, wb, s, x2, x2b, blocks);
+  else
+    launch_hconv3_t<TO, false>(x, w, y, g, ep, xb, wb, s, x2, x2b, blocks);
   return 256;
 }
 
 template int launch_hconv3<bf16_t>(const void*, const void*, void*, const ConvGeom&, const Epi<bf16_t>&, unsigned,
-                                   unsigned, hipStream_t, float*, const PhaseTab*, const void*, unsigned);
+                                   unsigned, hipStream_t, float*, const PhaseTab*, const void*, unsigned, int);
 template int launch_hconv3<f16_t>(const void*, const void*, void*, const ConvGeom&, const Epi<f16_t>&, unsigned,
-                                  unsigned, hipStream_t, float*, const PhaseTab*, const void*, unsigned);
+                                  unsigned, hipStream_t, float*, const PhaseTab*, const void*, unsigned, int);

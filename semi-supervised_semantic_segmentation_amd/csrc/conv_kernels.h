@@ -1456,7 +1456,8 @@ inline int plan_splits(const ConvGeom& g) {
 // autotuner (conv_hconv3.hip); returns the tile height 256, or -1 where it cannot run the launch
 template <typename TO>
 int launch_hconv3(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
-                  unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2, unsigned x2b);
+                  unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2, unsigned x2b,
+                  int mode = 0);
 
 // the same for 32 input and 32 output channels (conv_hconv3s.hip), variant 25; 256 or -1
 template <typename TO>

@@ -283,7 +283,7 @@ def test_conv_bn_act_fused_eval_grad(hip_device, mode, monkeypatch, kind, cin, c
     _close(mb.bias.grad, rb.bias.grad, mode, 'dbeta')
 
 
-ALL_VARIANTS = [11] + list(range(1, 11)) + list(range(12, 28))
+ALL_VARIANTS = [11] + list(range(1, 11)) + list(range(12, 29))
 
 
 @pytest.mark.parametrize('kind,cin,cout,k,H', [('conv', 64, 128, 3, 19), ('conv', 128, 64, 1, 17), ('conv', 192, 256, 3, 9),
