@@ -29,9 +29,32 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 # semi-supervised step GFLOP per labelled image (3F sup fwd+bwd + 2F teacher + 3F consistency fwd+bwd)
-STEP_GFLOP_PER_IMAGE = {'c3': 3855.8, 'c4': 3904.2, 'c5': 85.2}
+STEP_GFLOP_PER_IMAGE = {'c2': 765.1, 'c3': 3855.8, 'c4': 3904.2, 'c5': 85.2}
 PEAK = {'bfloat16': 2.5e15, 'float16': 2.5e15, 'float32': 0.16e15}   # dense MFMA (MI355X_MICROARCH.md)
-CFGS = {'c3': 'configs/c3_deeplabv3_r101.py', 'c4': 'configs/c4_msa_hrnet.py', 'c5': 'configs/c5_hardnet_disc.py'}
+CFGS = {'c2': 'configs/c2_unet_r50.py', 'c3': 'configs/c3_deeplabv3_r101.py', 'c4': 'configs/c4_msa_hrnet.py',
+        'c5': 'configs/c5_hardnet_disc.py'}
+
+
+def train_loop(name, path, dev, threshold, calibrate, n_warm=4, n_timed=10):
+    """The reference entry point (train.train, reference train.py:25-147) over in-HBM batches: a first call of n_warm
+    steps (two eager tuning steps, the first optimizer step, then the step captured as a HIP graph), a second call whose
+    step 0 (no optimizer step) captures its own graph, then a timed call of n_timed steps, every one replayed.  Returns
+    (ms per step of the timed call, captures, replays)."""
+    import train
+    model, ema, opt, cfg, tc, (img, mask, ua, ub), _, _ = build(name, path, dev, threshold, calibrate)
+    loader = lambda n: [{'image': img, 'semantic_mask': mask} for _ in range(n)]  # noqa: E731
+    unl = iter(lambda: {'image': ua}, None)
+    c0, r0 = train._GRAPH['captures'], train._GRAPH['replays']
+    train.train(model, ema, opt, loader(n_warm), unl, 30, 0, None, cfg, dev)
+    # (an epoch's step 0 takes no optimizer step, train.py:121: its own graph, captured by this second warm-up call)
+    train.train(model, ema, opt, loader(2), unl, 30, n_warm, None, cfg, dev)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    train.train(model, ema, opt, loader(n_timed), unl, 30, n_warm, None, cfg, dev)
+    torch.cuda.synchronize()
+    ms = 1e3 * (time.time() - t0) / n_timed
+    train.release_graphs()
+    return ms, train._GRAPH['captures'] - c0, train._GRAPH['replays'] - r0
 
 
 def rescale_heads(model, ncls=2):
@@ -146,7 +169,7 @@ def graph_steps(name, path, dev, threshold, calibrate, eager_losses, n_eager=3, 
     return ms, same, out, same_eager
 
 
-def run(name, path, dev, threshold=0.5, calibrate=True, layers=False, graph=False):
+def run(name, path, dev, threshold=0.5, calibrate=True, layers=False, graph=False, loop=False):
     import train
     from ssseg import nn as snn
     model, ema, opt, cfg, tc, (img, mask, ua, ub), b, s = build(name, path, dev, threshold, calibrate)
@@ -198,6 +221,11 @@ def run(name, path, dev, threshold=0.5, calibrate=True, layers=False, graph=Fals
                         'rebuild_eager_steps_bitwise_equal': same_eager,
                         'frac_of_dense_peak': round(STEP_GFLOP_PER_IMAGE[name] * b / (gms / 1e3) / 1e3 * 1e12 /
                                                     PEAK[rec['dtype']], 4)}
+    if loop:   # the same config through the reference entry point train.train (captured-step replay inside)
+        torch.cuda.empty_cache()
+        lms, caps, reps = train_loop(name, path, dev, threshold, calibrate)
+        rec['train_train'] = {'ms_per_step': round(lms, 1), 'captures': caps, 'replays': reps,
+                              'note': 'train.train over in-HBM batches: 10 timed steps (one epoch call) after 4 + 2 warm-up steps'}
     print(json.dumps(rec), flush=True)
     return rec['losses_finite'] and rec['params_finite']
 
@@ -210,13 +238,15 @@ def main():
     ap.add_argument('--layers', action='store_true', help='per-layer conv report of one extra step (stderr)')
     ap.add_argument('--graph', action='store_true', help='also replay a captured HIP graph of the step (5 eager steps '
                     'first; graph losses checked bitwise against eager steps 3 and 4)')
+    ap.add_argument('--train-loop', action='store_true', help='also time the config through train.train (the reference '
+                    'entry point, captured-step replay inside)')
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     dist.init_process_group('nccl', init_method='tcp://127.0.0.1:29533', rank=0, world_size=1)
     ok = True
     for name in a.configs.split(','):
-        ok &= run(name, CFGS[name], dev, a.threshold, not a.no_calibrate, a.layers, a.graph)
+        ok &= run(name, CFGS[name], dev, a.threshold, not a.no_calibrate, a.layers, a.graph, a.train_loop)
         torch.cuda.empty_cache()
     dist.destroy_process_group()
     sys.exit(0 if ok else 1)
