@@ -194,6 +194,13 @@ int ssseg_lovasz_fwd(const float* logits, const float* target, int64_t B, int64_
                      float* loss_out, void* ws, size_t ws_bytes, ssseg_stream_t stream);
 int ssseg_lovasz_bwd(const float* logits, const float* target, int64_t B, int64_t C, int64_t HW,
                      const float* gout, float* grad_out, void* ws, size_t ws_bytes, ssseg_stream_t stream);
+/* The backward of the immediately preceding ssseg_lovasz_fwd with the same logits, target and workspace (kept
+ * unchanged in between): the forward leaves the per-pixel Lovász gradient in sorted-rank terms and the per-image scale
+ * valid_b / denom in ws, so the backward is one scatter launch instead of a second sort (bitwise the same gradient as
+ * ssseg_lovasz_bwd). */
+int ssseg_lovasz_bwd_from_fwd(const float* logits, const float* target, int64_t B, int64_t C, int64_t HW,
+                              const float* gout, float* grad_out, const void* ws, size_t ws_bytes,
+                              ssseg_stream_t stream);
 
 /* RMILoss, sigmoid form (losses.RMILoss.forward -> forward_sigmoid -> rmi_lower_bound, losses.py:480-592; the
  * default-config loss, configs/default_config.py:147).  logits, target [N,C,H,W] f32 contiguous.

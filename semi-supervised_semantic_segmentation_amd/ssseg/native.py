@@ -52,6 +52,7 @@ SIGS = {
     'ssseg_lovasz_workspace_bytes': (sz, [i64, i64]),
     'ssseg_lovasz_fwd': (i32, [vp, vp, i64, i64, i64, vp, vp, sz, vp]),
     'ssseg_lovasz_bwd': (i32, [vp, vp, i64, i64, i64, vp, vp, vp, sz, vp]),
+    'ssseg_lovasz_bwd_from_fwd': (i32, [vp, vp, i64, i64, i64, vp, vp, vp, sz, vp]),
     'ssseg_rmi_workspace_bytes': (sz, [i64] * 9),
     'ssseg_rmi_fwd': (i32, [vp, vp] + [i64] * 9 + [i32, vp, vp, sz, vp]),
     'ssseg_rmi_bwd': (i32, [vp] + [i64] * 9 + [vp, vp, vp, sz, vp]),

@@ -280,6 +280,7 @@ class _Lovasz(torch.autograd.Function):
         N.call('ssseg_lovasz_fwd', N.dev_ptr(logits, 'logits'), N.dev_ptr(target, 'target'), B, C, HW,
                N.dev_ptr(out), N.dev_ptr(ws), nb, N.stream())
         ctx.save_for_backward(logits, target)
+        ctx.ws, ctx.nb = ws, nb   # the forward's per-pixel gradient and image scales: the backward does not re-sort
         return out
 
     @staticmethod
@@ -288,11 +289,10 @@ class _Lovasz(torch.autograd.Function):
         B, C = logits.shape[:2]
         HW = logits[0, 0].numel()
         gx = torch.empty_like(logits)
-        nb = N.lib().ssseg_lovasz_workspace_bytes(B, HW)
-        ws = N.workspace(nb, logits.device)
         g = _c(g.float())
-        N.call('ssseg_lovasz_bwd', N.dev_ptr(logits), N.dev_ptr(target), B, C, HW, N.dev_ptr(g), N.dev_ptr(gx),
-               N.dev_ptr(ws), nb, N.stream())
+        N.call('ssseg_lovasz_bwd_from_fwd', N.dev_ptr(logits), N.dev_ptr(target), B, C, HW, N.dev_ptr(g),
+               N.dev_ptr(gx), N.dev_ptr(ctx.ws), ctx.nb, N.stream())
+        ctx.ws = None
         return gx, None
 
 

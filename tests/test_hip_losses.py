@@ -244,6 +244,27 @@ def test_lovasz_vs_oracle(hip_device, B, H, W, empty):
     np.testing.assert_allclose(grad, ref_g * np.float32(0.7), rtol=1e-4, atol=2e-6)
 
 
+def test_lovasz_bwd_from_fwd_bitwise(hip_device):
+    """The autograd backward scatters the gradient the forward left in its workspace (ssseg_lovasz_bwd_from_fwd, no
+    second sort): bit-identical to the stand-alone backward that sorts again (ssseg_lovasz_bwd), ties included."""
+    from ssseg import native as N
+    rng = np.random.default_rng(3)
+    B, H, W = 3, 70, 66
+    x = rng.choice(np.array([-1, 0, 0.5, 1, 2, 0.25], np.float32), size=(B, 2, H, W))
+    fg = rng.random((B, 1, H, W)) > 0.5
+    t = np.concatenate([~fg, fg], 1).astype(np.float32)
+    _, grad = _lovasz_hip(x, t, hip_device, gscale=0.3)
+    xt, tt = torch.from_numpy(x).to(hip_device), torch.from_numpy(t).to(hip_device)
+    gx = torch.empty_like(xt)
+    go = torch.full((), 0.3, device=hip_device)
+    nb = N.lib().ssseg_lovasz_workspace_bytes(B, H * W)
+    ws = N.workspace(nb, hip_device)
+    N.call('ssseg_lovasz_bwd', N.dev_ptr(xt), N.dev_ptr(tt), B, 2, H * W, N.dev_ptr(go), N.dev_ptr(gx), N.dev_ptr(ws),
+           nb, N.stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(grad, gx.cpu().numpy())
+
+
 def test_lovasz_ties_loss_invariant(hip_device):
     """Heavily tied errors (logits on a 5-value grid): the per-pixel gradient inside a tie depends on the
     sort's tie order (the reference's torch.sort is unstable), the loss and the per-image gradient sums
