@@ -209,7 +209,9 @@ int ssseg_lovasz_bwd_from_fwd(const float* logits, const float* target, int64_t 
  * Forward: loss_out[0] = sum_k float(mean over rows of rmi.view(-1, num_classes)[:, k]) / D, rmi per (n, c) from
  * fp64 centred covariances, inverse and Cholesky log-det.  want_grad != 0 also leaves the backward coefficients in
  * ws; ssseg_rmi_bwd (same ws, same geometry) then writes grad_out [N,C,H,W] = gout[0] * d loss / d logits.
- * A non-positive-definite matrix gives a NaN loss (the reference's torch.cholesky raises).  Workspace 0 = the
+ * A non-positive-definite matrix gives a NaN loss (the reference's torch.cholesky raises); the +5e-4*I of
+ * losses.py:283,553-563 makes every covariance PD in exact arithmetic, so only degenerate fp64 input reaches it, and a
+ * NaN loss is visible to the caller (the fp16 loss scaler then skips the step).  Workspace 0 = the
  * geometry is not supported. */
 size_t ssseg_rmi_workspace_bytes(int64_t N, int64_t C, int64_t H, int64_t W, int64_t num_classes, int64_t radius,
                                  int64_t pool_k, int64_t pool_s, int64_t pool_pad);

@@ -231,7 +231,11 @@ def vpad(c):
     activation keeps its physical pixel stride c, so a 16-byte chunk past channel c reads the next pixel's first
     channels (finite data times zero weights; past the end of the buffer the bounded LDS-DMA reads return 0).
     The engine then refuses its register-staged kernels (plain loads) for such a launch.  Measured (tools/conv_ab.py,
-    16x256^2): 480->240 3x3 fwd 3.13 -> 2.2 ms, fwd+bwd 12.1 -> 6.7-8.3 ms."""
+    16x256^2): 480->240 3x3 fwd 3.13 -> 2.2 ms, fwd+bwd 12.1 -> 6.7-8.3 ms.
+    Caveat: a neighbouring pixel holding Inf/NaN couples in as 0 * Inf = NaN (IEEE), where the unpadded contraction
+    would keep the other outputs finite.  The reference has no such coupling, but in every path that uses vpad an Inf
+    activation already makes the step's loss non-finite (and the fp16 loss scaler skips the step), so no finite
+    result changes; set_virtual_pad(False) gives the strictly per-pixel contraction."""
     if not _CFG['vpad'] or _CFG['dtype'] == torch.float32 or c % 64 == 0:
         return c
     p = rup(c, 64)
