@@ -595,6 +595,27 @@ int ssseg_nhwc_copy(const void* src, void* dst, int64_t N, int64_t H, int64_t W,
                     int64_t sld, int64_t soy, int64_t sox, int64_t dH, int64_t dW, int64_t dld, int64_t doy, int64_t dox,
                     int dt, ssseg_stream_t stream);
 int ssseg_zero(void* p, size_t bytes, ssseg_stream_t stream);
+
+/* One operand of an n-way channel concat of same-size NHWC maps (torch.cat(tensors, 1): HarDNet's harmonic links and
+ * block outputs hardnet.py:67,78, TransitionUp hardnet.py:95; discriminator.py:56).  The concat packs the operands'
+ * REAL channel counts back to back. */
+typedef struct {
+  const void* src;   /* ssseg_nhwc_cat_n: operand [npix][ld] (16-bit or fp32 like the concat) */
+  void* dst;         /* ssseg_nhwc_split_n: operand gradient [npix][ld], 16-byte aligned */
+  const void* add;   /* ssseg_nhwc_split_n: NULL, or a pending gradient of the operand (dst's layout) added in the
+                        same pass (fp32 sum, one rounding: PyTorch's add of the two) */
+  int64_t ld;        /* the operand's pixel stride (physical channels); split: a multiple of 16 bytes */
+  int64_t c;         /* real channels, 0 <= c <= ld */
+} ssseg_cat_part;
+/* y[p][0..ldy) = parts' first c channels back to back, channels sum(c)..ldy-1 written zero: one launch for up to 16
+ * operands (no separate zero fill).  y 16-byte aligned, ldy a multiple of 16 bytes, npix = N*H*W. */
+int ssseg_nhwc_cat_n(const ssseg_cat_part* parts_host, int64_t nparts, void* y, int64_t npix, int64_t ldy, int dt,
+                     ssseg_stream_t stream);
+/* the concat's backward, one launch: parts[k].dst[p][j] = gy[p][c0_k + j] (+ parts[k].add[p][j]) for j < c_k and 0
+ * for c_k <= j < ld_k, with c0_k = c_0 + ... + c_(k-1); gy [npix][ldg]. */
+int ssseg_nhwc_split_n(const void* gy, int64_t ldg, const ssseg_cat_part* parts_host, int64_t nparts, int64_t npix,
+                       int dt, ssseg_stream_t stream);
+
 /* gx = gy * [y > 0]  (ReLU backward from the saved output; ConvTranspose2d+ReLU upsampler unet.py:21-22) */
 /* gx = gy * d act / d z evaluated from the activation output y (SSSEG_ACT_*; the cut gradient is selected
  * to 0, not multiplied, like PyTorch's threshold_backward) */

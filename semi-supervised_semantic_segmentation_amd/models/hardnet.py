@@ -3,9 +3,9 @@
 state_dicts load strictly.
 
 Forward on the ssseg kernels: ConvLayer = conv -> BN -> ReLU as one `conv_bn_act` (folded into the conv
-epilogue for eval BN); the harmonic-dense links and the up-path concatenations are `cat_n` (one NHWC copy per
-operand, real channel counts packed densely — HarDNet's widths are even but not multiples of the MFMA
-vector); AvgPool2d(2, 2) and the align_corners=True bilinear resizes run on their own kernels.  The output is
+epilogue for eval BN); the harmonic-dense links and the up-path concatenations are `cat_n` (one gather launch per
+concat, real channel counts packed densely — HarDNet's widths are even but not multiples of the MFMA vector; the
+backward is one split launch that also sums the gradients of layer outputs read by several consumers); AvgPool2d(2, 2) and the align_corners=True bilinear resizes run on their own kernels.  The output is
 fp32 NCHW logits at the input resolution (hardnet.py:207-212).
 """
 import torch.nn as nn
@@ -69,11 +69,13 @@ class HarDBlock(nn.Module):
         self.layers = nn.ModuleList(layers_)
 
     def forward(self, x):
-        layers_ = [x]
+        # every layer output feeds the next layer and up to three later link concats (+ the block's output concat):
+        # their input gradients are summed inside the consumers' kernels (snn.GradJoin), not by separate adds
+        layers_ = [snn.mark_join(x)]
         for layer in range(len(self.layers)):
             link = self.links[layer]
             x = snn.cat_n([layers_[i] for i in link], [self.layer_channels[i] for i in link])
-            layers_.append(self.layers[layer](x))
+            layers_.append(snn.mark_join(self.layers[layer](x)))
         t = len(layers_)
         keep = [i for i in range(t) if (i == 0 and self.keepBase) or (i == t - 1) or (i % 2 == 1)]
         return snn.cat_n([layers_[i] for i in keep], [self.layer_channels[i] for i in keep])

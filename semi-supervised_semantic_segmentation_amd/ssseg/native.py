@@ -21,6 +21,16 @@ vp, i64, i32, f32, f64, sz, u64 = (ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
                                    ctypes.c_size_t, ctypes.c_uint64)
 I64P = ctypes.POINTER(ctypes.c_int64)
 
+class CatPart(ctypes.Structure):
+    """ssseg_cat_part (include/ssseg.h): one operand of ssseg_nhwc_cat_n / ssseg_nhwc_split_n"""
+    _fields_ = [('src', vp), ('dst', vp), ('add', vp), ('ld', i64), ('c', i64)]
+
+
+def cat_parts(rows):
+    """host table of (src, dst, add, ld, c) rows for the concat entry points (kept alive by the caller)"""
+    return (CatPart * len(rows))(*[CatPart(*r) for r in rows])
+
+
 # name -> (restype, argtypes); every entry must match include/ssseg.h
 SIGS = {
     'ssseg_version': (ctypes.c_char_p, []),
@@ -121,6 +131,8 @@ SIGS = {
     'ssseg_maxpool_bwd_res': (i32, [vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, i32, vp]),
     'ssseg_nhwc_copy': (i32, [vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64, i32, vp]),
     'ssseg_zero': (i32, [vp, sz, vp]),
+    'ssseg_nhwc_cat_n': (i32, [vp, i64, vp, i64, i64, i32, vp]),
+    'ssseg_nhwc_split_n': (i32, [vp, i64, vp, i64, i64, i32, vp]),
     'ssseg_act_bwd': (i32, [vp, vp, vp, i64, i32, f32, i32, vp]),
     'ssseg_relu_bwd': (i32, [vp, vp, vp, i64, i32, vp]),
     # pooling / elementwise primitives of the C3-C5 model families (csrc/pool.hip)

@@ -11,6 +11,7 @@ a registered reducer (ssseg.ddp) is told when each parameter's gradient is compl
 all-reduce of its bucket can start during the rest of the backward pass.
 """
 import contextlib
+import ctypes
 import os
 
 import torch
@@ -1730,37 +1731,56 @@ def invalidate_packed(model):
 class _CatNFn(torch.autograd.Function):
     """torch.cat(tensors, 1) of same-size NHWC activations with REAL channel counts `chans` (hardnet.py:67,78,
     95; higher_hrnet.py:1033; discriminator.py:56): the result packs the real channels densely, padding to the
-    MFMA vector is zero.  Backward slices the gradient back out (zero padding in every slice)."""
+    MFMA vector is zero.  One ssseg_nhwc_cat_n launch (the padding written in the same pass); the backward is one
+    ssseg_nhwc_split_n launch that writes every operand's gradient (zero padding) and adds the pending gradient of
+    operands whose consumers share a GradJoin (HarDNet's layer outputs feed up to four concats and a conv)."""
 
     @staticmethod
-    def forward(ctx, chans, *ts):
+    def forward(ctx, chans, joins, *ts):
         n, _, H, W = ts[0].shape
         for t in ts:
             if t.shape[0] != n or t.shape[2] != H or t.shape[3] != W:
                 raise ValueError(f'cat_n: spatial shapes differ: {[tuple(t.shape) for t in ts]}')
-        total = sum(chans)
-        cp = rup(total, vec())
-        y = new_act(n, cp, H, W, ts[0].dtype, ts[0].device, zero=cp != total)
-        c0 = 0
-        for t, c in zip(ts, chans):
-            N.call('ssseg_nhwc_copy', N.dev_ptr(t), N.dev_ptr(y) + c0 * y.element_size(), n, H, W, c, H, W, t.shape[1],
-                   0, 0, H, W, cp, 0, 0, N.dt_code(t), N.stream())
-            c0 += c
+            if t.stride(1) != 1 or t.dtype != ts[0].dtype:
+                raise ValueError('cat_n: operands must be NHWC activations of one dtype')
+        if len(ts) > 16:
+            raise ValueError('cat_n: more than 16 operands')
+        cp = rup(sum(chans), vec())
+        y = new_act(n, cp, H, W, ts[0].dtype, ts[0].device)
+        tab = N.cat_parts([(N.dev_ptr(t), None, None, t.shape[1], c) for t, c in zip(ts, chans)])
+        N.call('ssseg_nhwc_cat_n', ctypes.addressof(tab), len(ts), N.dev_ptr(y), n * H * W, cp, N.dt_code(y),
+               N.stream())
         ctx.meta = (tuple(t.shape[1] for t in ts), tuple(chans), cp)
+        ctx.joins = joins
         return y
 
     @staticmethod
     def backward(ctx, gy):
         phys, chans, cp = ctx.meta
         n, _, H, W = gy.shape
-        out, c0 = [None], 0
-        for pc, c in zip(phys, chans):
-            g = new_act(n, pc, H, W, gy.dtype, gy.device, zero=pc != c)
-            N.call('ssseg_nhwc_copy', N.dev_ptr(gy) + c0 * gy.element_size(), N.dev_ptr(g), n, H, W, c, H, W, cp, 0, 0,
-                   H, W, pc, 0, 0, N.dt_code(gy), N.stream())
-            out.append(g)
-            c0 += c
-        return tuple(out)
+        if not _is_act(gy, cp):
+            gy = gy.contiguous(memory_format=torch.channels_last)
+        gs, rows, takes = [], [], []
+        for k, (pc, c) in enumerate(zip(phys, chans)):
+            j = ctx.joins[k] if ctx.joins is not None else None
+            pending, last = _join_take(j)
+            g = new_act(n, pc, H, W, gy.dtype, gy.device)
+            late = None
+            if pending is not None and (pending.shape != g.shape or pending.stride() != g.stride()
+                                        or pending.dtype != g.dtype):
+                pending, late = None, pending    # (not in the concat's layout: added after the split)
+            gs.append(g)
+            takes.append((j, last, late, pending))
+            rows.append((None, N.dev_ptr(g), N.dev_ptr(pending) if pending is not None else None, pc, c))
+        tab = N.cat_parts(rows)
+        N.call('ssseg_nhwc_split_n', N.dev_ptr(gy), cp, ctypes.addressof(tab), len(rows), n * H * W, N.dt_code(gy),
+               N.stream())
+        out = []
+        for (j, last, late, _), g in zip(takes, gs):
+            if late is not None:
+                g = g + late
+            out.append(_join_give(j, last, g))
+        return (None, None) + tuple(out)
 
 
 class _ResizeCatFn(torch.autograd.Function):
@@ -1834,7 +1854,12 @@ def cat_n(tensors, chans):
         _need_act(t, None, 'cat_n')
     if len(tensors) == 1:
         return tensors[0]
-    return _CatNFn.apply(tuple(int(c) for c in chans), *tensors)
+    joins = None
+    if torch.is_grad_enabled() and len({id(t) for t in tensors}) == len(tensors):
+        joins = tuple(_join_fwd(t) for t in tensors)
+        if all(j is None for j in joins):
+            joins = None
+    return _CatNFn.apply(tuple(int(c) for c in chans), joins, *tensors)
 
 
 class _AvgPoolFn(torch.autograd.Function):
