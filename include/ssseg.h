@@ -320,6 +320,14 @@ typedef struct ssseg_conv_epilogue {
 } ssseg_conv_epilogue;
 int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const ssseg_conv_desc* desc_host, int dt, int dt_out,
                          const ssseg_conv_epilogue* epi, void* ws, size_t ws_bytes, ssseg_stream_t stream);
+/* ssseg_conv_igemm_epi for an input gradient whose input was the forward output y of an activation (act =
+ * SSSEG_ACT_RELU or SSSEG_ACT_LEAKY with its slope; the discriminator's Conv4x4 + LeakyReLU(0.2) pairs,
+ * discriminator.py:14-17): epi->residual is that y (not an addend), and the stored value is the activation's backward
+ * applied in place, (y > 0 ? v : v * slope) -- the producer's separate activation-backward pass is not needed.
+ * epi carries no scale / shift / activation / statistics / aux. */
+int ssseg_conv_igemm_epi_actmask(const void* x, const void* w, void* y, const ssseg_conv_desc* desc_host, int dt,
+                                 int dt_out, const ssseg_conv_epilogue* epi, int act, float slope, void* ws,
+                                 size_t ws_bytes, ssseg_stream_t stream);
 /* Virtual channel concat of a conv input (reference models/unet.py:44-45, torch.cat((x, skip), 1) feeding
  * UpBlock.conv3_0): input channels [0, c1) are read from x (pixel stride desc.ldx) and [c1, desc.C) from x2
  * (pixel stride ldx2, channel 0 of x2 = input channel c1); same N x H x W.  c1 and C - c1 are multiples of 64
@@ -372,8 +380,9 @@ int ssseg_conv_igemm_phases_ws(const void* x, void* y, const ssseg_conv_desc* de
 int ssseg_conv_stem_epi(const void* x, const void* w4, void* y, const ssseg_conv_desc* desc_host, int dt,
                         const ssseg_conv_epilogue* epi, ssseg_stream_t stream);
 /* Workspace for ssseg_conv_igemm(_epi / _vcat / _vsplit): non-zero when the 16-bit launch splits K across workgroups
- * (deterministic split-K: fewer than 512 nominal 128 x 64 output tiles and >= 32 64-deep k-tiles -- ResNet layer3/4
- * at 32x32 / 16x16; S = 2, 4 or 8 k-slices chosen from the geometry alone, knob 14).  Each slice writes fp32 partials,
+ * (deterministic split-K, S chosen from the geometry alone, knob 14: fewer than 512 nominal 128 x 64 output tiles and
+ * >= 64 64-deep k-tiles -- ResNet layer3/4 at 32x32 / 16x16, S = 2 or 4 -- or fewer than 256 tiles and >= 8 k-tiles --
+ * HarDNet's growth layers at 8x8 - 32x32, the largest S of 8 / 4 / 2 with <= 512 blocks and >= 4 k-tiles a slice).  Each slice writes fp32 partials,
  * the last-arriving slice of a tile (an agent-scope ticket) sums the S partials in slice order and runs the full fused
  * epilogue (affine, residual, activation, raw copy, BN statistics): the result is bitwise reproducible and identical
  * for every tile config.  The workspace is caller-owned scratch (no contents carried between calls); passing none

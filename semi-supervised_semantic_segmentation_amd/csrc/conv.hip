@@ -243,8 +243,15 @@ static int dsplit_plan(const ConvGeom& g, int nph) {
   const int nk = (g.C % 64 == 0) ? g.R * g.S * (g.C / 64) : (g.KK + 63) / 64;
   if (kn > 0) return (kn == 2 || kn == 4 || kn == 8) && nk >= kn ? kn : 1;
   const long long t = (long long)nph * ((g.M + 127) / 128) * ((g.K + 63) / 64);
-  if (t >= 512 || nk < 64) return 1;
-  return (t < 128 && nk >= 128) ? 4 : 2;
+  if (t < 512 && nk >= 64) return (t < 128 && nk >= 128) ? 4 : 2;
+  // few tiles over a moderate contraction (HarDNet's growth layers at 8^2-32^2: 16-128 tiles, 8-63 k-tiles): the
+  // largest S with at most 512 blocks and at least 4 k-tiles per slice
+  if (t < 256 && nk >= 8) {
+    int S = 8;
+    while (S > 1 && (t * S > 512 || nk < 4 * S)) S >>= 1;
+    return S;
+  }
+  return 1;
 }
 
 // x2: second source of a virtual concat input (LDS-DMA configs only: the register-staged kernel returns -1)
@@ -362,7 +369,7 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
       if (v == 0) {
         const unsigned long long key =
             geom_key(g, (int)sizeof(TO) * 8 + (ep.stats ? 4 : 0) + (ep.res ? 2 : 0) + (ep.scale ? 1 : 0) + 16 * S +
-                        256 * nph + (x2 ? 4096 * (g.c1b + 1) : 0) + (ep.y2 ? (1 << 24) : 0));
+                        256 * nph + (x2 ? 4096 * (g.c1b + 1) : 0) + (ep.y2 ? (1 << 24) : 0) + (ep.rmask ? (1 << 25) : 0));
         std::lock_guard<std::mutex> lk(g_variant_mu);
         auto it = g_variant.find(key);
         if (it != g_variant.end()) {
@@ -439,7 +446,8 @@ extern "C" size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* d, int
 
 static int conv_igemm_epi(const void* x, const void* x2, int64_t c1, int64_t ldx2, const void* w, void* y,
                           const ssseg_conv_desc* d, int dt, int dt_out, const ssseg_conv_epilogue* epi, void* ws,
-                          size_t ws_bytes, ssseg_stream_t stream, const ssseg_vcat* ysplit = nullptr) {
+                          size_t ws_bytes, ssseg_stream_t stream, const ssseg_vcat* ysplit = nullptr,
+                          int mask_act = 0, float mask_slope = 0.f) {
   ConvGeom g;
   if (!make_geom(d, g) || !y) return SSSEG_EINVAL;
   if (!geom_ok(g, dt)) return SSSEG_EINVAL;
@@ -461,12 +469,19 @@ static int conv_igemm_epi(const void* x, const void* x2, int64_t c1, int64_t ldx
   if (g.M == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   if (e.relu < 0 || e.relu > SSSEG_ACT_LEAKY) return SSSEG_EINVAL;
-  const Epi<float> ef{e.scale, e.shift, (const float*)e.residual, (int)e.ldr, e.relu, (float*)e.aux, e.slope,
-                      e.stats, (int)e.stats_ld};
+  Epi<float> ef{e.scale, e.shift, (const float*)e.residual, (int)e.ldr, e.relu, (float*)e.aux, e.slope,
+                e.stats, (int)e.stats_ld};
   Epi<bf16_t> eb{e.scale, e.shift, (const bf16_t*)e.residual, (int)e.ldr, e.relu, (bf16_t*)e.aux, e.slope,
                  e.stats, (int)e.stats_ld};
   Epi<f16_t> eh{e.scale, e.shift, (const f16_t*)e.residual, (int)e.ldr, e.relu, (f16_t*)e.aux, e.slope,
                 e.stats, (int)e.stats_ld};
+  if (mask_act) {   // the residual is the input's producer's activation output: its backward applied in place
+    if (ysplit || x2 || !e.residual || e.stats || e.aux || e.relu || e.scale || e.shift ||
+        (mask_act != SSSEG_ACT_RELU && mask_act != SSSEG_ACT_LEAKY))
+      return SSSEG_EINVAL;
+    ef.rmask = eb.rmask = eh.rmask = mask_act;
+    ef.rslope = eb.rslope = eh.rslope = mask_slope;
+  }
   if (ysplit) {   // split output: channels [c1, K) to ysplit->x2 (pixel stride ldx2); 16-bit, plain epilogue
     const int64_t oc1 = ysplit->c1, ld2 = ysplit->ldx2;
     if (!ysplit->x2 || oc1 <= 0 || oc1 >= g.K || oc1 % 8 || g.ldy < oc1 || g.ldy % 8 || ld2 < g.K - oc1 || ld2 % 8 ||
@@ -537,6 +552,13 @@ static int conv_igemm_epi(const void* x, const void* x2, int64_t c1, int64_t ldx
 extern "C" int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const ssseg_conv_desc* d, int dt, int dt_out,
                                     const ssseg_conv_epilogue* epi, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
   return conv_igemm_epi(x, nullptr, 0, 0, w, y, d, dt, dt_out, epi, ws, ws_bytes, stream);
+}
+
+extern "C" int ssseg_conv_igemm_epi_actmask(const void* x, const void* w, void* y, const ssseg_conv_desc* d, int dt,
+                                            int dt_out, const ssseg_conv_epilogue* epi, int act, float slope, void* ws,
+                                            size_t ws_bytes, ssseg_stream_t stream) {
+  if (act != SSSEG_ACT_RELU && act != SSSEG_ACT_LEAKY) return SSSEG_EINVAL;
+  return conv_igemm_epi(x, nullptr, 0, 0, w, y, d, dt, dt_out, epi, ws, ws_bytes, stream, nullptr, act, slope);
 }
 
 extern "C" int ssseg_conv_igemm_epi_vcat(const void* x, const ssseg_vcat* vc, const void* w, void* y,

@@ -183,9 +183,11 @@ struct Epi {
   TO* y2 = nullptr;
   int oc1 = 0x40000000;
   int ldy2 = 0;
-  // rmask (split outputs only): res is not added but is the forward output of the first part's producer, whose
-  // ReLU backward is applied in place: channels [0, oc1) are stored as (res > 0 ? v : 0), channels >= oc1 read no res
+  // rmask (SSSEG_ACT_RELU / SSSEG_ACT_LEAKY): res is not added but is the forward output of the input's producer (of the
+  // first part's, for a split output), whose activation backward is applied in place: channels [0, oc1) are stored as
+  // (res > 0 ? v : 0) or (res > 0 ? v : v * rslope), channels >= oc1 read no res
   int rmask = 0;
+  float rslope = 0.f;   // rmask == SSSEG_ACT_LEAKY: (res > 0 ? v : v * rslope) (the producer's LeakyReLU backward)
   int sdbg = 0;   // experiment switch for the fused statistics (knob 12): 1 no sums, 2 no tile_stats, 4 no row write,
                   // 8 no cross-lane shuffles
 };
@@ -345,7 +347,7 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[FN][FM], long long
         if (ep.shift) a += sh[e];
         if (!ep.rmask) a += r[j][e];
         a = act_fwd(a, ep.relu, ep.slope);
-        if (ep.rmask && n < ep.oc1 && !(r[j][e] > 0.f)) a = 0.f;
+        if (ep.rmask && n < ep.oc1 && !(r[j][e] > 0.f)) a = ep.rmask == SSSEG_ACT_LEAKY ? a * ep.rslope : 0.f;
         v[e] = a;
         if constexpr (ST) {   // compile-time: the statistics arrays stay in registers
           if (n + e < g.K) {
@@ -597,9 +599,11 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = raw[e] * sc[e] + sh[e];
         act8(v, ep.relu, ep.slope);
-        if (n < ep.oc1)
+        if (n < ep.oc1) {
+          const float ms = ep.rmask == SSSEG_ACT_LEAKY ? ep.rslope : 0.f;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = r[p][e] > 0.f ? v[e] : 0.f;
+          for (int e = 0; e < 8; ++e) v[e] = r[p][e] > 0.f ? v[e] : v[e] * ms;
+        }
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = raw[e] * sc[e] + sh[e] + r[p][e];   // scale 1 / shift 0 when absent
@@ -1313,7 +1317,7 @@ __global__ void splitk_finalize_kernel(const float* __restrict__ ws, TO* __restr
     const float r = (ep.res && n < ep.oc1) ? io<TO>::ld(ep.res, op * ep.ldr + n) : 0.f;
     if (!ep.rmask) v += r;
     v = act_fwd(v, ep.relu, ep.slope);
-    if (ep.rmask && n < ep.oc1 && !(r > 0.f)) v = 0.f;
+    if (ep.rmask && n < ep.oc1 && !(r > 0.f)) v = ep.rmask == SSSEG_ACT_LEAKY ? v * ep.rslope : 0.f;
     io<TO>::st(out_at(ep, y, g.ldy, op, n), 0, v);
   }
 }
@@ -1329,11 +1333,11 @@ __global__ void phase_zero_vec_kernel(TO* y, ConvGeom g, Epi<TO> ep) {
     const long long m = i / kc;
     const long long op = out_pixel(g, (int)m);   // M < 2^31 (geom_ok)
     float r[8], v[8];
-    if (ep.res) Out8<TO>::ld(ep.res + op * ep.ldr + n, r);
+    if (ep.res && !ep.rmask) Out8<TO>::ld(ep.res + op * ep.ldr + n, r);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float t = ep.shift ? ep.shift[n + e] : 0.f;
-      if (ep.res) t += r[e];
+      if (ep.res && !ep.rmask) t += r[e];
       v[e] = act_fwd(t, ep.relu, ep.slope);
     }
     if (ep.aux) {
@@ -1353,7 +1357,7 @@ __global__ void phase_zero_kernel(TO* y, ConvGeom g, Epi<TO> ep) {
     const long long op = out_pixel(g, (int)m);   // M < 2^31 (geom_ok)
     float v = ep.shift ? ep.shift[n] : 0.f;
     if (ep.aux) io<TO>::st(ep.aux, op * g.ldy + n, 0.f);
-    if (ep.res) v += io<TO>::ld(ep.res, op * ep.ldr + n);
+    if (ep.res && !ep.rmask) v += io<TO>::ld(ep.res, op * ep.ldr + n);
     v = act_fwd(v, ep.relu, ep.slope);
     io<TO>::st(out_at(ep, y, g.ldy, op, n), 0, v);
   }

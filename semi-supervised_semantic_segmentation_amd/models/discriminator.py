@@ -36,7 +36,8 @@ class Discriminator(nn.Module):
         x = snn.to_act(input)
         for block in self.net:
             conv = block[0]
-            x = conv.forward_act(x, LEAKY) if len(block) > 1 else conv(x)
+            # each LeakyReLU output feeds only the next conv: its backward runs inside that conv's input gradient
+            x = conv.forward_act(x, LEAKY, single_use=True) if len(block) > 1 else conv(x)
         return x
 
 

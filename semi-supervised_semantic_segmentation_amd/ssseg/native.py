@@ -84,6 +84,7 @@ SIGS = {
     'ssseg_conv_igemm_phases_workspace_bytes': (sz, [vp, i64, i32]),
     'ssseg_conv_stem_epi': (i32, [vp, vp, vp, vp, i32, vp, vp]),
     'ssseg_conv_igemm_epi': (i32, [vp, vp, vp, vp, i32, i32, vp, vp, sz, vp]),
+    'ssseg_conv_igemm_epi_actmask': (i32, [vp, vp, vp, vp, i32, i32, vp, i32, f32, vp, sz, vp]),
     'ssseg_weight_pack_batch': (i32, [vp, i64, i32, vp]),
     'ssseg_dwconv_fwd': (i32, [vp, vp, vp, vp, i32, vp, vp]),
     'ssseg_dwconv_dgrad': (i32, [vp, vp, vp, vp, i32, vp]),

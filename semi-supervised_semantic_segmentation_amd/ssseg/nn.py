@@ -20,7 +20,8 @@ import torch.nn as nn
 
 from . import native as N
 
-_CFG = {'grad_join': True, 'stem': True, 'phases': True, 'eval_bwd_y': True, 'dtype': torch.bfloat16, 'sync_bn': True,
+_CFG = {'act_mask': os.environ.get('SSSEG_ACT_MASK', '1') != '0',
+        'grad_join': True, 'stem': True, 'phases': True, 'eval_bwd_y': True, 'dtype': torch.bfloat16, 'sync_bn': True,
         'fuse_stats': True, 'vcat': os.environ.get('SSSEG_VCAT', '1') != '0',
         'vpad': os.environ.get('SSSEG_VPAD', '1') != '0'}
 
@@ -530,6 +531,7 @@ class _ConvFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, mod, relu, handoff=None, stats=None, join=None):
         y = mod._ssseg_forward(x, relu, stats=stats)
         ctx.mod, ctx.relu, ctx.handoff, ctx.join, ctx.vcat = mod, relu, handoff, join, _vcat_of(x)
+        ctx.xmask = x.__dict__.get('_ssseg_act_out')   # x = a single-use activation output: mask in our dgrad
         ctx.save_for_backward(x, y if _act(relu)[0] else None)
         if _act(relu)[0] == ACT_RELU:
             # a ReLU output: a consumer's input-gradient launch may apply this ReLU's backward in place (the
@@ -556,6 +558,10 @@ class _ConvFn(torch.autograd.Function):
         pending = _sum_pending(_take(ctx.handoff), joined)
         if not ctx.needs_input_grad[0]:
             dx = None
+        elif (ctx.xmask is not None and pending is None and ctx.vcat is None and _CFG['act_mask']
+              and getattr(mod, '_ssseg_mask_dgrad_ok', lambda: False)()):
+            dx = mod._ssseg_dgrad(gy, x.shape, mask=(x,) + tuple(ctx.xmask))
+            dx.__dict__['_ssseg_premasked'] = True
         else:
             dx = _dgrad_acc(mod, gy, x.shape, pending, ctx.vcat)
         return _join_give(ctx.join, last, dx), None, None, None, None, None, None, None
@@ -650,7 +656,7 @@ class _ConvBase:
             _PACK_EPOCH[0] += 1
         return t
 
-    def _igemm(self, x, w, y, desc, out_dt, bias=None, relu=False, fold=None, stats=None, stem=False):
+    def _igemm(self, x, w, y, desc, out_dt, bias=None, relu=False, fold=None, stats=None, stem=False, mask=None):
         """One engine launch; epilogue y = act(acc*scale + shift + residual) with shift = bias, or
         fold = (scale, shift, residual, aux) from a folded eval BatchNorm (conv_bn_act); aux, when given,
         receives the raw accumulator (the pre-BN activation the differentiated eval pass needs).
@@ -659,13 +665,21 @@ class _ConvBase:
         nb = N.lib().ssseg_conv_igemm_workspace_bytes(dref, N.dt_code(x)) if (w is not None and not stem) else 0
         ws = N.workspace(nb, x.device) if nb else None
         scale, shift, res, aux = fold if fold is not None else (None, bias, None, None)
+        if mask is not None:
+            res = mask[0]
         sf = stats.launch_fields() if stats is not None else (None, 0, None)
         ep = N.ConvEpilogue(N.dev_ptr(scale) if scale is not None else None,
                             N.dev_ptr(shift) if shift is not None else None,
                             N.dev_ptr(res) if res is not None else None, res.shape[1] if res is not None else 0,
                             N.dev_ptr(aux) if aux is not None else None, *_act(relu), *sf)
         vc = _vcat_of(x)
-        if stem:
+        if mask is not None:
+            if vc is not None:
+                materialize(x)
+            N.call('ssseg_conv_igemm_epi_actmask', N.dev_ptr(x), N.dev_ptr(w) if w is not None else None,
+                   N.dev_ptr(y), dref, N.dt_code(x), out_dt, ctypes_ref(ep), int(mask[1]), float(mask[2]),
+                   N.dev_ptr(ws) if ws is not None else None, nb, N.stream())
+        elif stem:
             N.call('ssseg_conv_stem_epi', N.dev_ptr(x), N.dev_ptr(w), N.dev_ptr(y), dref, N.dt_code(x),
                    ctypes_ref(ep), N.stream())
         elif vc is not None and vc.ready(desc) and N.call_or_unsupported(
@@ -761,12 +775,18 @@ class Conv2d(nn.Conv2d, _ConvBase):
         """Conv2d followed by ReLU, fused into the GEMM epilogue (unet.py:27-28 with no norm)."""
         return self.forward_act(x, True)
 
-    def forward_act(self, x, act):
+    def forward_act(self, x, act, single_use=False):
         """Conv2d followed by an activation (True = ReLU, ACT_RELU6, ('leaky', slope)) in the epilogue
-        (discriminator.py:15-16 Conv + LeakyReLU(0.2))."""
+        (discriminator.py:15-16 Conv + LeakyReLU(0.2)).  single_use: the caller guarantees the output feeds exactly
+        one ssseg conv, whose input-gradient launch then applies this activation's backward in place
+        (ssseg_conv_igemm_epi_actmask) instead of a separate pass here."""
         if not _is_act(x):
             x = to_act(x)
-        return _ConvFn.apply(x, self.weight, self.bias, self, act, None, None, _join_fwd(x))
+        y = _ConvFn.apply(x, self.weight, self.bias, self, act, None, None, _join_fwd(x))
+        code, slope = _act(act)
+        if single_use and code in (ACT_RELU, ACT_LEAKY) and torch.is_grad_enabled() and y.requires_grad:
+            y.__dict__['_ssseg_act_out'] = (code, slope)
+        return y
 
     # ---- depthwise (groups == channels): ssseg_dwconv_* (MobileNetV2, mobilenetv2.py:58) ----
     def _dw_desc(self, n, H, W):
@@ -932,8 +952,12 @@ class Conv2d(nn.Conv2d, _ConvBase):
         else:
             _ready(self.weight)
 
-    def _ssseg_dgrad(self, gy, xshape, residual=None):
-        """dx of the conv; `residual` (a pending gradient of x, GradHandoff) is added in the epilogue."""
+    def _ssseg_mask_dgrad_ok(self):
+        return not self._ssseg_dw and _CFG['dtype'] in (torch.bfloat16, torch.float16, torch.float32)
+
+    def _ssseg_dgrad(self, gy, xshape, residual=None, mask=None):
+        """dx of the conv; `residual` (a pending gradient of x, GradHandoff) is added in the epilogue; `mask` = (y,
+        act, slope): x was the activation output y of its producer, whose backward the epilogue applies in place."""
         cin, cout = self._dims()
         n, _, H, W = xshape
         (R, S), (sh, sw), (ph, pw), (dh, dw) = self.kernel_size, self.stride, self.padding, self.dilation
@@ -958,7 +982,7 @@ class Conv2d(nn.Conv2d, _ConvBase):
                       ldy=cin, ldw=R * S * ce)
             with timer:
                 self._igemm(gy, w, dx, d, N.dt_code(dx),
-                            fold=(None, None, residual, None) if residual is not None else None)
+                            fold=(None, None, residual, None) if residual is not None else None, mask=mask)
             return dx
         timer.__enter__()
         for (phy, ry0, rny, dly, qy) in _phases(sh, ph, R, H, dh):
@@ -974,7 +998,7 @@ class Conv2d(nn.Conv2d, _ConvBase):
                 # each phase adds the pending gradient at its own output pixels (the residual is indexed by
                 # the output pixel, so the phases together cover it exactly once)
                 self._igemm(gy, w, dx, d, N.dt_code(dx),
-                            fold=(None, None, residual, None) if residual is not None else None)
+                            fold=(None, None, residual, None) if residual is not None else None, mask=mask)
         timer.__exit__()
         return dx
 

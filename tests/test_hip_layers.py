@@ -950,3 +950,76 @@ def test_wgrad_merged_two_passes(hip_device, mode, kind, cin, cout, k, s, H, n1,
     _close(w_s, ref_w, mode, 'separate dW')
     scale = float(w_s.abs().max())
     assert float((w_m - w_s).abs().max()) <= 1e-5 * scale + 1e-7, 'merged vs separate launches'
+
+
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize('cin,cout,H,n', [(176, 28, 16, 2), (133, 14, 32, 1), (78, 34, 8, 16), (512, 64, 4, 2)])
+def test_conv_split_k_small_maps(hip_device, dtype, cin, cout, H, n):
+    """deterministic split-K on tile-starved launches with a moderate contraction (HarDNet growth layers at 8^2-32^2,
+    C % 64 != 0: the general-k loader starting at a slice's k-tile): forward, input and weight gradients vs PyTorch
+    fp32 CPU, and run-to-run bitwise"""
+    from ssseg import native as N
+    from ssseg import nn as snn
+    mode = 'bf16' if dtype == torch.bfloat16 else 'f16'
+    snn.set_compute_dtype(dtype)
+    try:
+        cp = snn.rup(cin, snn.vec())
+        d = snn._desc(N=n, H=H, W=H, C=cp, ldx=cp, OH=H, OW=H, K=snn.rup(cout, snn.vec()), R=3, S=3, sy=1, sx=1, dy=1,
+                      dx=1, py=-1, px=-1, outH=H, outW=H, osy=1, osx=1, ooy=0, oox=0, ldy=snn.rup(cout, snn.vec()),
+                      ldw=9 * cp)
+        assert N.lib().ssseg_conv_igemm_workspace_bytes(snn.ctypes_ref(d), N.dt_code(torch.empty(0, dtype=dtype))) > 0
+        torch.manual_seed(1)
+        ref = torch.nn.Conv2d(cin, cout, 3, 1, 1, bias=False)
+        mod = snn.Conv2d(cin, cout, 3, 1, 1, bias=False).to(hip_device)
+        mod.load_state_dict(ref.state_dict())
+        with torch.no_grad():
+            ref.weight.copy_(_q(ref.weight, mode))
+        x = _q(torch.randn(n, cin, H, H), mode)
+        xr = x.clone().requires_grad_(True)
+        yr = ref(xr)
+        gy = _q(torch.randn_like(yr), mode)
+        yr.backward(gy)
+        outs = []
+        for _ in range(2):
+            mod.zero_grad(set_to_none=True)
+            xa = _act_in(x, hip_device).detach().requires_grad_(True)
+            y = mod(xa)
+            y.backward(snn.to_act(gy.to(hip_device)))
+            outs.append((y[:, :cout].float().cpu(), xa.grad[:, :cin].float().cpu(), mod.weight.grad.cpu().clone()))
+        _close(outs[0][0], yr, mode, 'y')
+        _close(outs[0][1], xr.grad, mode, 'dx')
+        _close(outs[0][2], ref.weight.grad, mode, 'dW')
+        for a, b in zip(outs[0], outs[1]):
+            assert torch.equal(a, b)
+    finally:
+        snn.set_compute_dtype(torch.bfloat16)
+
+
+@pytest.mark.parametrize('act', [('leaky', 0.2), True])
+def test_dgrad_applies_producer_activation_backward(hip_device, mode, act):
+    """Conv4x4/s2 + LeakyReLU (or ReLU) feeding exactly one conv (the discriminator, discriminator.py:14-17): the
+    consumer's input gradient applies the producer's activation backward in its epilogue
+    (ssseg_conv_igemm_epi_actmask) -- same gradients as the separate activation-backward pass, within rounding."""
+    from ssseg import nn as snn
+    torch.manual_seed(4)
+    c1 = snn.Conv2d(8, 32, 4, 2, 1).to(hip_device)
+    c2 = snn.Conv2d(32, 48, 4, 2, 1).to(hip_device)
+    x = _q(torch.randn(2, 8, 34, 30), mode)
+    outs = []
+    for on in (True, False):
+        snn._CFG['act_mask'] = on
+        try:
+            c1.zero_grad(set_to_none=True)
+            c2.zero_grad(set_to_none=True)
+            xa = _act_in(x, hip_device).detach().requires_grad_(True)
+            h = c1.forward_act(xa, act, single_use=True)
+            assert h.__dict__.get('_ssseg_act_out') is not None
+            y = c2(h)
+            g = snn.to_act(_q(torch.randn(y.shape[0], 48, y.shape[2], y.shape[3],
+                                          generator=torch.Generator().manual_seed(5)), mode).to(hip_device))
+            y.backward(g)
+            outs.append((xa.grad[:, :8].float().cpu(), c1.weight.grad.cpu().clone(), c1.bias.grad.cpu().clone()))
+        finally:
+            snn._CFG['act_mask'] = True
+    for a, b, what in zip(outs[0], outs[1], ('dx', 'dW1', 'db1')):
+        _close(a, b, mode, what)
