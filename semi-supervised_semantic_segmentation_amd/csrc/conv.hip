@@ -10,6 +10,26 @@ int g_knobs[16] = {0, -1, 0, 0, 0, 1, 0, 0, 0, 0, 100, 0, 0, 0, 0, 0};   // runt
 // sums are order-dependent; knob 14 is the deterministic split-K of the LDS-DMA configs)
 thread_local int t_dsplit = 1;
 
+// the ticket pool of the in-launch reductions (deterministic split-K): zero when the library loads, each ticket reset
+// by the block that draws last, so a launch only needs a range no launch in flight with it uses
+constexpr long long TICKET_POOL = 1 << 20;
+__device__ unsigned g_ticket_pool[TICKET_POOL];
+
+unsigned* ticket_slots(long long n) {
+  static unsigned* const base = [] {
+    void* p = nullptr;
+    return hipGetSymbolAddress(&p, HIP_SYMBOL(g_ticket_pool)) == hipSuccess ? (unsigned*)p : nullptr;
+  }();
+  static std::mutex mu;
+  static long long next = 0;
+  if (!base || n <= 0 || n > TICKET_POOL / 16) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  if (next + n > TICKET_POOL) next = 0;
+  unsigned* p = base + next;
+  next += n;
+  return p;
+}
+
 // ------------------------------------------------------------------------------------------------
 // weight packing: dst[k][rr][ss][c] (c < Cp; zero for c >= Cd) from an fp32 source
 //   layout 0: src[k][c][r][s]  (Conv2d OIHW; ConvTranspose2d used as a conv over its output grad)

@@ -953,7 +953,9 @@ __device__ __forceinline__ void ring_wait(int ahead) {
 constexpr unsigned OOB = 0x80000000u;   // > any num_records we build: the load returns zeros
 
 // ---- deterministic split-K (S k-slices per output tile, combined inside the launch) ---------------------------------
-// Workspace: [tickets: one u32 per (phase, tile), zeroed by the host before every launch, region padded to 256 B]
+// Tickets: one u32 per (phase, tile) in the library's ticket pool (ticket_slots: zero at load, a range per launch,
+// every ticket reset to zero by the block that draws last -- no memset launch before a split launch).
+// Workspace: [unused ticket-sized region, padded to 256 B]
 // [slabs: per (phase, tile) S slices x NW waves x FN*FM fragments x 64 lanes x 16 B of fp32 partials].
 // Every slice block writes its partial accumulators with write-through (sc1) 16-byte stores, every wave drains its
 // stores, then one lane adds to the tile's ticket (agent scope); the block that draws S-1 is the last one and sums the
@@ -965,12 +967,11 @@ constexpr int DSPLIT_MAX_FRAGS = 8;   // per wave: the combine keeps 2-3 accumul
 __host__ __device__ inline long long dsplit_ticket_bytes(long long ntiles) { return (ntiles * 4 + 255) / 256 * 256; }
 
 template <int FN, int FM, int NW>
-__device__ __forceinline__ bool dsplit_combine(f32x4 (&acc)[FN][FM], float* ws, int tg, int slice, int splits,
-                                               int ntiles, char* smem) {
+__device__ __forceinline__ bool dsplit_combine(f32x4 (&acc)[FN][FM], float* ws, unsigned* tick, int tg, int slice,
+                                               int splits, int ntiles, char* smem) {
   constexpr int F = FN * FM;
   constexpr unsigned TILE_BYTES = NW * F * 1024;   // one slice's partial tile
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  unsigned* tick = (unsigned*)ws;
   char* base = (char*)ws + dsplit_ticket_bytes(ntiles) + (long long)tg * splits * TILE_BYTES;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(splits * TILE_BYTES), 0x00020000);
@@ -985,7 +986,10 @@ __device__ __forceinline__ bool dsplit_combine(f32x4 (&acc)[FN][FM], float* ws, 
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned old = __hip_atomic_fetch_add(tick + tg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *(volatile int*)smem = old == (unsigned)(splits - 1);
+    const bool is_last = old == (unsigned)(splits - 1);
+    // every slice has drawn: the last one leaves the ticket at zero for the next launch that uses this pool slot
+    if (is_last) __hip_atomic_store(tick + tg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *(volatile int*)smem = is_last;
   }
   __syncthreads();
   const bool last = *(volatile int*)smem != 0;
@@ -1035,7 +1039,7 @@ __global__ void __launch_bounds__(NW * 64, GLDS_OCC(BM, BN, NW, NS)) igemm_glds_
                                                                 const TO* __restrict__ w, TO* __restrict__ y,
                                                                 ConvGeom g, Epi<TO> ep, unsigned xbytes,
                                                                 unsigned wbytes, int g_epi_lds, int splits,
-                                                                float* __restrict__ ws, PhaseTab ph,
+                                                                float* __restrict__ ws, unsigned* tix, PhaseTab ph,
                                                                 const TO* __restrict__ x2, unsigned x2bytes) {
   constexpr int ROW = 128;                       // bytes per LDS row = 64 bf16 of k
   constexpr bool VC = KM == 1, GK = KM == 2;
@@ -1278,7 +1282,7 @@ __global__ void __launch_bounds__(NW * 64, GLDS_OCC(BM, BN, NW, NS)) igemm_glds_
   if constexpr (FN * FM <= DSPLIT_MAX_FRAGS) {
     if (splits > 1) {   // the last-arriving slice of the tile sums all S partials in slice order, then the epilogue
       const int tpp = (int)(gridDim.x >> lsp);   // tiles per phase
-      if (!dsplit_combine<FN, FM, NW>(acc, ws, (ph.n > 1 ? (int)blockIdx.y : 0) * tpp + tile, slice, splits,
+      if (!dsplit_combine<FN, FM, NW>(acc, ws, tix, (ph.n > 1 ? (int)blockIdx.y : 0) * tpp + tile, slice, splits,
                                       tpp * (int)gridDim.y, smem))
         return;
     }
@@ -1373,6 +1377,10 @@ __global__ void splitk_finalize_kernel(const float* __restrict__ ws, TO* __restr
 // config whose per-wave fragment count exceeds DSPLIT_MAX_FRAGS cannot run a split launch (-1)
 extern thread_local int t_dsplit;
 
+// n consecutive self-resetting tickets of the library's pool (conv.hip): ranges rotate over the pool, so launches in
+// flight together (a few streams) never share one
+unsigned* ticket_slots(long long n);
+
 template <typename TO, int BM, int BN, int WM, int WN, int NW, int NS, int VC>
 int launch_glds_vc(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
                    unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2, unsigned x2b) {
@@ -1387,14 +1395,15 @@ int launch_glds_vc(const void* x, const void* w, void* y, const ConvGeom& g, con
   const unsigned nph = phased ? (unsigned)ph->n : 1u;
   const int sp = ws ? t_dsplit : 1;
   if (sp > 1 && (FRAGS > DSPLIT_MAX_FRAGS || tiles * sp > 0x7fffffffLL)) return -1;
-  if (sp > 1) (void)hipMemsetAsync(ws, 0, dsplit_ticket_bytes(tiles * nph), s);
+  unsigned* tix = sp > 1 ? ticket_slots(tiles * nph) : nullptr;
+  if (sp > 1 && !tix) return -1;
   const dim3 grid((unsigned)(tiles * sp), nph);
   if (ep.stats)
     hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, true, VC>), grid, dim3(NW * 64), 0, s,
-                       (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, epi, sp, ws, pt, xa, x2b);
+                       (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, epi, sp, ws, tix, pt, xa, x2b);
   else
     hipLaunchKernelGGL((igemm_glds_kernel<TO, BM, BN, WM, WN, NW, NS, false, VC>), grid, dim3(NW * 64), 0, s,
-                       (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, epi, sp, ws, pt, xa, x2b);
+                       (const TO*)x, (const TO*)w, (TO*)y, g, ep, xb, wb, epi, sp, ws, tix, pt, xa, x2b);
   return BM;
 }
 

@@ -76,6 +76,39 @@ __global__ void bilinear_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, 
   }
 }
 
+// fp32 logits resizes (train.py:71,74,93, losses.py:18: the head's 2-channel logits, NHWC with a padded pixel
+// stride, to the image size): one thread per output pixel and ALL channels (C <= 4), so the source indices and
+// weights are computed once per pixel and each input pixel's channels come from one sector.  Per channel the
+// arithmetic is the generic kernel's (same roundings, same order): bit-identical results.
+template <typename T, int C>
+__global__ void bilinear_fwd_pix_kernel(const T* __restrict__ x, T* __restrict__ y, Axis ah, Axis aw, Strides xs,
+                                        Strides ys) {
+  const int ow = blockIdx.x * blockDim.x + threadIdx.x, oh = blockIdx.y, n = blockIdx.z;
+  if (ow >= aw.out) return;
+  int h0, h1, w0, w1;
+  float lh0, lh1, lw0, lw1;
+  src_index(ah, oh, h0, h1, lh0, lh1);
+  src_index(aw, ow, w0, w1, lw0, lw1);
+  const T* xb = x + (int64_t)n * xs.n;
+  const int64_t o00 = h0 * xs.h + w0 * xs.w, o01 = h0 * xs.h + w1 * xs.w;
+  const int64_t o10 = h1 * xs.h + w0 * xs.w, o11 = h1 * xs.h + w1 * xs.w;
+  float v[C][4];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    v[c][0] = io<T>::ld(xb, o00 + c * xs.c);
+    v[c][1] = io<T>::ld(xb, o01 + c * xs.c);
+    v[c][2] = io<T>::ld(xb, o10 + c * xs.c);
+    v[c][3] = io<T>::ld(xb, o11 + c * xs.c);
+  }
+  T* yb = y + (int64_t)n * ys.n + (int64_t)oh * ys.h + (int64_t)ow * ys.w;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const float t0 = __fadd_rn(__fmul_rn(v[c][0], lw0), __fmul_rn(v[c][1], lw1));
+    const float t1 = __fadd_rn(__fmul_rn(v[c][2], lw0), __fmul_rn(v[c][3], lw1));
+    io<T>::st(yb, (int64_t)c * ys.c, __fadd_rn(__fmul_rn(t0, lh0), __fmul_rn(t1, lh1)));
+  }
+}
+
 // outputs o whose source pair (i0, i1) contains input i lie within [lo, hi]
 __device__ __forceinline__ void out_window(const Axis& a, int i, int& lo, int& hi) {
   if (a.scale <= 0.f) {
@@ -130,6 +163,48 @@ __global__ void bilinear_bwd_kernel(const T* __restrict__ gy, T* __restrict__ gx
     }
     io<T>::st(gx, (int64_t)n * gxs.n + (int64_t)c * gxs.c + (int64_t)h * gxs.h + (int64_t)w * gxs.w, acc);
   }
+}
+
+// backward of bilinear_fwd_pix_kernel: one thread per input pixel and all C <= 4 channels (the output window and
+// its weights computed once per pixel); per channel the generic kernel's gather in the same order: bit-identical
+template <typename T, int C>
+__global__ void bilinear_bwd_pix_kernel(const T* __restrict__ gy, T* __restrict__ gx, Axis ah, Axis aw, Strides gys,
+                                        Strides gxs) {
+  const int w = blockIdx.x * blockDim.x + threadIdx.x, h = blockIdx.y, n = blockIdx.z;
+  if (w >= aw.in) return;
+  int ohlo, ohhi, owlo, owhi;
+  out_window(ah, h, ohlo, ohhi);
+  out_window(aw, w, owlo, owhi);
+  const T* gb = gy + (int64_t)n * gys.n;
+  float acc[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) acc[c] = 0.f;
+  for (int oh = ohlo; oh <= ohhi; ++oh) {
+    int h0, h1;
+    float l0, l1;
+    src_index(ah, oh, h0, h1, l0, l1);
+    const float wh = (h0 == h ? l0 : 0.f) + (h1 == h ? l1 : 0.f);
+    if (wh == 0.f) continue;
+    float row[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) row[c] = 0.f;
+    for (int ow = owlo; ow <= owhi; ++ow) {
+      int w0, w1;
+      float m0, m1;
+      src_index(aw, ow, w0, w1, m0, m1);
+      const float ww = (w0 == w ? m0 : 0.f) + (w1 == w ? m1 : 0.f);
+      if (ww != 0.f) {
+        const int64_t o = (int64_t)oh * gys.h + (int64_t)ow * gys.w;
+#pragma unroll
+        for (int c = 0; c < C; ++c) row[c] = fmaf(io<T>::ld(gb, o + c * gys.c), ww, row[c]);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = fmaf(row[c], wh, acc[c]);
+  }
+  T* xb = gx + (int64_t)n * gxs.n + (int64_t)h * gxs.h + (int64_t)w * gxs.w;
+#pragma unroll
+  for (int c = 0; c < C; ++c) io<T>::st(xb, (int64_t)c * gxs.c, acc[c]);
 }
 
 // 16-bit NHWC activations (the HRNet / UNet feature maps: channels fastest, C % 8 == 0, 16-byte aligned rows): one
@@ -290,6 +365,15 @@ static bool nhwc_ok(const void* a, const void* b, int64_t N, int64_t C, int64_t 
 
 static Strides to_strides(const int64_t* s) { return Strides{s[0], s[1], s[2], s[3]}; }
 
+// the per-pixel fp32 kernels apply: C <= 4 channels, grid dims in range (SSSEG_BIL_PIX=0 turns them off for A/B)
+static bool pix_ok(int64_t N, int64_t C, int64_t rows, int64_t cols, int dt) {
+  static const bool on = [] {
+    const char* e = getenv("SSSEG_BIL_PIX");
+    return !(e && e[0] == '0');
+  }();
+  return on && dt == SSSEG_F32 && C >= 1 && C <= 4 && N <= 65535 && rows <= 65535 && cols < (1 << 24);
+}
+
 }  // namespace
 
 extern "C" int ssseg_bilinear_fwd(const void* x, void* y, int64_t N, int64_t C, int64_t H, int64_t W, int64_t Ho,
@@ -309,6 +393,14 @@ extern "C" int ssseg_bilinear_fwd(const void* x, void* y, int64_t N, int64_t C, 
       hipLaunchKernelGGL(bilinear_fwd_nhwc_kernel<bf16_t>, g, b, 0, s, (const bf16_t*)x, (bf16_t*)y, C8, ah, aw, xs, ys);
     else
       hipLaunchKernelGGL(bilinear_fwd_nhwc_kernel<f16_t>, g, b, 0, s, (const f16_t*)x, (f16_t*)y, C8, ah, aw, xs, ys);
+    SSSEG_LAUNCH_CHECK();
+    return 0;
+  }
+  if (pix_ok(N, C, Ho, Wo, dt)) {   // few channels (the logits): one thread per output pixel, all channels
+    const dim3 g((unsigned)((Wo + 255) / 256), (unsigned)Ho, (unsigned)N), b(256);
+    auto k = C == 1 ? bilinear_fwd_pix_kernel<float, 1> : C == 2 ? bilinear_fwd_pix_kernel<float, 2>
+           : C == 3 ? bilinear_fwd_pix_kernel<float, 3> : bilinear_fwd_pix_kernel<float, 4>;
+    hipLaunchKernelGGL(k, g, b, 0, s, (const float*)x, (float*)y, ah, aw, xs, ys);
     SSSEG_LAUNCH_CHECK();
     return 0;
   }
@@ -386,6 +478,14 @@ extern "C" int ssseg_bilinear_bwd(const void* gy, void* gx, int64_t N, int64_t C
     else
       hipLaunchKernelGGL(bilinear_bwd_nhwc_kernel<f16_t>, g, b, 0, s, (const f16_t*)gy, (f16_t*)gx, C8, ah, aw, gys,
                          gxs);
+    SSSEG_LAUNCH_CHECK();
+    return 0;
+  }
+  if (pix_ok(N, C, H, W, dt)) {
+    const dim3 g((unsigned)((W + 255) / 256), (unsigned)H, (unsigned)N), b(256);
+    auto k = C == 1 ? bilinear_bwd_pix_kernel<float, 1> : C == 2 ? bilinear_bwd_pix_kernel<float, 2>
+           : C == 3 ? bilinear_bwd_pix_kernel<float, 3> : bilinear_bwd_pix_kernel<float, 4>;
+    hipLaunchKernelGGL(k, g, b, 0, s, (const float*)gy, (float*)gx, ah, aw, gys, gxs);
     SSSEG_LAUNCH_CHECK();
     return 0;
   }
