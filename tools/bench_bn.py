@@ -68,6 +68,9 @@ def main():
         t = timeit(lambda: N.call('ssseg_bn_bwd_reduce', p(dy), p(x), p(r), P, C, C, C, C, p(mean), p(inv), p(g),
                                   p(b), 1, bf, p(sums), p(ws), nb, s))
         rows.append(('bwd_reduce+res', t, 6 * e))
+        t = timeit(lambda: N.call('ssseg_bn_bwd_reduce', p(dy), p(x), None, P, C, C, C, C, p(mean), p(inv), p(g),
+                                  p(b), 1, bf, p(sums), p(ws), nb, s))
+        rows.append(('bwd_reduce', t, 4 * e))
         t = timeit(lambda: N.call('ssseg_bn_bwd_apply', p(dy), p(x), p(r), p(dx), p(dres), P, C, C, C, C, C, p(mean),
                                   p(inv), p(g), p(b), 1, 1, p(sums), float(P), bf, s))
         rows.append(('bwd_apply+res', t, 10 * e))
