@@ -36,19 +36,23 @@ __device__ __forceinline__ int hc_swz(int r) { return (r >> 1) & 7; }   // 16-by
 // while the other multiplies (2 waves per SIMD); the double-buffered form (variant 24) has one 151.5 KB block per CU,
 // one wave per SIMD, whose MFMA and LDS latencies do not overlap and whose prologue / epilogue latency is exposed on
 // every tile
-template <typename TO, bool STATS, bool VC, bool TWO>
+// TW: tile width (64; 32 / 16 on the 32^2 / 16^2 maps: 8 / 16 rows of 32 / 16 pixels, the same 256 pixels, a 10 x 34 /
+// 18 x 18 halo in the same buffer); wave w owns tile pixels 64 w .. 64 w + 63 (row-major), fragment j = 16 of them
+template <typename TO, bool STATS, bool VC, bool TWO, int TW = 64>
 __global__ void __launch_bounds__(256, TWO ? 2 : 1) hconv3_kernel(const TO* __restrict__ x, const TO* __restrict__ w,
                                                                   TO* __restrict__ y, ConvGeom g, Epi<TO> ep,
                                                                   unsigned xbytes, unsigned wbytes,
                                                                   const TO* __restrict__ x2, unsigned x2bytes) {
+  constexpr int TR = 256 / TW, HW = TW + 2, NPX = (TR + 2) * HW;   // tile rows, halo row width, halo pixels
+  static_assert(NPX <= HC_PX && TW >= 16, "the halo fits the buffer");
   __shared__ __attribute__((aligned(1024))) char smem[TWO ? HC_SMEM1 : HC_SMEM];
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int nkb = g.K >> 6, nstrips = g.W >> 6, nrg = g.H >> 2;
+  const int nkb = g.K >> 6, nstrips = g.W / TW, nrg = g.H / TR;
   const int tile = xcd_tile(blockIdx.x, gridDim.x);   // consecutive ids (the k-blocks of one pixel tile) share an XCD
   const int kb = tile % nkb, pt = tile / nkb;
   const int strip = pt % nstrips, q = pt / nstrips;
   const int rg = q % nrg, n = q / nrg;
-  const int y0 = rg * 4, x0 = strip * 64;
+  const int y0 = rg * TR, x0 = strip * TW;
   const int H = g.H, W = g.W, C = g.C, ncb = g.C >> 6;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, (int)wbytes, 0x00020000);
@@ -64,10 +68,10 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) hconv3_kernel(const TO* __re
     const int ld = second ? g.ldx2 : g.ldx, cc = (second ? cb - g.c1b : cb) * 64;
     for (int i = wave; i < HC_PX / 8; i += 4) {
       const int p = 8 * i + (lane >> 3);
-      const int row = p / 66, col = p - row * 66;
+      const int row = p / HW, col = p - row * HW;
       const int yy = y0 - 1 + row, xx = x0 - 1 + col;
       unsigned off = OOB;
-      if (p < 396 && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
+      if (p < NPX && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
         off = (unsigned)(((n * H + yy) * W + xx) * ld + cc + 8 * ((lane & 7) ^ hc_swz(p))) * 2u;
       if (VC && second) bldslds16_nt(xr2, XB + b * HC_XBUF + i * 1024, off, 0);
       else bldslds16_nt(xr, XB + b * HC_XBUF + i * 1024, off, 0);
@@ -109,7 +113,8 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) hconv3_kernel(const TO* __re
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int p = (wave + r) * 66 + j * 16 + li + s;
+          const int tp = wave * 64 + j * 16;   // first tile pixel of the fragment (16 | TW: one tile row)
+          const int p = (tp / TW + r) * HW + tp % TW + li + s;
           bfr[j] = *(const bf16x8*)(X + p * 128 + ((ch ^ hc_swz(p)) << 4));
         }
 #pragma unroll
@@ -154,38 +159,56 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) hconv3_kernel(const TO* __re
   }
 
   // LDS-staged epilogue over the 4 x 64 pixel tile (the ring is idle: the loop ended on a barrier)
-  const Tile2D t2{n, y0, x0, min(4, H - y0), (long long)pt};
+  const Tile2D t2{n, y0, x0, min(TR, H - y0), (long long)pt, TW == 64 ? 6 : (TW == 32 ? 5 : 4)};
   store_tile_lds<TO, 256, 64, 4, 4, 256, STATS, 1, true>(acc, smem, 0, kb * 64, wave * 64, 0, lane, g, y, ep,
                                                          PreRes<1>{{}, false}, t2);
 }
 
 }  // namespace
 
+// tile width for the map: 64 (W % 64 == 0, H % 4 == 0), else 32 (W % 32, H % 8) or 16 (W % 16, H % 16); 0 = none
+static int hconv3_tw(const ConvGeom& g) {
+  if (g.W % 64 == 0 && g.H % 4 == 0) return 64;
+  if (g_knobs[16] < 0) return 0;   // knob 16 = -1: the 64-wide tile only (A/B)
+  if (g.W % 32 == 0 && g.H % 8 == 0) return 32;
+  if (g.W % 16 == 0 && g.H % 16 == 0) return 16;
+  return 0;
+}
+
 bool hconv3_ok(const ConvGeom& g, const PhaseTab* ph, const float* ws) {
   return g_knobs[11] >= 0 && !ws && !(ph && ph->n > 1) && g.R == 3 && g.S == 3 && g.sy == 1 && g.sx == 1 &&
          g.dy == 1 && g.dx == 1 && g.py == -1 && g.px == -1 && g.oident && g.H == g.OH && g.W == g.OW &&
-         g.W % 64 == 0 && g.H % 4 == 0 && g.C % 64 == 0 && g.K % 64 == 0 && g.ldw == 9 * g.C && g.ldx % 8 == 0 &&
+         hconv3_tw(g) > 0 && g.C % 64 == 0 && g.K % 64 == 0 && g.ldw == 9 * g.C && g.ldx % 8 == 0 &&
          g.ldy % 8 == 0 && g.ldx >= g.C && g.M < 0x7fffffffLL;
 }
 
-template <typename TO, bool TWO>
+template <typename TO, bool TWO, int TW>
 static void launch_hconv3_t(const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep, unsigned xb,
                             unsigned wb, hipStream_t s, const void* x2, unsigned x2b, long long blocks) {
   const TO* xa = (const TO*)x2;
+  const dim3 grid((unsigned)blocks), blk(256);
   if (x2) {
     if (ep.stats)
-      hipLaunchKernelGGL((hconv3_kernel<TO, true, true, TWO>), dim3((unsigned)blocks), dim3(256), 0, s, (const TO*)x,
-                         (const TO*)w, (TO*)y, g, ep, xb, wb, xa, x2b);
+      hipLaunchKernelGGL((hconv3_kernel<TO, true, true, TWO, TW>), grid, blk, 0, s, (const TO*)x, (const TO*)w, (TO*)y,
+                         g, ep, xb, wb, xa, x2b);
     else
-      hipLaunchKernelGGL((hconv3_kernel<TO, false, true, TWO>), dim3((unsigned)blocks), dim3(256), 0, s, (const TO*)x,
-                         (const TO*)w, (TO*)y, g, ep, xb, wb, xa, x2b);
+      hipLaunchKernelGGL((hconv3_kernel<TO, false, true, TWO, TW>), grid, blk, 0, s, (const TO*)x, (const TO*)w,
+                         (TO*)y, g, ep, xb, wb, xa, x2b);
   } else if (ep.stats) {
-    hipLaunchKernelGGL((hconv3_kernel<TO, true, false, TWO>), dim3((unsigned)blocks), dim3(256), 0, s, (const TO*)x,
-                       (const TO*)w, (TO*)y, g, ep, xb, wb, xa, x2b);
+    hipLaunchKernelGGL((hconv3_kernel<TO, true, false, TWO, TW>), grid, blk, 0, s, (const TO*)x, (const TO*)w, (TO*)y,
+                       g, ep, xb, wb, xa, x2b);
   } else {
-    hipLaunchKernelGGL((hconv3_kernel<TO, false, false, TWO>), dim3((unsigned)blocks), dim3(256), 0, s, (const TO*)x,
-                       (const TO*)w, (TO*)y, g, ep, xb, wb, xa, x2b);
+    hipLaunchKernelGGL((hconv3_kernel<TO, false, false, TWO, TW>), grid, blk, 0, s, (const TO*)x, (const TO*)w,
+                       (TO*)y, g, ep, xb, wb, xa, x2b);
   }
+}
+
+template <typename TO, bool TWO>
+static void launch_hconv3_w(int tw, const void* x, const void* w, void* y, const ConvGeom& g, const Epi<TO>& ep,
+                            unsigned xb, unsigned wb, hipStream_t s, const void* x2, unsigned x2b, long long blocks) {
+  if (tw == 64) launch_hconv3_t<TO, TWO, 64>(x, w, y, g, ep, xb, wb, s, x2, x2b, blocks);
+  else if (tw == 32) launch_hconv3_t<TO, TWO, 32>(x, w, y, g, ep, xb, wb, s, x2, x2b, blocks);
+  else launch_hconv3_t<TO, TWO, 16>(x, w, y, g, ep, xb, wb, s, x2, x2b, blocks);
 }
 
 // mode 0: the double-buffered kernel (variant 24), 1: the single-buffered two-blocks-per-CU kernel (variant 28)
@@ -194,12 +217,13 @@ int launch_hconv3(const void* x, const void* w, void* y, const ConvGeom& g, cons
                   unsigned wb, hipStream_t s, float* ws, const PhaseTab* ph, const void* x2, unsigned x2b, int mode) {
   if (!hconv3_ok(g, ph, ws) || (x2 && (g.ldx2 % 8 || g.c1b < 1 || g.c1b >= g.C / 64))) return -1;
   if (mode == 1 && g_knobs[15] < 0) return -1;   // knob 15 = -1: no variant 28 (A/B)
-  const long long blocks = (long long)g.N * (g.H / 4) * (g.W / 64) * (g.K / 64);
+  const int tw = hconv3_tw(g);
+  const long long blocks = (long long)g.N * (g.H / (256 / tw)) * (g.W / tw) * (g.K / 64);
   if (blocks > 0x7fffffffLL) return -1;
   if (mode == 1)
-    launch_hconv3_t<TO, true>(x, w, y, g, ep, xb, wb, s, x2, x2b, blocks);
+    launch_hconv3_w<TO, true>(tw, x, w, y, g, ep, xb, wb, s, x2, x2b, blocks);
   else
-    launch_hconv3_t<TO, false>(x, w, y, g, ep, xb, wb, s, x2, x2b, blocks);
+    launch_hconv3_w<TO, false>(tw, x, w, y, g, ep, xb, wb, s, x2, x2b, blocks);
   return 256;
 }
 

@@ -426,11 +426,12 @@ template <int NP> struct PreRes {   // residual chunks an epilogue thread loaded
   bool on;
 };
 
-// T2D (the halo-tiled 3x3 kernel, conv_hconv3.hip): the tile is t2.rows image rows x 64 columns of image t2.n starting
+// T2D (the halo-tiled 3x3 kernel, conv_hconv3.hip): the tile is t2.rows image rows x 2^t2.lw columns of image t2.n starting
 // at (t2.y0, t2.x0) instead of BM consecutive GEMM rows; its statistics row is t2.tile (output grid == GEMM grid)
 struct Tile2D {
   int n, y0, x0, rows;
   long long tile;
+  int lw = 6;   // log2 of the tile width (64 columns; 32 / 16 on the 32^2 / 16^2 maps)
 };
 
 template <typename TO, int BM, int BN, int FM, int FN, int NT, bool STATS, int NPRE = 1, bool T2D = false>
@@ -464,7 +465,7 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
 #pragma unroll
         for (int j = 0; j < FM; ++j) {
           const int row = wmo + j * 16 + (lane & 15);
-          const bool rv = T2D ? (row >> 6) < t2.rows : m0 + row < g.M;
+          const bool rv = T2D ? (row >> t2.lw) < t2.rows : m0 + row < g.M;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const float q = (rv && nb + e < g.K) ? stored<TO>(acc[i][j][e] + sh[e]) : 0.f;
@@ -559,8 +560,8 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
       const int row = r0 + p * RPP;
       op[p] = -1;
       if constexpr (T2D) {
-        if (row < BM && (row >> 6) < t2.rows)
-          op[p] = ((long long)t2.n * g.outH + t2.y0 + (row >> 6)) * g.outW + t2.x0 + (row & 63);
+        if (row < BM && (row >> t2.lw) < t2.rows)
+          op[p] = ((long long)t2.n * g.outH + t2.y0 + (row >> t2.lw)) * g.outW + t2.x0 + (row & ((1 << t2.lw) - 1));
       } else {
         const long long m = m0 + row;
         if (row < BM && m < g.M) {
@@ -695,7 +696,7 @@ constexpr int ROWB = 80;   // 64 data bytes + 16 pad per LDS row
 // ------------------------------------------------------------------------------------------------
 // forward / dgrad / transposed-conv gather GEMM
 // ------------------------------------------------------------------------------------------------
-extern int g_knobs[16];   // runtime variant switches (ssseg_set_knob), defined in conv.hip
+extern int g_knobs[17];   // runtime variant switches (ssseg_set_knob), defined in conv.hip
 // 0: reg-staged pipeline depth; 1: split-K cap (-1 off = default, 0 auto: the autotuner also times each variant with
 // its split plan, fp32-atomic partials + finalize, and keeps it where faster); 2: 64x64 small-M tiles (reg-staged path);
 // 3: bf16 LDS-DMA path (0 on, -1 off); 4: variant (0 auto, 1..10 / 12..23 LDS-DMA config, 11 register-staged, 24 the

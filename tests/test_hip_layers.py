@@ -297,6 +297,9 @@ ALL_VARIANTS = [11] + list(range(1, 11)) + list(range(12, 29))
                                                # W % 64 == 0, H % 4 == 0: the halo-tiled 3x3 kernel (variant 24)
                                                ('conv64', 64, 64, 3, 8), ('conv64', 128, 128, 3, 12),
                                                ('conv64', 192, 64, 3, 4), ('conv64', 64, 192, 3, 20),
+                                               # 32 x 32 / 16 x 16 maps: the halo kernel's 32- and 16-wide tiles
+                                               ('conv32', 64, 64, 3, 16), ('conv32', 128, 192, 3, 8),
+                                               ('conv16', 64, 128, 3, 16), ('conv16', 192, 64, 3, 32),
                                                # 32 -> 32 channels: its halo form (variant 25)
                                                ('conv64', 32, 32, 3, 8), ('conv64', 32, 32, 3, 12),
                                                # vpad: 240 / 120 channels run the 64-aligned path over 256 / 128
@@ -318,6 +321,8 @@ def test_conv_variants_bitwise(hip_device, kind, cin, cout, k, H):
     Wd = H + 3
     if kind == 'conv64':
         kind, Wd = 'conv', 64 if cin != 64 or cout != 192 else 128
+    elif kind in ('conv32', 'conv16'):
+        kind, Wd = 'conv', int(kind[4:])
     if kind == 'conv':
         mod = snn.Conv2d(cin, cout, k, 1, k // 2, bias=False).to(hip_device)
     elif kind == 'conv_s2':
