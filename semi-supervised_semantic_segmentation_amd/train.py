@@ -116,7 +116,8 @@ def _scaled(loss, optimizer):
 # concurrently on the side stream would skew those timings -- and with them the variant choices kept for the rest of
 # the run.  Counted per step key (a second model, a new batch size or dtype in the same process tunes serially too).
 _OVERLAP = {'teacher': os.environ.get('SSSEG_OVERLAP_TEACHER', '1') != '0', 'streams': {}, 'steps': 0,
-            'serial_steps': 2, 'seen': {}}
+            'serial_steps': 2, 'seen': {},
+            'consistency': os.environ.get('SSSEG_OVERLAP_CONSISTENCY', '1') != '0'}
 
 
 def _step_key(model, ema_model, image, unsup_a):
@@ -147,6 +148,20 @@ def _teacher_targets(ema_model, unsup_a, unsup_b, tc):
         mixed_ema_pred = cowmix.mix_with_mask(ema_pred_a, ema_pred_b, cmask)
         mixed_images = cowmix.mix_with_mask(unsup_a, unsup_b, cmask)
     return mixed_ema_pred, mixed_images
+
+
+def _consistency_forward(model, targets, tc, epoch):
+    """train.py:87-112: the student's eval-mode forward on the mixed images (with grad), resized, and the weighted
+    consistency loss.  Returns (unsup_loss, cm_mean)."""
+    mixed_ema_pred, mixed_images = targets
+    model.eval()
+    with snn.folded(_inner(model)):
+        student_pred = model(mixed_images)[-1][-1]
+    model.train()
+    student_pred = ops.interpolate_bilinear(student_pred, mixed_images.shape[2:4], align_corners=False)
+    consistency, cm_mean = ops.consistency_loss(student_pred, mixed_ema_pred, tc['confidence_threshold'])
+    # consistency * weight * float(epoch > 25) (train.py:112; a 0/0 NaN survives the 0.0 gate, as there)
+    return ops.scale(consistency, float(tc['consistency_loss_weight']) * float(epoch > 25)), cm_mean
 
 
 def _side_stream(device):
@@ -185,7 +200,7 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
                and seen >= _OVERLAP['serial_steps'])
     _OVERLAP['seen'][key] = seen + 1
     _OVERLAP['steps'] += 1
-    targets = None
+    targets = cons = None
     if overlap:
         main = torch.cuda.current_stream()
         side = _side_stream(image.device)
@@ -194,6 +209,11 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
             t.record_stream(side)
         with torch.cuda.stream(side):
             targets = _teacher_targets(ema_model, unsup_a, unsup_b, tc)
+            if _OVERLAP['consistency']:
+                # the consistency forward needs the student's weights and running statistics as the supervised
+                # forward left them -- the supervised backward changes neither -- so it runs on the side stream
+                # too, concurrently with that backward; its backward (main stream) waits for it
+                cons = _consistency_forward(model, targets, tc, epoch)
         for t in targets:
             t.record_stream(main)
     if ddp is not None and not semi:
@@ -214,22 +234,22 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
         if semi:
             if overlap:
                 torch.cuda.current_stream().wait_stream(_side_stream(image.device))
-                mixed_ema_pred, mixed_images = targets
             else:
-                mixed_ema_pred, mixed_images = _teacher_targets(ema_model, unsup_a, unsup_b, tc)
-            del targets
-            model.eval()
-            with snn.folded(_inner(model)):
-                student_pred = model(mixed_images)[-1][-1]
-            model.train()
-            student_pred = ops.interpolate_bilinear(student_pred, mixed_images.shape[2:4], align_corners=False)
-            consistency, cm_mean = ops.consistency_loss(student_pred, mixed_ema_pred, tc['confidence_threshold'])
-            # consistency * weight * float(epoch > 25) (train.py:112; a 0/0 NaN survives the 0.0 gate, as there)
-            unsup_loss = ops.scale(consistency, float(tc['consistency_loss_weight']) * float(epoch > 25))
+                targets = _teacher_targets(ema_model, unsup_a, unsup_b, tc)
+            side_fwd = cons is not None
+            unsup_loss, cm_mean = cons if side_fwd else _consistency_forward(model, targets, tc, epoch)
+            del targets, cons
             if ddp is not None:
                 ddp.arm()
             with snn.defer_param_grads():   # the eval BNs' parameter gradients: one batched reduction at the end
+                if side_fwd:
+                    # autograd runs each backward node on its forward's stream: the consistency backward runs on the
+                    # side stream, after the supervised backward's gradient writes (main) and before what follows
+                    side = _side_stream(image.device)
+                    side.wait_stream(torch.cuda.current_stream())
                 ops.backward(_scaled(unsup_loss, optimizer))
+                if side_fwd:
+                    torch.cuda.current_stream().wait_stream(side)
         snn.flush_wgrad()
     if ddp is not None:
         ddp.finish()
