@@ -180,9 +180,13 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
     supervised forward only -- the running statistics its eval BatchNorms read are the ones that forward updated
     (the teacher's BN buffers alias the student's, mean_teacher.py:13-18), and the supervised backward neither
     changes them nor draws random numbers -- so it is issued on a side HIP stream right after the supervised forward
-    and runs concurrently with the supervised backward; the consistency forward waits for it.  The consistency
-    backward can put its (merged) weight gradients on a side stream too (ssseg.nn.wgrad_side_stream; off by default,
-    measured neutral).  Measured on the C2 step (A/B in one call): 443.9 img/s serial, 452.9 with the teacher overlap."""
+    and runs concurrently with the supervised backward (and, in C5, the discriminator step).  The consistency forward
+    (train.py:87-112) reads the same weights and statistics, so it follows the teacher on the side stream; its
+    backward runs after the supervised backward's gradient writes (autograd runs it on the side stream, its forward's:
+    explicit waits on both sides).  The consistency backward can put its (merged) weight gradients on a side stream too
+    (ssseg.nn.wgrad_side_stream; off by default, measured neutral).  Measured (A/B in one call): C2 443.9 img/s serial,
+    452.9 with the teacher overlap (round 4); 499.7 / 501.9 -> 512.9 / 514.8 with the consistency forward on the side
+    stream too; C5 25.5 -> 21.9 ms (the overlap was off for the adversarial config before)."""
     tc = config['train']
     ddp = model if isinstance(model, _DDP) else None
     semi = tc['use_semi_supervised']
@@ -196,7 +200,7 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
         sup_loss = ops.add_scaled(sup_loss, adv_loss)
     key = _step_key(model, ema_model, image, unsup_a)
     seen = _OVERLAP['seen'].get(key, 0)
-    overlap = (semi and adv is None and _OVERLAP['teacher'] and image.is_cuda and unsup_a.is_cuda
+    overlap = (semi and _OVERLAP['teacher'] and image.is_cuda and unsup_a.is_cuda
                and seen >= _OVERLAP['serial_steps'])
     _OVERLAP['seen'][key] = seen + 1
     _OVERLAP['steps'] += 1
