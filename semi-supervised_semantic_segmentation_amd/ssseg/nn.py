@@ -105,6 +105,46 @@ def flush_wgrad():
             mod._ssseg_wgrad(*pair, bias_grad=False, want=(True, False))
 
 
+# ---- held weight-gradient calls: two backward passes issued on two streams, their gradient writes replayed after ------
+_HOLD = {'on': False, 'tag': None, 'calls': []}
+
+
+@contextlib.contextmanager
+def hold_wgrad(tag):
+    """Inside: every conv's weight (and bias) gradient call is recorded with its operands instead of launched.  The
+    training step issues the consistency backward on the side stream and the supervised backward on the main stream
+    under this, so the two run concurrently without touching the shared gradient arena; replay_held() then issues
+    the recorded calls on the caller's stream exactly as the serial schedule would (the first pass deferred, the
+    second merged with it, one launch per conv over both pixel sets)."""
+    prev = _HOLD['on'], _HOLD['tag']
+    _HOLD['on'], _HOLD['tag'] = True, tag
+    try:
+        yield
+    finally:
+        _HOLD['on'], _HOLD['tag'] = prev
+
+
+def _held(mod, x, gy, bias_grad, want):
+    if not _HOLD['on']:
+        return False
+    _HOLD['calls'].append((_HOLD['tag'], mod, (x, gy), {'bias_grad': bias_grad, 'want': want}))
+    return True
+
+
+def replay_held(order):
+    """Issue the held calls: those of pass order[0] inside defer_wgrad(), then those of order[1] (each merges with its
+    conv's deferred one), then flush_wgrad() -- the launches and the summation order of the serial schedule."""
+    calls, _HOLD['calls'] = _HOLD['calls'], []
+    with defer_wgrad():
+        for tag, mod, args, kw in calls:
+            if tag == order[0]:
+                mod._ssseg_wgrad(*args, **kw)
+    for tag, mod, args, kw in calls:
+        if tag == order[1]:
+            mod._ssseg_wgrad(*args, **kw)
+    flush_wgrad()
+
+
 # ---- deferred BN parameter gradients of the differentiated eval pass ---------------------------------------------------
 _PGRAD = {'on': os.environ.get('SSSEG_DEFER_BN_PGRAD', '1') != '0', 'live': False, 'pending': [], 'table': None}
 
@@ -883,6 +923,8 @@ class Conv2d(nn.Conv2d, _ConvBase):
 
     def _ssseg_wgrad(self, x, gy, bias_grad=True, want=None):
         """dW (+ db) of this conv; want = (weight, bias) requires_grad as captured at forward time (None: live)."""
+        if _held(self, x, gy, bias_grad, want):
+            return
         ww = self.weight.requires_grad if want is None else want[0]
         if bias_grad:
             _bias_grad(self, gy, None if want is None else want[1])
@@ -1147,6 +1189,8 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
         return gy
 
     def _ssseg_wgrad(self, x, gy, bias_grad=True, want=None):
+        if _held(self, x, gy, bias_grad, want):
+            return
         ww = self.weight.requires_grad if want is None else want[0]
         if bias_grad:
             _bias_grad(self, gy, None if want is None else want[1])

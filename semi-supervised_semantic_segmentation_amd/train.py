@@ -117,7 +117,8 @@ def _scaled(loss, optimizer):
 # the run.  Counted per step key (a second model, a new batch size or dtype in the same process tunes serially too).
 _OVERLAP = {'teacher': os.environ.get('SSSEG_OVERLAP_TEACHER', '1') != '0', 'streams': {}, 'steps': 0,
             'serial_steps': 2, 'seen': {},
-            'consistency': os.environ.get('SSSEG_OVERLAP_CONSISTENCY', '1') != '0'}
+            'consistency': os.environ.get('SSSEG_OVERLAP_CONSISTENCY', '1') != '0',
+            'consistency_bwd': os.environ.get('SSSEG_OVERLAP_CONSISTENCY_BWD', '1') != '0'}
 
 
 def _step_key(model, ema_model, image, unsup_a):
@@ -205,6 +206,10 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
     _OVERLAP['seen'][key] = seen + 1
     _OVERLAP['steps'] += 1
     targets = cons = None
+    # the consistency backward too, when no DDP reducer needs its gradients as they are written: both backward passes
+    # then run concurrently, their weight / bias gradients held (snn.hold_wgrad) and replayed after both
+    side_bwd = overlap and ddp is None and _OVERLAP['consistency'] and _OVERLAP['consistency_bwd']
+    pgrad_ctx = contextlib.ExitStack()
     if overlap:
         main = torch.cuda.current_stream()
         side = _side_stream(image.device)
@@ -216,15 +221,21 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
             if _OVERLAP['consistency']:
                 # the consistency forward needs the student's weights and running statistics as the supervised
                 # forward left them -- the supervised backward changes neither -- so it runs on the side stream
-                # too, concurrently with that backward; its backward (main stream) waits for it
+                # too, concurrently with that backward
                 cons = _consistency_forward(model, targets, tc, epoch)
+            if side_bwd:
+                # its backward writes no gradient now: the eval BNs' parameter gradients are reduced after the join
+                # (defer_param_grads, left open until then) and the conv weight / bias gradients are held
+                pgrad_ctx.enter_context(snn.defer_param_grads())
+                with snn.hold_wgrad('cons'):
+                    ops.backward(_scaled(cons[0], optimizer))
         for t in targets:
             t.record_stream(main)
     if ddp is not None and not semi:
         ddp.arm()
     # with a consistency backward to follow, each conv's supervised weight gradient is merged into that pass's
     # (one launch over both batches' pixels; ssseg.nn.defer_wgrad) -- the .grad sum is the same
-    with (snn.defer_wgrad() if semi else contextlib.nullcontext()):
+    with (snn.hold_wgrad('sup') if side_bwd else snn.defer_wgrad() if semi else contextlib.nullcontext()):
         vbm = tc['virtual_batch_size_multiplier']
         ops.backward(_scaled(ops.scale(sup_loss, 1.0 / vbm) if vbm != 1 else sup_loss, optimizer))
     del pred_maps, features
@@ -234,8 +245,17 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
         adv['last_loss_adv'] = adv_loss.detach()
         del prob
     unsup_loss = cm_mean = None
+    if side_bwd:
+        torch.cuda.current_stream().wait_stream(_side_stream(image.device))
+        unsup_loss, cm_mean = cons
+        del targets, cons
+        snn.replay_held(('sup', 'cons'))   # the serial schedule's weight-gradient launches, on this stream
+        pgrad_ctx.close()                  # the eval BNs' parameter gradients: one batched reduction
+        semi_rest = False
+    else:
+        semi_rest = semi
     with snn.wgrad_side_stream():
-        if semi:
+        if semi_rest:
             if overlap:
                 torch.cuda.current_stream().wait_stream(_side_stream(image.device))
             else:
