@@ -106,22 +106,40 @@ def flush_wgrad():
 
 
 # ---- held weight-gradient calls: two backward passes issued on two streams, their gradient writes replayed after ------
-_HOLD = {'on': False, 'tag': None, 'calls': []}
+_HOLD = {'on': False, 'tag': None, 'calls': [], 'params': False, 'adds': []}
 
 
 @contextlib.contextmanager
-def hold_wgrad(tag):
+def hold_wgrad(tag, params=False):
     """Inside: every conv's weight (and bias) gradient call is recorded with its operands instead of launched.  The
     training step issues the consistency backward on the side stream and the supervised backward on the main stream
     under this, so the two run concurrently without touching the shared gradient arena; replay_held() then issues
     the recorded calls on the caller's stream exactly as the serial schedule would (the first pass deferred, the
-    second merged with it, one launch per conv over both pixel sets)."""
-    prev = _HOLD['on'], _HOLD['tag']
-    _HOLD['on'], _HOLD['tag'] = True, tag
+    second merged with it, one launch per conv over both pixel sets).  params=True (the pass on the side stream): the
+    other parameter gradients its backward adds (a standalone BatchNorm's weight / bias) go to zeroed temporaries,
+    added into .grad by replay_held after the other pass's own writes -- the serial order, the same fp32 sums."""
+    prev = _HOLD['on'], _HOLD['tag'], _HOLD['params']
+    _HOLD['on'], _HOLD['tag'], _HOLD['params'] = True, tag, params
     try:
         yield
     finally:
-        _HOLD['on'], _HOLD['tag'] = prev
+        _HOLD['on'], _HOLD['tag'], _HOLD['params'] = prev
+
+
+def _grad_ptrs(*params):
+    """device pointers a backward kernel ADDS parameter gradients into: the params' .grad, or inside
+    hold_wgrad(params=True) zeroed temporaries that replay_held adds into .grad (None for an absent parameter)."""
+    if not (_HOLD['on'] and _HOLD['params']):
+        return tuple(N.dev_ptr(_grad_of(p)) if p is not None else None for p in params)
+    out = []
+    for p in params:
+        if p is None:
+            out.append(None)
+            continue
+        tmp = torch.zeros_like(_grad_of(p))
+        _HOLD['adds'].append((p, tmp))
+        out.append(N.dev_ptr(tmp))
+    return tuple(out)
 
 
 def _held(mod, x, gy, bias_grad, want):
@@ -135,6 +153,10 @@ def replay_held(order):
     """Issue the held calls: those of pass order[0] inside defer_wgrad(), then those of order[1] (each merges with its
     conv's deferred one), then flush_wgrad() -- the launches and the summation order of the serial schedule."""
     calls, _HOLD['calls'] = _HOLD['calls'], []
+    adds, _HOLD['adds'] = _HOLD['adds'], []
+    for p, tmp in adds:   # grad += tmp (tmp = the one fp32 term the kernel would have added): bitwise the same sum
+        g = _grad_of(p)
+        N.call('ssseg_axpby', N.dev_ptr(g), 1.0, N.dev_ptr(tmp), 1.0, N.dev_ptr(g), g.numel(), N.stream())
     with defer_wgrad():
         for tag, mod, args, kw in calls:
             if tag == order[0]:
@@ -1340,8 +1362,7 @@ class _BNFn(torch.autograd.Function):
         N.call('ssseg_bn_bwd_reduce_grad', N.dev_ptr(gy), N.dev_ptr(x), res_p, P, C, cp, cp, cp, N.dev_ptr(mean),
                N.dev_ptr(invstd), N.dev_ptr(wt) if wt is not None else None,
                N.dev_ptr(bs) if bs is not None else None, _act(ctx.relu)[0], N.dt_code(x), N.dev_ptr(sums),
-               N.dev_ptr(ws), nb, N.dev_ptr(_grad_of(mod.weight)) if pgrad else None,
-               N.dev_ptr(_grad_of(mod.bias)) if pgrad else None, N.stream())
+               N.dev_ptr(ws), nb, *(_grad_ptrs(mod.weight, mod.bias) if pgrad else (None, None)), N.stream())
         if pgrad:
             _ready(mod.weight, mod.bias)
         count = ctx.count
@@ -1441,6 +1462,10 @@ class _ConvBNEvalFn(torch.autograd.Function):
                    _act(ctx.relu)[0], N.dt_code(y), N.dev_ptr(part), nb, ctypes.byref(rows), N.stream())
             _PGRAD['pending'].append({'bn': bn, 'part': part, 'nparts': rows.value, 'C': C, 'scale': scale,
                                       'dg': grads[0] or 0, 'db': grads[1] or 0, 'dbias': grads[2] or 0})
+        else:   # immediate parameter gradients (temporaries inside hold_wgrad(params=True))
+            grads = _grad_ptrs(*[p if want(p) else None for p in (bn.weight, bn.bias, conv.bias)])
+        if defer:
+            pass
         elif aux is None:   # x_hat from y (no residual): ssseg_bn_eval_bwd_grad_y
             N.call('ssseg_bn_eval_bwd_grad_y', N.dev_ptr(gy), N.dev_ptr(y), N.dev_ptr(dconv),
                    N.dev_ptr(dres) if dres is not None else None, n * h * w, C, cp, N.dev_ptr(scale), N.dev_ptr(shift),
