@@ -142,6 +142,12 @@ def _grad_ptrs(*params):
     return tuple(out)
 
 
+def clear_held():
+    """Drop held calls left by a backward that raised (their gradients are void with it)."""
+    _HOLD['calls'] = []
+    _HOLD['adds'] = []
+
+
 def _held(mod, x, gy, bias_grad, want):
     if not _HOLD['on']:
         return False

@@ -226,6 +226,7 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
             if side_bwd:
                 # its backward writes no gradient now: the eval BNs' parameter gradients are reduced after the join
                 # (defer_param_grads, left open until then) and the conv weight / bias gradients are held
+                snn.clear_held()
                 pgrad_ctx.enter_context(snn.defer_param_grads())
                 with snn.hold_wgrad('cons', params=True):
                     ops.backward(_scaled(cons[0], optimizer))
