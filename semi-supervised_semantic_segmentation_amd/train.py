@@ -210,51 +210,53 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
     # then run concurrently, their weight / bias gradients held (snn.hold_wgrad) and replayed after both
     side_bwd = overlap and ddp is None and _OVERLAP['consistency'] and _OVERLAP['consistency_bwd']
     pgrad_ctx = contextlib.ExitStack()
-    if overlap:
-        main = torch.cuda.current_stream()
-        side = _side_stream(image.device)
-        side.wait_stream(main)                # the supervised forward (and its running statistics) first
-        for t in (unsup_a, unsup_b):
-            t.record_stream(side)
-        with torch.cuda.stream(side):
-            targets = _teacher_targets(ema_model, unsup_a, unsup_b, tc)
-            if _OVERLAP['consistency']:
-                # the consistency forward needs the student's weights and running statistics as the supervised
-                # forward left them -- the supervised backward changes neither -- so it runs on the side stream
-                # too, concurrently with that backward
-                cons = _consistency_forward(model, targets, tc, epoch)
-            if side_bwd:
-                # its backward writes no gradient now: the eval BNs' parameter gradients are reduced after the join
-                # (defer_param_grads, left open until then) and the conv weight / bias gradients are held
-                snn.clear_held()
-                pgrad_ctx.enter_context(snn.defer_param_grads())
-                with snn.hold_wgrad('cons', params=True):
-                    ops.backward(_scaled(cons[0], optimizer))
-        for t in targets:
-            t.record_stream(main)
-    if ddp is not None and not semi:
-        ddp.arm()
-    # with a consistency backward to follow, each conv's supervised weight gradient is merged into that pass's
-    # (one launch over both batches' pixels; ssseg.nn.defer_wgrad) -- the .grad sum is the same
-    with (snn.hold_wgrad('sup') if side_bwd else snn.defer_wgrad() if semi else contextlib.nullcontext()):
-        vbm = tc['virtual_batch_size_multiplier']
-        ops.backward(_scaled(ops.scale(sup_loss, 1.0 / vbm) if vbm != 1 else sup_loss, optimizer))
-    del pred_maps, features
-    if adv is not None:
-        _set_requires_grad(adv['discriminator'], True)   # frozen since adversarial_terms; the student backward is done
-        adv['last_loss_d'] = discriminator_step(mask, prob, adv)
-        adv['last_loss_adv'] = adv_loss.detach()
-        del prob
-    unsup_loss = cm_mean = None
-    if side_bwd:
-        torch.cuda.current_stream().wait_stream(_side_stream(image.device))
-        unsup_loss, cm_mean = cons
-        del targets, cons
-        snn.replay_held(('sup', 'cons'))   # the serial schedule's weight-gradient launches, on this stream
-        pgrad_ctx.close()                  # the eval BNs' parameter gradients: one batched reduction
-        semi_rest = False
-    else:
-        semi_rest = semi
+    with pgrad_ctx:   # (closed early on the normal path; on an exception it leaves defer_param_grads too)
+        if overlap:
+            main = torch.cuda.current_stream()
+            side = _side_stream(image.device)
+            side.wait_stream(main)                # the supervised forward (and its running statistics) first
+            for t in (unsup_a, unsup_b):
+                t.record_stream(side)
+            with torch.cuda.stream(side):
+                targets = _teacher_targets(ema_model, unsup_a, unsup_b, tc)
+                if _OVERLAP['consistency']:
+                    # the consistency forward needs the student's weights and running statistics as the supervised
+                    # forward left them -- the supervised backward changes neither -- so it runs on the side stream
+                    # too, concurrently with that backward
+                    cons = _consistency_forward(model, targets, tc, epoch)
+                if side_bwd:
+                    # its backward writes no gradient now: the eval BNs' parameter gradients are reduced after the join
+                    # (defer_param_grads, left open until then) and the conv weight / bias gradients are held
+                    snn.clear_held()
+                    pgrad_ctx.enter_context(snn.defer_param_grads())
+                    with snn.hold_wgrad('cons', params=True):
+                        ops.backward(_scaled(cons[0], optimizer))
+            for t in targets:
+                t.record_stream(main)
+        if ddp is not None and not semi:
+            ddp.arm()
+        # with a consistency backward to follow, each conv's supervised weight gradient is merged into that pass's
+        # (one launch over both batches' pixels; ssseg.nn.defer_wgrad) -- the .grad sum is the same
+        with (snn.hold_wgrad('sup') if side_bwd else snn.defer_wgrad() if semi else contextlib.nullcontext()):
+            vbm = tc['virtual_batch_size_multiplier']
+            ops.backward(_scaled(ops.scale(sup_loss, 1.0 / vbm) if vbm != 1 else sup_loss, optimizer))
+        del pred_maps, features
+        if adv is not None:
+            # frozen since adversarial_terms; the student backward is done
+            _set_requires_grad(adv['discriminator'], True)
+            adv['last_loss_d'] = discriminator_step(mask, prob, adv)
+            adv['last_loss_adv'] = adv_loss.detach()
+            del prob
+        unsup_loss = cm_mean = None
+        if side_bwd:
+            torch.cuda.current_stream().wait_stream(_side_stream(image.device))
+            unsup_loss, cm_mean = cons
+            del targets, cons
+            snn.replay_held(('sup', 'cons'))   # the serial schedule's weight-gradient launches, on this stream
+            pgrad_ctx.close()                  # the eval BNs' parameter gradients: one batched reduction
+            semi_rest = False
+        else:
+            semi_rest = semi
     with snn.wgrad_side_stream():
         if semi_rest:
             if overlap:
