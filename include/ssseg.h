@@ -324,7 +324,11 @@ int ssseg_conv_igemm_epi(const void* x, const void* w, void* y, const ssseg_conv
  * SSSEG_ACT_RELU or SSSEG_ACT_LEAKY with its slope; the discriminator's Conv4x4 + LeakyReLU(0.2) pairs,
  * discriminator.py:14-17): epi->residual is that y (not an addend), and the stored value is the activation's backward
  * applied in place, (y > 0 ? v : v * slope) -- the producer's separate activation-backward pass is not needed.
- * epi carries no scale / shift / activation / statistics / aux. */
+ * epi carries no shift / activation / aux.  Optional: epi->scale multiplies the masked value (a folded eval
+ * BatchNorm's backward, dconv = scale * mask(dy)); epi->stats makes the rows the GRADIENT statistics of the
+ * BatchNorm that produced y: per tile row r, (sum m, sum m * y) of the masked value m before the scale, rounded to
+ * the output type (fp64 sums) -- reduce them with ssseg_bn_gstat_finalize instead of a ssseg_bn_bwd_reduce pass over
+ * dy and x (the reference's BN backward, unet.py:9-10 / resnet Bottleneck bn1, bn2 -> ReLU -> next conv). */
 int ssseg_conv_igemm_epi_actmask(const void* x, const void* w, void* y, const ssseg_conv_desc* desc_host, int dt,
                                  int dt_out, const ssseg_conv_epilogue* epi, int act, float slope, void* ws,
                                  size_t ws_bytes, ssseg_stream_t stream);
@@ -495,6 +499,16 @@ int ssseg_bn_stats_finalize(const void* x, int64_t P, int64_t C, int64_t ldx, in
 int ssseg_bn_partials_finalize(double* part, int64_t nparts, int64_t C, double* sums, double count, float eps,
                                float momentum, float* mean_out, float* invstd_out, float* running_mean,
                                float* running_var, int64_t* num_batches_tracked, ssseg_stream_t stream);
+/* The backward sums of a BatchNorm(+ReLU) from the gradient-statistics rows of its consumer's input-gradient launch
+ * (ssseg_conv_igemm_epi_actmask with stats): sums[0:C] = sum m, sums[C:2C] = sum m * x_hat, with x_hat recovered from
+ * y wherever m != 0 -- training BN (mean_eff NULL): x_hat = (y - beta) / gamma (gamma / beta NULL: 1 / 0); folded
+ * eval BN (mean_eff non-NULL, gamma = its scale, beta = its shift): x_hat = (y - mean_eff*scale - shift) * invstd /
+ * scale.  A channel whose gamma (scale) is 0 gets sum m * x_hat = 0 (y carries no x_hat there).  Then dbeta += sums[c],
+ * dgamma += sums[C + c], dconv_bias += scale * sums[c] (eval only) for the non-NULL ones.  part is scratch as in
+ * ssseg_bn_partials_finalize; sums feed ssseg_bn_bwd_apply (train = 1, relu = 0: dy is the masked gradient). */
+int ssseg_bn_gstat_finalize(double* part, int64_t nparts, int64_t C, double* sums, const float* gamma,
+                            const float* beta, const float* mean_eff, const float* invstd, float* dgamma, float* dbeta,
+                            float* dconv_bias, ssseg_stream_t stream);
 /* eval mode: mean = running_mean, invstd = 1/sqrt(running_var + eps) */
 int ssseg_bn_eval_params(const float* running_mean, const float* running_var, float eps, int64_t C, float* mean_out,
                          float* invstd_out, ssseg_stream_t stream);
@@ -552,7 +566,9 @@ int ssseg_bn_eval_bwd_part(const void* dy, const void* y, const void* aux, void*
                            ssseg_stream_t stream);
 /* ONE launch for many deferred reductions: per descriptor, dbeta[c] += sum of part rows 2r, dgamma[c] += sum of rows
  * 2r + 1, dconv_bias[c] += scale[c] * (the first sum) (NULL pointers skipped); fixed-order fp64 column sums.  descs
- * points to DEVICE memory; max_c >= every descriptor's C. */
+ * points to DEVICE memory; max_c >= every descriptor's C.  mean_eff non-NULL: the rows are gradient-statistics rows
+ * (sum m, sum m * y) of a consumer's input-gradient launch, turned into the x_hat moment as ssseg_bn_gstat_finalize
+ * does for a folded eval BN (scale, shift, mean_eff, invstd) before the same tail. */
 typedef struct ssseg_pgrad_desc {
   const double* part;
   int64_t nparts, C;
@@ -560,6 +576,9 @@ typedef struct ssseg_pgrad_desc {
   float* dgamma;
   float* dbeta;
   float* dconv_bias;
+  const float* shift;      /* gradient-statistics rows only (else NULL) */
+  const float* mean_eff;
+  const float* invstd;
 } ssseg_pgrad_desc;
 int ssseg_bn_param_grad_batch(const ssseg_pgrad_desc* descs, int64_t n, int64_t max_c, ssseg_stream_t stream);
 /* y = act(gamma*(x-mean)*invstd + beta [+ residual]); channels [C, rup(C, 16 bytes)) of y are written 0; relu = 1 for ReLU (unet.py:10, Bottleneck add+relu) */

@@ -300,7 +300,26 @@ struct FinalEpi {
   float *dgamma, *dbeta;
   const float* scale;   // mode 2, folded eval BN: dbias += scale * sums[0:C]
   float* dbias;
+  // mode 3 (gradient statistics from a dgrad epilogue, rows of (sum m, sum m * y)): sum m * x_hat = (sum m * y -
+  // B * sum m) * A with training: B = beta, A = 1 / gamma; folded eval (gmean set): B = mean_eff * scale + shift,
+  // A = invstd / scale (A = 0 where gamma / scale is 0: x_hat is not recoverable from y there); then mode 2's tail
+  const float *ggamma, *gbeta, *gmean, *ginvstd;
 };
+
+// mode 3: the x_hat moment of channel c from the (sum m, sum m * y) moments
+__device__ __forceinline__ double gstat_xhat_moment(const FinalEpi& fe, int c, double a, double b) {
+  double B, A;
+  if (fe.gmean) {
+    const float sc = fe.ggamma[c];
+    B = (double)fe.gmean[c] * sc + (fe.gbeta ? fe.gbeta[c] : 0.f);
+    A = sc != 0.f ? (double)fe.ginvstd[c] / sc : 0.0;
+  } else {
+    const float ga = fe.ggamma ? fe.ggamma[c] : 1.f;
+    B = fe.gbeta ? fe.gbeta[c] : 0.f;
+    A = ga != 0.f ? 1.0 / ga : 0.0;
+  }
+  return (b - B * a) * A;
+}
 
 __device__ __forceinline__ void finalize_channel(double s1, double s2, int c, double count, float eps, float momentum,
                                                  float* mean_out, float* invstd_out, float* rmean, float* rvar) {
@@ -408,11 +427,12 @@ __global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* par
   partial_col_sums<CH>(part, nparts, C, rs, blockIdx.x, a, b);
   const int c = blockIdx.x * CH + threadIdx.x;
   if (threadIdx.x < CH && c < C) {
+    if (fe.mode == 3) b = gstat_xhat_moment(fe, c, a, b);
     sums[c] = a;
     sums[C + c] = b;
     if (fe.mode == 1) {
       finalize_channel(a, b, c, fe.count, fe.eps, fe.momentum, fe.mean_out, fe.invstd_out, fe.rmean, fe.rvar);
-    } else if (fe.mode == 2) {
+    } else if (fe.mode >= 2) {
       if (fe.dbeta) fe.dbeta[c] += (float)a;
       if (fe.dgamma) fe.dgamma[c] += (float)b;
       if (fe.dbias) fe.dbias[c] += fe.scale[c] * (float)a;
@@ -430,6 +450,14 @@ __global__ void __launch_bounds__(256) bn_pgrad_batch_kernel(const ssseg_pgrad_d
   partial_col_sums<8>(d.part, (int)d.nparts, C, 1, blockIdx.x, a, b);
   const int c = blockIdx.x * 8 + threadIdx.x;
   if (threadIdx.x < 8 && c < C) {
+    if (d.mean_eff) {   // gradient-statistics rows: (sum m, sum m * y) -> (sum m, sum m * x_hat)
+      FinalEpi fe{};
+      fe.ggamma = d.scale;
+      fe.gbeta = d.shift;
+      fe.gmean = d.mean_eff;
+      fe.ginvstd = d.invstd;
+      b = gstat_xhat_moment(fe, c, a, b);
+    }
     if (d.dbeta) d.dbeta[c] += (float)a;
     if (d.dgamma) d.dgamma[c] += (float)b;
     if (d.dconv_bias) d.dconv_bias[c] += d.scale[c] * (float)a;
@@ -898,6 +926,27 @@ extern "C" int ssseg_bn_partials_finalize(double* part, int64_t nparts, int64_t 
     fe.rvar = running_var;
     fe.nbt = num_batches_tracked;
   }
+  launch_partial_final(part, nparts, C, sums, (hipStream_t)stream, fe);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_bn_gstat_finalize(double* part, int64_t nparts, int64_t C, double* sums, const float* gamma,
+                                       const float* beta, const float* mean_eff, const float* invstd, float* dgamma,
+                                       float* dbeta, float* dconv_bias, ssseg_stream_t stream) {
+  if (!part || !sums || nparts < 1 || C < 1 || nparts > 0x7fffffff) return SSSEG_EINVAL;
+  if (mean_eff && (!gamma || !invstd)) return SSSEG_EINVAL;   // folded eval: scale, (shift,) mean_eff, invstd
+  if (dconv_bias && !mean_eff) return SSSEG_EINVAL;
+  FinalEpi fe{};
+  fe.mode = 3;
+  fe.dgamma = dgamma;
+  fe.dbeta = dbeta;
+  fe.scale = gamma;
+  fe.dbias = dconv_bias;
+  fe.ggamma = gamma;
+  fe.gbeta = beta;
+  fe.gmean = mean_eff;
+  fe.ginvstd = invstd;
   launch_partial_final(part, nparts, C, sums, (hipStream_t)stream, fe);
   SSSEG_LAUNCH_CHECK();
   return 0;

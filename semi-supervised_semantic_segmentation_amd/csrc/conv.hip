@@ -389,7 +389,7 @@ int dispatch_igemm(const void* x, const void* w, void* y, const ConvGeom& g, con
       if (v == 0) {
         const unsigned long long key =
             geom_key(g, (int)sizeof(TO) * 8 + (ep.stats ? 4 : 0) + (ep.res ? 2 : 0) + (ep.scale ? 1 : 0) + 16 * S +
-                        256 * nph + (x2 ? 4096 * (g.c1b + 1) : 0) + (ep.y2 ? (1 << 24) : 0) + (ep.rmask ? (1 << 25) : 0));
+                        256 * nph + (x2 ? 4096 * (g.c1b + 1) : 0) + (ep.y2 ? (1 << 24) : 0) + (ep.rmask ? (1 << 25) : 0) + (ep.gstat ? (1 << 26) : 0));
         std::lock_guard<std::mutex> lk(g_variant_mu);
         auto it = g_variant.find(key);
         if (it != g_variant.end()) {
@@ -483,8 +483,10 @@ static int conv_igemm_epi(const void* x, const void* x2, int64_t c1, int64_t ldx
   const ssseg_conv_epilogue& e = epi ? *epi : none;
   if (e.residual && ((!ysplit && e.ldr < g.K) || e.ldr > 0x7fffffff)) return SSSEG_EINVAL;
   if (e.stats && (!e.stats_rows_host || e.stats_ld < 1 || e.stats_ld > g.K)) return SSSEG_EINVAL;
-  // fused statistics are of acc + shift: the conv feeding a training BatchNorm has no affine / residual / act
-  if (e.stats && (e.scale || e.residual || e.relu || e.aux)) return SSSEG_EINVAL;
+  // fused statistics are of acc + shift: the conv feeding a training BatchNorm has no affine / residual / act (with
+  // mask_act they are the gradient statistics of a BatchNorm backward instead: Epi::gstat)
+  const bool gst = mask_act != 0 && e.stats != nullptr;
+  if (e.stats && !gst && (e.scale || e.residual || e.relu || e.aux)) return SSSEG_EINVAL;
   if (e.stats_rows_host) *e.stats_rows_host = 0;
   if (g.M == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
@@ -496,11 +498,13 @@ static int conv_igemm_epi(const void* x, const void* x2, int64_t c1, int64_t ldx
   Epi<f16_t> eh{e.scale, e.shift, (const f16_t*)e.residual, (int)e.ldr, e.relu, (f16_t*)e.aux, e.slope,
                 e.stats, (int)e.stats_ld};
   if (mask_act) {   // the residual is the input's producer's activation output: its backward applied in place
-    if (ysplit || x2 || !e.residual || e.stats || e.aux || e.relu || e.scale || e.shift ||
+    // (a scale multiplies the masked value: the folded eval BatchNorm's backward, dconv = scale * mask(dy))
+    if (ysplit || x2 || !e.residual || e.aux || e.relu || e.shift ||
         (mask_act != SSSEG_ACT_RELU && mask_act != SSSEG_ACT_LEAKY))
       return SSSEG_EINVAL;
     ef.rmask = eb.rmask = eh.rmask = mask_act;
     ef.rslope = eb.rslope = eh.rslope = mask_slope;
+    ef.gstat = eb.gstat = eh.gstat = gst ? 1 : 0;
   }
   if (ysplit) {   // split output: channels [c1, K) to ysplit->x2 (pixel stride ldx2); 16-bit, plain epilogue
     const int64_t oc1 = ysplit->c1, ld2 = ysplit->ldx2;

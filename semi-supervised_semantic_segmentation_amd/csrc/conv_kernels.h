@@ -188,7 +188,11 @@ struct Epi {
   // (res > 0 ? v : 0) or (res > 0 ? v : v * rslope), channels >= oc1 read no res
   int rmask = 0;
   float rslope = 0.f;   // rmask == SSSEG_ACT_LEAKY: (res > 0 ? v : v * rslope) (the producer's LeakyReLU backward)
-  int sdbg = 0;   // experiment switch for the fused statistics (knob 12): 1 no sums, 2 no tile_stats, 4 no row write,
+  // gstat (with rmask and stats): the statistics rows hold (sum m, sum m * res) of the masked gradient m BEFORE the
+  // scale, rounded to TO -- the two sums a BatchNorm backward reduces (res = its output y, from which x_hat follows
+  // wherever m != 0); the stored value is scale * m
+  int gstat = 0;
+  int sdbg = 0;  // experiment switch for the fused statistics (knob 12): 1 no sums, 2 no tile_stats, 4 no row write,
                   // 8 no cross-lane shuffles
 };
 
@@ -351,9 +355,17 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[FN][FM], long long
         v[e] = a;
         if constexpr (ST) {   // compile-time: the statistics arrays stay in registers
           if (n + e < g.K) {
-            const double q = (double)stored<TO>(a);
-            st1[i][e] += q;
-            st2[i][e] += q * q;
+            if (ep.gstat) {   // (sum m, sum m * res) of the unscaled masked gradient m
+              float m = acc[i][j][e];
+              if (n < ep.oc1 && !(r[j][e] > 0.f)) m = ep.rmask == SSSEG_ACT_LEAKY ? m * ep.rslope : 0.f;
+              const double q = (double)stored<TO>(m);
+              st1[i][e] += q;
+              st2[i][e] += q * (double)r[j][e];
+            } else {
+              const double q = (double)stored<TO>(a);
+              st1[i][e] += q;
+              st2[i][e] += q * q;
+            }
           }
         }
       }
@@ -449,7 +461,7 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
   // and reduced them with 48 LDS permutes + 2 barriers per tile).  ep.sdbg & 16 = that older path (A/B).
   constexpr int WTM = FM * 16, WM_ = BM / WTM;
   constexpr bool REGST = STATS && BN <= 32 * FM;
-  const bool regst = REGST && !(ep.sdbg & 16);
+  const bool regst = REGST && !(ep.sdbg & 16) && !ep.gstat;   // (gradient statistics: the store pass, below)
   float rs1[REGST ? FN : 1][4], rs2[REGST ? FN : 1][4];
   if constexpr (REGST) {
     if (regst) {
@@ -611,12 +623,23 @@ __device__ __forceinline__ void store_tile_lds(const f32x4 (&acc)[FN][FM], char*
         act8(v, ep.relu, ep.slope);
       }
       if constexpr (STATS) {
-        if (!regst && !(ep.sdbg & 1))
+        if (ep.gstat) {   // (sum m, sum m * res) of the unscaled masked gradient (bf16 x bf16: exact fp32 products)
+          const float ms = ep.rmask == SSSEG_ACT_LEAKY ? ep.rslope : 0.f;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const SA q = n + e < g.K ? (SA)stored<TO>(v[e]) : (SA)0;
-          s1[e] += q;
-          s2[e] += q * q;
+          for (int e = 0; e < 8; ++e) {
+            const float m = (n < ep.oc1 && !(r[p][e] > 0.f)) ? (ep.rmask == SSSEG_ACT_LEAKY ? raw[e] * ms : 0.f)
+                                                              : raw[e];
+            const SA q = n + e < g.K ? (SA)stored<TO>(m) : (SA)0;
+            s1[e] += q;
+            s2[e] += q * (SA)r[p][e];
+          }
+        } else if (!regst && !(ep.sdbg & 1)) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const SA q = n + e < g.K ? (SA)stored<TO>(v[e]) : (SA)0;
+            s1[e] += q;
+            s2[e] += q * q;
+          }
         }
       }
       const long long o = op[p] * g.ldy + n;

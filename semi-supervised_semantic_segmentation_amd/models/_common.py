@@ -28,11 +28,12 @@ class ConvBlock(nn.Module):
             nn.ReLU(),
         )
 
-    def forward(self, x):
+    def forward(self, x, single_use=False):
+        """single_use: the output feeds exactly one conv (UpBlock conv3_0 -> conv3_1; snn.conv_bn_act)."""
         conv, norm, _ = self.conv_block
         if isinstance(norm, nn.Identity):
             return conv.forward_relu(x)
-        return snn.conv_bn_act(conv, x, norm, relu=True)
+        return snn.conv_bn_act(conv, x, norm, relu=True, single_use=single_use)
 
 
 def center_crop(tensor, target_size):

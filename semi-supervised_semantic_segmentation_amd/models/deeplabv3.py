@@ -48,8 +48,8 @@ class Bottleneck(nn.Module):
             identity = snn.conv_bn_act(conv, x, bn, relu=False)
         else:
             identity = x
-        out = snn.conv_bn_act(self.conv1, x, self.bn1)
-        out = snn.conv_bn_act(self.conv2, out, self.bn2)
+        out = snn.conv_bn_act(self.conv1, x, self.bn1, single_use=True)
+        out = snn.conv_bn_act(self.conv2, out, self.bn2, single_use=True)
         return snn.conv_bn_act(self.conv3, out, self.bn3, relu=True, residual=identity)
 
 

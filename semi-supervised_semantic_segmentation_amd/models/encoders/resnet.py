@@ -35,8 +35,8 @@ class Bottleneck(nn.Module):
             shortcut = x
         # identity shortcut: its gradient is added in conv1's dgrad epilogue (snn.GradHandoff)
         h = snn.GradHandoff() if self.downsample is None else None
-        y = snn.conv_bn_act(self.conv1, x, self.bn1, grad_in=h)
-        y = snn.conv_bn_act(self.conv2, y, self.bn2)
+        y = snn.conv_bn_act(self.conv1, x, self.bn1, grad_in=h, single_use=True)
+        y = snn.conv_bn_act(self.conv2, y, self.bn2, single_use=True)
         return snn.conv_bn_act(self.conv3, y, self.bn3, relu=True, residual=shortcut, grad_out=h)
 
 

@@ -38,7 +38,7 @@ class UpBlock(nn.Module):
         x = self._upsample(x)
         # conv3_0 is the concat's only consumer: it reads [x | skip] part by part (virtual concat, no copy)
         x = snn.cat_crop(x, skip, self.out_channels, self.skip_channels, lazy=True)
-        return self.conv3_1(self.conv3_0(x))
+        return self.conv3_1(self.conv3_0(x, single_use=True))
 
 
 class UNet(nn.Module):

@@ -23,7 +23,16 @@ from . import native as N
 _CFG = {'act_mask': os.environ.get('SSSEG_ACT_MASK', '1') != '0',
         'grad_join': True, 'stem': True, 'phases': True, 'eval_bwd_y': True, 'dtype': torch.bfloat16, 'sync_bn': True,
         'fuse_stats': True, 'vcat': os.environ.get('SSSEG_VCAT', '1') != '0',
-        'vpad': os.environ.get('SSSEG_VPAD', '1') != '0'}
+        'vpad': os.environ.get('SSSEG_VPAD', '1') != '0',
+        'bn_gstat': os.environ.get('SSSEG_BN_GSTAT', '1') != '0'}
+
+
+def set_bn_grad_stats(on):
+    """A training BN(+ReLU) whose output feeds exactly one conv (conv_bn_act(..., single_use=True)): that conv's
+    input-gradient launch applies the ReLU backward and writes the BN backward's two channel sums in its epilogue
+    (ssseg_conv_igemm_epi_actmask with stats), so the BN backward skips its reduction pass over dy and x (default
+    on)."""
+    _CFG['bn_gstat'] = bool(on)
 
 
 def set_virtual_concat(on):
@@ -201,20 +210,27 @@ def flush_param_grads():
     pend, _PGRAD['pending'] = _PGRAD['pending'], []
     if not pend:
         return
+    # (gradient-statistics rows of a consumer's input-gradient launch carry their x_hat transform: shift, mean_eff,
+    # invstd; ssseg_pgrad_desc)
     rows = tuple((e['part'].data_ptr(), e['nparts'], e['C'], e['scale'].data_ptr(), e['dg'], e['db'], e['dbias'])
-                 for e in pend)
+                 + (e.get('gs') or (0, 0, 0)) for e in pend)
     ent = _PGRAD['table']
     if ent is None or ent[0] != rows:
         if torch.cuda.is_current_stream_capturing():
             # (a new descriptor table needs a host-to-device copy): reduce each layer on its own
             for e in pend:
                 sums = torch.empty(2 * e['C'], dtype=torch.float64, device=e['part'].device)
+                if e.get('gs'):
+                    N.call('ssseg_bn_gstat_finalize', N.dev_ptr(e['part']), e['nparts'], e['C'], N.dev_ptr(sums),
+                           N.dev_ptr(e['scale']), *e['gs'], e['dg'] or None, e['db'] or None, e['dbias'] or None,
+                           N.stream())
+                    continue
                 N.call('ssseg_bn_partials_finalize', N.dev_ptr(e['part']), e['nparts'], e['C'], N.dev_ptr(sums), 0.0,
                        0.0, 0.0, None, None, None, None, None, N.stream())
                 N.call('ssseg_bn_eval_param_grad', N.dev_ptr(sums), e['C'], N.dev_ptr(e['scale']), e['dg'] or None,
                        e['db'] or None, e['dbias'] or None, N.stream())
             return
-        blob = b''.join(struct.pack('<7q', *r) for r in rows)
+        blob = b''.join(struct.pack('<10q', *r) for r in rows)
         ent = (rows, torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(pend[0]['part'].device))
         _PGRAD['table'] = ent
     N.call('ssseg_bn_param_grad_batch', N.dev_ptr(ent[1]), len(rows), max(e['C'] for e in pend), N.stream())
@@ -575,10 +591,12 @@ class StatRows:
     reading y again."""
     __slots__ = ('part', 'C', 'rows', 'cap', '_out')
 
-    def __init__(self, C, max_rows, device):
+    def __init__(self, C, max_rows, device, part=None):
         import ctypes
         self.C, self.cap, self.rows = int(C), int(max_rows), 0
-        self.part = torch.empty(2 * self.cap * self.C, dtype=torch.float64, device=device)
+        need = 2 * self.cap * self.C
+        ok = part is not None and part.numel() >= need and part.device == torch.device(device)
+        self.part = part if ok else torch.empty(need, dtype=torch.float64, device=device)
         self._out = ctypes.c_int64(0)
 
     def launch_fields(self):
@@ -600,6 +618,7 @@ class _ConvFn(torch.autograd.Function):
         y = mod._ssseg_forward(x, relu, stats=stats)
         ctx.mod, ctx.relu, ctx.handoff, ctx.join, ctx.vcat = mod, relu, handoff, join, _vcat_of(x)
         ctx.xmask = x.__dict__.get('_ssseg_act_out')   # x = a single-use activation output: mask in our dgrad
+        ctx.xgstat = x.__dict__.get('_ssseg_gstat')   # ... of a training BN: its backward sums in our dgrad too
         ctx.save_for_backward(x, y if _act(relu)[0] else None)
         if _act(relu)[0] == ACT_RELU:
             # a ReLU output: a consumer's input-gradient launch may apply this ReLU's backward in place (the
@@ -626,13 +645,38 @@ class _ConvFn(torch.autograd.Function):
         pending = _sum_pending(_take(ctx.handoff), joined)
         if not ctx.needs_input_grad[0]:
             dx = None
-        elif (ctx.xmask is not None and pending is None and ctx.vcat is None and _CFG['act_mask']
-              and getattr(mod, '_ssseg_mask_dgrad_ok', lambda: False)()):
-            dx = mod._ssseg_dgrad(gy, x.shape, mask=(x,) + tuple(ctx.xmask))
-            dx.__dict__['_ssseg_premasked'] = True
         else:
-            dx = _dgrad_acc(mod, gy, x.shape, pending, ctx.vcat)
+            dx = _masked_dgrad(mod, gy, x, ctx.xmask, ctx.xgstat, pending, ctx.vcat)
+            if dx is None:
+                dx = _dgrad_acc(mod, gy, x.shape, pending, ctx.vcat)
         return _join_give(ctx.join, last, dx), None, None, None, None, None, None, None
+
+
+def _masked_dgrad(conv, gy, x, xmask, xgstat, pending, vc):
+    """The input gradient of a conv whose input x is the single-use activation output of its producer (xmask = (act,
+    slope)): the producer's activation backward is applied in the epilogue (ssseg_conv_igemm_epi_actmask), and for a
+    BN(+ReLU) producer (xgstat = (C, scale, bn)) that BN's backward sums are written as gradient-statistics rows and a
+    folded eval BN's scale (scale not None) is applied: the producer's backward then skips its reduction (and, eval,
+    its whole elementwise pass).  None where the engine cannot (the caller runs the plain dgrad)."""
+    if not (xmask is not None and pending is None and vc is None and _CFG['act_mask']
+            and getattr(conv, '_ssseg_mask_dgrad_ok', lambda: False)()):
+        return None
+    sr = scale = None
+    if xgstat is not None and _CFG['bn_gstat'] and conv._ssseg_gstat_ok():
+        C, scale, bn = xgstat
+        n, _, H, W = x.shape
+        buf = None
+        if scale is not None and not any(e['bn'] is bn for e in _PGRAD['pending']):
+            buf = bn.__dict__.get('_ssseg_gs_part')   # (a deferred eval BN keeps its rows until the flush)
+        sr = StatRows(C, (n * H * W + 63) // 64 + 4, x.device, part=buf)
+        if scale is not None:
+            bn.__dict__['_ssseg_gs_part'] = sr.part
+    dx = conv._ssseg_dgrad(gy, x.shape, mask=(x,) + tuple(xmask), stats=sr, scale=scale)
+    dx.__dict__['_ssseg_premasked'] = True
+    if sr is not None:
+        dx.__dict__['_ssseg_gstats'] = sr
+        dx.__dict__['_ssseg_prescaled'] = scale is not None
+    return dx
 
 
 def _dgrad_acc(mod, gy, xshape, pending, vc=None):
@@ -1025,9 +1069,22 @@ class Conv2d(nn.Conv2d, _ConvBase):
     def _ssseg_mask_dgrad_ok(self):
         return not self._ssseg_dw and _CFG['dtype'] in (torch.bfloat16, torch.float16, torch.float32)
 
-    def _ssseg_dgrad(self, gy, xshape, residual=None, mask=None):
+    def _ssseg_gstat_ok(self):
+        """Gradient statistics in the masked dgrad: every output phase has taps (an empty phase's zero launch
+        writes no statistics rows)."""
+        (R, S), (sh, sw) = self.kernel_size, self.stride
+        return (sh == 1 and sw == 1) or (R >= sh and S >= sw and self.dilation in (1, (1, 1)))
+
+    def _ssseg_dgrad(self, gy, xshape, residual=None, mask=None, stats=None, scale=None):
         """dx of the conv; `residual` (a pending gradient of x, GradHandoff) is added in the epilogue; `mask` = (y,
-        act, slope): x was the activation output y of its producer, whose backward the epilogue applies in place."""
+        act, slope): x was the activation output y of its producer, whose backward the epilogue applies in place;
+        `stats` (with mask, a StatRows): the epilogue also writes that producer BN's backward sums (gradient
+        statistics rows, ssseg_conv_igemm_epi_actmask); `scale` (with mask): per-channel factor of the stored value
+        (a folded eval BN producer's scale: dx is that producer's conv-output gradient)."""
+        if (stats is not None or scale is not None) and (mask is None or residual is not None):
+            raise ValueError('ssseg.nn.Conv2d: gradient statistics / scale need the masked input gradient')
+        fold = (None, None, residual, None) if residual is not None else (
+            (scale, None, None, None) if scale is not None else None)
         cin, cout = self._dims()
         n, _, H, W = xshape
         (R, S), (sh, sw), (ph, pw), (dh, dw) = self.kernel_size, self.stride, self.padding, self.dilation
@@ -1051,8 +1108,7 @@ class Conv2d(nn.Conv2d, _ConvBase):
                       py=ph - (R - 1) * dh, px=pw - (S - 1) * dw, outH=H, outW=W, osy=1, osx=1, ooy=0, oox=0,
                       ldy=cin, ldw=R * S * ce)
             with timer:
-                self._igemm(gy, w, dx, d, N.dt_code(dx),
-                            fold=(None, None, residual, None) if residual is not None else None, mask=mask)
+                self._igemm(gy, w, dx, d, N.dt_code(dx), fold=fold, mask=mask, stats=stats)
             return dx
         timer.__enter__()
         for (phy, ry0, rny, dly, qy) in _phases(sh, ph, R, H, dh):
@@ -1067,8 +1123,7 @@ class Conv2d(nn.Conv2d, _ConvBase):
                           ldw=max(rr * ss * ce, ce))
                 # each phase adds the pending gradient at its own output pixels (the residual is indexed by
                 # the output pixel, so the phases together cover it exactly once)
-                self._igemm(gy, w, dx, d, N.dt_code(dx),
-                            fold=(None, None, residual, None) if residual is not None else None, mask=mask)
+                self._igemm(gy, w, dx, d, N.dt_code(dx), fold=fold, mask=mask, stats=stats)
         timer.__exit__()
         return dx
 
@@ -1293,7 +1348,7 @@ def _pad16(C, dtype):
 
 class _BNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, mod, relu, handoff=None, pre=None):
+    def forward(ctx, x, weight, bias, residual, mod, relu, handoff=None, pre=None, single_use=False):
         C = mod.num_features
         n, cp, h, w = x.shape
         P = n * h * w
@@ -1346,6 +1401,12 @@ class _BNFn(torch.autograd.Function):
                N.dev_ptr(bs) if bs is not None else None, _act(relu)[0], N.dt_code(x), N.stream())
         ctx.save_for_backward(x, residual, mean, invstd)
         ctx.mod, ctx.relu, ctx.training, ctx.count, ctx.handoff = mod, relu, training, count, handoff
+        if single_use and training and residual is None and _act(relu)[0] == ACT_RELU and _CFG['bn_gstat']:
+            # y feeds exactly one conv (the caller's guarantee): that conv's input-gradient launch applies this
+            # ReLU's backward and writes this BN's backward sums (_ConvFn.backward); backward() then skips its
+            # reduction pass
+            y.__dict__['_ssseg_act_out'] = (ACT_RELU, 0.0)
+            y.__dict__['_ssseg_gstat'] = (C, None, mod)
         return y
 
     @staticmethod
@@ -1364,11 +1425,20 @@ class _BNFn(torch.autograd.Function):
         ws = N.workspace(nb, dev)
         res_p = N.dev_ptr(residual) if residual is not None else None
         pgrad = mod.weight is not None and ctx.needs_input_grad[1]   # forward-time requires_grad
-        # reduction + (dgamma, dbeta) from the local sums in one launch (ssseg_bn_bwd_reduce_grad)
-        N.call('ssseg_bn_bwd_reduce_grad', N.dev_ptr(gy), N.dev_ptr(x), res_p, P, C, cp, cp, cp, N.dev_ptr(mean),
-               N.dev_ptr(invstd), N.dev_ptr(wt) if wt is not None else None,
-               N.dev_ptr(bs) if bs is not None else None, _act(ctx.relu)[0], N.dt_code(x), N.dev_ptr(sums),
-               N.dev_ptr(ws), nb, *(_grad_ptrs(mod.weight, mod.bias) if pgrad else (None, None)), N.stream())
+        # the consumer's input-gradient launch applied the ReLU backward already (and may have written our sums)
+        act = 0 if gy.__dict__.get('_ssseg_premasked', False) else _act(ctx.relu)[0]
+        gs = gy.__dict__.get('_ssseg_gstats')
+        if gs is not None and ctx.training and gs.rows > 0 and gs.C == C and residual is None and act == 0:
+            # (sum dy, sum dy * y) rows from that epilogue -> (sum dy, sum dy * x_hat) + (dgamma, dbeta)
+            N.call('ssseg_bn_gstat_finalize', N.dev_ptr(gs.part), gs.rows, C, N.dev_ptr(sums),
+                   N.dev_ptr(wt) if wt is not None else None, N.dev_ptr(bs) if bs is not None else None, None, None,
+                   *(_grad_ptrs(mod.weight, mod.bias) if pgrad else (None, None)), None, N.stream())
+        else:
+            # reduction + (dgamma, dbeta) from the local sums in one launch (ssseg_bn_bwd_reduce_grad)
+            N.call('ssseg_bn_bwd_reduce_grad', N.dev_ptr(gy), N.dev_ptr(x), res_p, P, C, cp, cp, cp, N.dev_ptr(mean),
+                   N.dev_ptr(invstd), N.dev_ptr(wt) if wt is not None else None,
+                   N.dev_ptr(bs) if bs is not None else None, act, N.dt_code(x), N.dev_ptr(sums),
+                   N.dev_ptr(ws), nb, *(_grad_ptrs(mod.weight, mod.bias) if pgrad else (None, None)), N.stream())
         if pgrad:
             _ready(mod.weight, mod.bias)
         count = ctx.count
@@ -1380,12 +1450,12 @@ class _BNFn(torch.autograd.Function):
         N.call('ssseg_bn_bwd_apply', N.dev_ptr(gy), N.dev_ptr(x), res_p, N.dev_ptr(dx),
                N.dev_ptr(dres) if dres is not None else None, P, C, cp, cp, cp, cp, N.dev_ptr(mean),
                N.dev_ptr(invstd), N.dev_ptr(wt) if wt is not None else None,
-               N.dev_ptr(bs) if bs is not None else None, _act(ctx.relu)[0], int(bool(ctx.training)),
+               N.dev_ptr(bs) if bs is not None else None, act, int(bool(ctx.training)),
                N.dev_ptr(sums), float(count), N.dt_code(x), N.stream())
         if dres is not None and ctx.handoff is not None:
             ctx.handoff.put(dres)
             dres = None
-        return dx, None, None, dres, None, None, None, None
+        return dx, None, None, dres, None, None, None, None, None
 
 
 class BatchNorm2d(nn.BatchNorm2d):
@@ -1412,7 +1482,8 @@ class _ConvBNEvalFn(torch.autograd.Function):
     (and the residual's) plus the BN parameter sums in one pass; then the ordinary conv backward."""
 
     @staticmethod
-    def forward(ctx, x, cweight, cbias, gamma, beta, residual, conv, bn, relu, grad_in=None, grad_out=None, join=None):
+    def forward(ctx, x, cweight, cbias, gamma, beta, residual, conv, bn, relu, grad_in=None, grad_out=None, join=None,
+                single_use=False):
         # without a residual, y itself carries the pre-activation wherever the gradient survives the activation:
         # no raw accumulator copy (ssseg_bn_eval_bwd_grad_y recovers x_hat from y)
         ycopy = residual is None and _CFG['eval_bwd_y']
@@ -1421,6 +1492,14 @@ class _ConvBNEvalFn(torch.autograd.Function):
         ctx.save_for_backward(x, y, aux, scale, mean_eff, invstd, shift)
         ctx.conv, ctx.bn, ctx.relu, ctx.has_res = conv, bn, relu, residual is not None
         ctx.grad_in, ctx.grad_out, ctx.join, ctx.vcat = grad_in, grad_out, join, _vcat_of(x)
+        ctx.xmask = x.__dict__.get('_ssseg_act_out')   # x = a single-use BN+ReLU output: its backward in our dgrad
+        ctx.xgstat = x.__dict__.get('_ssseg_gstat')
+        if (single_use and aux is None and residual is None and _act(relu)[0] == ACT_RELU and _CFG['bn_gstat']
+                and shift is not None):
+            # y feeds exactly one conv: that conv's input-gradient launch applies this ReLU's backward and this BN's
+            # scale and writes its backward sums (_masked_dgrad), so backward() gets dconv itself
+            y.__dict__['_ssseg_act_out'] = (ACT_RELU, 0.0)
+            y.__dict__['_ssseg_gstat'] = (bn.num_features, scale, bn)
         return y
 
     @staticmethod
@@ -1432,7 +1511,13 @@ class _ConvBNEvalFn(torch.autograd.Function):
         C = bn.num_features
         _need_act(gy, cp, 'conv_bn_act backward')
         dev = y.device
-        dconv = new_act(n, cp, h, w, y.dtype, dev, zero=cp > _pad16(C, y.dtype))
+        gs = gy.__dict__.get('_ssseg_gstats')
+        # the consumer's input-gradient launch wrote dconv (ReLU backward and BN scale applied) and this BN's backward
+        # sums (gradient-statistics rows, x_hat from y)
+        pre = (gs is not None and gy.__dict__.get('_ssseg_prescaled', False) and aux is None and not ctx.has_res
+               and gs.rows > 0 and gs.C == C)
+        act = 0 if gy.__dict__.get('_ssseg_premasked', False) else _act(ctx.relu)[0]
+        dconv = gy if pre else new_act(n, cp, h, w, y.dtype, dev, zero=cp > _pad16(C, y.dtype))
         want_res = ctx.has_res and ctx.needs_input_grad[5]
         dres = new_act(n, cp, h, w, y.dtype, dev, zero=cp > _pad16(C, y.dtype)) if want_res else None
         sums = torch.empty(2 * C, dtype=torch.float64, device=dev)
@@ -1450,7 +1535,15 @@ class _ConvBNEvalFn(torch.autograd.Function):
         defer = (_PGRAD['live'] and any(g is not None for g in grads)
                  and not any(getattr(p, '_ssseg_reducer', None) is not None for p in (bn.weight, bn.bias, conv.bias)
                              if want(p)))
-        if defer:   # partial rows only; defer_param_grads() reduces every layer's in one launch
+        if pre and defer:   # the gradient-statistics rows wait for defer_param_grads()' one launch
+            _PGRAD['pending'].append({'bn': bn, 'part': gs.part, 'nparts': gs.rows, 'C': C, 'scale': scale,
+                                      'dg': grads[0] or 0, 'db': grads[1] or 0, 'dbias': grads[2] or 0,
+                                      'gs': (N.dev_ptr(shift), N.dev_ptr(mean_eff), N.dev_ptr(invstd))})
+        elif pre:
+            grads = _grad_ptrs(*[p if want(p) else None for p in (bn.weight, bn.bias, conv.bias)])
+            N.call('ssseg_bn_gstat_finalize', N.dev_ptr(gs.part), gs.rows, C, N.dev_ptr(sums), N.dev_ptr(scale),
+                   N.dev_ptr(shift), N.dev_ptr(mean_eff), N.dev_ptr(invstd), *grads, N.stream())
+        elif defer:   # partial rows only; defer_param_grads() reduces every layer's in one launch
             import ctypes
             parts = bn.__dict__.setdefault('_ssseg_pg_parts', [])
             k = sum(1 for e in _PGRAD['pending'] if e['bn'] is bn)   # a module run twice in the pass (MSA)
@@ -1465,22 +1558,22 @@ class _ConvBNEvalFn(torch.autograd.Function):
             N.call('ssseg_bn_eval_bwd_part', N.dev_ptr(gy), N.dev_ptr(y), N.dev_ptr(aux) if aux is not None else None,
                    N.dev_ptr(dconv), N.dev_ptr(dres) if dres is not None else None, n * h * w, C, cp, N.dev_ptr(scale),
                    N.dev_ptr(shift) if aux is None else None, N.dev_ptr(mean_eff), N.dev_ptr(invstd),
-                   _act(ctx.relu)[0], N.dt_code(y), N.dev_ptr(part), nb, ctypes.byref(rows), N.stream())
+                   act, N.dt_code(y), N.dev_ptr(part), nb, ctypes.byref(rows), N.stream())
             _PGRAD['pending'].append({'bn': bn, 'part': part, 'nparts': rows.value, 'C': C, 'scale': scale,
                                       'dg': grads[0] or 0, 'db': grads[1] or 0, 'dbias': grads[2] or 0})
         else:   # immediate parameter gradients (temporaries inside hold_wgrad(params=True))
             grads = _grad_ptrs(*[p if want(p) else None for p in (bn.weight, bn.bias, conv.bias)])
-        if defer:
+        if defer or pre:
             pass
         elif aux is None:   # x_hat from y (no residual): ssseg_bn_eval_bwd_grad_y
             N.call('ssseg_bn_eval_bwd_grad_y', N.dev_ptr(gy), N.dev_ptr(y), N.dev_ptr(dconv),
                    N.dev_ptr(dres) if dres is not None else None, n * h * w, C, cp, N.dev_ptr(scale), N.dev_ptr(shift),
-                   N.dev_ptr(mean_eff), N.dev_ptr(invstd), _act(ctx.relu)[0], N.dt_code(y), N.dev_ptr(sums),
+                   N.dev_ptr(mean_eff), N.dev_ptr(invstd), act, N.dt_code(y), N.dev_ptr(sums),
                    N.dev_ptr(ws), nb, *grads, N.stream())
         else:
             N.call('ssseg_bn_eval_bwd_grad', N.dev_ptr(gy), N.dev_ptr(y), N.dev_ptr(aux), N.dev_ptr(dconv),
                    N.dev_ptr(dres) if dres is not None else None, n * h * w, C, cp, N.dev_ptr(scale),
-                   N.dev_ptr(mean_eff), N.dev_ptr(invstd), _act(ctx.relu)[0], N.dt_code(y), N.dev_ptr(sums),
+                   N.dev_ptr(mean_eff), N.dev_ptr(invstd), act, N.dt_code(y), N.dev_ptr(sums),
                    N.dev_ptr(ws), nb, *grads, N.stream())
         if want(bn.weight) or want(bn.bias):
             _ready(*[p for p in (bn.weight, bn.bias) if want(p)])
@@ -1490,21 +1583,26 @@ class _ConvBNEvalFn(torch.autograd.Function):
         if not ctx.needs_input_grad[0]:
             dx = None
         else:
-            dx = _dgrad_acc(conv, dconv, x.shape, pending, ctx.vcat)
+            dx = _masked_dgrad(conv, dconv, x, ctx.xmask, ctx.xgstat, pending, ctx.vcat)
+            if dx is None:
+                dx = _dgrad_acc(conv, dconv, x.shape, pending, ctx.vcat)
         if dres is not None and ctx.grad_out is not None:
             ctx.grad_out.put(dres)
             dres = None
-        return _join_give(ctx.join, last, dx), None, None, None, None, dres, None, None, None, None, None, None
+        return _join_give(ctx.join, last, dx), None, None, None, None, dres, None, None, None, None, None, None, None
 
 
-def conv_bn_act(conv, x, bn, relu=True, residual=None, grad_in=None, grad_out=None):
+def conv_bn_act(conv, x, bn, relu=True, residual=None, grad_in=None, grad_out=None, single_use=False):
     """act(bn(conv(x)) [+ residual]).  With an eval-mode BatchNorm the BN, residual add and ReLU run in
     the conv's epilogue (ssseg_bn_fold + ssseg_conv_igemm_epi): one kernel, each activation written once.
     Without gradients (the teacher forwards, reference train.py:69-94) that is all; when the eval pass
     is differentiated (the consistency pass) the epilogue also keeps the raw accumulator and
     _ConvBNEvalFn's backward runs the fused BN backward.  Training-mode BN needs the batch statistics
     of the conv output first, so it runs as conv, then bn_act.  grad_in / grad_out (a GradHandoff shared by
-    a block's first conv and its residual join) fuse the shortcut gradient into the first conv's dgrad."""
+    a block's first conv and its residual join) fuse the shortcut gradient into the first conv's dgrad.
+    single_use: the caller guarantees the output feeds exactly one ssseg conv (Bottleneck bn1 -> conv2, bn2 -> conv3;
+    a ConvBlock's first BN+ReLU): that conv's input gradient carries this BN's backward sums (training BN) or is
+    this conv's output gradient itself (differentiated eval BN: ReLU backward and BN scale applied in its epilogue)."""
     fusable = (isinstance(conv, (Conv2d, ConvTranspose2d)) and not conv._ssseg_head and isinstance(bn, BatchNorm2d)
                and not bn.training and bn.track_running_stats)
     if fusable:
@@ -1513,7 +1611,7 @@ def conv_bn_act(conv, x, bn, relu=True, residual=None, grad_in=None, grad_out=No
         if _no_grad(x, conv.weight, conv.bias, bn.weight, bn.bias, residual):
             return conv._ssseg_forward(x, relu, bn=bn, residual=residual)
         return _ConvBNEvalFn.apply(x, conv.weight, conv.bias, bn.weight, bn.bias, residual, conv, bn, relu, grad_in,
-                                   grad_out, _join_fwd(x))
+                                   grad_out, _join_fwd(x), bool(single_use))
     stats = None
     if (_CFG['fuse_stats'] and isinstance(conv, (Conv2d, ConvTranspose2d)) and isinstance(bn, BatchNorm2d)
             and (bn.training or not bn.track_running_stats) and bn.num_features == conv.out_channels and x.dim() == 4):
@@ -1524,16 +1622,16 @@ def conv_bn_act(conv, x, bn, relu=True, residual=None, grad_in=None, grad_out=No
         y = conv(x, handoff=grad_in, stats=stats)
     else:
         y = conv(x, stats=stats) if stats is not None else conv(x)
-    return bn_act(y, bn, relu=relu, residual=residual, grad_out=grad_out, pre=stats)
+    return bn_act(y, bn, relu=relu, residual=residual, grad_out=grad_out, pre=stats, single_use=single_use)
 
 
-def bn_act(x, bn, relu=True, residual=None, grad_out=None, pre=None):
+def bn_act(x, bn, relu=True, residual=None, grad_out=None, pre=None, single_use=False):
     """act(bn(x) [+ residual]) in one pass: ConvBlock's BN+ReLU (unet.py:9-10), Bottleneck's bn3+add+relu.
     pre: StatRows the producing conv's epilogue filled (fused training statistics)."""
     if not isinstance(bn, BatchNorm2d):
         raise TypeError('ssseg.nn.bn_act needs an ssseg BatchNorm2d')
     _need_act(x, rup(bn.num_features, vec()), 'BatchNorm2d')
-    return _BNFn.apply(x, bn.weight, bn.bias, residual, bn, relu, grad_out, pre)
+    return _BNFn.apply(x, bn.weight, bn.bias, residual, bn, relu, grad_out, pre, bool(single_use))
 
 
 # ------------------------------------------------------------------------------------------------

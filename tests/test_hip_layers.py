@@ -1028,3 +1028,130 @@ def test_dgrad_applies_producer_activation_backward(hip_device, mode, act):
             snn._CFG['act_mask'] = True
     for a, b, what in zip(outs[0], outs[1], ('dx', 'dW1', 'db1')):
         _close(a, b, mode, what)
+
+
+@pytest.mark.parametrize('k2,s2,cout2,H,W', [(3, 1, 48, 19, 21), (1, 1, 128, 17, 18), (3, 2, 64, 20, 22),
+                                             (3, 1, 64, 16, 64)])
+def test_bn_backward_sums_from_consumer_dgrad(hip_device, mode, monkeypatch, k2, s2, cout2, H, W):
+    """Training conv -> BN -> ReLU whose output feeds exactly one conv (Bottleneck bn1 / bn2, UNet conv3_0; reference
+    resnet Bottleneck and unet.py:9-10): the consumer's input-gradient launch applies the ReLU backward and writes the
+    BN backward's two channel sums in its epilogue (gradient statistics rows, ssseg_bn_gstat_finalize), and the BN
+    backward skips its reduction pass over dy and x -- the same gradients as the separate pass within rounding (x_hat
+    comes from y instead of x), for every engine variant (the (3, 1, 64, 16, 64) case reaches the halo kernels)."""
+    from ssseg import native as N
+    from ssseg import nn as snn
+    torch.manual_seed(6)
+    c1 = snn.Conv2d(16, 64, 3, 1, 1, bias=False).to(hip_device)
+    bn = snn.BatchNorm2d(64).to(hip_device)
+    c2 = snn.Conv2d(64, cout2, k2, s2, k2 // 2, bias=False).to(hip_device)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.3, 0.3)
+    x = _q(torch.randn(2, 16, H, W), mode)
+    calls = []
+    real = N.call
+
+    def spy(name, *a):
+        calls.append(name)
+        return real(name, *a)
+
+    monkeypatch.setattr(N, 'call', spy)
+
+    def run(on):
+        snn.set_bn_grad_stats(on)
+        for m in (c1, bn, c2):
+            m.zero_grad(set_to_none=True)
+        calls.clear()
+        xa = _act_in(x, hip_device).detach().requires_grad_(True)
+        h = snn.conv_bn_act(c1, xa, bn, relu=True, single_use=True)
+        y = c2(h)
+        g = snn.to_act(_q(torch.randn(y.shape[0], cout2, y.shape[2], y.shape[3],
+                                      generator=torch.Generator().manual_seed(7)), mode).to(hip_device))
+        y.backward(g)
+        torch.cuda.synchronize()
+        assert ('ssseg_bn_gstat_finalize' in calls) == on and ('ssseg_bn_bwd_reduce_grad' in calls) != on
+        return (xa.grad[:, :16].float().cpu(), c1.weight.grad.cpu().clone(), bn.weight.grad.cpu().clone(),
+                bn.bias.grad.cpu().clone(), c2.weight.grad.cpu().clone())
+
+    variants = [0] if mode == 'f32' else ALL_VARIANTS
+    try:
+        ref = run(False)
+        for v in variants:
+            N.call('ssseg_set_knob', 4, v)
+            got = run(True)
+            for a, b, what in zip(got, ref, ('dx', 'dW1', 'dgamma', 'dbeta', 'dW2')):
+                _close(a, b, mode, f'variant {v} {what}')
+    finally:
+        N.call('ssseg_set_knob', 4, 0)
+        snn.set_bn_grad_stats(True)
+
+
+@pytest.mark.parametrize('deferred', [False, True])
+@pytest.mark.parametrize('k2,s2,H,W', [(3, 1, 19, 21), (1, 1, 17, 18), (3, 2, 20, 22), (3, 1, 16, 64)])
+def test_eval_bn_backward_in_consumer_dgrad(hip_device, mode, monkeypatch, deferred, k2, s2, H, W):
+    """The differentiated eval pass (the consistency forward, reference train.py:90-92): conv -> eval BN -> ReLU whose
+    output feeds exactly one conv (Bottleneck bn1 / bn2).  The consumer's input-gradient launch applies the ReLU
+    backward AND the folded BN scale and writes the BN backward sums (gradient-statistics rows), so the producer's
+    backward runs no BN pass at all (no ssseg_bn_eval_bwd_* for it): its parameter gradients come from
+    ssseg_bn_gstat_finalize, or from the one deferred launch (ssseg_bn_param_grad_batch with the descriptor's x_hat
+    transform).  Same gradients as the separate pass within rounding, for every engine variant."""
+    from ssseg import native as N
+    from ssseg import nn as snn
+    torch.manual_seed(8)
+    c1 = snn.Conv2d(16, 64, 3, 1, 1, bias=True).to(hip_device)
+    bn1 = snn.BatchNorm2d(64).to(hip_device)
+    c2 = snn.Conv2d(64, 64, k2, s2, k2 // 2, bias=False).to(hip_device)
+    bn2 = snn.BatchNorm2d(64).to(hip_device)
+    with torch.no_grad():
+        for bn in (bn1, bn2):
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.3, 0.3)
+            bn.running_mean.uniform_(-0.2, 0.2)
+            bn.running_var.uniform_(0.5, 2.0)
+    bn1.eval()
+    bn2.eval()
+    x = _q(torch.randn(2, 16, H, W), mode)
+    calls = []
+    real = N.call
+
+    def spy(name, *a):
+        calls.append(name)
+        return real(name, *a)
+
+    monkeypatch.setattr(N, 'call', spy)
+
+    def run(on):
+        snn.set_bn_grad_stats(on)
+        for m in (c1, bn1, c2, bn2):
+            m.zero_grad(set_to_none=True)
+        calls.clear()
+        xa = _act_in(x, hip_device).detach().requires_grad_(True)
+        h = snn.conv_bn_act(c1, xa, bn1, relu=True, single_use=True)
+        y = snn.conv_bn_act(c2, h, bn2, relu=True)
+        g = snn.to_act(_q(torch.randn(y.shape[0], 64, y.shape[2], y.shape[3],
+                                      generator=torch.Generator().manual_seed(9)), mode).to(hip_device))
+        if deferred:
+            with snn.defer_param_grads():
+                y.backward(g)
+        else:
+            y.backward(g)
+        torch.cuda.synchronize()
+        n_bwd = sum(1 for c in calls if c.startswith('ssseg_bn_eval_bwd'))
+        assert n_bwd == (1 if on else 2), (on, calls)
+        if on and not deferred:
+            assert 'ssseg_bn_gstat_finalize' in calls
+        return (xa.grad[:, :16].float().cpu(), c1.weight.grad.cpu().clone(), c1.bias.grad.cpu().clone(),
+                bn1.weight.grad.cpu().clone(), bn1.bias.grad.cpu().clone(), c2.weight.grad.cpu().clone(),
+                bn2.weight.grad.cpu().clone())
+
+    variants = [0] if mode == 'f32' else ALL_VARIANTS
+    try:
+        ref = run(False)
+        for v in variants:
+            N.call('ssseg_set_knob', 4, v)
+            got = run(True)
+            for a, b, what in zip(got, ref, ('dx', 'dW1', 'db1', 'dgamma1', 'dbeta1', 'dW2', 'dgamma2')):
+                _close(a, b, mode, f'variant {v} {what}')
+    finally:
+        N.call('ssseg_set_knob', 4, 0)
+        snn.set_bn_grad_stats(True)
