@@ -42,40 +42,41 @@ static size_t carve(CowmixWs* w, void* base, int64_t B, int64_t H, int64_t W) {
 
 // K = int(round(max sigma * 3) * 2) + 1 (cowmix.py:30; Python round = half-to-even = rint),
 // taps_b[k] = exp(-x_k^2 / (2 sigma_b^2)) / sum, x_k = k + floor(-K/2) (+0.5 if K even) (cowmix.py:6-11).
+// One block per sample b (every block derives K from all B sigmas itself; block 0 publishes it).
 __global__ void __launch_bounds__(256) cowmix_taps_kernel(const float* sigma, int B, float* taps, int* Kout) {
   __shared__ float smax;
   __shared__ float red[4];
   if (threadIdx.x == 0) {
     float m = sigma[0];
-    for (int b = 1; b < B; ++b) m = fmaxf(m, sigma[b]);
+    for (int i = 1; i < B; ++i) m = fmaxf(m, sigma[i]);
     smax = m;
   }
   __syncthreads();
   const double r = rint((double)smax * 3.0);
   long long Kl = (long long)r * 2 + 1;
   const int K = (Kl > KCAP || Kl < 1) ? -1 : (int)Kl;
-  if (threadIdx.x == 0) *Kout = K;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *Kout = K;
   if (K < 0) return;
   const int x_first = (-K) >> 1;        // floor(-K/2)
   const float half = (K % 2 == 0) ? 0.5f : 0.f;
-  for (int b = 0; b < B; ++b) {
-    const float s = sigma[b];
-    const float denom = 2.f * (s * s);
-    float part = 0.f;
-    for (int k = threadIdx.x; k < K; k += blockDim.x) {
-      const float x = (float)(x_first + k) + half;
-      const float g = expf(-(x * x) / denom);
-      taps[(size_t)b * KCAP + k] = g;
-      part += g;
-    }
-    const float tot = block_sum(part, red);
-    for (int k = threadIdx.x; k < K; k += blockDim.x) taps[(size_t)b * KCAP + k] /= tot;
-    __syncthreads();
+  const int b = blockIdx.x;
+  const float s = sigma[b];
+  const float denom = 2.f * (s * s);
+  float part = 0.f;
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    const float x = (float)(x_first + k) + half;
+    const float g = expf(-(x * x) / denom);
+    taps[(size_t)b * KCAP + k] = g;
+    part += g;
   }
+  const float tot = block_sum(part, red);
+  for (int k = threadIdx.x; k < K; k += blockDim.x) taps[(size_t)b * KCAP + k] /= tot;
 }
 
 // Vertical pass: out[b][y][x] = sum_k g[k] * in[b][y - K/2 + k][x] (zero outside).
-// Block: 64 columns x 64 rows; thread (ty, tx) owns column tx and rows ty*16 .. ty*16+15.
+// Block: 64 columns x 64 rows; thread (ty, tx) owns column tx and rows ty*16 .. ty*16+15.  Register window: per 8 taps
+// a thread reads the 23 staged rows its 16 outputs x 8 taps touch once (not 128 LDS reads), then 128 FMAs in the
+// same order per output (k ascending): bit-identical to the one-read-per-FMA loop it replaces (64 -> LDS-light).
 constexpr int VTH = 64;
 __global__ void __launch_bounds__(256) cowmix_vblur_kernel(const float* __restrict__ in, const float* __restrict__ taps,
                                                            const int* Kp, float* __restrict__ out, int H, int W) {
@@ -100,7 +101,19 @@ __global__ void __launch_bounds__(256) cowmix_vblur_kernel(const float* __restri
     }
     __syncthreads();
     const float* col = tile + (ty * 16) * 64 + tx;
-    for (int k = 0; k < kc; ++k) {
+    int k = 0;
+    for (; k + 8 <= kc; k += 8) {
+      float win[23];
+#pragma unroll
+      for (int i = 0; i < 23; ++i) win[i] = col[(k + i) * 64];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float g = tp[k + u];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[j] = fmaf(g, win[u + j], acc[j]);
+      }
+    }
+    for (; k < kc; ++k) {
       const float g = tp[k];
 #pragma unroll
       for (int j = 0; j < 16; ++j) acc[j] = fmaf(g, col[(j + k) * 64], acc[j]);
@@ -116,45 +129,65 @@ __global__ void __launch_bounds__(256) cowmix_vblur_kernel(const float* __restri
   }
 }
 
-// Horizontal pass + per-sample statistics.  Block: 4 rows x 256 columns; thread (ty, tx) owns row
-// ty and columns tx + 64*j, j < 4.
-constexpr int HTW = 256;
+// Horizontal pass + per-sample statistics.  Block: 8 rows x 256 columns; thread (ty, tx) owns row ty and the 8
+// consecutive columns 8 tx .. 8 tx + 7.  Register window: per 8 taps a thread reads the 16 staged values its 8 outputs
+// x 8 taps touch as four 16-byte LDS reads, then 64 FMAs in the same order per output (k ascending, bit-identical).
+constexpr int HTW = 256, HJ = 8, HROWS = 8, HLD = HTW + KC;   // (row stride a multiple of 4 floats: aligned reads)
 __global__ void __launch_bounds__(256) cowmix_hblur_kernel(const float* __restrict__ in, const float* __restrict__ taps,
                                                            const int* Kp, float* __restrict__ out, double* stats,
                                                            int H, int W) {
-  __shared__ float tile[4 * (HTW + KC - 1)];
+  __shared__ __attribute__((aligned(16))) float tile[HROWS * HLD];
   __shared__ float tp[KC];
   __shared__ double red[4];
   const int K = *Kp;
   if (K < 0) return;
-  const int b = blockIdx.z, x0 = blockIdx.x * HTW, y = blockIdx.y * 4 + (threadIdx.x >> 6);
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int b = blockIdx.z, x0 = blockIdx.x * HTW, y = blockIdx.y * HROWS + ty;
   const int pad = K >> 1;
-  constexpr int LD = HTW + KC - 1;
   const float* src = in + ((size_t)b * H + min(y, H - 1)) * W;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float acc[HJ];
+#pragma unroll
+  for (int j = 0; j < HJ; ++j) acc[j] = 0.f;
   for (int k0 = 0; k0 < K; k0 += KC) {
     const int kc = min(KC, K - k0);
     if (threadIdx.x < kc) tp[threadIdx.x] = taps[(size_t)b * KCAP + k0 + threadIdx.x];
     const int cols = HTW + kc - 1;
-    for (int c = tx; c < cols; c += 64) {
+    for (int c = tx; c < cols; c += 32) {
       const int ix = x0 - pad + k0 + c;
-      tile[ty * LD + c] = (ix >= 0 && ix < W && y < H) ? src[ix] : 0.f;
+      tile[ty * HLD + c] = (ix >= 0 && ix < W && y < H) ? src[ix] : 0.f;
     }
     __syncthreads();
-    const float* row = tile + ty * LD + tx;
-    for (int k = 0; k < kc; ++k) {
+    const float* row = tile + ty * HLD + tx * HJ;
+    int k = 0;
+    for (; k + 8 <= kc; k += 8) {
+      float win[16];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float4 v = *(const float4*)(row + k + 4 * i);
+        win[4 * i] = v.x;
+        win[4 * i + 1] = v.y;
+        win[4 * i + 2] = v.z;
+        win[4 * i + 3] = v.w;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float g = tp[k + u];
+#pragma unroll
+        for (int j = 0; j < HJ; ++j) acc[j] = fmaf(g, win[u + j], acc[j]);
+      }
+    }
+    for (; k < kc; ++k) {
       const float g = tp[k];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = fmaf(g, row[64 * j + k], acc[j]);
+      for (int j = 0; j < HJ; ++j) acc[j] = fmaf(g, row[k + j], acc[j]);
     }
     __syncthreads();
   }
   double s1 = 0.0, s2 = 0.0;
   if (y < H) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int x = x0 + tx + 64 * j;
+    for (int j = 0; j < HJ; ++j) {
+      const int x = x0 + tx * HJ + j;
       if (x < W) {
         out[((size_t)b * H + y) * W + x] = acc[j];
         s1 += (double)acc[j];
@@ -291,10 +324,11 @@ extern "C" int ssseg_cowmix_mask(const float* noise, const float* sigma, const f
   carve(&w, workspace, B, H, W);
   float* field = field_out ? field_out : mask_out;   // threshold pass is in-place safe
   SSSEG_TRY(hipMemsetAsync(w.stats, 0, sizeof(double) * 2 * B, s));
-  hipLaunchKernelGGL(cowmix_taps_kernel, dim3(1), dim3(256), 0, s, sigma, (int)B, w.taps, w.K);
+  hipLaunchKernelGGL(cowmix_taps_kernel, dim3((unsigned)B), dim3(256), 0, s, sigma, (int)B, w.taps, w.K);
   hipLaunchKernelGGL(cowmix_vblur_kernel, dim3((W + 63) / 64, (H + VTH - 1) / VTH, B), dim3(256), 0, s, noise,
                      w.taps, w.K, w.tmp, (int)H, (int)W);
-  hipLaunchKernelGGL(cowmix_hblur_kernel, dim3((W + HTW - 1) / HTW, (H + 3) / 4, B), dim3(256), 0, s, w.tmp, w.taps,
+  hipLaunchKernelGGL(cowmix_hblur_kernel, dim3((W + HTW - 1) / HTW, (H + HROWS - 1) / HROWS, B), dim3(256), 0, s, w.tmp,
+                     w.taps,
                      w.K, field, w.stats, (int)H, (int)W);
   hipLaunchKernelGGL(cowmix_finalize_kernel, dim3((B + 63) / 64), dim3(64), 0, s, w.stats, p, w.K, (int)B, H * W,
                      w.thr, thr_out);
