@@ -7,10 +7,15 @@ x2 (align_corners=True) + 1x1 conv with a fused ReLU, the concat read part by pa
 ssseg_vcat; one copy where the parts do not qualify), Conv+BN+ReLU blocks.
 The input may be an NCHW image batch (converted once to NHWC) and the logits come back fp32.
 """
+import os
+
 import torch.nn as nn
 
 from ssseg import nn as snn
 from ._common import ConvBlock, center_crop as _center_crop  # noqa: F401  (reference names)
+
+# the decoder blocks' outputs marked single-use (their consumer conv carries conv3_1's BN backward); 0: A/B off
+_DEC_SINGLE_USE = os.environ.get('SSSEG_UNET_SINGLE_USE', '1') != '0'
 
 
 class UpBlock(nn.Module):
@@ -34,11 +39,13 @@ class UpBlock(nn.Module):
             return self.upsampler[0].forward_relu(x)
         return self.upsampler[1].forward_relu(self.upsampler[0](x))
 
-    def forward(self, x, skip):
+    def forward(self, x, skip, single_use=False):
+        """single_use: the caller guarantees the block's output feeds exactly one conv (UNet: the next block's
+        upsampler or the 1x1 head), whose input gradient then carries conv3_1's BN backward (snn.conv_bn_act)."""
         x = self._upsample(x)
         # conv3_0 is the concat's only consumer: it reads [x | skip] part by part (virtual concat, no copy)
         x = snn.cat_crop(x, skip, self.out_channels, self.skip_channels, lazy=True)
-        return self.conv3_1(self.conv3_0(x, single_use=True))
+        return self.conv3_1(self.conv3_0(x, single_use=True), single_use=single_use)
 
 
 class UNet(nn.Module):
@@ -63,7 +70,8 @@ class UNet(nn.Module):
         feats = self.encoder(snn.to_act(x))
         y = feats[-1]
         for i, block in enumerate(self.decoder):
-            y = block(y, feats[len(feats) - 2 - i])
+            # (each block's output feeds only the next block's upsampler conv / the head conv)
+            y = block(y, feats[len(feats) - 2 - i], single_use=_DEC_SINGLE_USE)
         return self.final_block(y)
 
     def get_params_with_layerwise_lr(self, encoder_lr, decoder_lr, classifier_lr):

@@ -1316,7 +1316,17 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
         wb = self.bias is not None and (self.bias.requires_grad if want is None else want[1])
         _ready(*[p for p, on in ((self.weight, True), (self.bias, wb)) if on])
 
-    def _ssseg_dgrad(self, gy, xshape):
+    def _ssseg_mask_dgrad_ok(self):
+        return _CFG['dtype'] in (torch.bfloat16, torch.float16, torch.float32)
+
+    def _ssseg_gstat_ok(self):
+        return True   # one strided launch over every input pixel
+
+    def _ssseg_dgrad(self, gy, xshape, mask=None, stats=None, scale=None):
+        """dx of the transposed conv (a strided conv of gy); mask / stats / scale as Conv2d._ssseg_dgrad (x was the
+        single-use BN+ReLU output of UpBlock.conv3_1)."""
+        if (stats is not None or scale is not None) and mask is None:
+            raise ValueError('ssseg.nn.ConvTranspose2d: gradient statistics / scale need the masked input gradient')
         cin, cout = self._dims()
         n, _, H, W = xshape
         (R, S), (sh, sw), (ph, pw) = self.kernel_size, self.stride, self.padding
@@ -1326,7 +1336,8 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
         d = _desc(N=n, H=OH, W=OW, C=cout, ldx=cout, OH=H, OW=W, K=cin, R=R, S=S, sy=sh, sx=sw, dy=1, dx=1, py=-ph,
                   px=-pw, outH=H, outW=W, osy=1, osx=1, ooy=0, oox=0, ldy=cin, ldw=R * S * cout)
         with _Timed(_conv_flops(n, H, W, self.out_channels, self.in_channels, R, S), 'dgrad', _tag(self, n, H, W)):
-            self._igemm(gy, w, dx, d, N.dt_code(dx))
+            self._igemm(gy, w, dx, d, N.dt_code(dx), fold=(scale, None, None, None) if scale is not None else None,
+                        mask=mask, stats=stats)
         return dx
 
 

@@ -1155,3 +1155,60 @@ def test_eval_bn_backward_in_consumer_dgrad(hip_device, mode, monkeypatch, defer
     finally:
         N.call('ssseg_set_knob', 4, 0)
         snn.set_bn_grad_stats(True)
+
+
+@pytest.mark.parametrize('train', [True, False])
+@pytest.mark.parametrize('head', [False, True])
+def test_bn_backward_in_upsampler_or_head_dgrad(hip_device, mode, monkeypatch, train, head):
+    """UNet decoder: UpBlock.conv3_1's BN+ReLU output feeds only the next block's ConvTranspose2d(4, 2, 1) upsampler
+    (or the 1x1 head): that conv's input gradient carries the BN backward (gradient statistics; eval: also the folded
+    scale) -- same gradients as the separate BN pass within rounding (reference unet.py:16-50, 63-102)."""
+    from ssseg import native as N
+    from ssseg import nn as snn
+    torch.manual_seed(10)
+    c1 = snn.Conv2d(16, 64, 3, 1, 1, bias=False).to(hip_device)
+    bn = snn.BatchNorm2d(64).to(hip_device)
+    c2 = (snn.Conv2d(64, 2, 1, bias=False, head=True) if head
+          else snn.ConvTranspose2d(64, 32, 4, 2, 1)).to(hip_device)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.3, 0.3)
+        bn.running_mean.uniform_(-0.2, 0.2)
+        bn.running_var.uniform_(0.5, 2.0)
+    bn.train(train)
+    x = _q(torch.randn(2, 16, 18, 20), mode)
+    calls = []
+    real = N.call
+
+    def spy(name, *a):
+        calls.append(name)
+        return real(name, *a)
+
+    monkeypatch.setattr(N, 'call', spy)
+
+    def run(on):
+        snn.set_bn_grad_stats(on)
+        for m in (c1, bn, c2):
+            m.zero_grad(set_to_none=True)
+        calls.clear()
+        xa = _act_in(x, hip_device).detach().requires_grad_(True)
+        h = snn.conv_bn_act(c1, xa, bn, relu=True, single_use=True)
+        y = c2(h) if head else c2.forward_relu(h)
+        gen = torch.Generator().manual_seed(11)
+        if head:
+            g = _q(torch.randn(tuple(y.shape), generator=gen), mode).to(hip_device)
+        else:
+            g = snn.to_act(_q(torch.randn(y.shape[0], 32, y.shape[2], y.shape[3], generator=gen), mode).to(hip_device))
+        y.backward(g)
+        torch.cuda.synchronize()
+        assert ('ssseg_bn_gstat_finalize' in calls) == on, (on, calls)
+        return (xa.grad[:, :16].float().cpu(), c1.weight.grad.cpu().clone(), bn.weight.grad.cpu().clone(),
+                bn.bias.grad.cpu().clone(), c2.weight.grad.cpu().clone())
+
+    try:
+        ref = run(False)
+        got = run(True)
+        for a, b, what in zip(got, ref, ('dx', 'dW1', 'dgamma', 'dbeta', 'dW2')):
+            _close(a, b, mode, what)
+    finally:
+        snn.set_bn_grad_stats(True)
