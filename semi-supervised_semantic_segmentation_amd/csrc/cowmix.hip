@@ -129,10 +129,12 @@ __global__ void __launch_bounds__(256) cowmix_vblur_kernel(const float* __restri
   }
 }
 
-// Horizontal pass + per-sample statistics.  Block: 8 rows x 256 columns; thread (ty, tx) owns row ty and the 8
-// consecutive columns 8 tx .. 8 tx + 7.  Register window: per 8 taps a thread reads the 16 staged values its 8 outputs
-// x 8 taps touch as four 16-byte LDS reads, then 64 FMAs in the same order per output (k ascending, bit-identical).
-constexpr int HTW = 256, HJ = 8, HROWS = 8, HLD = HTW + KC;   // (row stride a multiple of 4 floats: aligned reads)
+// Horizontal pass + per-sample statistics.  Block: 8 rows x 256 columns; thread (ty, tx) owns row ty and the two runs
+// of 4 consecutive columns 4 tx .. 4 tx + 3 and 128 + 4 tx .. 128 + 4 tx + 3 (lanes 16 bytes apart: conflict-free
+// 16-byte LDS reads; the row stride is 4 banks off the next row's).  Register window: per 8 taps a thread reads the 12
+// staged values each run's 4 outputs x 8 taps touch (three 16-byte reads), then 32 FMAs per run in the same order per
+// output (k ascending): bit-identical to the one-read-per-FMA loop.
+constexpr int HTW = 256, HROWS = 8, HLD = HTW + KC + 4;
 __global__ void __launch_bounds__(256) cowmix_hblur_kernel(const float* __restrict__ in, const float* __restrict__ taps,
                                                            const int* Kp, float* __restrict__ out, double* stats,
                                                            int H, int W) {
@@ -145,9 +147,11 @@ __global__ void __launch_bounds__(256) cowmix_hblur_kernel(const float* __restri
   const int b = blockIdx.z, x0 = blockIdx.x * HTW, y = blockIdx.y * HROWS + ty;
   const int pad = K >> 1;
   const float* src = in + ((size_t)b * H + min(y, H - 1)) * W;
-  float acc[HJ];
+  float acc[2][4];
 #pragma unroll
-  for (int j = 0; j < HJ; ++j) acc[j] = 0.f;
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[g][j] = 0.f;
   for (int k0 = 0; k0 < K; k0 += KC) {
     const int kc = min(KC, K - k0);
     if (threadIdx.x < kc) tp[threadIdx.x] = taps[(size_t)b * KCAP + k0 + threadIdx.x];
@@ -157,43 +161,50 @@ __global__ void __launch_bounds__(256) cowmix_hblur_kernel(const float* __restri
       tile[ty * HLD + c] = (ix >= 0 && ix < W && y < H) ? src[ix] : 0.f;
     }
     __syncthreads();
-    const float* row = tile + ty * HLD + tx * HJ;
+    const float* row = tile + ty * HLD + 4 * tx;
     int k = 0;
     for (; k + 8 <= kc; k += 8) {
-      float win[16];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float4 v = *(const float4*)(row + k + 4 * i);
-        win[4 * i] = v.x;
-        win[4 * i + 1] = v.y;
-        win[4 * i + 2] = v.z;
-        win[4 * i + 3] = v.w;
-      }
+      for (int g = 0; g < 2; ++g) {
+        float win[12];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const float g = tp[k + u];
+        for (int i = 0; i < 3; ++i) {
+          const float4 v = *(const float4*)(row + 128 * g + k + 4 * i);
+          win[4 * i] = v.x;
+          win[4 * i + 1] = v.y;
+          win[4 * i + 2] = v.z;
+          win[4 * i + 3] = v.w;
+        }
 #pragma unroll
-        for (int j = 0; j < HJ; ++j) acc[j] = fmaf(g, win[u + j], acc[j]);
+        for (int u = 0; u < 8; ++u) {
+          const float gk = tp[k + u];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[g][j] = fmaf(gk, win[u + j], acc[g][j]);
+        }
       }
     }
     for (; k < kc; ++k) {
-      const float g = tp[k];
+      const float gk = tp[k];
 #pragma unroll
-      for (int j = 0; j < HJ; ++j) acc[j] = fmaf(g, row[k + j], acc[j]);
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[g][j] = fmaf(gk, row[128 * g + k + j], acc[g][j]);
     }
     __syncthreads();
   }
   double s1 = 0.0, s2 = 0.0;
   if (y < H) {
 #pragma unroll
-    for (int j = 0; j < HJ; ++j) {
-      const int x = x0 + tx * HJ + j;
-      if (x < W) {
-        out[((size_t)b * H + y) * W + x] = acc[j];
-        s1 += (double)acc[j];
-        s2 += (double)acc[j] * (double)acc[j];
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int x = x0 + 128 * g + 4 * tx + j;
+        if (x < W) {
+          out[((size_t)b * H + y) * W + x] = acc[g][j];
+          s1 += (double)acc[g][j];
+          s2 += (double)acc[g][j] * (double)acc[g][j];
+        }
       }
-    }
   }
   s1 = block_sum(s1, red);
   s2 = block_sum(s2, red);
