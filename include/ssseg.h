@@ -568,7 +568,8 @@ int ssseg_bn_eval_bwd_part(const void* dy, const void* y, const void* aux, void*
  * 2r + 1, dconv_bias[c] += scale[c] * (the first sum) (NULL pointers skipped); fixed-order fp64 column sums.  descs
  * points to DEVICE memory; max_c >= every descriptor's C.  mean_eff non-NULL: the rows are gradient-statistics rows
  * (sum m, sum m * y) of a consumer's input-gradient launch, turned into the x_hat moment as ssseg_bn_gstat_finalize
- * does for a folded eval BN (scale, shift, mean_eff, invstd) before the same tail. */
+ * does for a folded eval BN (scale, shift, mean_eff, invstd) before the same tail.  part is scratch: a table of >= 512
+ * rows is first folded in place to <= 256 group sums (fixed order; a second launch in the same call). */
 typedef struct ssseg_pgrad_desc {
   const double* part;
   int64_t nparts, C;

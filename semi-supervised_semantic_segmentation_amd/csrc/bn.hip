@@ -440,6 +440,26 @@ __global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* par
   }
 }
 
+// a long deferred table (>= PG_FOLD rows: the gradient-statistics rows of a consumer's dgrad, one per output tile) is
+// first folded in place to <= 256 group rows (groups of S consecutive rows, row g*S = their sum, in row order) by
+// bn_pgrad_fold_kernel, so the column sums below walk <= 256 rows instead of up to 8K
+constexpr int PG_FOLD = 512;
+__device__ __forceinline__ int pg_fold_stride(int nparts) { return nparts >= PG_FOLD ? (nparts + 255) / 256 : 1; }
+
+// blockIdx.y = descriptor, blockIdx.x = group
+__global__ void __launch_bounds__(256) bn_pgrad_fold_kernel(const ssseg_pgrad_desc* __restrict__ descs) {
+  const ssseg_pgrad_desc& d = descs[blockIdx.y];
+  const int nparts = (int)d.nparts, S = pg_fold_stride(nparts);
+  if (S == 1 || (int)blockIdx.x * S >= nparts) return;   // uniform per block
+  const int C = (int)d.C, r0 = blockIdx.x * S, r1 = min(nparts, r0 + S);
+  double* part = (double*)d.part;
+  for (int k = threadIdx.x; k < 2 * C; k += 256) {   // both rows (2r, 2r + 1) of a partial: 2C contiguous values
+    double a = 0.0;
+    for (int r = r0; r < r1; ++r) a += part[(int64_t)(2 * r) * C + k];
+    part[(int64_t)(2 * r0) * C + k] = a;
+  }
+}
+
 // the deferred parameter gradients of many eval BNs in one launch (blockIdx.y = descriptor): the same column sums and
 // the same mode-2 tail as bn_partial_final_kernel<8>
 __global__ void __launch_bounds__(256) bn_pgrad_batch_kernel(const ssseg_pgrad_desc* __restrict__ descs) {
@@ -447,7 +467,8 @@ __global__ void __launch_bounds__(256) bn_pgrad_batch_kernel(const ssseg_pgrad_d
   const int C = (int)d.C;
   if ((int)blockIdx.x * 8 >= C) return;   // uniform per block
   double a, b;
-  partial_col_sums<8>(d.part, (int)d.nparts, C, 1, blockIdx.x, a, b);
+  const int S = pg_fold_stride((int)d.nparts);
+  partial_col_sums<8>(d.part, ((int)d.nparts + S - 1) / S, C, S, blockIdx.x, a, b);
   const int c = blockIdx.x * 8 + threadIdx.x;
   if (threadIdx.x < 8 && c < C) {
     if (d.mean_eff) {   // gradient-statistics rows: (sum m, sum m * y) -> (sum m, sum m * x_hat)
@@ -1090,6 +1111,7 @@ extern "C" int ssseg_bn_param_grad_batch(const ssseg_pgrad_desc* descs, int64_t 
                                          ssseg_stream_t stream) {
   if (n < 0 || n > 65535 || (n > 0 && !descs) || max_c < 0 || max_c > 0x7fffffff) return SSSEG_EINVAL;
   if (n == 0 || max_c == 0) return 0;
+  hipLaunchKernelGGL(bn_pgrad_fold_kernel, dim3(256, (unsigned)n), dim3(256), 0, (hipStream_t)stream, descs);
   hipLaunchKernelGGL(bn_pgrad_batch_kernel, dim3((unsigned)((max_c + 7) / 8), (unsigned)n), dim3(256), 0,
                      (hipStream_t)stream, descs);
   SSSEG_LAUNCH_CHECK();

@@ -1212,3 +1212,39 @@ def test_bn_backward_in_upsampler_or_head_dgrad(hip_device, mode, monkeypatch, t
             _close(a, b, mode, what)
     finally:
         snn.set_bn_grad_stats(True)
+
+
+@pytest.mark.parametrize('nparts', [300, 511, 512, 700, 8200])
+def test_pgrad_batch_long_tables(hip_device, nparts):
+    """ssseg_bn_param_grad_batch over partial tables of every length the deferred eval-BN gradients produce (the
+    consumer-dgrad gradient-statistics rows reach thousands: tables of >= 512 rows are folded in place first): the
+    same sums as a float64 reference, with and without the descriptor's x_hat transform (scale, shift, mean_eff,
+    invstd)."""
+    import struct
+    from ssseg import native as N
+    g = torch.Generator().manual_seed(nparts)
+    C = 72
+    descs, outs, refs = [], [], []
+    for gst in (False, True):
+        part = torch.randn(2 * nparts, C, generator=g, dtype=torch.float64)
+        scale = torch.rand(C, generator=g) + 0.5
+        shift, mean, inv = torch.randn(C, generator=g), torch.randn(C, generator=g), torch.rand(C, generator=g) + 0.5
+        a = part[0::2].sum(0)
+        b = part[1::2].sum(0)
+        if gst:
+            B = mean.double() * scale.double() + shift.double()
+            b = (b - B * a) * (inv.double() / scale.double())
+        dg, db, dbias = (torch.zeros(C, device=hip_device) for _ in range(3))
+        dev = [t.to(hip_device) for t in (part, scale, shift, mean, inv)]
+        outs.append((dg, db, dbias, dev))
+        refs.append((b, a, scale.double() * a))
+        gs = (dev[2].data_ptr(), dev[3].data_ptr(), dev[4].data_ptr()) if gst else (0, 0, 0)
+        descs.append((dev[0].data_ptr(), nparts, C, dev[1].data_ptr(), dg.data_ptr(), db.data_ptr(), dbias.data_ptr())
+                     + gs)
+    blob = b''.join(struct.pack('<10q', *d) for d in descs)
+    table = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(hip_device)
+    N.call('ssseg_bn_param_grad_batch', N.dev_ptr(table), len(descs), C, N.stream())
+    torch.cuda.synchronize()
+    for (dg, db, dbias, _), (rg, rb, rbias) in zip(outs, refs):
+        for got, ref in ((dg, rg), (db, rb), (dbias, rbias)):
+            assert torch.allclose(got.cpu().double(), ref, rtol=1e-5, atol=1e-4 * (1 + float(ref.abs().max())))
