@@ -343,7 +343,12 @@ int tune_variant(const void* x, const void* w, void* y, const ConvGeom& g, const
       // warm (code load, caches); a variant that cannot run this launch (-1) is skipped
       if (run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, wsv, ph, x2, x2b) <= 0) continue;
       float ms = 1e30f;
-      for (int rep = 0; rep < 5; ++rep) {
+      static const int reps = [] {   // best of `reps` timed launches (SSSEG_TUNE_REPS: A/B of the tuning depth)
+        const char* e = getenv("SSSEG_TUNE_REPS");
+        const int v = e ? atoi(e) : 5;
+        return v >= 1 && v <= 64 ? v : 5;
+      }();
+      for (int rep = 0; rep < reps; ++rep) {
         (void)hipEventRecord(e0, s);
         run_variant<T, TO>(v, x, w, y, g, ep, xb, wb, s, wsv, ph, x2, x2b);
         (void)hipEventRecord(e1, s);
