@@ -499,6 +499,11 @@ int ssseg_bn_stats_finalize(const void* x, int64_t P, int64_t C, int64_t ldx, in
 int ssseg_bn_partials_finalize(double* part, int64_t nparts, int64_t C, double* sums, double count, float eps,
                                float momentum, float* mean_out, float* invstd_out, float* running_mean,
                                float* running_var, int64_t* num_batches_tracked, ssseg_stream_t stream);
+/* A conv bias gradient (unet.py UpBlock ConvTranspose2d / 1x1 upsampler biases): dsum[c] += sum over P pixels of
+ * x[p][c] (fp64 partials, fixed order), in the reduction's own tail; sums receives the fp64 column sums (sums[C:2C]
+ * the sums of squares). */
+int ssseg_channel_sum_grad(const void* x, int64_t P, int64_t C, int64_t ldx, int dt, float* dsum, double* sums,
+                           void* ws, size_t ws_bytes, ssseg_stream_t stream);
 /* The backward sums of a BatchNorm(+ReLU) from the gradient-statistics rows of its consumer's input-gradient launch
  * (ssseg_conv_igemm_epi_actmask with stats): sums[0:C] = sum m, sums[C:2C] = sum m * x_hat, with x_hat recovered from
  * y wherever m != 0 -- training BN (mean_eff NULL): x_hat = (y - beta) / gamma (gamma / beta NULL: 1 / 0); folded

@@ -490,7 +490,9 @@ __global__ void __launch_bounds__(256) bn_pgrad_batch_kernel(const ssseg_pgrad_d
 static void launch_partial_final(const double* part, int64_t nparts, int64_t C, double* sums, hipStream_t s,
                                  FinalEpi fe = FinalEpi{}) {
   int rs = 1;
-  if (nparts >= 1024) {   // fold to ~256 rows first
+  // (folding only tables of > 64 rows per lane measured slower: the final kernels' longer walks cost more than the
+  // fold launches saved, 0.80 vs 0.64 + 0.12 ms/step)
+  if (nparts >= 1024) {
     rs = (int)((nparts + 255) / 256);
     const int64_t g = (nparts + rs - 1) / rs;
     hipLaunchKernelGGL(bn_partial_rows_kernel, dim3((unsigned)g), dim3(256), 0, s, (double*)part, (int)nparts, (int)C,
@@ -891,6 +893,26 @@ extern "C" int ssseg_bn_stats(const void* x, int64_t P, int64_t C, int64_t ldx, 
     partials<f16_t, 0>((const f16_t*)x, nullptr, nullptr, P, C, ldx, 0, 0, ChanParams{}, 0, sums, ws, s);
   else if (dt == SSSEG_F32)
     partials<float, 0>((const float*)x, nullptr, nullptr, P, C, ldx, 0, 0, ChanParams{}, 0, sums, ws, s);
+  else
+    return SSSEG_EUNSUPPORTED;
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_channel_sum_grad(const void* x, int64_t P, int64_t C, int64_t ldx, int dt, float* dsum,
+                                      double* sums, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
+  if (!x || !dsum || !sums || P < 1 || C < 1 || ld_bad(C, ldx)) return SSSEG_EINVAL;
+  if (!ws || ws_bytes < ssseg_bn_workspace_bytes(C)) return SSSEG_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  FinalEpi fe{};
+  fe.mode = 2;
+  fe.dbeta = dsum;   // the mode-2 tail: dsum[c] += sums[c]
+  if (dt == SSSEG_BF16)
+    partials<bf16_t, 0>((const bf16_t*)x, nullptr, nullptr, P, C, ldx, 0, 0, ChanParams{}, 0, sums, ws, s, fe);
+  else if (dt == SSSEG_F16)
+    partials<f16_t, 0>((const f16_t*)x, nullptr, nullptr, P, C, ldx, 0, 0, ChanParams{}, 0, sums, ws, s, fe);
+  else if (dt == SSSEG_F32)
+    partials<float, 0>((const float*)x, nullptr, nullptr, P, C, ldx, 0, 0, ChanParams{}, 0, sums, ws, s, fe);
   else
     return SSSEG_EUNSUPPORTED;
   SSSEG_LAUNCH_CHECK();

@@ -107,6 +107,7 @@ SIGS = {
     'ssseg_bn_stats': (i32, [vp, i64, i64, i64, i32, vp, vp, sz, vp]),
     'ssseg_bn_partials_finalize': (i32, [vp, i64, i64, vp, f64, f32, f32, vp, vp, vp, vp, vp, vp]),
     'ssseg_bn_gstat_finalize': (i32, [vp, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    'ssseg_channel_sum_grad': (i32, [vp, i64, i64, i64, i32, vp, vp, vp, sz, vp]),
     'ssseg_bn_finalize': (i32, [vp, i64, f64, f32, f32, vp, vp, vp, vp, vp, vp]),
     'ssseg_bn_eval_params': (i32, [vp, vp, f32, i64, vp, vp, vp]),
     'ssseg_bn_fold': (i32, [vp, vp, vp, vp, vp, f32, i64, i64, vp, vp, vp, vp, vp]),

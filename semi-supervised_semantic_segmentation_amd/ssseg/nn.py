@@ -705,9 +705,9 @@ def _bias_grad(mod, gy, want=None):
     sums = torch.empty(2 * C, dtype=torch.float64, device=gy.device)
     nb = N.lib().ssseg_bn_workspace_bytes(C)
     ws = N.workspace(nb, gy.device)
-    N.call('ssseg_bn_stats', N.dev_ptr(gy), n * h * w, C, cp, N.dt_code(gy), N.dev_ptr(sums), N.dev_ptr(ws), nb,
-           N.stream())
-    N.call('ssseg_bn_param_grad', N.dev_ptr(sums), C, None, N.dev_ptr(_grad_of(mod.bias)), N.stream())
+    # one reduction with the gradient add in its tail (ssseg_channel_sum_grad)
+    N.call('ssseg_channel_sum_grad', N.dev_ptr(gy), n * h * w, C, cp, N.dt_code(gy), N.dev_ptr(_grad_of(mod.bias)),
+           N.dev_ptr(sums), N.dev_ptr(ws), nb, N.stream())
 
 
 _PACK_EPOCH = [0]   # bumped whenever any conv's set of packed layouts changes (fast path of invalidate_packed)
