@@ -179,6 +179,7 @@ def _oracle(dt=torch.float32, semi=True, pert=0.0, world=WORLD):
 
 
 @pytest.mark.parametrize('semi,world', [(False, WORLD), (True, WORLD), (True, 4)])
+@pytest.mark.timeout(400)
 def test_ddp_syncbn_product_path(hip_device, semi, world):
     """world 2 (both step kinds) and world 4 (semi-supervised): 4 ranks share the one GPU over gloo -- the same
     product code an 8-GPU node runs over RCCL."""
@@ -192,7 +193,7 @@ def test_ddp_syncbn_product_path(hip_device, semi, world):
     res = {}
     try:
         for _ in range(world):
-            r, out = q.get(timeout=110)
+            r, out = q.get(timeout=300)
             res[r] = out
     finally:
         for p in procs:
@@ -376,6 +377,7 @@ def _worker_rccl(port, q):
             dist.destroy_process_group()
 
 
+@pytest.mark.timeout(400)
 def test_rccl_world1_forced_collectives_bitwise(hip_device):
     import torch.multiprocessing as mp
     ctx = mp.get_context('spawn')
@@ -383,7 +385,7 @@ def test_rccl_world1_forced_collectives_bitwise(hip_device):
     p = ctx.Process(target=_worker_rccl, args=(_free_port(), q))
     p.start()
     try:
-        out = q.get(timeout=110)
+        out = q.get(timeout=300)
     finally:
         p.join(30)
         if p.is_alive():
