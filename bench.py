@@ -251,6 +251,13 @@ def timed_run(args, world, rank, device, dtype, probe=True, eager_n1=False):
     for _ in range(max(args.warmup, 2)):
         one_step()
     torch.cuda.synchronize()
+    # N > 1: rank 0 tuned the conv geometries in the warm-up, the other ranks ran the static rule and now take its
+    # table (ssseg.tune); every rank's table must be the same
+    from ssseg import tune
+    tune.sync()
+    tune_digests = tune.digests()
+    if len(set(tune_digests)) != 1:
+        raise RuntimeError(f'bench: conv variant tables differ across ranks: {tune_digests}')
     rows = []
     if probe:   # instrumented step: HIP events around every conv-engine launch (dominant kernel family)
         # serial schedule for this one step: with the teacher pass overlapping the supervised backward on a side
@@ -263,11 +270,12 @@ def timed_run(args, world, rank, device, dtype, probe=True, eager_n1=False):
         torch.cuda.synchronize()
         train._OVERLAP['teacher'] = overlap
     graph = None
-    # N = 1: the step captured as a HIP graph and replayed; N > 1: eager launches (the host reducer issues the RCCL bucket
-    # all-reduces and SyncBN reductions each step: a captured DDP step -- RCCL collectives inside a HIP graph -- hung at
-    # world 1 on this image's RCCL 2.26.6).  The N = 1 record also carries the eager rate ('eager_n1'),
-    # the like-for-like base of the N > 1 lines.
-    if args.graph and world == 1:
+    # the step captured as a HIP graph and replayed, at N = 1 and at N > 1 on an RCCL group: the gradient buckets and the
+    # SyncBN sums are enqueued on the native communicator (ssseg.comm), which a capture records like a kernel.  Eager
+    # launches only where the collectives run on torch.distributed (gloo, SSSEG_COMM=c10d: DESIGN.md §6).  The N = 1
+    # record also carries the eager rate ('eager_n1').
+    from ssseg import comm as scomm
+    if args.graph and (world == 1 or scomm.kind() == 'native'):
         # the step captured once as a HIP graph (ssseg.graph.StepGraph) and replayed: each replay copies the next
         # batch into the captured input buffers and runs the whole step (fresh CowMix draws from the device counter)
         from ssseg.graph import StepGraph
@@ -318,7 +326,7 @@ def timed_run(args, world, rank, device, dtype, probe=True, eager_n1=False):
         eager = timed_steps(eager_step, args.steps)
     live = torch.stack([torch.stack([c.float(), u.float(), m.float()]) for c, u, m in recs]).cpu()
     snn.set_compute_dtype(torch.bfloat16)
-    return elapsed, rows, live, model, graph is not None, eager
+    return elapsed, rows, live, model, graph is not None, eager, tune_digests
 
 
 def main():
@@ -352,8 +360,10 @@ def main():
               f'{dist.get_backend()}, device cuda:{dev_idx}', file=sys.stderr, flush=True)
     device = torch.device('cuda', dev_idx)
 
-    elapsed, rows, live, model, graphed, eager = timed_run(args, world, rank, device, torch.bfloat16,
-                                                           eager_n1=(world == 1))
+    from ssseg import comm as scomm
+    from ssseg import tune
+    elapsed, rows, live, model, graphed, eager, tune_digests = timed_run(args, world, rank, device, torch.bfloat16,
+                                                                         eager_n1=(world == 1))
     finite = bool(torch.isfinite(live).all())
     if not finite:
         raise RuntimeError(f'bench: non-finite loss in the timed steps (rank {rank}): {live.tolist()}')
@@ -378,7 +388,14 @@ def main():
                      'conv_ms_per_step': round(conv_ms, 3), 'conv_gflop_per_step': round(conv_flops / 1e9, 1),
                      'launches_per_step': len(rows), 'mfma_pmc': pmc_mfma()},
         'execution': ('HIP graph replay of the captured step (ssseg.graph.StepGraph), one per step' if graphed
-                      else 'eager launches from Python (the host reducer issues the RCCL bucket all-reduces)'),
+                      else 'eager launches from Python (the host reducer issues the bucket all-reduces)'),
+        'conv_variant_table': {'rows': len(tune.export()),
+                               'digest_per_rank': tune_digests,
+                               'note': 'rank 0 tunes, the other ranks import its table (ssseg.tune.sync)'},
+        'collectives': (None if world == 1 else
+                        {'transport': scomm.kind(), 'backend': dist.get_backend(),
+                         'note': 'native = libssseg RCCL communicator (ssseg_allreduce_buckets), gradient buckets on a '
+                                 'side stream + SyncBN sums, inside the captured step'}),
         'step_tflops': round(8 * FWD_GFLOP_PER_IMAGE * args.batch * world / (elapsed / args.steps) / 1e3, 2),
         'liveness': {'losses_finite': finite, 'sup_loss_last': round(float(live[-1, 0]), 6),
                      'unsup_loss_last': round(float(live[-1, 1]), 6),
@@ -391,7 +408,7 @@ def main():
                                       'of the N>1 lines)'}
     if rank == 0 and world == 1 and not args.no_fp32:
         try:
-            f_el, _, f_live, _, _, _ = timed_run(argparse.Namespace(**dict(vars(args), steps=min(args.steps, 5), warmup=2)),
+            f_el, _, f_live, _, _, _, _ = timed_run(argparse.Namespace(**dict(vars(args), steps=min(args.steps, 5), warmup=2)),
                                         world, rank, device, torch.float32, probe=False)
             n = min(args.steps, 5)
             result['fp32_mode'] = {'value': round(args.batch * n / f_el, 3), 'unit': 'images/sec',
@@ -412,6 +429,7 @@ def main():
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
+        scomm.reset()
         dist.destroy_process_group()
 
 

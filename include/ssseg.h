@@ -29,8 +29,8 @@ extern "C" {
 
 typedef struct ihipStream_t* ssseg_stream_t;   /* == hipStream_t */
 
-enum { SSSEG_F32 = 0, SSSEG_BF16 = 1, SSSEG_F16 = 2 };
-enum { SSSEG_OK = 0, SSSEG_EINVAL = -1, SSSEG_EUNSUPPORTED = -2, SSSEG_EWORKSPACE = -3 };
+enum { SSSEG_F32 = 0, SSSEG_BF16 = 1, SSSEG_F16 = 2, SSSEG_F64 = 3 /* collectives only */ };
+enum { SSSEG_OK = 0, SSSEG_EINVAL = -1, SSSEG_EUNSUPPORTED = -2, SSSEG_EWORKSPACE = -3, SSSEG_ECOMM = -4 };
 
 /* library identity: returns a static string "ssseg <version> gfx950" */
 const char* ssseg_version(void);
@@ -411,6 +411,15 @@ size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* desc_host, int dt
  * weight-gradient knobs change the fp32 summation order of dW.  Not thread-safe. */
 int ssseg_set_knob(int id, int value);
 
+/* The conv engine's variant table (geometry key -> chosen variant; host memory).  export: writes min(n, cap) rows in
+ * key order and returns n (cap 0: the count only).  import: adds rows (overwrite != 0: replaces existing ones); a
+ * variant id the engine does not have is SSSEG_EINVAL.  Lets rank 0 of a data-parallel job tune and the other ranks
+ * take its table (ssseg/tune.py), so every rank launches the same kernels and only one tunes.  Not thread-safe with
+ * concurrent launches of unseen geometries. */
+int64_t ssseg_tune_table_export(unsigned long long* keys_host, int32_t* variants_host, int64_t cap);
+int ssseg_tune_table_import(const unsigned long long* keys_host, const int32_t* variants_host, int64_t n,
+                            int overwrite);
+
 /* dW = sum over output pixels of dY[p][k] * x_col[p][(r,s,c)] (split-K fp32 slabs + deterministic
  * reduce).  dy is [N][OH][OW] with pixel stride desc.ldy.  layout 0: dw [K][R][S][C];
  * layout 1: dw [k_real][c_real][R][S] (PyTorch OIHW / ConvTranspose2d [Cin][Cout][R][S]).
@@ -514,6 +523,15 @@ int ssseg_channel_sum_grad(const void* x, int64_t P, int64_t C, int64_t ldx, int
 int ssseg_bn_gstat_finalize(double* part, int64_t nparts, int64_t C, double* sums, const float* gamma,
                             const float* beta, const float* mean_eff, const float* invstd, float* dgamma, float* dbeta,
                             float* dconv_bias, ssseg_stream_t stream);
+/* as ssseg_bn_gstat_finalize for a TRAINING BN (mean_eff NULL) whose input x [P][ld] and masked output gradient dy
+ * [P][ld] (dtype dt; the consumer's dgrad applied the ReLU backward) are at hand, with mean / invstd of the forward:
+ * channels where x_hat is not recoverable from the stored y -- gamma == 0, or |beta| >= 8 |gamma| (y ~ beta, its
+ * rounding swamps gamma * x_hat) -- take sum dy * x_hat = sum dy * (x - mean) * invstd from dy and x (the unfused
+ * reduction's arithmetic) in the same launch; the others use the rows as ssseg_bn_gstat_finalize does. */
+int ssseg_bn_gstat_finalize_x(double* part, int64_t nparts, int64_t C, double* sums, const float* gamma,
+                              const float* beta, const void* dy, const void* x, int64_t P, int64_t ld, int dt,
+                              const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                              ssseg_stream_t stream);
 /* eval mode: mean = running_mean, invstd = 1/sqrt(running_var + eps) */
 int ssseg_bn_eval_params(const float* running_mean, const float* running_var, float eps, int64_t C, float* mean_out,
                          float* invstd_out, ssseg_stream_t stream);
@@ -717,6 +735,40 @@ int ssseg_seg_metrics(const float* logits, const int64_t* l_strides4_host, int64
 /* InferenceWrapper head (models/inference_wrapper.py:17-24): logits contiguous [B][2][HW] f32 ->
  * prob = sigmoid(logits), onehot = one_hot(argmax_c logits) (first max, NaN is max), both [B][2][HW] f32. */
 int ssseg_prob_onehot(const float* logits, int64_t B, int64_t HW, float* prob, float* onehot, ssseg_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Collectives: the data-parallel gradient all-reduce and the SyncBN sums
+ * (reference distributed_trainer.py:34-38 -- SyncBatchNorm.convert_sync_batchnorm + DistributedDataParallel,
+ * whose reducer all-reduces gradient buckets during backward; SyncBN all-reduces per-channel sums)
+ *
+ * One RCCL communicator per process (one process per GPU), owned by the caller.  The all-reduce is an RCCL
+ * enqueue on the caller's stream: no host synchronisation, no completion objects, so it is captured into a
+ * hipGraph like a kernel (c10d's ProcessGroupNCCL keeps per-collective Work objects polled by a watchdog
+ * thread, which breaks the capture of a step).  RCCL is resolved at run time (dlopen; PyTorch's already
+ * loaded copy first).  Errors: SSSEG_ECOMM, message in ssseg_comm_last_error().
+ * ------------------------------------------------------------------------------------------- */
+typedef struct ssseg_comm_s* ssseg_comm_t;
+enum { SSSEG_SUM = 0, SSSEG_AVG = 1 };
+
+/* bytes of the unique id that rank 0 creates and every rank passes to ssseg_comm_init (128) */
+size_t ssseg_comm_unique_id_bytes(void);
+/* rank 0: fill uid_host (host memory, ssseg_comm_unique_id_bytes() bytes) -- replaces the c10d store rendezvous of
+ * init_process_group(backend='nccl') (distributed_trainer.py:59 in this repo, utils/utils.py in the reference) */
+int ssseg_comm_get_unique_id(void* uid_host);
+/* collective over all `world` ranks (blocks until every rank has called it): selects `device` and creates the
+ * communicator of this rank */
+int ssseg_comm_init(ssseg_comm_t* comm_out, const void* uid_host, int rank, int world, int device);
+int ssseg_comm_destroy(ssseg_comm_t comm);
+/* 0, or SSSEG_ECOMM when RCCL reported an asynchronous error on the communicator */
+int ssseg_comm_async_error(ssseg_comm_t comm);
+/* static message of the last SSSEG_ECOMM */
+const char* ssseg_comm_last_error(void);
+/* n in-place all-reduces (ptrs_host[i]: device buffer of counts_host[i] elements of dtype dt -- SSSEG_F32 / BF16 /
+ * F16 / F64) in one RCCL group on `stream`; op SSSEG_SUM or SSSEG_AVG.  Replaces DDP's bucket all-reduce
+ * (torch/nn/parallel/distributed.py reducer, called from the backward of train.py:61,115) and SyncBN's
+ * all_reduce of (sum x, sum x^2) / (sum dy, sum dy*x_hat) (torch/nn/modules/_functions.py, forward and backward). */
+int ssseg_allreduce_buckets(ssseg_comm_t comm, void* const* ptrs_host, const int64_t* counts_host, int64_t n, int dt,
+                            int op, ssseg_stream_t stream);
 
 #ifdef __cplusplus
 }

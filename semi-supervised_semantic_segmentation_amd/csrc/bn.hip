@@ -12,6 +12,7 @@
 //             dres = dyr (residual branch gradient)
 #include <cstdlib>
 #include <initializer_list>
+#include <type_traits>
 
 #include "common.h"
 
@@ -304,7 +305,69 @@ struct FinalEpi {
   // B * sum m) * A with training: B = beta, A = 1 / gamma; folded eval (gmean set): B = mean_eff * scale + shift,
   // A = invstd / scale (A = 0 where gamma / scale is 0: x_hat is not recoverable from y there); then mode 2's tail
   const float *ggamma, *gbeta, *gmean, *ginvstd;
+  // mode 3, training BN with the pre-BN input at hand (ssseg_bn_gstat_finalize_x): channels where x_hat is not
+  // recoverable from y to bf16 accuracy -- gamma == 0, or |beta| >= GSTAT_COND * |gamma|, where y ~ beta and y's
+  // rounding swamps gamma * x_hat -- take sum m * x_hat from the masked gradient and x instead (the unfused pass's
+  // arithmetic), inside the same launch
+  const void *gx_dy, *gx_x;
+  int64_t gx_P, gx_ld;
+  int gx_dt;
+  const float *gx_mean, *gx_invstd;
 };
+
+constexpr float GSTAT_COND = 8.f;
+
+__device__ __forceinline__ bool gstat_ill(const FinalEpi& fe, int c) {
+  const float ga = fe.ggamma ? fe.ggamma[c] : 1.f, be = fe.gbeta ? fe.gbeta[c] : 0.f;
+  return !(fabsf(ga) * GSTAT_COND > fabsf(be));   // (NaN gamma: ill as well)
+}
+
+template <typename T>
+__device__ __forceinline__ float ld_f32(const T* p, int64_t i) {
+  if constexpr (sizeof(T) == 4) return p[i];
+  else if constexpr (std::is_same<T, bf16_t>::value) return bf16_to_f32(p[i]);
+  else return (float)p[i];
+}
+
+// sum_p dy[p][c] * (x[p][c] - mean) * invstd over all P pixels by the whole block (256 threads, 8 loads in flight per
+// thread, fp32 per 8-pixel batch, fp64 across batches, a fixed-order butterfly + 4 wave slots): the result is returned
+// on every thread.  Strided 2-byte reads (one channel of every pixel) -- the fallback of an ill-conditioned channel,
+// not a fast path.
+template <typename T>
+__device__ double gstat_x_moment_t(const T* dy, const T* x, int64_t P, int64_t ld, int c, float mu, float is,
+                                   double* red4) {
+  constexpr int U = 8;
+  double acc = 0.0;
+  for (int64_t p0 = threadIdx.x; p0 < P; p0 += 256 * U) {
+    float g[U], v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t p = p0 + u * 256 < P ? p0 + u * 256 : P - 1;
+      g[u] = ld_f32(dy, p * ld + c);
+      v[u] = ld_f32(x, p * ld + c);
+    }
+    float f = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (p0 + u * 256 < P) f = fmaf(g[u], (v[u] - mu) * is, f);
+    acc += (double)f;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  __syncthreads();   // red4 reuse across calls
+  if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  return (red4[0] + red4[1]) + (red4[2] + red4[3]);
+}
+
+__device__ double gstat_x_moment(const FinalEpi& fe, int c, double* red4) {
+  const float mu = fe.gx_mean[c], is = fe.gx_invstd[c];
+  if (fe.gx_dt == SSSEG_BF16)
+    return gstat_x_moment_t((const bf16_t*)fe.gx_dy, (const bf16_t*)fe.gx_x, fe.gx_P, fe.gx_ld, c, mu, is, red4);
+  if (fe.gx_dt == SSSEG_F16)
+    return gstat_x_moment_t((const f16_t*)fe.gx_dy, (const f16_t*)fe.gx_x, fe.gx_P, fe.gx_ld, c, mu, is, red4);
+  return gstat_x_moment_t((const float*)fe.gx_dy, (const float*)fe.gx_x, fe.gx_P, fe.gx_ld, c, mu, is, red4);
+}
 
 // mode 3: the x_hat moment of channel c from the (sum m, sum m * y) moments
 __device__ __forceinline__ double gstat_xhat_moment(const FinalEpi& fe, int c, double a, double b) {
@@ -426,8 +489,21 @@ __global__ void __launch_bounds__(256) bn_partial_final_kernel(const double* par
   double a, b;
   partial_col_sums<CH>(part, nparts, C, rs, blockIdx.x, a, b);
   const int c = blockIdx.x * CH + threadIdx.x;
+  __shared__ double xfix[CH];
+  __shared__ int xill[CH];
+  if (fe.mode == 3 && fe.gx_x) {   // (uniform) the ill-conditioned channels of this block, recomputed from x
+    __shared__ double red4[4];
+    if (threadIdx.x < CH) xill[threadIdx.x] = c < C && gstat_ill(fe, c);
+    __syncthreads();
+    for (int k = 0; k < CH; ++k)
+      if (xill[k]) {   // (uniform)
+        const double v = gstat_x_moment(fe, blockIdx.x * CH + k, red4);
+        if (threadIdx.x == 0) xfix[k] = v;
+      }
+    __syncthreads();
+  }
   if (threadIdx.x < CH && c < C) {
-    if (fe.mode == 3) b = gstat_xhat_moment(fe, c, a, b);
+    if (fe.mode == 3) b = (fe.gx_x && xill[threadIdx.x]) ? xfix[threadIdx.x] : gstat_xhat_moment(fe, c, a, b);
     sums[c] = a;
     sums[C + c] = b;
     if (fe.mode == 1) {
@@ -990,6 +1066,31 @@ extern "C" int ssseg_bn_gstat_finalize(double* part, int64_t nparts, int64_t C, 
   fe.gbeta = beta;
   fe.gmean = mean_eff;
   fe.ginvstd = invstd;
+  launch_partial_final(part, nparts, C, sums, (hipStream_t)stream, fe);
+  SSSEG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ssseg_bn_gstat_finalize_x(double* part, int64_t nparts, int64_t C, double* sums, const float* gamma,
+                                         const float* beta, const void* dy, const void* x, int64_t P, int64_t ld, int dt,
+                                         const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                                         ssseg_stream_t stream) {
+  if (!part || !sums || nparts < 1 || C < 1 || nparts > 0x7fffffff) return SSSEG_EINVAL;
+  if (!dy || !x || !mean || !invstd || P < 1 || ld < C) return SSSEG_EINVAL;
+  if (dt != SSSEG_F32 && dt != SSSEG_BF16 && dt != SSSEG_F16) return SSSEG_EUNSUPPORTED;
+  FinalEpi fe{};
+  fe.mode = 3;
+  fe.dgamma = dgamma;
+  fe.dbeta = dbeta;
+  fe.ggamma = gamma;
+  fe.gbeta = beta;
+  fe.gx_dy = dy;
+  fe.gx_x = x;
+  fe.gx_P = P;
+  fe.gx_ld = ld;
+  fe.gx_dt = dt;
+  fe.gx_mean = mean;
+  fe.gx_invstd = invstd;
   launch_partial_final(part, nparts, C, sums, (hipStream_t)stream, fe);
   SSSEG_LAUNCH_CHECK();
   return 0;

@@ -1,7 +1,9 @@
 // Implicit-GEMM convolution engine: host dispatch, variant autotune, register-staged launches, weight
 // packing.  Device code: conv_kernels.h; LDS-DMA configs: conv_glds_*.hip; weight gradients: conv_wgrad.hip.
 #include <mutex>
+#include <algorithm>
 #include <unordered_map>
+#include <vector>
 
 #include "conv_kernels.h"
 
@@ -454,6 +456,39 @@ extern "C" int ssseg_set_knob(int id, int value) {
     return 0;
   }
   g_knobs[id] = value;
+  return 0;
+}
+
+// the variant table (geometry key -> variant): exported by one rank and imported by the others, so every rank of a
+// data-parallel job launches the same kernels without tuning them itself (ssseg/tune.py)
+extern "C" int64_t ssseg_tune_table_export(unsigned long long* keys_host, int32_t* variants_host, int64_t cap) {
+  std::lock_guard<std::mutex> lk(g_variant_mu);
+  if (cap > 0 && (!keys_host || !variants_host)) return SSSEG_EINVAL;
+  std::vector<std::pair<unsigned long long, int>> rows(g_variant.begin(), g_variant.end());
+  std::sort(rows.begin(), rows.end());   // a canonical order: equal tables export equal arrays
+  const int64_t n = (int64_t)rows.size();
+  for (int64_t i = 0; i < n && i < cap; ++i) {
+    keys_host[i] = rows[i].first;
+    variants_host[i] = rows[i].second;
+  }
+  return n;
+}
+
+extern "C" int ssseg_tune_table_import(const unsigned long long* keys_host, const int32_t* variants_host, int64_t n,
+                                       int overwrite) {
+  if (n < 0 || (n > 0 && (!keys_host || !variants_host))) return SSSEG_EINVAL;
+  for (int64_t i = 0; i < n; ++i) {
+    bool known = false;
+    for (int c : kCandidates) known = known || c == variants_host[i];
+    if (!known) return SSSEG_EINVAL;
+  }
+  std::lock_guard<std::mutex> lk(g_variant_mu);
+  for (int64_t i = 0; i < n; ++i) {
+    if (overwrite)
+      g_variant[keys_host[i]] = variants_host[i];
+    else
+      g_variant.emplace(keys_host[i], variants_host[i]);
+  }
   return 0;
 }
 

@@ -17,6 +17,11 @@ racing with the in-flight all-reduce.
 
 Reduction op: AVG on RCCL; SUM + a native 1/world scale on the side stream for gloo (which has no AVG).
 
+Transport: on an RCCL process group the buckets go through the process's native communicator (ssseg.comm,
+libssseg ssseg_allreduce_buckets): an RCCL enqueue on the side stream with no completion object, so a step with live
+collectives captures into a HIP graph.  torch.distributed's own all_reduce (async Work objects, waited in finish()) is the
+path of gloo groups and of SSSEG_COMM=c10d.
+
 Reference semantics: DDP all-reduces after EACH of the two backward passes of a step (train.py:61,115).
 Gradients accumulate between them and the all-reduce is linear, so reducing once — armed on the last
 backward of the step — gives the same averaged gradient (up to fp summation order) with half the
@@ -29,6 +34,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from . import arena as _arena
+from . import comm as _comm
 
 _FORCE = {'on': False}
 
@@ -82,6 +88,11 @@ class DistributedDataParallel(nn.Module):
         self._launched = None
         self._works = []
         self._stream = torch.cuda.Stream() if (self._active and a.data.is_cuda) else None
+        # the native communicator (created here, on every rank at the same point: a collective call)
+        self._comm = _comm.get() if (self._active and a.data.is_cuda) else None
+        if self.world > 1:   # rank 0 tunes the conv geometries, the others take its table (ssseg.tune.sync)
+            from . import tune
+            tune.follow_rank0()
 
     def forward(self, *args, **kwargs):
         return self.module(*args, **kwargs)
@@ -130,7 +141,10 @@ class DistributedDataParallel(nn.Module):
             ev.record(torch.cuda.current_stream())
             with torch.cuda.stream(self._stream):
                 self._stream.wait_event(ev)
-                self._works.append((view, dist.all_reduce(view, op=op, async_op=True)))
+                if self._comm is not None:   # RCCL enqueue on the side stream, nothing to wait on but the stream
+                    self._comm.all_reduce([view], 'avg', stream=self._stream)
+                else:
+                    self._works.append((view, dist.all_reduce(view, op=op, async_op=True)))
         else:   # CPU tensors (gloo): synchronous
             dist.all_reduce(view, op=op)
             if not self._avg:

@@ -11,9 +11,10 @@ pairs, the second builds the teacher's BN fold table, a host-to-device copy that
 device-side Philox counter (ssseg_cowmix_draw_dev), so every replay draws fresh masks -- the same sequence the eager
 steps would.  Host-side values are baked in at capture: a replay repeats the captured step's Python decisions (the
 optimizer step taken or skipped, the epoch gate of the consistency weight, the learning rate), so capture a step with
-step != 0 and recapture when those change.  Steps without collectives only: a DDP step with its RCCL collectives
-captured (gradient buckets on the side stream, SyncBN sums) hung on replay at world 1 on this image's RCCL 2.26.6, and
-gloo collectives run on the host.
+step != 0 and recapture when those change.  Collectives: a DDP step captures when its gradient buckets and SyncBN sums
+go through the native RCCL communicator (ssseg.comm: an enqueue on the stream, recorded like a kernel); c10d's
+collectives do not (its watchdog polls their Work events, which a capture refuses -- DESIGN.md §6), and gloo runs on the
+host.
 
     step = StepGraph(lambda img, mask, ua, ub: train.train_step(model, teacher, opt, img, mask, ua, ub, epoch, 1, cfg),
                      img, mask, ua, ub)
@@ -37,9 +38,13 @@ class StepGraph:
         for _ in range(warmup):   # eager steps first (they tune every conv geometry); callers usually ran them
             fn(*self.static_in)
         torch.cuda.synchronize()
+        from . import nn as snn
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, capture_error_mode=_capture_mode()):
-            self.static_out = fn(*self.static_in)
+        # the descriptor tables the captured launches read by pointer stay alive as long as the graph
+        with snn.graph_refs() as refs:
+            with torch.cuda.graph(self.graph, capture_error_mode=_capture_mode()):
+                self.static_out = fn(*self.static_in)
+        self.refs = list(refs)
 
     def __call__(self, *inputs):
         for dst, src in zip(self.static_in, inputs):

@@ -14,8 +14,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('SSSEG_LIB_PATH') or os.path.join(_HERE, 'libssseg.so')   # override: A/B builds only
 HEADER = os.path.join(_HERE, '..', '..', 'include', 'ssseg.h')
 
-F32, BF16, F16 = 0, 1, 2
-_ERRS = {-1: 'SSSEG_EINVAL', -2: 'SSSEG_EUNSUPPORTED', -3: 'SSSEG_EWORKSPACE'}
+F32, BF16, F16, F64 = 0, 1, 2, 3
+SSSEG_SUM, SSSEG_AVG = 0, 1
+_ERRS = {-1: 'SSSEG_EINVAL', -2: 'SSSEG_EUNSUPPORTED', -3: 'SSSEG_EWORKSPACE', -4: 'SSSEG_ECOMM'}
 
 vp, i64, i32, f32, f64, sz, u64 = (ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_double,
                                    ctypes.c_size_t, ctypes.c_uint64)
@@ -92,6 +93,8 @@ SIGS = {
     'ssseg_dwconv_wgrad': (i32, [vp, vp, vp, vp, i32, i64, i32, vp, sz, vp]),
     'ssseg_conv_igemm_workspace_bytes': (sz, [vp, i32]),
     'ssseg_set_knob': (i32, [i32, i32]),
+    'ssseg_tune_table_export': (i64, [vp, vp, i64]),
+    'ssseg_tune_table_import': (i32, [vp, vp, i64, i32]),
     'ssseg_conv_wgrad_workspace_bytes': (sz, [vp, i32]),
     'ssseg_conv_wgrad': (i32, [vp, vp, vp, vp, i32, i64, i64, i32, i32, vp, sz, vp]),
     'ssseg_conv_wgrad2_workspace_bytes': (sz, [vp, i64, i32]),
@@ -107,6 +110,7 @@ SIGS = {
     'ssseg_bn_stats': (i32, [vp, i64, i64, i64, i32, vp, vp, sz, vp]),
     'ssseg_bn_partials_finalize': (i32, [vp, i64, i64, vp, f64, f32, f32, vp, vp, vp, vp, vp, vp]),
     'ssseg_bn_gstat_finalize': (i32, [vp, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    'ssseg_bn_gstat_finalize_x': (i32, [vp, i64, i64, vp, vp, vp, vp, vp, i64, i64, i32, vp, vp, vp, vp, vp]),
     'ssseg_channel_sum_grad': (i32, [vp, i64, i64, i64, i32, vp, vp, vp, sz, vp]),
     'ssseg_bn_finalize': (i32, [vp, i64, f64, f32, f32, vp, vp, vp, vp, vp, vp]),
     'ssseg_bn_eval_params': (i32, [vp, vp, f32, i64, vp, vp, vp]),
@@ -150,6 +154,14 @@ SIGS = {
     'ssseg_rng_take': (i32, [vp, vp, u64, vp]),
     'ssseg_att_blend_fwd': (i32, [vp, I64P, vp, I64P, vp, I64P, vp, i64, i64, i64, i64, vp]),
     'ssseg_att_blend_bwd': (i32, [vp, I64P, vp, I64P, vp, I64P, vp, I64P, vp, vp, vp, i64, i64, i64, i64, vp]),
+    # collectives (csrc/comm.hip; ssseg/comm.py)
+    'ssseg_comm_unique_id_bytes': (sz, []),
+    'ssseg_comm_get_unique_id': (i32, [vp]),
+    'ssseg_comm_init': (i32, [ctypes.POINTER(ctypes.c_void_p), vp, i32, i32, i32]),
+    'ssseg_comm_destroy': (i32, [vp]),
+    'ssseg_comm_async_error': (i32, [vp]),
+    'ssseg_comm_last_error': (ctypes.c_char_p, []),
+    'ssseg_allreduce_buckets': (i32, [vp, ctypes.POINTER(ctypes.c_void_p), I64P, i64, i32, i32, vp]),
 }
 
 

@@ -18,6 +18,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from . import comm as _comm
 from . import native as N
 
 _CFG = {'act_mask': os.environ.get('SSSEG_ACT_MASK', '1') != '0',
@@ -205,6 +206,28 @@ def defer_param_grads():
         flush_param_grads()
 
 
+# device tensors a launch reads through a raw pointer baked into a kernel argument (descriptor tables): while a HIP graph
+# is captured (ssseg.graph.StepGraph) each one used is recorded here and the graph keeps it alive, so a later table
+# replacing it (new rows) cannot free memory a cached graph still reads
+_GRAPH_REFS = {'live': None}
+
+
+def _graph_ref(t):
+    if _GRAPH_REFS['live'] is not None and torch.cuda.is_current_stream_capturing():
+        _GRAPH_REFS['live'].append(t)
+    return t
+
+
+@contextlib.contextmanager
+def graph_refs():
+    """Collect the descriptor tables the launches captured inside the block read (yields the list)."""
+    prev, _GRAPH_REFS['live'] = _GRAPH_REFS['live'], []
+    try:
+        yield _GRAPH_REFS['live']
+    finally:
+        _GRAPH_REFS['live'] = prev
+
+
 def flush_param_grads():
     import struct
     pend, _PGRAD['pending'] = _PGRAD['pending'], []
@@ -233,7 +256,8 @@ def flush_param_grads():
         blob = b''.join(struct.pack('<10q', *r) for r in rows)
         ent = (rows, torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(pend[0]['part'].device))
         _PGRAD['table'] = ent
-    N.call('ssseg_bn_param_grad_batch', N.dev_ptr(ent[1]), len(rows), max(e['C'] for e in pend), N.stream())
+    N.call('ssseg_bn_param_grad_batch', N.dev_ptr(_graph_ref(ent[1])), len(rows), max(e['C'] for e in pend),
+           N.stream())
 
 
 def wgrad_pending():
@@ -1386,7 +1410,7 @@ class _BNFn(torch.autograd.Function):
                 if _sync_group(True):
                     N.call('ssseg_bn_partials_finalize', N.dev_ptr(pre.part), pre.rows, C, N.dev_ptr(sums), 0.0, 0.0,
                            0.0, None, None, None, None, None, N.stream())
-                    dist.all_reduce(sums)
+                    _comm.all_reduce_sum(sums)
                     count = float(P * dist.get_world_size())
                     N.call('ssseg_bn_finalize', N.dev_ptr(sums), C, count, *fin[2:], N.stream())
                 else:
@@ -1395,7 +1419,7 @@ class _BNFn(torch.autograd.Function):
             elif _sync_group(True):
                 N.call('ssseg_bn_stats', N.dev_ptr(x), P, C, cp, N.dt_code(x), N.dev_ptr(sums), N.dev_ptr(ws), nb,
                        N.stream())
-                dist.all_reduce(sums)
+                _comm.all_reduce_sum(sums)
                 count = float(P * dist.get_world_size())
                 N.call('ssseg_bn_finalize', N.dev_ptr(sums), C, count, *fin[2:], N.stream())
             else:   # one launch: the finalize runs in the reduction's tail
@@ -1440,10 +1464,12 @@ class _BNFn(torch.autograd.Function):
         act = 0 if gy.__dict__.get('_ssseg_premasked', False) else _act(ctx.relu)[0]
         gs = gy.__dict__.get('_ssseg_gstats')
         if gs is not None and ctx.training and gs.rows > 0 and gs.C == C and residual is None and act == 0:
-            # (sum dy, sum dy * y) rows from that epilogue -> (sum dy, sum dy * x_hat) + (dgamma, dbeta)
-            N.call('ssseg_bn_gstat_finalize', N.dev_ptr(gs.part), gs.rows, C, N.dev_ptr(sums),
-                   N.dev_ptr(wt) if wt is not None else None, N.dev_ptr(bs) if bs is not None else None, None, None,
-                   *(_grad_ptrs(mod.weight, mod.bias) if pgrad else (None, None)), None, N.stream())
+            # (sum dy, sum dy * y) rows from that epilogue -> (sum dy, sum dy * x_hat) + (dgamma, dbeta); channels
+            # whose x_hat y cannot resolve (gamma == 0, |beta| >= 8 |gamma|) are summed from gy (premasked) and x
+            N.call('ssseg_bn_gstat_finalize_x', N.dev_ptr(gs.part), gs.rows, C, N.dev_ptr(sums),
+                   N.dev_ptr(wt) if wt is not None else None, N.dev_ptr(bs) if bs is not None else None,
+                   N.dev_ptr(gy), N.dev_ptr(x), P, cp, N.dt_code(x), N.dev_ptr(mean), N.dev_ptr(invstd),
+                   *(_grad_ptrs(mod.weight, mod.bias) if pgrad else (None, None)), N.stream())
         else:
             # reduction + (dgamma, dbeta) from the local sums in one launch (ssseg_bn_bwd_reduce_grad)
             N.call('ssseg_bn_bwd_reduce_grad', N.dev_ptr(gy), N.dev_ptr(x), res_p, P, C, cp, cp, cp, N.dev_ptr(mean),
@@ -1454,7 +1480,7 @@ class _BNFn(torch.autograd.Function):
             _ready(mod.weight, mod.bias)
         count = ctx.count
         if ctx.training and _sync_group(True):
-            dist.all_reduce(sums)
+            _comm.all_reduce_sum(sums)
         dx = new_act(n, cp, h, w, x.dtype, dev, zero=cp > _pad16(C, x.dtype))
         want_res = residual is not None and ctx.needs_input_grad[3]
         dres = new_act(n, cp, h, w, x.dtype, dev, zero=cp > _pad16(C, x.dtype)) if want_res else None
@@ -1873,7 +1899,7 @@ def folded(model):
             blob = b''.join(struct.pack('<6q2qd', *r[3], float(r[0].eps)) for r in rows)
             dev = rows[0][2].device
             cache[0], cache[1] = sig, torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
-        N.call('ssseg_bn_fold_batch', N.dev_ptr(cache[1]), len(rows), N.stream())
+        N.call('ssseg_bn_fold_batch', N.dev_ptr(_graph_ref(cache[1])), len(rows), N.stream())
     try:
         for bn, conv, buf, _ in rows:
             bn.__dict__['_ssseg_fold_live'] = (conv, buf)

@@ -303,10 +303,14 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
 # or skipped (train.py:121, step % virtual_batch_size_multiplier), the epoch gate of the consistency weight
 # (train.py:112), every learning rate, the input geometry and compute dtype -- a new key captures a new graph (the two
 # most recent are kept).  Not captured (eager steps instead): CowMix drawn from the CPU generator (parity mode), steps
-# with collectives (world > 1: DDP buckets and SyncBN), the first optimizer step (SGD's momentum buffer starts from it),
+# with collectives on torch.distributed (gloo, or SSSEG_COMM=c10d: the native RCCL communicator's steps ARE captured),
+# the first optimizer step (SGD's momentum buffer starts from it),
 # and SSSEG_TRAIN_GRAPH=0.
 _GRAPH = {'on': os.environ.get('SSSEG_TRAIN_GRAPH', '1') != '0', 'cache': {}, 'eager_steps': 2, 'max_graphs': 2,
           'captures': 0, 'replays': 0}
+
+
+_TUNE = {'steps': 0}
 
 
 def _optimizers(optimizer, config):
@@ -322,7 +326,11 @@ def _graph_key(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
     if tc['use_semi_supervised'] and cowmix.NOISE_SOURCE != 'device':
         return None
     if torch.distributed.is_initialized() and (_world() > 1 or getattr(model, '_active', False)):
-        return None   # collectives in the step (DDP buckets, SyncBN): RCCL inside a captured graph hung
+        # collectives in the step (DDP buckets, SyncBN): capturable only on the native communicator (ssseg.comm; c10d's
+        # Work objects and watchdog break a capture, gloo runs on the host) -- DESIGN.md §6
+        from ssseg import comm as scomm
+        if scomm.kind() != 'native':
+            return None
     opts = _optimizers(optimizer, config)
     opt_step = step % tc['virtual_batch_size_multiplier'] == 0 and step != 0
     # the first SGD step initialises the momentum buffer (a different kernel argument): run it eagerly (the
@@ -369,6 +377,13 @@ def _graph_step(key, model, ema_model, optimizer, image, mask, unsup_a, unsup_b,
 
 def run_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch, step, config):
     """train_step, replayed from a captured HIP graph where the step's key allows it (see _GRAPH)."""
+    if _world() > 1 and image.is_cuda:
+        # rank 0's conv variant table to every rank once the eager tuning steps are done (ssseg.tune: ranks > 0 ran
+        # the static rule meanwhile), before any capture -- the same kernels on every rank
+        from ssseg import tune
+        _TUNE['steps'] += 1
+        if not tune.synced() and _TUNE['steps'] > _GRAPH['eager_steps']:
+            tune.sync()
     key = _graph_key(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch, step, config)
     if key is None:
         return train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch, step, config)

@@ -62,12 +62,24 @@ class _CollectiveLog:
     """Counts every torch.distributed.all_reduce of the step (ssseg.ddp's gradient buckets, ssseg.nn's SyncBN
     statistic sums, utils.reduce_tensor): (tensor dtype, bytes) per call."""
     def __init__(self, dist):
+        from ssseg import comm
         self.calls, self._orig, self._dist = [], dist.all_reduce, dist
+        self._comm_cls, self._orig_native = comm.NativeComm, comm.NativeComm.all_reduce
 
         def wrapped(tensor, *a, **k):
             self.calls.append((str(tensor.dtype), tensor.numel() * tensor.element_size()))
             return self._orig(tensor, *a, **k)
         dist.all_reduce = wrapped
+
+        def wrapped_native(comm_self, tensors, *a, **k):   # the native communicator (RCCL groups): one row per tensor
+            for t in tensors:
+                self.calls.append((str(t.dtype), t.numel() * t.element_size()))
+            return self._orig_native(comm_self, tensors, *a, **k)
+        comm.NativeComm.all_reduce = wrapped_native
+
+    def restore(self):
+        self._dist.all_reduce = self._orig
+        self._comm_cls.all_reduce = self._orig_native
 
     def take(self):
         c, self.calls = self.calls, []
@@ -346,7 +358,7 @@ def _worker_rccl(port, q):
                     early.append(model.last_early)
                     calls.append(log.take())
             if log is not None:
-                dist.all_reduce = log._orig
+                log.restore()
             n_bn = sum(1 for m in student.modules() if isinstance(m, snn.BatchNorm2d))
             return (grads, [v.detach().clone() for v in student.state_dict().values()],
                     [v.detach().clone() for v in teacher.state_dict().values()], early, calls, n_bn,
@@ -357,7 +369,9 @@ def _worker_rccl(port, q):
         got = run(True)
         ddp.force_collectives(False)
         ref = run(False)
-        out = {'backend': dist.get_backend(), 'early': got[3], 'nbuckets': got[6], 'n_bn': got[5],
+        from ssseg import comm
+        out = {'backend': dist.get_backend(), 'transport': comm.kind(), 'early': got[3], 'nbuckets': got[6],
+               'n_bn': got[5],
                'ncalls': [len(c) for c in got[4]], 'mismatch': []}
         for k, (ga, gb) in enumerate(zip(got[0], ref[0])):
             for i, (a, b) in enumerate(zip(ga, gb)):
@@ -392,6 +406,7 @@ def test_rccl_world1_forced_collectives_bitwise(hip_device):
             p.kill()
     assert not isinstance(out, str), out
     assert out['backend'] == 'nccl'
+    assert out['transport'] == 'native'     # the step's collectives went through libssseg's RCCL communicator
     assert out['ngrads'] == STEPS
     # the learning backward launches every bucket in finish(); later armed backwards launch from inside the backward
     assert out['early'][0] == 0 and all(e > 0 for e in out['early'][1:]), out['early']
@@ -399,3 +414,115 @@ def test_rccl_world1_forced_collectives_bitwise(hip_device):
     assert all(n == out['nbuckets'] + 2 * out['n_bn'] for n in out['ncalls']), out['ncalls']
     assert not out['mismatch'], out['mismatch'][:10]
 
+
+
+def _worker_rccl_graph(port, q):
+    """world-1 RCCL process group, collectives forced on, on the native communicator (ssseg.comm): the C2 step (UNet-R50
+    at 64², bs 2, bench.build: DDP + SyncBN, teacher pass and consistency forward on the side stream) run eagerly and
+    replayed from a captured HIP graph must give bit-identical losses, parameters, running statistics and teacher
+    weights -- and equal the same steps without any collective."""
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    import torch.distributed as dist
+    try:
+        import bench
+        import cowmix
+        import train
+        from ssseg import comm, ddp
+        from ssseg import native as N
+        from ssseg import nn as snn
+        from ssseg.graph import StepGraph
+        dev = torch.device('cuda:0')
+        torch.cuda.set_device(dev)
+        N.call('ssseg_set_knob', 5, 0)          # static variants: every run launches the same kernels
+        snn.set_compute_dtype(torch.bfloat16)
+        cowmix.NOISE_SOURCE = 'device'
+        dist.init_process_group('nccl', rank=0, world_size=1, device_id=dev)
+        steps, size, batch = 3, 64, 2
+
+        def run(mode):
+            ddp.force_collectives(mode != 'plain')
+            model, teacher, opt, cfg = bench.build(batch, size, dev)
+            data = bench.synthetic_batches(steps + 2, batch, size, dev, 0)
+            for c in cowmix._DEVICE_RNG['ctr'].values():
+                c.zero_()
+            model.train()
+            opt.zero_grad()
+            log = _CollectiveLog(dist)
+            losses = [train.train_step(model, teacher, opt, *data[k], 30, k, cfg) for k in range(2)]
+            torch.cuda.synchronize()
+            eager_calls = len(log.take())
+            replays = 0
+            if mode == 'graph':
+                g = StepGraph(lambda i, m, a, b: train.train_step(model, teacher, opt, i, m, a, b, 30, 2, cfg),
+                              *data[2])
+                capture_calls = len(log.take())
+                for k in range(2, steps + 2):
+                    losses.append(tuple(t.clone() for t in g(*data[k])))
+                    replays += 1
+                replay_calls = len(log.take())     # a replay issues nothing from Python
+            else:
+                for k in range(2, steps + 2):
+                    losses.append(train.train_step(model, teacher, opt, *data[k], 30, k, cfg))
+                capture_calls = replay_calls = None
+            torch.cuda.synchronize()
+            log.restore()
+            ddp.force_collectives(False)
+            state = {**{'s.' + k: v.detach().clone() for k, v in model.state_dict().items()},
+                     **{'t.' + k: v.detach().clone() for k, v in teacher.state_dict().items()}}
+            n_bn = sum(1 for m in model.modules() if isinstance(m, snn.BatchNorm2d))
+            nb = len(model.buckets) if getattr(model, '_active', False) else 0
+            return dict(losses=[tuple(float(t) for t in l) for l in losses], state=state, eager_calls=eager_calls,
+                        capture_calls=capture_calls, replay_calls=replay_calls, replays=replays, n_bn=n_bn, nb=nb)
+
+        eager = run('eager')
+        graph = run('graph')
+        plain = run('plain')
+        out = {'transport': comm.kind(), 'losses': (eager['losses'], graph['losses'], plain['losses']),
+               'eager_calls': eager['eager_calls'], 'capture_calls': graph['capture_calls'],
+               'replay_calls': graph['replay_calls'], 'replays': graph['replays'], 'n_bn': eager['n_bn'],
+               'nb': eager['nb'], 'plain_calls': plain['eager_calls'], 'mismatch': []}
+        for name, other in (('graph', graph), ('plain', plain)):
+            for k in eager['state']:
+                if not torch.equal(eager['state'][k], other['state'][k]):
+                    out['mismatch'].append((name, k))
+        out['finite'] = all(np.isfinite(v).all() for v in eager['losses'])
+        q.put(out)
+    except Exception as exc:
+        import traceback
+        q.put('ERROR ' + repr(exc) + '\n' + traceback.format_exc())
+    finally:
+        if dist.is_initialized():
+            from ssseg import comm
+            comm.reset()
+            dist.destroy_process_group()
+
+
+@pytest.mark.timeout(400)
+def test_rccl_world1_captured_step_bitwise(hip_device):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_rccl_graph, args=(_free_port(), q))
+    p.start()
+    try:
+        out = q.get(timeout=300)
+    finally:
+        p.join(30)
+        if p.is_alive():
+            p.kill()
+    assert not isinstance(out, str), out
+    assert out['transport'] == 'native'
+    e, g, pl = out['losses']
+    assert out['finite'], e
+    assert e == g, (e, g)              # captured replay == eager, bitwise
+    assert e == pl, (e, pl)            # world-1 collectives change nothing
+    assert not out['mismatch'], out['mismatch'][:10]
+    # two eager steps: one AVG bucket group per gradient bucket + 2 SyncBN sums per training BatchNorm, each step;
+    # the capture records one step's worth, a replay issues none from Python
+    per_step = out['nb'] + 2 * out['n_bn']
+    assert out['nb'] >= 1 and out['n_bn'] > 0
+    assert out['eager_calls'] == 2 * per_step, (out['eager_calls'], per_step)
+    assert out['capture_calls'] == per_step, (out['capture_calls'], per_step)
+    assert out['replays'] == 3 and out['replay_calls'] == 0, out
+    assert out['plain_calls'] == 0
