@@ -170,6 +170,15 @@ def replay_held(order):
     conv's deferred one), then flush_wgrad() -- the launches and the summation order of the serial schedule."""
     calls, _HOLD['calls'] = _HOLD['calls'], []
     adds, _HOLD['adds'] = _HOLD['adds'], []
+    # the held operands and temporaries were allocated on the side stream; they are consumed here on this stream:
+    # record it, so the allocator does not hand their blocks to later side-stream work while these launches read them
+    cur = torch.cuda.current_stream()
+    for _, tmp in adds:
+        tmp.record_stream(cur)
+    for _, _, args, kw in calls:
+        for t in list(args) + list(kw.values()):
+            if isinstance(t, torch.Tensor) and t.is_cuda:
+                t.record_stream(cur)
     for p, tmp in adds:   # grad += tmp (tmp = the one fp32 term the kernel would have added): bitwise the same sum
         g = _grad_of(p)
         N.call('ssseg_axpby', N.dev_ptr(g), 1.0, N.dev_ptr(tmp), 1.0, N.dev_ptr(g), g.numel(), N.stream())
@@ -1097,7 +1106,8 @@ class Conv2d(nn.Conv2d, _ConvBase):
         """Gradient statistics in the masked dgrad: every output phase has taps (an empty phase's zero launch
         writes no statistics rows)."""
         (R, S), (sh, sw) = self.kernel_size, self.stride
-        return (sh == 1 and sw == 1) or (R >= sh and S >= sw and self.dilation in (1, (1, 1)))
+        # (at most 4 output phases: _masked_dgrad sizes the statistics table for that many phase tails)
+        return (sh == 1 and sw == 1) or (R >= sh and S >= sw and sh * sw <= 4 and self.dilation in (1, (1, 1)))
 
     def _ssseg_dgrad(self, gy, xshape, residual=None, mask=None, stats=None, scale=None):
         """dx of the conv; `residual` (a pending gradient of x, GradHandoff) is added in the epilogue; `mask` = (y,

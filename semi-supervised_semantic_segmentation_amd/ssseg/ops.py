@@ -292,7 +292,7 @@ class _Lovasz(torch.autograd.Function):
         g = _c(g.float())
         N.call('ssseg_lovasz_bwd_from_fwd', N.dev_ptr(logits), N.dev_ptr(target), B, C, HW, N.dev_ptr(g),
                N.dev_ptr(gx), N.dev_ptr(ctx.ws), ctx.nb, N.stream())
-        ctx.ws = None
+        # (ctx.ws stays for the lifetime of ctx: a second backward through a retained graph reads it again)
         return gx, None
 
 

@@ -128,3 +128,111 @@ def test_grad_scaler_floor_after_many_overflows(hip_device):
     w = m.weight.detach()
     assert bool(torch.isfinite(w).all())
     np.testing.assert_allclose((before[0] - w).cpu().numpy(), 0.1, rtol=1e-6)
+
+
+def test_c5_fp16_vs_oracle(hip_device):
+    """C5's fp16 arithmetic against the oracle (verdict r5 ask 4a): FC-HarDNet student (oracle/hardnet_ref.py, pinned
+    bit-exact to the reference network by golden G6b) + EMA teacher + Discriminator(5, 2, 64, 512, 1) with the
+    adversarial branch, two semi-supervised steps at 128^2, bs 2 (step 0: no student optimizer step, train.py:121;
+    step 1: clip + SGD; a discriminator SGD step each step).  The HIP run is in the fp16 compute mode (IEEE-half
+    activations and packed weights, fp32 accumulation and master weights, device loss scaling); the oracle runs the
+    same steps in fp64 (the yardstick) and in torch-CPU fp16 (the model, data and optimizer in half -- what fp16
+    rounding of the reference itself costs).  Every loss and every parameter / BN buffer of the student and of D must
+    lie within max(1e-3 relative, 2x the oracle-fp16 drift from fp64): the HIP fp16 path is no worse than the
+    reference computed in fp16."""
+    import cowmix
+    import losses
+    import train
+    from models.adapters import ListOutput
+    from models.discriminator import Discriminator
+    from models.hardnet import HarDNet
+    from oracle import hardnet_ref, models_ref, train_ref
+    from parity import loss_bound, tensor_outliers
+    from ssseg import amp, arena, optim
+    from ssseg import nn as snn
+    steps = 2
+    torch.manual_seed(0)
+    s_ref = models_ref.ListOutput(hardnet_ref.HarDNet(2))
+    torch.manual_seed(1)    # the teacher differs from the student (an EMA teacher some steps in): a live consistency term
+    t_ref = models_ref.ListOutput(hardnet_ref.HarDNet(2))
+    d_ref = models_ref.Discriminator(5, 2, 64, 512, 1)
+    for p in t_ref.parameters():
+        p.detach_()
+    g = torch.Generator().manual_seed(4)
+    imgs = torch.rand(steps, B, 3, H, H, generator=g)
+    fg = (torch.rand(steps, B, 1, H, H, generator=g) > 0.5).float()
+    masks = torch.cat([1 - fg, fg], 2)
+    unl = torch.rand(2 * steps, B, 3, H, H, generator=g)
+    cfg = dict(sigma_range=(4, 8), confidence_threshold=0.0)
+
+    def oracle(dt):
+        s, t, d = (copy.deepcopy(m).to(dt) for m in (s_ref, t_ref, d_ref))
+        t.eval()
+        opt = torch.optim.SGD(s.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-4)
+        optd = torch.optim.SGD(d.parameters(), lr=0.01, momentum=0.9)
+        torch.manual_seed(3)
+        logs = train_ref.train_epoch(s, t, opt, list(zip(imgs.to(dt), masks.to(dt))), iter(unl.to(dt)), 30,
+                                     train_ref.default_cfg(**cfg), adv=dict(D=d, opt=optd, weight=0.01))
+        return logs, s, d
+
+    r64, s64, d64 = oracle(torch.float64)
+    r16, s16, d16 = oracle(torch.float16)
+
+    snn.set_compute_dtype(torch.float16)
+    try:
+        student, teacher = ListOutput(HarDNet(n_classes=2)), ListOutput(HarDNet(n_classes=2))
+        D = Discriminator(5, 2, 64, 512, 1)
+        student.load_state_dict(s_ref.state_dict())
+        teacher.load_state_dict(t_ref.state_dict())
+        D.load_state_dict(d_ref.state_dict())
+        student, teacher, D = student.to(hip_device), teacher.to(hip_device), D.to(hip_device)
+        for p in teacher.parameters():
+            p.detach_()
+        teacher.eval()
+        arena.attach(student)
+        arena.attach(teacher, with_grads=False)
+        arena.attach(D)
+        opt = optim.SGD(student.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-4)
+        optd = optim.SGD(D.parameters(), lr=0.01, momentum=0.9)
+        # a scale that cannot overflow here (the per-pixel loss gradients are ~1e-5): no step is skipped
+        opt.grad_scaler = amp.GradScaler(hip_device, init_scale=2.0 ** 12)
+        optd.grad_scaler = amp.GradScaler(hip_device, init_scale=2.0 ** 12)
+        adv = dict(discriminator=D, optimizer=optd, weight=0.01)
+        tcfg = dict(loss=losses.CalculateLoss([{'loss_fn': losses.DenseBinaryCrossEntropyLossWithLogits('mean'),
+                                                'weight': [0.5]}]),
+                    virtual_batch_size_multiplier=1, use_semi_supervised=True, mask_proportion_range=(0.45, 0.55),
+                    consistency_loss_weight=10, ema_model_alpha=0.99, print_freq=1, gradient_clip_value=5.0,
+                    adversarial=adv, **cfg)
+        old = cowmix.NOISE_SOURCE
+        cowmix.NOISE_SOURCE = 'cpu'
+        logs = []
+        try:
+            torch.manual_seed(3)
+            student.train()
+            opt.zero_grad()
+            for k in range(steps):
+                c, u, _ = train.train_step(student, teacher, opt, imgs[k].to(hip_device), masks[k].to(hip_device),
+                                           unl[2 * k].to(hip_device), unl[2 * k + 1].to(hip_device), 30, k,
+                                           {'train': tcfg})
+                logs.append((float(c), float(adv['last_loss_adv']), float(adv['last_loss_d']), float(u)))
+        finally:
+            cowmix.NOISE_SOURCE = old
+        assert not opt.grad_scaler.found_inf() and not optd.grad_scaler.found_inf()
+        keys = ('sup_loss', 'adv_loss', 'd_loss', 'unsup_loss')
+        bad = []
+        for k in range(steps):
+            for j, n in enumerate(keys):
+                h, a, b = logs[k][j], r16[k][n], r64[k][n]
+                lim = loss_bound(a, b, strict=False)
+                print(f'step {k} {n}: hip-fp16 {h:.8g} oracle-fp16 {a:.8g} oracle-fp64 {b:.8g} |hip-64| '
+                      f'{abs(h - b):.2e} |o16-64| {abs(a - b):.2e} bound {lim:.2e}')
+                if not abs(h - b) <= lim:
+                    bad.append((k, n, h, a, b))
+        assert not bad, bad
+        np_sd = lambda m: {k: v.detach().cpu().double().numpy() for k, v in m.state_dict().items()}  # noqa: E731
+        out_s = tensor_outliers(np_sd(student), np_sd(s16), np_sd(s64))
+        out_d = tensor_outliers(np_sd(D), np_sd(d16), np_sd(d64))
+        print('student outliers', out_s[:5], 'discriminator outliers', out_d[:5])
+        assert not out_s and not out_d, (out_s[:5], out_d[:5])
+    finally:
+        snn.set_compute_dtype(torch.bfloat16)

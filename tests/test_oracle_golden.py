@@ -170,3 +170,36 @@ def test_inference_head_vs_reference_golden():
     mask, prob = losses_ref.inference_head(g['logits'], tuple(int(v) for v in g['image_hw']))
     np.testing.assert_array_equal(mask, g['mask'])
     np.testing.assert_allclose(prob, g["prob"], rtol=0, atol=5e-6)
+
+
+def test_hardnet_restatement_vs_reference_golden():
+    """oracle/hardnet_ref.py (the C5 network's CPU restatement) against the reference's own FC-HarDNet (golden G6b,
+    model2_hardnet.npz): the same seed + perturbation gives the reference's weights (SHA-256 of the state_dict), and the
+    eval / train forwards and the stored parameter gradients agree to fp32 rounding."""
+    import seeded
+    from oracle import hardnet_ref
+    g = golden('model2_hardnet.npz')
+    seed = int(g['seed'])
+    torch.manual_seed(seed)
+    m = hardnet_ref.HarDNet(n_classes=2)
+    seeded.perturb(m, seed + 1000, None)
+    assert seeded.state_sha(m) == str(g['sha'])
+    gen = torch.Generator().manual_seed(seed + 2000)
+    x = torch.rand(*[int(v) for v in g['shape0']], generator=gen)
+    assert seeded.array_sha(x) == str(g['x0_sha'])
+    m.eval()
+    with torch.no_grad():
+        ye = m(x)
+    scale = float(np.abs(g['y_eval']).max())
+    assert np.abs(ye.numpy() - g['y_eval']).max() <= 1e-5 * scale
+    m.train()
+    y = m(x)
+    gy = torch.randn(y.shape, generator=gen)
+    assert seeded.array_sha(gy) == str(g['gy_sha'])
+    (y * gy).sum().backward()
+    assert np.abs(y.detach().numpy() - g['y_train']).max() <= 1e-5 * float(np.abs(g['y_train']).max())
+    params = dict(m.named_parameters())
+    for k in g.keys():
+        if k.startswith('grad.'):
+            ref = g[k]
+            assert np.abs(params[k[5:]].grad.numpy() - ref).max() <= 1e-4 * (np.abs(ref).max() + 1e-30), k

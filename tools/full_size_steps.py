@@ -204,7 +204,8 @@ def run(name, path, dev, threshold=0.5, calibrate=True, layers=False, graph=Fals
            'confidence_threshold': threshold, 'bn_calibrated': calibrate,
            'cm_mean': [row[2] for row in out], 'losses': out, 'losses_finite': losses_finite, 'params_finite': params_finite,
            'ms_per_step_last2': round(1e3 * sum(times[-2:]) / 2, 1), 'first_step_s': round(times[0], 1),
-           'peak_mem_GB': round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)}
+           'peak_mem_GB': round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1),
+           'collectives': getattr(model, '_active', False) and __import__('ssseg.comm', fromlist=['kind']).kind()}
     step_s = sum(times[-2:]) / 2
     tf = STEP_GFLOP_PER_IMAGE[name] * b / step_s / 1e3
     rec['conv_tflops'] = round(tf, 1)
@@ -240,14 +241,22 @@ def main():
                     'first; graph losses checked bitwise against eager steps 3 and 4)')
     ap.add_argument('--train-loop', action='store_true', help='also time the config through train.train (the reference '
                     'entry point, captured-step replay inside)')
+    ap.add_argument('--collectives', action='store_true', help='world 1 with the DDP bucket all-reduces and SyncBN sums '
+                    'forced on (ssseg.ddp.force_collectives): the multi-GPU step\'s collectives on the native RCCL '
+                    'communicator, eager and captured')
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     dist.init_process_group('nccl', init_method='tcp://127.0.0.1:29533', rank=0, world_size=1)
+    if a.collectives:
+        from ssseg import ddp
+        ddp.force_collectives(True)
     ok = True
     for name in a.configs.split(','):
         ok &= run(name, CFGS[name], dev, a.threshold, not a.no_calibrate, a.layers, a.graph, a.train_loop)
         torch.cuda.empty_cache()
+    from ssseg import comm
+    comm.reset()
     dist.destroy_process_group()
     sys.exit(0 if ok else 1)
 
