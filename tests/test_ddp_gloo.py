@@ -162,3 +162,42 @@ def test_reduce_tensor_and_meters_gloo_world2():
     assert res[1][0] == [2.0, 20.0]          # rank 1's tensor is not the destination
     assert res[0][1] == res[1][1] == 3.0     # (2 + 4) / 2
     assert res[0][2] == res[1][2] == -4.5    # (-3 + -6) / 2
+
+
+def _tune_worker(rank, world, port, q):
+    """rank 0's conv variant table reaches every rank (ssseg.tune): the ranks > 0 stop tuning (knob 5 = 0) until
+    sync(), which imports rank 0's rows over their own (static-rule) picks; afterwards every digest is equal."""
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from ssseg import tune
+        tune.follow_rank0()
+        # a table as each rank would have it after the warm-up: rank 0's tuned picks, the others' static rule (and
+        # rank 1 saw one geometry rank 0 keeps too)
+        rows0 = [(11, 3), (12, 14), (13, 26), (99, 6)]
+        rows1 = [(11, 0), (12, 5), (13, 5)]
+        tune.import_(rows0 if rank == 0 else rows1, overwrite=True)
+        before = tune.digest()
+        tune.sync()
+        got = dict(tune.export())
+        q.put((rank, before, tune.digests(), got, tune.synced()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tune_table_sync_gloo_world2():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_tune_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=120) for _ in ps))
+    for p in ps:
+        p.join(30)
+    (b0, d0, t0, s0), (b1, d1, t1, s1) = res[0], res[1]
+    assert b0 != b1                       # the ranks disagreed before the sync
+    assert d0 == d1 and len(set(d0)) == 1  # ... and agree after it
+    assert t1[11] == 3 and t1[12] == 14 and t1[13] == 26 and t1[99] == 6 and t0 == t1
+    assert s0 and s1

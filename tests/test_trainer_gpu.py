@@ -86,7 +86,7 @@ def _run(tmp, graph):
     p = ctx.Process(target=_worker, args=(cfg, _free_port(), graph, q))
     p.start()
     try:
-        res = q.get(timeout=300)
+        res = q.get(timeout=110)
     finally:
         p.join(30)
         if p.is_alive():
@@ -95,7 +95,7 @@ def _run(tmp, graph):
     return out, res
 
 
-@pytest.mark.timeout(700)   # two spawned trainer processes, each up to 300 s on a busy box
+@pytest.mark.timeout(300)   # two spawned trainer processes, each up to 110 s
 def test_distributed_train_one_epoch_graph_vs_eager(hip_device, tmp_path):
     tmp = str(tmp_path)
     out_g, res_g = _run(tmp, True)

@@ -13,5 +13,10 @@ case "$1" in
     "400 r6_bench python bench.py" ;;
   quick) bash tools/gpu_steps.sh \
     "600 r6_qtests python -u -m pytest -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_c5_fp16.py tests/test_bench_parity.py tests/test_hip_layers.py -k 'oracle or tie_band or ill_conditioned or consumer_dgrad'" ;;
-  *) echo "usage: $0 tests|full|bench|quick"; exit 2 ;;
+  fix) bash tools/gpu_steps.sh \
+    "700 r6_fixtests python -u -m pytest -q --durations=12 --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_c5_fp16.py tests/test_bench_ddp.py tests/test_trainer_gpu.py tests/test_ddp_gpu.py tests/test_hip_layers.py -k 'c5 or bench_two or distributed_train or rccl or world or upsampler or ill_conditioned'" ;;
+  study) bash tools/gpu_steps.sh \
+    "400 r6_pmc_layers bash tools/r6_pmc_layers.sh" \
+    "400 r6_split_ab env SSSEG_TUNE_LOG=1 python tools/split_ab.py" ;;
+  *) echo "usage: $0 tests|full|bench|quick|fix|study"; exit 2 ;;
 esac
