@@ -327,6 +327,12 @@ class DeviceAugment:
         x, mask = self.train(img, m)
         return dict(batch, image=x, semantic_mask=mask)
 
+    def unsupervised_batch(self, batch):
+        """A collated UnsupervisedImagesDataset batch (image uint8 [B, 3, H, W], host-only transforms) -> the same dict
+        with the device-augmented float image (train['unsupervised_augmentations'], unsupervised_dataset.py:20-21)."""
+        img = batch['image'].cuda(non_blocking=True).permute(0, 2, 3, 1).contiguous()
+        return dict(batch, image=self.unsupervised(img))
+
     def unsupervised(self, images):
         """train['unsupervised_augmentations']: RandomResizedCrop(ratio=(1, 1)) + HorizontalFlip + ToFloat."""
         self._check(images, 3)

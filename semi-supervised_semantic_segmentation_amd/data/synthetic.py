@@ -8,9 +8,12 @@ import torch.nn.functional as F
 
 
 class SyntheticSegDataset(torch.utils.data.Dataset):
-    def __init__(self, length=64, size=512, seed=0, with_masks=True, blob_sigma=16.0, fg_fraction=0.4):
+    def __init__(self, length=64, size=512, seed=0, with_masks=True, blob_sigma=16.0, fg_fraction=0.4, uint8=False):
         self.length, self.size, self.seed = length, size, seed
         self.with_masks, self.sigma, self.fg = with_masks, blob_sigma, fg_fraction
+        # uint8: the image as the reference's host loader leaves it before ToFloat (LongestMaxSize + PadIfNeeded
+        # output, data/dataset.py:70-72), for the device augmentation pipeline (data.device_augment)
+        self.uint8 = uint8
 
     def __len__(self):
         return self.length
@@ -28,6 +31,8 @@ class SyntheticSegDataset(torch.utils.data.Dataset):
     def __getitem__(self, i):
         g = torch.Generator().manual_seed(self.seed * 1_000_003 + i)
         out = {'image': torch.rand(3, self.size, self.size, generator=g)}
+        if self.uint8:
+            out['image'] = (out['image'] * 255).round().to(torch.uint8)
         if self.with_masks:
             fg = self._blobs(g)
             out['semantic_mask'] = torch.cat([1 - fg, fg], 0)

@@ -114,6 +114,10 @@ def distributed_train(rank, cfg_path):
                                            num_workers=workers), sampler
 
     tc = cfg['train']
+    if tc.get('device_augmentations') is not None:
+        # train['device_augmentations'] = partial(DeviceAugment, crop_size, ...): the datasets deliver the host-only
+        # transforms' uint8 output and train.train augments each batch on the device (a per-rank draw stream)
+        tc['device_augment'] = tc['device_augmentations'](seed=1000 + rank)
     train_ds = tc['dataset']()
     train_dl, train_sampler = loader(train_ds, tc['batch_size_per_worker'], tc['num_dataloader_workers'])
     unsup_dl, _ = loader(tc['unsupervised_dataset'](), tc['batch_size_per_worker'], tc['num_dataloader_workers'])

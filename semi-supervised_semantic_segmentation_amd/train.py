@@ -419,15 +419,23 @@ def train(model, ema_model, optimizer, dataloader, unsupervised_dataloader, epoc
     world = _world()
     optimizer.zero_grad()
     tc = config['train']
+    # the reference's per-sample albumentations pipelines (dataset.py:70-74, default_config.py:179-212) as batched device
+    # kernels: the loaders then deliver the host-only transforms' uint8 output (data.device_augment)
+    aug = tc.get('device_augment')
     for step, sample in enumerate(dataloader):
         tic = time.time()
         global_step = initial_step + step
+        if aug is not None:
+            sample = aug.train_batch(sample)
         image = sample['image'].to(device, non_blocking=True)
         mask = sample['semantic_mask'].to(device, non_blocking=True)
         ua = ub = None
         if tc['use_semi_supervised']:
-            ua = next(unsupervised_dataloader)['image'].to(device, non_blocking=True)
-            ub = next(unsupervised_dataloader)['image'].to(device, non_blocking=True)
+            us = [next(unsupervised_dataloader) for _ in range(2)]
+            if aug is not None:
+                us = [aug.unsupervised_batch(u) for u in us]
+            ua = us[0]['image'].to(device, non_blocking=True)
+            ub = us[1]['image'].to(device, non_blocking=True)
         cls, unsup, cm = run_step(model, ema_model, optimizer, image, mask, ua, ub, epoch, step, config)
         meters['cls'].update(cls)
         meters['sup'].update(cls)

@@ -244,3 +244,66 @@ def test_pipelines_end_to_end(hip_device):
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
     assert math.isfinite(float(x.sum()))
+
+
+@pytest.mark.gpu
+def test_train_loop_applies_device_augment(hip_device):
+    """train.train with train['device_augment'] (distributed_trainer builds it from train['device_augmentations']): the
+    loaders deliver the host-only transforms' uint8 output (SyntheticSegDataset(uint8=True) stands in for
+    SkinSegDataset with LongestMaxSize + PadIfNeeded, data/dataset.py:70-72), every labelled batch goes through
+    DeviceAugment.train_batch and every unlabelled one through .unsupervised_batch before the step (the reference
+    augments per sample on the host, dataset.py:73-74 / unsupervised_dataset.py:20-21): the step sees float NCHW
+    crops, the same tensors a direct call with the same seed produces, and trains to finite losses."""
+    import losses
+    import train
+    from data.synthetic import SyntheticSegDataset
+    from models import simple_unet
+    from models.adapters import ListOutput
+    from ssseg import arena, optim
+    DA = _aug()
+    n, H, S = 2, 96, 64
+    lab = SyntheticSegDataset(length=4, size=H, seed=1, uint8=True)
+    unl = SyntheticSegDataset(length=8, size=H, seed=3, with_masks=False, uint8=True)
+    dl = torch.utils.data.DataLoader(lab, batch_size=n)
+    udl = torch.utils.data.DataLoader(unl, batch_size=n)
+    torch.manual_seed(0)
+    student = ListOutput(simple_unet.UNet(2, 3, 8, 32)).to(hip_device)
+    teacher = ListOutput(simple_unet.UNet(2, 3, 8, 32)).to(hip_device)
+    for p in teacher.parameters():
+        p.detach_()
+    teacher.eval()
+    arena.attach(student)
+    arena.attach(teacher, with_grads=False)
+    opt = optim.SGD(student.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-4)
+    tc = dict(loss=losses.CalculateLoss([{'loss_fn': losses.DenseBinaryCrossEntropyLossWithLogits('mean'),
+                                          'weight': [0.5]}]),
+              virtual_batch_size_multiplier=1, use_semi_supervised=True, mask_proportion_range=(0.45, 0.55),
+              sigma_range=(2, 4), confidence_threshold=0.0, consistency_loss_weight=10, ema_model_alpha=0.99,
+              print_freq=10 ** 9, gradient_clip_value=5.0, device_augment=DA.DeviceAugment(S, seed=7))
+    seen = []
+    real = train.run_step
+
+    def spy(model, ema, o, image, mask, ua, ub, epoch, step, config):
+        seen.append((image.clone(), mask.clone(), ua.clone(), ub.clone()))
+        return real(model, ema, o, image, mask, ua, ub, epoch, step, config)
+
+    train.run_step = spy
+    try:
+        train.train(student, teacher, opt, dl, iter(udl), 30, 0, None, {'train': tc}, hip_device)
+    finally:
+        train.run_step = real
+    torch.cuda.synchronize()
+    assert len(seen) == 2
+    for image, mask, ua, ub in seen:
+        assert image.shape == (n, 3, S, S) and image.dtype == torch.float32 and mask.shape == (n, 2, S, S)
+        assert ua.shape == (n, 3, S, S) and ub.shape == (n, 3, S, S)
+        assert float(image.max()) <= 1.0 and float(image.min()) >= 0.0
+    # the same draws issued directly: labelled batch, then the two unlabelled batches, per step
+    ref = DA.DeviceAugment(S, seed=7)
+    uit = iter(udl)
+    for (image, mask, ua, ub), batch in zip(seen, dl):
+        b = ref.train_batch(batch)
+        u0, u1 = ref.unsupervised_batch(next(uit)), ref.unsupervised_batch(next(uit))
+        assert torch.equal(b['image'], image) and torch.equal(b['semantic_mask'], mask)
+        assert torch.equal(u0['image'], ua) and torch.equal(u1['image'], ub)
+    assert all(torch.isfinite(p).all() for p in student.parameters())

@@ -17,6 +17,7 @@ case "$1" in
     "700 r6_fixtests python -u -m pytest -q --durations=12 --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_c5_fp16.py tests/test_bench_ddp.py tests/test_trainer_gpu.py tests/test_ddp_gpu.py tests/test_hip_layers.py -k 'c5 or bench_two or distributed_train or rccl or world or upsampler or ill_conditioned'" ;;
   study) bash tools/gpu_steps.sh \
     "400 r6_pmc_layers bash tools/r6_pmc_layers.sh" \
-    "400 r6_split_ab env SSSEG_TUNE_LOG=1 python tools/split_ab.py" ;;
+    "400 r6_split_ab env SSSEG_TUNE_LOG=1 python tools/split_ab.py" \
+    "200 r6_gemm_ceiling python tools/gemm_ceiling.py" ;;
   *) echo "usage: $0 tests|full|bench|quick|fix|study"; exit 2 ;;
 esac
