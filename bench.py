@@ -284,6 +284,7 @@ def timed_run(args, world, rank, device, dtype, probe=True, eager_n1=False):
     # launches only where the collectives run on torch.distributed (gloo, SSSEG_COMM=c10d: DESIGN.md §6).  The N = 1
     # record also carries the eager rate ('eager_n1').
     from ssseg import comm as scomm
+    capture_error = [None]
     if args.graph and (world == 1 or scomm.kind() == 'native'):
         # the step captured once as a HIP graph (ssseg.graph.StepGraph) and replayed: each replay copies the next
         # batch into the captured input buffers and runs the whole step (fresh CowMix draws from the device counter)
@@ -291,13 +292,24 @@ def timed_run(args, world, rank, device, dtype, probe=True, eager_n1=False):
         # the replay repeats the captured step's host decisions: the optimizer step (step 2 % 1 == 0) and the epoch gate
         # (epoch 30 > 25) are the same for every timed step only with no gradient accumulation
         assert cfg['train']['virtual_batch_size_multiplier'] == 1, 'graph replay needs an optimizer step every step'
-        graph = StepGraph(lambda img, mask, ua, ub: train.train_step(model, teacher, opt, img, mask, ua, ub, 30, 2, cfg),
-                          *data[0])
+        try:
+            graph = StepGraph(lambda img, mask, ua, ub: train.train_step(model, teacher, opt, img, mask, ua, ub, 30, 2,
+                                                                         cfg), *data[0])
+        except RuntimeError as exc:
+            if world == 1:
+                raise
+            # N > 1: the native communicator's collectives inside a capture run here for the first time at this world
+            # size (the one-GPU test box covers world 1 only); report and time the eager step rather than nothing
+            graph = None
+            capture_error[0] = repr(exc)[:300]
+            print(f'[bench rank {rank}] step capture failed, timing eager steps: {exc}', file=sys.stderr, flush=True)
+            torch.cuda.synchronize()
 
-        def one_step():
-            out = graph(*data[step_idx[0] % len(data)])
-            step_idx[0] += 1
-            return tuple(t.clone() for t in out)
+        if graph is not None:
+            def one_step():
+                out = graph(*data[step_idx[0] % len(data)])
+                step_idx[0] += 1
+                return tuple(t.clone() for t in out)
 
     def timed_steps(step_fn, n):
         # the timed region: barrier + device sync on both sides, MAX of the elapsed time over ranks
@@ -335,7 +347,7 @@ def timed_run(args, world, rank, device, dtype, probe=True, eager_n1=False):
         eager = timed_steps(eager_step, args.steps)
     live = torch.stack([torch.stack([c.float(), u.float(), m.float()]) for c, u, m in recs]).cpu()
     snn.set_compute_dtype(torch.bfloat16)
-    return elapsed, rows, live, model, graph is not None, eager, tune_digests
+    return elapsed, rows, live, model, (graph is not None, capture_error[0]), eager, tune_digests
 
 
 def main():
@@ -396,8 +408,9 @@ def main():
                      'traffic_unit': 'HBM bytes per step, conv engine (rocprofv3 PMC, ' + os.path.relpath(PMC_PROFILE, ROOT) + ')',
                      'conv_ms_per_step': round(conv_ms, 3), 'conv_gflop_per_step': round(conv_flops / 1e9, 1),
                      'launches_per_step': len(rows), 'mfma_pmc': pmc_mfma()},
-        'execution': ('HIP graph replay of the captured step (ssseg.graph.StepGraph), one per step' if graphed
-                      else 'eager launches from Python (the host reducer issues the bucket all-reduces)'),
+        'execution': ('HIP graph replay of the captured step (ssseg.graph.StepGraph), one per step' if graphed[0]
+                      else 'eager launches from Python (the host reducer issues the bucket all-reduces)'
+                      + (f'; capture failed: {graphed[1]}' if graphed[1] else '')),
         'conv_variant_table': {'rows': len(tune.export()),
                                'digest_per_rank': tune_digests,
                                'note': 'rank 0 tunes, the other ranks import its table (ssseg.tune.sync)'},
