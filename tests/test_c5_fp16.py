@@ -165,18 +165,22 @@ def test_c5_fp16_vs_oracle(hip_device):
     unl = torch.rand(2 * steps, B, 3, H, H, generator=g)
     cfg = dict(sigma_range=(4, 8), confidence_threshold=0.0)
 
-    def oracle(dt):
+    def oracle(dt, pert=0.0):
         s, t, d = (copy.deepcopy(m).to(dt) for m in (s_ref, t_ref, d_ref))
         t.eval()
         opt = torch.optim.SGD(s.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-4)
         optd = torch.optim.SGD(d.parameters(), lr=0.01, momentum=0.9)
+        x = imgs.to(dt)
+        if pert:
+            x = x * (1 + pert * torch.randn(x.shape, generator=torch.Generator().manual_seed(99), dtype=dt))
         torch.manual_seed(3)
-        logs = train_ref.train_epoch(s, t, opt, list(zip(imgs.to(dt), masks.to(dt))), iter(unl.to(dt)), 30,
+        logs = train_ref.train_epoch(s, t, opt, list(zip(x, masks.to(dt))), iter(unl.to(dt)), 30,
                                      train_ref.default_cfg(**cfg), adv=dict(D=d, opt=optd, weight=0.01))
         return logs, s, d
 
     r64, s64, d64 = oracle(torch.float64)
     r16, s16, d16 = oracle(torch.float16)
+    _, sp, dp = oracle(torch.float64, pert=1e-6)
 
     snn.set_compute_dtype(torch.float16)
     try:
@@ -230,16 +234,18 @@ def test_c5_fp16_vs_oracle(hip_device):
                     bad.append((k, n, h, a, b))
         assert not bad, bad
         np_sd = lambda m: {k: v.detach().cpu().double().numpy() for k, v in m.state_dict().items()}  # noqa: E731
-        # the tests/parity.py rules of the C1 test (test_bench_geometry.py): a floor at 1e-3 of the network's parameter
-        # scale keeps mathematically near-zero tensors from being judged on rounding noise (HarDNet's deepest BN biases
-        # move by 1e-7..2e-5 in these two steps: fp32 itself misses them by 3-13 %, the torch-CPU fp16 run leaves them at
-        # 0), and the BN running means of the 4x4-map blocks (32 pixels per channel at bs 2: means of nearly cancelling
-        # conv outputs) amplify any rounding, there the fp16 oracle drifts by ~7 % -- factor 4 on that drift, as C1's
-        # tiny-batch blocks
+        # the tests/parity.py rules of the C1 test (test_bench_geometry.py): this network's gradients at random init are
+        # chaotic at 128^2 / bs 2 -- its deepest blocks normalise 2x2 and 4x4 maps (8-32 values per channel), and
+        # tools/diag_c5.py measures the step-0 student gradients of the reference's own fp32 arithmetic 8 % (median
+        # rel-RMS) away from fp64, any other summation order (the HIP fp32 path) 100+ % away, fp16 likewise -- so, as
+        # there: the drift of an fp64 run on inputs perturbed by 1e-6 (the ReLU / max switches of tiny-batch
+        # activations) joins the fp16 oracle's drift as yardstick, factor 4, and a floor at 1e-3 of the network's
+        # parameter scale keeps mathematically near-zero tensors (the deepest BN biases move by 1e-7..2e-5 in these two
+        # steps) from being judged on rounding noise
         sd64, dd64 = np_sd(s64), np_sd(d64)
         fl = lambda sd: 1e-3 * max(float(np.abs(v).max()) for k, v in sd.items() if 'running' not in k and v.ndim)  # noqa: E731
-        out_s = tensor_outliers(np_sd(student), np_sd(s16), sd64, floor=fl(sd64), factor=4.0)
-        out_d = tensor_outliers(np_sd(D), np_sd(d16), dd64, floor=fl(dd64), factor=4.0)
+        out_s = tensor_outliers(np_sd(student), np_sd(s16), sd64, np_sd(sp), floor=fl(sd64), factor=4.0)
+        out_d = tensor_outliers(np_sd(D), np_sd(d16), dd64, np_sd(dp), floor=fl(dd64), factor=4.0)
         print('student outliers', out_s[:5], 'discriminator outliers', out_d[:5])
         assert not out_s and not out_d, (out_s[:5], out_d[:5])
     finally:
