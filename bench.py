@@ -39,6 +39,7 @@ FWD_GFLOP_PER_IMAGE = 95.94     # UNet-R50 mw128 ConvT @512 (verifie
 # MI355X_MICROARCH.md gfx950 correction).  PMC cannot run inside the timed process, so the committed
 # measurement of the same workload is reported next to the live flop rate.
 THRESHOLD = 0.5                 # see the module docstring (liveness)
+PROBE_HOLD_CYCLES = int(3e8)    # spin of the instrumented step's head (~0.12 s at the shader clock; see timed_run)
 PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r5_pmc_traffic.json')
 # MFMA utilisation of the same workload from rocprofv3 PMC (tools/pmc_step.py --mfma: SQ_VALU_MFMA_BUSY_CYCLES over
 # 1024 SIMDs x GRBM_GUI_ACTIVE / 8), committed next to the traffic; like the traffic it cannot be collected inside
@@ -274,6 +275,11 @@ def timed_run(args, world, rank, device, dtype, probe=True, eager_n1=False):
         overlap = train._OVERLAP['teacher']
         train._OVERLAP['teacher'] = False
         rows = snn.probe(True)
+        # the device held by a spin kernel while the host enqueues the instrumented step: every conv launch then
+        # starts right behind its predecessor, so an event interval is the launch's device time, not host issue gaps
+        # (the eager step issues ~1,000 launches + ~800 events from Python)
+        torch.cuda.synchronize()
+        torch.cuda._sleep(PROBE_HOLD_CYCLES)
         one_step()
         snn.probe(False)
         torch.cuda.synchronize()

@@ -14,10 +14,14 @@ case "$1" in
   quick) bash tools/gpu_steps.sh \
     "600 r6_qtests python -u -m pytest -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_c5_fp16.py tests/test_bench_parity.py tests/test_hip_layers.py -k 'oracle or tie_band or ill_conditioned or consumer_dgrad'" ;;
   fix) bash tools/gpu_steps.sh \
-    "700 r6_fixtests python -u -m pytest -q --durations=12 --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_c5_fp16.py tests/test_bench_ddp.py tests/test_trainer_gpu.py tests/test_ddp_gpu.py tests/test_hip_layers.py -k 'c5 or bench_two or distributed_train or rccl or world or upsampler or ill_conditioned'" ;;
+    "700 r6_fixtests python -u -m pytest -q --durations=12 --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_c5_fp16.py tests/test_bench_ddp.py tests/test_trainer_gpu.py tests/test_ddp_gpu.py tests/test_hip_layers.py tests/test_augment.py -k 'c5 or bench_two or distributed_train or rccl or world or upsampler or ill_conditioned or train_loop'" ;;
   study) bash tools/gpu_steps.sh \
     "400 r6_pmc_layers bash tools/r6_pmc_layers.sh" \
     "400 r6_split_ab env SSSEG_TUNE_LOG=1 python tools/split_ab.py" \
     "200 r6_gemm_ceiling python tools/gemm_ceiling.py" ;;
-  *) echo "usage: $0 tests|full|bench|quick|fix|study"; exit 2 ;;
+  probe) bash tools/gpu_steps.sh \
+    "300 r6_c5 python -u -m pytest -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_c5_fp16.py" \
+    "400 r6_bench2 python bench.py --no-cpu-baseline --no-fp32" \
+    "300 r6_btrace env SSSEG_OVERLAP_TEACHER=0 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r6_btrace -o b -- python bench.py --steps 8 --warmup 3 --no-cpu-baseline --no-fp32 --no-graph" ;;
+  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe"; exit 2 ;;
 esac
