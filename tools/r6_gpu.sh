@@ -23,5 +23,8 @@ case "$1" in
     "300 r6_c5 python -u -m pytest -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_c5_fp16.py" \
     "400 r6_bench2 python bench.py --no-cpu-baseline --no-fp32" \
     "300 r6_btrace env SSSEG_OVERLAP_TEACHER=0 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r6_btrace -o b -- python bench.py --steps 8 --warmup 3 --no-cpu-baseline --no-fp32 --no-graph" ;;
-  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe"; exit 2 ;;
+  diag) bash tools/gpu_steps.sh \
+    "400 r6_diag_c5v python tools/diag_c5.py full noadv sup" \
+    "300 r6_gtrace rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r6_gtrace -o g -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp32" ;;
+  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag"; exit 2 ;;
 esac
