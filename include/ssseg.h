@@ -428,6 +428,17 @@ size_t ssseg_conv_wgrad_workspace_bytes(const ssseg_conv_desc* desc_host, int dt
 int ssseg_conv_wgrad(const void* x, const void* dy, float* dw, const ssseg_conv_desc* desc_host, int dt, int64_t c_real,
                      int64_t k_real, int layout, int accumulate, void* ws, size_t ws_bytes, ssseg_stream_t stream);
 
+/* Deferred split reductions: with ssseg_wgrad_defer_reduce(1) (per host thread) the weight-gradient entry points below
+ * launch their split kernels but only RECORD the slab reduction each would launch (the slab workspace must then stay
+ * valid until the flush); ssseg_wgrad_reduce_flush launches every recorded reduction on `stream`, up to 40 per launch
+ * (descriptors in the kernel arguments: capturable), with the same per-element summation as the immediate reduction
+ * (bitwise the same dW).  The training step's weight gradients, issued back to back after its two backward passes
+ * join (train.py:61 and :115 accumulate into .grad before clip + SGD), become one or two reduction launches instead of
+ * one per conv.  pending: the number recorded and not yet flushed. */
+int ssseg_wgrad_defer_reduce(int on);
+int64_t ssseg_wgrad_reduce_pending(void);
+int ssseg_wgrad_reduce_flush(ssseg_stream_t stream);
+
 /* The same weight gradient over TWO pixel sets in one launch: dw (+)= sum over (x, dy) of batch desc.N plus
  * (x2, dy2) of batch n2 (same geometry and strides otherwise).  The supervised and the consistency backward
  * of a student conv (train.py:61 and :115, accumulated into one .grad before clip + SGD) become one

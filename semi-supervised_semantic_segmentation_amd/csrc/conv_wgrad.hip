@@ -1,5 +1,8 @@
 // Weight gradients of the implicit-GEMM conv engine (split-K over pixels into fp32 slabs + deterministic
 // reduce, or direct when one split suffices).  Split from conv.hip for parallel compilation.
+#include <algorithm>
+#include <vector>
+
 #include "conv_kernels.h"
 
 // ------------------------------------------------------------------------------------------------
@@ -799,10 +802,89 @@ extern "C" size_t ssseg_conv_wgrad_workspace_bytes(const ssseg_conv_desc* d, int
   return wgrad_ws_bytes(g, dt);
 }
 
+// ---- deferred split reductions (ssseg_wgrad_defer_reduce / ssseg_wgrad_reduce_flush) --------------------------------
+// The weight gradients of a training step run back to back after the backward passes join (train.train_step's held
+// calls); each one's split slabs were reduced by a launch of its own (66 per C2 step, 12-15 us each).  With deferral
+// on, the reductions are recorded instead and one flush launches them together, up to RB_MAX per launch, the
+// descriptors passed by value in the kernel arguments (no table upload: capturable).  Per output element the sum is
+// the one wgrad_reduce_kernel / wgrad_reduce_wide_kernel computes (same chains, same order): bitwise the same dW.
+struct ReduceDesc {
+  const float* slab;
+  float* dst;
+  int splits, K, R, S, C, c_real, k_real;
+  short layout, accumulate;
+};
+constexpr int RB_MAX = 40;
+struct ReduceBatch {
+  ReduceDesc d[RB_MAX];
+  int n;
+};
+thread_local bool t_defer_reduce = false;
+thread_local std::vector<ReduceDesc> t_pending_reduce;
+
+__device__ __forceinline__ void reduce_store(const ReduceDesc& d, long long i, long long KK, float sum) {
+  const int kk = (int)(i % KK), k = (int)(i / KK);
+  const int c = kk % d.C, tap = kk / d.C, r = tap / d.S, s = tap % d.S;
+  if (c >= d.c_real || k >= d.k_real) return;
+  long long o;
+  if (d.layout == 0) o = ((long long)k * d.R * d.S + tap) * d.C + c;
+  else o = (((long long)k * d.c_real + c) * d.R + r) * d.S + s;
+  d.dst[o] = d.accumulate ? d.dst[o] + sum : sum;
+}
+
+// blockIdx.y = descriptor; 1024 threads.  splits >= 64: the wide kernel's form (64 outputs per block, wave w sums
+// splits w, w + 16, ... in two chains, then the 16 wave partials in order); else the plain kernel's (one output per
+// thread, four chains over the splits), grid-stride over the descriptor's outputs
+__global__ void __launch_bounds__(1024) wgrad_reduce_batch_kernel(ReduceBatch b) {
+  const ReduceDesc& d = b.d[blockIdx.y];
+  const long long KK = (long long)d.R * d.S * d.C, total = (long long)d.K * KK;
+  if (d.splits >= 64) {
+    __shared__ float red[16][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long long i = (long long)blockIdx.x * 64 + lane;
+    if ((long long)blockIdx.x * 64 >= total) return;   // (uniform)
+    float a0 = 0.f, a1 = 0.f;
+    if (i < total) {
+      int z = w;
+#pragma unroll 8
+      for (; z + 16 < d.splits; z += 32) {
+        a0 += d.slab[(long long)z * total + i];
+        a1 += d.slab[(long long)(z + 16) * total + i];
+      }
+      if (z < d.splits) a0 += d.slab[(long long)z * total + i];
+    }
+    red[w][lane] = a0 + a1;
+    __syncthreads();
+    if (w != 0 || i >= total) return;
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) sum += red[k][lane];
+    reduce_store(d, i, KK, sum);
+    return;
+  }
+  for (long long i = (long long)blockIdx.x * 1024 + threadIdx.x; i < total; i += (long long)gridDim.x * 1024) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int z = 0;
+    for (; z + 4 <= d.splits; z += 4) {
+      s0 += d.slab[(long long)z * total + i];
+      s1 += d.slab[(long long)(z + 1) * total + i];
+      s2 += d.slab[(long long)(z + 2) * total + i];
+      s3 += d.slab[(long long)(z + 3) * total + i];
+    }
+    for (; z < d.splits; ++z) s0 += d.slab[(long long)z * total + i];
+    reduce_store(d, i, KK, (s0 + s1) + (s2 + s3));
+  }
+}
+
 namespace {
 
 void launch_reduce(const float* slab, const ConvGeom& g, int splits, int64_t c_real, int64_t k_real, float* dw,
                    int layout, int accumulate, hipStream_t s) {
+  if (t_defer_reduce) {
+    t_pending_reduce.push_back(ReduceDesc{slab, dw, splits, g.K, g.R, g.S, g.C, (int)c_real, (int)k_real,
+                                          (short)layout, (short)accumulate});
+    return;
+  }
   const long long total = (long long)g.K * g.KK;
   if (splits >= 64)   // many splits: spread them over the 16 waves of a block
     hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)((total + 63) / 64)), dim3(1024), 0, s, slab, splits,
@@ -1045,4 +1127,33 @@ extern "C" int ssseg_conv_wgrad2_vcat(const void* x, const ssseg_vcat* vc, const
                                       int accumulate, void* ws, size_t ws_bytes, ssseg_stream_t stream) {
   if (!vc || !vc2) return SSSEG_EINVAL;
   return wgrad_two(x, vc, dy, x2, vc2, dy2, n2, dw, d, dt, c_real, k_real, layout, accumulate, ws, ws_bytes, stream);
+}
+
+extern "C" int ssseg_wgrad_defer_reduce(int on) {
+  t_defer_reduce = on != 0;
+  return 0;
+}
+
+extern "C" int64_t ssseg_wgrad_reduce_pending(void) { return (int64_t)t_pending_reduce.size(); }
+
+extern "C" int ssseg_wgrad_reduce_flush(ssseg_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  std::vector<ReduceDesc> pend;
+  pend.swap(t_pending_reduce);
+  for (size_t at = 0; at < pend.size(); at += RB_MAX) {
+    ReduceBatch b{};
+    b.n = (int)std::min<size_t>(RB_MAX, pend.size() - at);
+    long long blocks = 1;
+    for (int k = 0; k < b.n; ++k) {
+      b.d[k] = pend[at + k];
+      const long long total = (long long)b.d[k].K * b.d[k].R * b.d[k].S * b.d[k].C;
+      // wide descriptors: one block per 64 outputs; plain: the plain kernel's grid over 1024-thread blocks
+      const long long need = b.d[k].splits >= 64 ? (total + 63) / 64 : (long long)ssseg_grid(total, 1024);
+      blocks = std::max(blocks, need);
+    }
+    if (blocks > 0x7fffffffLL) return SSSEG_EINVAL;
+    hipLaunchKernelGGL(wgrad_reduce_batch_kernel, dim3((unsigned)blocks, (unsigned)b.n), dim3(1024), 0, s, b);
+    SSSEG_LAUNCH_CHECK();
+  }
+  return 0;
 }

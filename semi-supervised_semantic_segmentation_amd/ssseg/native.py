@@ -98,6 +98,9 @@ SIGS = {
     'ssseg_conv_wgrad_workspace_bytes': (sz, [vp, i32]),
     'ssseg_conv_wgrad': (i32, [vp, vp, vp, vp, i32, i64, i64, i32, i32, vp, sz, vp]),
     'ssseg_conv_wgrad2_workspace_bytes': (sz, [vp, i64, i32]),
+    'ssseg_wgrad_defer_reduce': (i32, [i32]),
+    'ssseg_wgrad_reduce_pending': (i64, []),
+    'ssseg_wgrad_reduce_flush': (i32, [vp]),
     'ssseg_conv_wgrad2': (i32, [vp, vp, vp, vp, i64, vp, vp, i32, i64, i64, i32, i32, vp, sz, vp]),
     # virtual concat inputs (ssseg_vcat)
     'ssseg_conv_igemm_epi_vcat': (i32, [vp, vp, vp, vp, vp, i32, i32, vp, vp, sz, vp]),

@@ -115,6 +115,42 @@ def flush_wgrad():
             mod._ssseg_wgrad(*pair, bias_grad=False, want=(True, False))
 
 
+# ---- deferred split reductions of the weight gradients (ssseg_wgrad_defer_reduce / _flush) ---------------------------
+_WRED = {'on': os.environ.get('SSSEG_WGRAD_BATCH_REDUCE', '1') != '0', 'live': False, 'keep': []}
+
+
+def _wgrad_ws(nb, device):
+    """The split-slab workspace of one weight-gradient launch; inside batched_wgrad_reduce() it is kept alive until the
+    deferred reductions that read it have been launched."""
+    ws = N.workspace(nb, device)
+    if _WRED['live']:
+        _WRED['keep'].append(ws)
+    return ws
+
+
+@contextlib.contextmanager
+def batched_wgrad_reduce():
+    """Inside: the weight-gradient launches record their split-slab reductions instead of launching them; on exit ONE
+    flush launches all of them (up to 40 per launch) on the current stream -- the same per-element sums, so the same dW
+    bit for bit.  Wraps the block of weight gradients train.train_step issues after its backward passes join (66
+    reduction launches per C2 step otherwise).  Nothing inside may read a .grad those launches write."""
+    if not _WRED['on'] or _WRED['live'] or _WSTREAM['on'] or not torch.cuda.is_available():
+        yield
+        return
+    _WRED['live'] = True
+    N.call('ssseg_wgrad_defer_reduce', 1)
+    try:
+        yield
+    finally:
+        N.call('ssseg_wgrad_defer_reduce', 0)
+        _WRED['live'] = False
+        try:
+            N.call('ssseg_wgrad_reduce_flush', N.stream())
+        finally:
+            keep, _WRED['keep'] = _WRED['keep'], []
+            del keep   # (stream-ordered frees: after the flush launch that reads them)
+
+
 # ---- held weight-gradient calls: two backward passes issued on two streams, their gradient writes replayed after ------
 _HOLD = {'on': False, 'tag': None, 'calls': [], 'params': False, 'adds': []}
 
@@ -182,14 +218,15 @@ def replay_held(order):
     for p, tmp in adds:   # grad += tmp (tmp = the one fp32 term the kernel would have added): bitwise the same sum
         g = _grad_of(p)
         N.call('ssseg_axpby', N.dev_ptr(g), 1.0, N.dev_ptr(tmp), 1.0, N.dev_ptr(g), g.numel(), N.stream())
-    with defer_wgrad():
+    with batched_wgrad_reduce():
+        with defer_wgrad():
+            for tag, mod, args, kw in calls:
+                if tag == order[0]:
+                    mod._ssseg_wgrad(*args, **kw)
         for tag, mod, args, kw in calls:
-            if tag == order[0]:
+            if tag == order[1]:
                 mod._ssseg_wgrad(*args, **kw)
-    for tag, mod, args, kw in calls:
-        if tag == order[1]:
-            mod._ssseg_wgrad(*args, **kw)
-    flush_wgrad()
+        flush_wgrad()
 
 
 # ---- deferred BN parameter gradients of the differentiated eval pass ---------------------------------------------------
@@ -1060,7 +1097,7 @@ class Conv2d(nn.Conv2d, _ConvBase):
         if pend is None:
             d = self._fwd_desc(n, H, W)
             nb = N.lib().ssseg_conv_wgrad_workspace_bytes(ctypes_ref(d), N.dt_code(x))
-            ws = N.workspace(nb, x.device)
+            ws = _wgrad_ws(nb, x.device)
             vc = _vcat_of(x)
             with _Timed(_conv_flops(n, d.OH, d.OW, self.out_channels, self.in_channels, R, S), 'wgrad',
                         _tag(self, n, H, W)):
@@ -1078,7 +1115,7 @@ class Conv2d(nn.Conv2d, _ConvBase):
             n1 = x1.shape[0]
             d = self._fwd_desc(n1, H, W)
             nb = N.lib().ssseg_conv_wgrad2_workspace_bytes(ctypes_ref(d), n, N.dt_code(x))
-            ws = N.workspace(nb, x.device)
+            ws = _wgrad_ws(nb, x.device)
             v1, v2 = _vcat_of(x1), _vcat_of(x)
             with _Timed(_conv_flops(n1 + n, d.OH, d.OW, self.out_channels, self.in_channels, R, S), 'wgrad',
                         _tag(self, n1 + n, H, W)):
@@ -1332,7 +1369,7 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
                   py=-ph, px=-pw, outH=H, outW=W, osy=1, osx=1, ooy=0, oox=0, ldy=cin, ldw=R * S * cout)
         if pend is None:
             nb = N.lib().ssseg_conv_wgrad_workspace_bytes(ctypes_ref(d), N.dt_code(x))
-            ws = N.workspace(nb, x.device)
+            ws = _wgrad_ws(nb, x.device)
             with _Timed(_conv_flops(n, H, W, self.out_channels, self.in_channels, R, S), 'wgrad',
                         _tag(self, n, H, W)):
                 N.call('ssseg_conv_wgrad', N.dev_ptr(gy), N.dev_ptr(x), N.dev_ptr(_grad_of(self.weight)),
@@ -1341,7 +1378,7 @@ class ConvTranspose2d(nn.ConvTranspose2d, _ConvBase):
         else:   # the deferred pass and this one: one launch over both pixel sets (operands in (gy, x) order)
             x1, gy1 = pend
             nb = N.lib().ssseg_conv_wgrad2_workspace_bytes(ctypes_ref(d), n, N.dt_code(x))
-            ws = N.workspace(nb, x.device)
+            ws = _wgrad_ws(nb, x.device)
             with _Timed(_conv_flops(n1 + n, H, W, self.out_channels, self.in_channels, R, S), 'wgrad',
                         _tag(self, n1 + n, H, W)):
                 N.call('ssseg_conv_wgrad2', N.dev_ptr(gy1), N.dev_ptr(x1), N.dev_ptr(gy), N.dev_ptr(x), n,

@@ -135,11 +135,17 @@ def test_c5_fp16_vs_oracle(hip_device):
     bit-exact to the reference network by golden G6b) + EMA teacher + Discriminator(5, 2, 64, 512, 1) with the
     adversarial branch, two semi-supervised steps at 128^2, bs 2 (step 0: no student optimizer step, train.py:121;
     step 1: clip + SGD; a discriminator SGD step each step).  The HIP run is in the fp16 compute mode (IEEE-half
-    activations and packed weights, fp32 accumulation and master weights, device loss scaling); the oracle runs the
-    same steps in fp64 (the yardstick) and in torch-CPU fp16 (the model, data and optimizer in half -- what fp16
-    rounding of the reference itself costs).  Every loss must lie within max(1e-3 relative, 2x the oracle-fp16 drift
-    from fp64), every parameter / BN buffer of the student and of D within max(1e-3 of its scale, 4x that drift) with
-    the parity floor (below): the HIP fp16 path is no worse than the reference computed in fp16."""
+    activations and packed weights, fp32 accumulation and master weights, device loss scaling); the oracle runs the same
+    steps in fp64 (the yardstick) and in torch-CPU fp16 (model, data and optimizer in half: what fp16 rounding of the
+    reference itself costs) -- the pattern of the UNet-R50 bf16 test (test_hip_models.py, bounded by torch's own
+    reduced-precision error against fp64):
+      * every loss of both steps within max(1e-3 relative, 2x the oracle-fp16 drift from fp64);
+      * the student's step-0 gradients (same weights on both sides), per tensor, rel-RMS error against fp64 within
+        1.5x the oracle-fp16 run's own + 2e-2.
+    Parameters after the optimizer step are not compared tensor by tensor: at 128^2 / bs 2 the deepest HarDNet blocks
+    normalise 2x2 and 4x4 maps, so the gradients there are chaotic (tools/diag_c5.py, profiles/r6_diag_c5.txt: the
+    reference's own fp32 is 8 % rel-RMS from fp64 at the median tensor, any other summation order and fp16 100+ %),
+    and clip_grad_norm_'s factor 5 / ||g|| hands that chaos to every update."""
     import cowmix
     import losses
     import train
@@ -147,7 +153,7 @@ def test_c5_fp16_vs_oracle(hip_device):
     from models.discriminator import Discriminator
     from models.hardnet import HarDNet
     from oracle import hardnet_ref, models_ref, train_ref
-    from parity import loss_bound, tensor_outliers
+    from parity import loss_bound
     from ssseg import amp, arena, optim
     from ssseg import nn as snn
     steps = 2
@@ -165,22 +171,23 @@ def test_c5_fp16_vs_oracle(hip_device):
     unl = torch.rand(2 * steps, B, 3, H, H, generator=g)
     cfg = dict(sigma_range=(4, 8), confidence_threshold=0.0)
 
-    def oracle(dt, pert=0.0):
+    def oracle(dt):
         s, t, d = (copy.deepcopy(m).to(dt) for m in (s_ref, t_ref, d_ref))
         t.eval()
         opt = torch.optim.SGD(s.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-4)
         optd = torch.optim.SGD(d.parameters(), lr=0.01, momentum=0.9)
-        x = imgs.to(dt)
-        if pert:
-            x = x * (1 + pert * torch.randn(x.shape, generator=torch.Generator().manual_seed(99), dtype=dt))
-        torch.manual_seed(3)
-        logs = train_ref.train_epoch(s, t, opt, list(zip(x, masks.to(dt))), iter(unl.to(dt)), 30,
-                                     train_ref.default_cfg(**cfg), adv=dict(D=d, opt=optd, weight=0.01))
-        return logs, s, d
+        g0 = {}
 
-    r64, s64, d64 = oracle(torch.float64)
-    r16, s16, d16 = oracle(torch.float16)
-    _, sp, dp = oracle(torch.float64, pert=1e-6)
+        def grab(step, rec):   # step 0 takes no optimizer step: .grad holds its gradients here
+            if step == 0:
+                g0.update({n: p.grad.detach().double().clone() for n, p in s.named_parameters()})
+        torch.manual_seed(3)
+        logs = train_ref.train_epoch(s, t, opt, list(zip(imgs.to(dt), masks.to(dt))), iter(unl.to(dt)), 30,
+                                     train_ref.default_cfg(**cfg), adv=dict(D=d, opt=optd, weight=0.01), on_step=grab)
+        return logs, g0
+
+    r64, g64 = oracle(torch.float64)
+    r16, g16 = oracle(torch.float16)
 
     snn.set_compute_dtype(torch.float16)
     try:
@@ -199,8 +206,9 @@ def test_c5_fp16_vs_oracle(hip_device):
         opt = optim.SGD(student.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-4)
         optd = optim.SGD(D.parameters(), lr=0.01, momentum=0.9)
         # a scale that cannot overflow here (the per-pixel loss gradients are ~1e-5): no step is skipped
-        opt.grad_scaler = amp.GradScaler(hip_device, init_scale=2.0 ** 12)
-        optd.grad_scaler = amp.GradScaler(hip_device, init_scale=2.0 ** 12)
+        S = 2.0 ** 12
+        opt.grad_scaler = amp.GradScaler(hip_device, init_scale=S)
+        optd.grad_scaler = amp.GradScaler(hip_device, init_scale=S)
         adv = dict(discriminator=D, optimizer=optd, weight=0.01)
         tcfg = dict(loss=losses.CalculateLoss([{'loss_fn': losses.DenseBinaryCrossEntropyLossWithLogits('mean'),
                                                 'weight': [0.5]}]),
@@ -209,7 +217,7 @@ def test_c5_fp16_vs_oracle(hip_device):
                     adversarial=adv, **cfg)
         old = cowmix.NOISE_SOURCE
         cowmix.NOISE_SOURCE = 'cpu'
-        logs = []
+        logs, ghip = [], None
         try:
             torch.manual_seed(3)
             student.train()
@@ -219,6 +227,9 @@ def test_c5_fp16_vs_oracle(hip_device):
                                            unl[2 * k].to(hip_device), unl[2 * k + 1].to(hip_device), 30, k,
                                            {'train': tcfg})
                 logs.append((float(c), float(adv['last_loss_adv']), float(adv['last_loss_d']), float(u)))
+                if k == 0:   # loss-scaled gradients of step 0 (the SGD step unscales them at step 1)
+                    torch.cuda.synchronize()
+                    ghip = {n: p.grad.detach().double().cpu() / S for n, p in student.named_parameters()}
         finally:
             cowmix.NOISE_SOURCE = old
         assert not opt.grad_scaler.found_inf() and not optd.grad_scaler.found_inf()
@@ -233,20 +244,17 @@ def test_c5_fp16_vs_oracle(hip_device):
                 if not abs(h - b) <= lim:
                     bad.append((k, n, h, a, b))
         assert not bad, bad
-        np_sd = lambda m: {k: v.detach().cpu().double().numpy() for k, v in m.state_dict().items()}  # noqa: E731
-        # the tests/parity.py rules of the C1 test (test_bench_geometry.py): this network's gradients at random init are
-        # chaotic at 128^2 / bs 2 -- its deepest blocks normalise 2x2 and 4x4 maps (8-32 values per channel), and
-        # tools/diag_c5.py measures the step-0 student gradients of the reference's own fp32 arithmetic 8 % (median
-        # rel-RMS) away from fp64, any other summation order (the HIP fp32 path) 100+ % away, fp16 likewise -- so, as
-        # there: the drift of an fp64 run on inputs perturbed by 1e-6 (the ReLU / max switches of tiny-batch
-        # activations) joins the fp16 oracle's drift as yardstick, factor 4, and a floor at 1e-3 of the network's
-        # parameter scale keeps mathematically near-zero tensors (the deepest BN biases move by 1e-7..2e-5 in these two
-        # steps) from being judged on rounding noise
-        sd64, dd64 = np_sd(s64), np_sd(d64)
-        fl = lambda sd: 1e-3 * max(float(np.abs(v).max()) for k, v in sd.items() if 'running' not in k and v.ndim)  # noqa: E731
-        out_s = tensor_outliers(np_sd(student), np_sd(s16), sd64, np_sd(sp), floor=fl(sd64), factor=4.0)
-        out_d = tensor_outliers(np_sd(D), np_sd(d16), dd64, np_sd(dp), floor=fl(dd64), factor=4.0)
-        print('student outliers', out_s[:5], 'discriminator outliers', out_d[:5])
-        assert not out_s and not out_d, (out_s[:5], out_d[:5])
+        gbad, e_h, e_o = [], [], []
+        for n, r in g64.items():
+            nrm = float(r.pow(2).mean().sqrt()) + 1e-30
+            eh = float((ghip[n] - r).pow(2).mean().sqrt()) / nrm
+            eo = float((g16[n] - r).pow(2).mean().sqrt()) / nrm
+            e_h.append(eh)
+            e_o.append(eo)
+            if not eh <= 1.5 * eo + 2e-2:
+                gbad.append((n, eh, eo))
+        print(f'step-0 gradient rel-RMS vs fp64, median over {len(e_h)} tensors: hip-fp16 {np.median(e_h):.3g}, '
+              f'oracle-fp16 {np.median(e_o):.3g}')
+        assert not gbad, gbad[:5]
     finally:
         snn.set_compute_dtype(torch.bfloat16)
