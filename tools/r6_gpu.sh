@@ -26,5 +26,11 @@ case "$1" in
   diag) bash tools/gpu_steps.sh \
     "400 r6_diag_c5v python tools/diag_c5.py full noadv sup" \
     "300 r6_gtrace rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r6_gtrace -o g -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp32" ;;
-  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag"; exit 2 ;;
+  wred) bash tools/gpu_steps.sh \
+    "600 r6_wred_tests python -u -m pytest -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_overlap.py tests/test_graph.py tests/test_determinism.py tests/test_c5_fp16.py tests/test_trainer_gpu.py" \
+    "200 r6_wred_b1 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_wred_b0 env SSSEG_WGRAD_BATCH_REDUCE=0 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_wred_b1b python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_wred_b0b env SSSEG_WGRAD_BATCH_REDUCE=0 python bench.py --no-cpu-baseline --no-fp32" ;;
+  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred"; exit 2 ;;
 esac
