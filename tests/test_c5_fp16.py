@@ -141,7 +141,8 @@ def test_c5_fp16_vs_oracle(hip_device):
     reduced-precision error against fp64):
       * every loss of both steps within max(1e-3 relative, 2x the oracle-fp16 drift from fp64);
       * the student's step-0 gradients (same weights on both sides), per tensor, rel-RMS error against fp64 within
-        1.5x the oracle-fp16 run's own + 2e-2.
+        1.5x the larger of the oracle-fp16 run's own and the drift of fp64 under a 1e-6 input perturbation (the
+        chaos yardstick of tests/parity.py), + 2e-2.
     Parameters after the optimizer step are not compared tensor by tensor: at 128^2 / bs 2 the deepest HarDNet blocks
     normalise 2x2 and 4x4 maps, so the gradients there are chaotic (tools/diag_c5.py, profiles/r6_diag_c5.txt: the
     reference's own fp32 is 8 % rel-RMS from fp64 at the median tensor, any other summation order and fp16 100+ %),
@@ -171,7 +172,7 @@ def test_c5_fp16_vs_oracle(hip_device):
     unl = torch.rand(2 * steps, B, 3, H, H, generator=g)
     cfg = dict(sigma_range=(4, 8), confidence_threshold=0.0)
 
-    def oracle(dt):
+    def oracle(dt, pert=0.0):
         s, t, d = (copy.deepcopy(m).to(dt) for m in (s_ref, t_ref, d_ref))
         t.eval()
         opt = torch.optim.SGD(s.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-4)
@@ -181,13 +182,17 @@ def test_c5_fp16_vs_oracle(hip_device):
         def grab(step, rec):   # step 0 takes no optimizer step: .grad holds its gradients here
             if step == 0:
                 g0.update({n: p.grad.detach().double().clone() for n, p in s.named_parameters()})
+        x = imgs.to(dt)
+        if pert:
+            x = x * (1 + pert * torch.randn(x.shape, generator=torch.Generator().manual_seed(99), dtype=dt))
         torch.manual_seed(3)
-        logs = train_ref.train_epoch(s, t, opt, list(zip(imgs.to(dt), masks.to(dt))), iter(unl.to(dt)), 30,
+        logs = train_ref.train_epoch(s, t, opt, list(zip(x, masks.to(dt))), iter(unl.to(dt)), 30,
                                      train_ref.default_cfg(**cfg), adv=dict(D=d, opt=optd, weight=0.01), on_step=grab)
         return logs, g0
 
     r64, g64 = oracle(torch.float64)
     r16, g16 = oracle(torch.float16)
+    _, gp = oracle(torch.float64, pert=1e-6)   # the chaos yardstick of tests/parity.py: fp64 on inputs moved by 1e-6
 
     snn.set_compute_dtype(torch.float16)
     try:
@@ -249,10 +254,11 @@ def test_c5_fp16_vs_oracle(hip_device):
             nrm = float(r.pow(2).mean().sqrt()) + 1e-30
             eh = float((ghip[n] - r).pow(2).mean().sqrt()) / nrm
             eo = float((g16[n] - r).pow(2).mean().sqrt()) / nrm
+            ep = float((gp[n] - r).pow(2).mean().sqrt()) / nrm
             e_h.append(eh)
             e_o.append(eo)
-            if not eh <= 1.5 * eo + 2e-2:
-                gbad.append((n, eh, eo))
+            if not eh <= 1.5 * max(eo, ep) + 2e-2:
+                gbad.append((n, eh, eo, ep))
         print(f'step-0 gradient rel-RMS vs fp64, median over {len(e_h)} tensors: hip-fp16 {np.median(e_h):.3g}, '
               f'oracle-fp16 {np.median(e_o):.3g}')
         assert not gbad, gbad[:5]

@@ -32,5 +32,11 @@ case "$1" in
     "200 r6_wred_b0 env SSSEG_WGRAD_BATCH_REDUCE=0 python bench.py --no-cpu-baseline --no-fp32" \
     "200 r6_wred_b1b python bench.py --no-cpu-baseline --no-fp32" \
     "200 r6_wred_b0b env SSSEG_WGRAD_BATCH_REDUCE=0 python bench.py --no-cpu-baseline --no-fp32" ;;
-  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred"; exit 2 ;;
+  stem) bash tools/gpu_steps.sh \
+    "300 r6_c5b python -u -m pytest -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_c5_fp16.py tests/test_overlap.py" \
+    "200 r6_stem1 python tools/bench_stem.py" \
+    "200 r6_stem0 env SSSEG_STEM=0 SSSEG_TUNE_LOG=1 python tools/bench_stem.py" \
+    "200 r6_stem_b1 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_stem_b0 env SSSEG_STEM=0 python bench.py --no-cpu-baseline --no-fp32" ;;
+  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem"; exit 2 ;;
 esac

@@ -12,11 +12,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('trace')
     ap.add_argument('--steps', type=int, default=7)
+    ap.add_argument('--skip-last', type=int, default=0, help='steps at the end to leave out (e.g. bench.py\'s eager_n1 '
+                    'steps after the graph-replayed ones)')
     a = ap.parse_args()
     rows = sorted((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name'])
                   for r in csv.DictReader(open(a.trace)))
     sgd = sorted(e for s, e, n in rows if 'sgd_kernel' in n)
-    t0, t1 = sgd[-(a.steps + 1)], sgd[-1]
+    end = len(sgd) - 1 - a.skip_last
+    t0, t1 = sgd[end - a.steps], sgd[end]
     sel = [(s, e) for s, e, _ in rows if s >= t0 and e <= t1]
     ev = sorted([(s, 1) for s, _ in sel] + [(e, -1) for _, e in sel])
     busy = multi = 0
