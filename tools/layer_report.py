@@ -62,6 +62,7 @@ def main():
     train._OVERLAP['teacher'] = False   # per-launch event timings of the serial schedule (no concurrent teacher)
     rows = snn.probe(True)
     img, mask, ua, ub = data[1]
+    torch.cuda._sleep(bench.PROBE_HOLD_CYCLES)   # bench.py's probe: the device held while the host enqueues the step
     train.train_step(model, teacher, opt, img, mask, ua, ub, 30, 3, cfg)
     snn.probe(False)
     torch.cuda.synchronize()
