@@ -457,6 +457,9 @@ def main():
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
+        import gc
+        gc.collect()               # the captured step (its RCCL persistent plans) goes before the communicator
+        torch.cuda.synchronize()
         scomm.reset()
         dist.destroy_process_group()
 
