@@ -38,5 +38,8 @@ case "$1" in
     "200 r6_stem0 env SSSEG_STEM=0 SSSEG_TUNE_LOG=1 python tools/bench_stem.py" \
     "200 r6_stem_b1 python bench.py --no-cpu-baseline --no-fp32" \
     "200 r6_stem_b0 env SSSEG_STEM=0 python bench.py --no-cpu-baseline --no-fp32" ;;
-  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem"; exit 2 ;;
+  pmc) bash tools/gpu_steps.sh \
+    "300 r6_layers python tools/layer_report.py" \
+    "700 r6_pmc bash tools/pmc_run.sh" ;;
+  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc"; exit 2 ;;
 esac
