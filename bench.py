@@ -432,8 +432,8 @@ def main():
     if eager is not None:
         result['eager_n1'] = {'value': round(world * args.batch * args.steps / eager, 3), 'unit': 'images/sec',
                               'ms_per_step': round(eager / args.steps * 1e3, 3), 'steps': args.steps,
-                              'note': 'the same N=1 workload, every launch issued from Python (the execution mode '
-                                      'of the N>1 lines)'}
+                              'note': 'the same N=1 workload, every launch issued from Python instead of the '
+                                      'captured-step replay'}
     if rank == 0 and world == 1 and not args.no_fp32:
         try:
             f_el, _, f_live, _, _, _, _ = timed_run(argparse.Namespace(**dict(vars(args), steps=min(args.steps, 5), warmup=2)),
