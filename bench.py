@@ -40,11 +40,11 @@ FWD_GFLOP_PER_IMAGE = 95.94     # UNet-R50 mw128 ConvT @512 (verifie
 # measurement of the same workload is reported next to the live flop rate.
 THRESHOLD = 0.5                 # see the module docstring (liveness)
 PROBE_HOLD_CYCLES = int(3e8)    # spin of the instrumented step's head (~0.12 s at the shader clock; see timed_run)
-PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r5_pmc_traffic.json')
+PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r6_pmc_traffic.json')
 # MFMA utilisation of the same workload from rocprofv3 PMC (tools/pmc_step.py --mfma: SQ_VALU_MFMA_BUSY_CYCLES over
 # 1024 SIMDs x GRBM_GUI_ACTIVE / 8), committed next to the traffic; like the traffic it cannot be collected inside
 # the timed process
-PMC_MFMA = os.path.join(ROOT, 'profiles', 'r5_pmc_mfma.json')
+PMC_MFMA = os.path.join(ROOT, 'profiles', 'r6_pmc_mfma.json')
 
 
 def pmc_traffic():
