@@ -41,5 +41,8 @@ case "$1" in
   pmc) bash tools/gpu_steps.sh \
     "300 r6_layers python tools/layer_report.py" \
     "700 r6_pmc bash tools/pmc_run.sh" ;;
-  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc"; exit 2 ;;
+  full3) bash tools/gpu_steps.sh \
+    "500 r6_full_c3 python tools/full_size_steps.py --configs c3 --graph --train-loop --collectives" \
+    "300 r6_full_c5plain python tools/full_size_steps.py --configs c5 --graph --train-loop" ;;
+  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3"; exit 2 ;;
 esac
