@@ -201,3 +201,34 @@ def test_tune_table_sync_gloo_world2():
     assert d0 == d1 and len(set(d0)) == 1  # ... and agree after it
     assert t1[11] == 3 and t1[12] == 14 and t1[13] == 26 and t1[99] == 6 and t0 == t1
     assert s0 and s1
+
+
+def _comm_worker(rank, world, port, q):
+    """ssseg.comm on a gloo group: no native communicator (RCCL needs the nccl backend and GPU tensors), the SyncBN sum
+    helper falls through to torch.distributed and sums across ranks; kind() reports the transport bench.py prints."""
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from ssseg import comm
+        t = torch.full((4,), float(rank + 1), dtype=torch.float64)
+        comm.all_reduce_sum(t)
+        q.put((rank, comm.wanted(), comm.get(), comm.kind(), t.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_comm_falls_back_to_c10d_on_gloo():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_comm_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=120) for _ in ps))
+    for p in ps:
+        p.join(30)
+    for r in range(2):
+        wanted, c, kind, vals = res[r]
+        assert wanted is False and c is None and kind == 'c10d'
+        assert vals == [3.0] * 4
