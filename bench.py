@@ -277,7 +277,9 @@ def timed_run(args, world, rank, device, dtype, probe=True, eager_n1=False):
         rows = snn.probe(True)
         # the device held by a spin kernel while the host enqueues the instrumented step: every conv launch then
         # starts right behind its predecessor, so an event interval is the launch's device time, not host issue gaps
-        # (the eager step issues ~1,000 launches + ~800 events from Python)
+        # (the eager step issues ~1,000 launches + ~800 events from Python).  The events are fence-free
+        # (snn.ProbeEvent, csrc/probe.hip): a default event's system-scope release writes back and invalidates the L2
+        # after every record, which starts each bracketed conv colder than in the captured step.
         torch.cuda.synchronize()
         torch.cuda._sleep(PROBE_HOLD_CYCLES)
         one_step()

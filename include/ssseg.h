@@ -781,6 +781,17 @@ const char* ssseg_comm_last_error(void);
 int ssseg_allreduce_buckets(ssseg_comm_t comm, void* const* ptrs_host, const int64_t* counts_host, int64_t n, int dt,
                             int op, ssseg_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Timing events for the live kernel probe (bench.py's roofline leg; csrc/probe.hip).  Created with
+ * hipEventDisableSystemFence: recording one writes a timestamp without the system-scope cache writeback and
+ * invalidation a default event performs, so a kernel bracketed by probe events runs with the caches its
+ * predecessor left, as in the captured step.  ssseg_probe_event_elapsed waits for ev1 and returns ev1 - ev0 in ms.
+ * ------------------------------------------------------------------------------------------- */
+int ssseg_probe_event_create(void** ev_out);
+int ssseg_probe_event_record(void* ev, ssseg_stream_t stream);
+int ssseg_probe_event_elapsed(void* ev0, void* ev1, float* ms_out);
+int ssseg_probe_event_destroy(void* ev);
+
 #ifdef __cplusplus
 }
 #endif

@@ -165,6 +165,11 @@ SIGS = {
     'ssseg_comm_async_error': (i32, [vp]),
     'ssseg_comm_last_error': (ctypes.c_char_p, []),
     'ssseg_allreduce_buckets': (i32, [vp, ctypes.POINTER(ctypes.c_void_p), I64P, i64, i32, i32, vp]),
+    # probe timing events (csrc/probe.hip)
+    'ssseg_probe_event_create': (i32, [ctypes.POINTER(ctypes.c_void_p)]),
+    'ssseg_probe_event_record': (i32, [vp, vp]),
+    'ssseg_probe_event_elapsed': (i32, [vp, vp, ctypes.POINTER(ctypes.c_float)]),
+    'ssseg_probe_event_destroy': (i32, [vp]),
 }
 
 

@@ -424,7 +424,37 @@ def _need_act(x, c_phys, what):
 # ------------------------------------------------------------------------------------------------
 # live kernel instrumentation (bench.py roofline): HIP events around every conv-engine launch
 # ------------------------------------------------------------------------------------------------
-_PROBE = {'on': False, 'rows': []}
+_PROBE = {'on': False, 'rows': [], 'fenced': os.environ.get('SSSEG_PROBE_FENCED', '0') == '1'}
+
+
+class ProbeEvent:
+    """A HIP timing event without the system-scope fence (ssseg_probe_event_*, csrc/probe.hip): recording it leaves
+    the caches as the previous kernel left them, so the bracketed conv runs as warm as in the captured step.  Same
+    record() / elapsed_time() surface as torch.cuda.Event; recorded on torch's current stream."""
+    __slots__ = ('ev',)
+
+    def __init__(self):
+        h = ctypes.c_void_p()
+        N.call('ssseg_probe_event_create', ctypes.byref(h))
+        self.ev = h.value
+
+    def record(self):
+        N.call('ssseg_probe_event_record', self.ev, N.stream())
+
+    def elapsed_time(self, end):
+        ms = ctypes.c_float()
+        N.call('ssseg_probe_event_elapsed', self.ev, end.ev, ctypes.byref(ms))
+        return ms.value
+
+    def __del__(self):
+        if self.ev and N._lib is not None:
+            N._lib.ssseg_probe_event_destroy(self.ev)
+            self.ev = None
+
+
+def _probe_event():
+    # SSSEG_PROBE_FENCED=1: torch's default events (system-scope release after every record: cold L2 per conv)
+    return torch.cuda.Event(enable_timing=True) if _PROBE['fenced'] else ProbeEvent()
 
 
 def probe(enable):
@@ -441,13 +471,13 @@ class _Timed:
 
     def __enter__(self):
         if _PROBE['on']:
-            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e0 = _probe_event()
             self.e0.record()
         return self
 
     def __exit__(self, *a):
         if _PROBE['on']:
-            e1 = torch.cuda.Event(enable_timing=True)
+            e1 = _probe_event()
             e1.record()
             _PROBE['rows'].append((self.e0, e1, self.flops, self.kind, self.tag))
 

@@ -44,5 +44,10 @@ case "$1" in
   full3) bash tools/gpu_steps.sh \
     "500 r6_full_c3 python tools/full_size_steps.py --configs c3 --graph --train-loop --collectives" \
     "300 r6_full_c5plain python tools/full_size_steps.py --configs c5 --graph --train-loop" ;;
-  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3"; exit 2 ;;
+  events) bash tools/gpu_steps.sh \
+    "200 r6_ev_tests python -u -m pytest -q --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_probe_events.py" \
+    "300 r6_ev_free python bench.py --no-cpu-baseline --no-fp32" \
+    "300 r6_ev_fenced env SSSEG_PROBE_FENCED=1 python bench.py --no-cpu-baseline --no-fp32" \
+    "300 r6_ev_trace rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r6_ev_trace -o b -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-fp32" ;;
+  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3|events"; exit 2 ;;
 esac
