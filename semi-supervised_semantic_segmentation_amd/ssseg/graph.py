@@ -20,6 +20,8 @@ host.
                      img, mask, ua, ub)
     cls, unsup, cm = step(img2, mask2, ua2, ub2)    # copies the inputs into the captured buffers, replays
 """
+import os
+
 import torch
 
 
@@ -39,12 +41,17 @@ class StepGraph:
             fn(*self.static_in)
         torch.cuda.synchronize()
         from . import nn as snn
-        self.graph = torch.cuda.CUDAGraph()
+        # SSSEG_GRAPH_KEEP=1 keeps the captured hipGraph_t next to its executable instance (raw_cuda_graph(), read by
+        # tools/graph_dag.py)
+        keep = os.environ.get('SSSEG_GRAPH_KEEP', '0') == '1'
+        self.graph = torch.cuda.CUDAGraph(keep_graph=keep)
         # the descriptor tables the captured launches read by pointer stay alive as long as the graph
         with snn.graph_refs() as refs:
             with torch.cuda.graph(self.graph, capture_error_mode=_capture_mode()):
                 self.static_out = fn(*self.static_in)
         self.refs = list(refs)
+        if keep:
+            self.graph.instantiate()
 
     def __call__(self, *inputs):
         for dst, src in zip(self.static_in, inputs):

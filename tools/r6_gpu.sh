@@ -49,5 +49,46 @@ case "$1" in
     "300 r6_ev_free python bench.py --no-cpu-baseline --no-fp32" \
     "300 r6_ev_fenced env SSSEG_PROBE_FENCED=1 python bench.py --no-cpu-baseline --no-fp32" \
     "300 r6_ev_trace rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r6_ev_trace -o b -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-fp32" ;;
-  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3|events"; exit 2 ;;
+  order) bash tools/gpu_steps.sh \
+    "200 r6_ord_b1 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_ord_b0 env SSSEG_SUP_BWD_FIRST=0 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_ord_b1b python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_ord_b0b env SSSEG_SUP_BWD_FIRST=0 python bench.py --no-cpu-baseline --no-fp32" \
+    "300 r6_ord_trace rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r6_ord_trace -o b -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp32" \
+    "700 r6_ord_tests python -u -m pytest -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_overlap.py tests/test_graph.py tests/test_determinism.py tests/test_c5_fp16.py tests/test_trainer_gpu.py tests/test_ddp_gpu.py" ;;
+  gq) bash tools/gpu_steps.sh \
+    "200 r6_gq_pc0 env DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_gq_pc0o env DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 SSSEG_SUP_BWD_FIRST=0 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_gq_q1 env DEBUG_HIP_FORCE_GRAPH_QUEUES=1 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_gq_q8 env DEBUG_HIP_FORCE_GRAPH_QUEUES=8 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_gq_bs env DEBUG_HIP_GRAPH_BATCH_SIZE=1024 python bench.py --no-cpu-baseline --no-fp32" \
+    "300 r6_gq_trace env DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r6_gq_trace -o b -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp32" ;;
+  gb) bash tools/gpu_steps.sh \
+    "200 r6_gb_1 env DEBUG_HIP_GRAPH_BATCH_SIZE=1 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_gb_8 env DEBUG_HIP_GRAPH_BATCH_SIZE=8 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_gb_32 env DEBUG_HIP_GRAPH_BATCH_SIZE=32 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_gb_128 env DEBUG_HIP_GRAPH_BATCH_SIZE=128 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_gb_def python bench.py --no-cpu-baseline --no-fp32" \
+    "300 r6_gb_trace env DEBUG_HIP_GRAPH_BATCH_SIZE=8 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r6_gb_trace -o b -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp32" ;;
+  io) bash tools/gpu_steps.sh \
+    "200 r6_io_2 env SSSEG_ISSUE_ORDER=2 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_io_0 env SSSEG_ISSUE_ORDER=0 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_io_1 env SSSEG_ISSUE_ORDER=1 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_io_mb env DEBUG_CLR_MAX_BATCH_SIZE=4096 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_io_cs env DEBUG_CLR_BATCH_CPU_SYNC_SIZE=4096 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_io_cb env GPU_MAX_COMMAND_BUFFERS=4096 python bench.py --no-cpu-baseline --no-fp32" \
+    "300 r6_io_trace env SSSEG_ISSUE_ORDER=2 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r6_io_trace -o b -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp32" ;;
+  fe) bash tools/gpu_steps.sh \
+    "200 r6_fe_1 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_fe_0 env SSSEG_FORK_EVENT=0 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_fe_1o0 env SSSEG_ISSUE_ORDER=0 python bench.py --no-cpu-baseline --no-fp32" \
+    "300 r6_fe_trace rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r6_fe_trace -o b -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp32" ;;
+  seg) bash tools/gpu_steps.sh \
+    "300 r6_seg_tests python -u -m pytest -q -x --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_graph.py tests/test_overlap.py" \
+    "200 r6_seg_1 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_seg_0 env SSSEG_GRAPH_SEGMENTS=0 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_seg_1b python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_seg_0b env SSSEG_GRAPH_SEGMENTS=0 python bench.py --no-cpu-baseline --no-fp32" \
+    "300 r6_seg_trace rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r6_seg_trace -o b -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp32" ;;
+  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3|events|order|gq|gb|io|fe|seg"; exit 2 ;;
 esac
