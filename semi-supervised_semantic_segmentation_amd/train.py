@@ -118,7 +118,8 @@ def _scaled(loss, optimizer):
 _OVERLAP = {'teacher': os.environ.get('SSSEG_OVERLAP_TEACHER', '1') != '0', 'streams': {}, 'steps': 0,
             'serial_steps': 2, 'seen': {},
             'consistency': os.environ.get('SSSEG_OVERLAP_CONSISTENCY', '1') != '0',
-            'consistency_bwd': os.environ.get('SSSEG_OVERLAP_CONSISTENCY_BWD', '1') != '0'}
+            'consistency_bwd': os.environ.get('SSSEG_OVERLAP_CONSISTENCY_BWD', '1') != '0',
+            'merge_wgrad': os.environ.get('SSSEG_MERGE_WGRAD', '1') != '0'}
 
 
 def _step_key(model, ema_model, image, unsup_a):
@@ -237,7 +238,11 @@ def train_step(model, ema_model, optimizer, image, mask, unsup_a, unsup_b, epoch
             ddp.arm()
         # with a consistency backward to follow, each conv's supervised weight gradient is merged into that pass's
         # (one launch over both batches' pixels; ssseg.nn.defer_wgrad) -- the .grad sum is the same
-        with (snn.hold_wgrad('sup') if side_bwd else snn.defer_wgrad() if semi else contextlib.nullcontext()):
+        # (merge_wgrad off: the supervised weight gradients are launched in its backward -- written into .grad while
+        # the side stream still runs the teacher and consistency passes -- and the consistency pass's add to them)
+        merge = _OVERLAP['merge_wgrad']
+        with (snn.hold_wgrad('sup') if side_bwd and merge else snn.defer_wgrad() if semi and merge
+              else contextlib.nullcontext()):
             vbm = tc['virtual_batch_size_multiplier']
             ops.backward(_scaled(ops.scale(sup_loss, 1.0 / vbm) if vbm != 1 else sup_loss, optimizer))
         del pred_maps, features

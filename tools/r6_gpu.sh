@@ -90,5 +90,11 @@ case "$1" in
     "200 r6_seg_1b python bench.py --no-cpu-baseline --no-fp32" \
     "200 r6_seg_0b env SSSEG_GRAPH_SEGMENTS=0 python bench.py --no-cpu-baseline --no-fp32" \
     "300 r6_seg_trace rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r6_seg_trace -o b -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp32" ;;
-  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3|events|order|gq|gb|io|fe|seg"; exit 2 ;;
+  mw) bash tools/gpu_steps.sh \
+    "200 r6_mw_0 env SSSEG_MERGE_WGRAD=0 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_mw_1 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_mw_0b env SSSEG_MERGE_WGRAD=0 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_mw_1b python bench.py --no-cpu-baseline --no-fp32" \
+    "600 r6_mw_tests env SSSEG_MERGE_WGRAD=0 python -u -m pytest -q -x --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_graph.py tests/test_overlap.py tests/test_determinism.py" ;;
+  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3|events|order|gq|gb|io|fe|seg|mw"; exit 2 ;;
 esac
