@@ -20,11 +20,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('trace')
     ap.add_argument('--steps', type=int, default=7)
+    ap.add_argument('--skip-last', type=int, default=0, help="steps at the end to leave out (bench.py's eager_n1 steps)")
     a = ap.parse_args()
     rows = [(r['Kernel_Name'], int(r['Start_Timestamp']), int(r['End_Timestamp'])) for r in csv.DictReader(open(a.trace))]
-    sgd = [s for n, s, e in rows if 'sgd_kernel' in n]
-    t0 = sgd[-(a.steps + 1)]
-    sel = [(n, s, e) for n, s, e in rows if s > t0]
+    sgd = sorted(s for n, s, e in rows if 'sgd_kernel' in n)
+    end = len(sgd) - 1 - a.skip_last
+    t0, t1 = sgd[end - a.steps], sgd[end]
+    sel = [(n, s, e) for n, s, e in rows if t0 < s <= t1]
     agg = collections.defaultdict(lambda: [0, 0.0])
     for n, s, e in sel:
         agg[base(n)][0] += 1
