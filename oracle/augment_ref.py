@@ -109,8 +109,10 @@ def color(img, p):
     if p.get('bc'):
         al, be = p['alpha'], p['beta']
         r, g, b = (np.floor(np.clip(t * al + be * 255, 0, 255)) for t in (r, g, b))
-    if p.get('gray'):
-        y = np.rint(np.clip(0.299 * r + 0.587 * g + 0.114 * b, 0, 255))
+    if p.get('gray'):   # albumentations to_gray = cv2 RGB2GRAY -> GRAY2RGB; OpenCV's 8-bit RGB2GRAY is the Q14 fixed
+        # point CV_DESCALE(R*4899 + G*9617 + B*1868, 14) (coefficients 0.299 / 0.587 / 0.114 scaled by 2^14)
+        ri, gi, bi = (t.astype(np.int64) for t in (r, g, b))
+        y = ((ri * 4899 + gi * 9617 + bi * 1868 + 8192) >> 14).astype(np.float64)
         r = g = b = y
     if p.get('rgb'):
         r, g, b = (np.floor(np.clip(t + s, 0, 255)) for t, s in zip((r, g, b), p['shift']))

@@ -169,9 +169,10 @@ __global__ void aug_color_kernel(float* __restrict__ img, int64_t HW, const ssse
       g = floorf(clamp255(g * p.alpha + p.beta * 255.f));
       b = floorf(clamp255(b * p.alpha + p.beta * 255.f));
     }
-    if (p.gray) {   // ToGray: RGB2GRAY (0.299, 0.587, 0.114), replicated to 3 channels
-      const float y = round_u8(0.299f * r + 0.587f * g + 0.114f * b);
-      r = g = b = y;
+    if (p.gray) {   // ToGray: cv2 COLOR_RGB2GRAY on uint8 -- Q14 fixed point (0.299, 0.587, 0.114) = (4899, 9617,
+                    // 1868) / 2^14, rounded (+2^13) -- replicated to 3 channels (GRAY2RGB); r, g, b are integers here
+      const int y = ((int)r * 4899 + (int)g * 9617 + (int)b * 1868 + 8192) >> 14;
+      r = g = b = (float)y;
     }
     if (p.rgb) {   // RGBShift (uint8 LUT): clip(v + shift).astype(uint8)
       r = floorf(clamp255(r + p.shift[0]));

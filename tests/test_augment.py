@@ -137,7 +137,7 @@ def test_color_matches_oracle(hip_device):
     specs = [dict(bc=1, alpha=1.13, beta=-0.07), dict(bc=1, alpha=0.85, beta=0.12, gray=1),
              dict(bc=1, alpha=1.0, beta=0.0, rgb=1, shift=[7.3, -9.1, 2.2]),
              dict(bc=1, alpha=0.93, beta=0.05, hsv=1, hsv_shift=[8.6, -7.2, 0.6]),
-             dict(hsv=1, hsv_shift=[-9.5, 9.9, -0.8]), dict()]
+             dict(hsv=1, hsv_shift=[-9.5, 9.9, -0.8]), dict(gray=1)]
     for i, sp in enumerate(specs):
         for k, v in sp.items():
             if isinstance(v, list):
@@ -151,8 +151,26 @@ def test_color_matches_oracle(hip_device):
     for i, sp in enumerate(specs):
         ref = R.color(img[i], sp)
         d = np.abs(got[i] - ref)
+        if set(sp) == {'gray'}:   # integer arithmetic (cv2's Q14 RGB2GRAY): bit-exact
+            assert d.max() == 0, (i, d.max())
         assert d.max() <= 1.0, (i, d.max())
         assert (d == 0).mean() > 0.98, (i, (d == 0).mean())
+
+
+def test_to_gray_known_answers():
+    """The oracle's ToGray is OpenCV's 8-bit RGB2GRAY (albumentations to_gray): known answers of that conversion --
+    pure red / green / blue -> 76 / 150 / 29, white -> 255 -- and its Q14 rounding (0.299 / 0.587 / 0.114 * 2^14 =
+    4899 / 9617 / 1868, + 2^13, >> 14) where the float formula rounds the other way."""
+    img = np.array([[[255, 0, 0], [0, 255, 0], [0, 0, 255], [255, 255, 255], [0, 0, 0], [1, 0, 1]]], np.float64)
+    y = R.color(img, dict(gray=1))[..., 0]
+    assert y.tolist() == [[76, 150, 29, 255, 0, 0]]
+    r, g, b = np.meshgrid(np.arange(0, 256, 3), np.arange(0, 256, 5), np.arange(0, 256, 7), indexing='ij')
+    rgb = np.stack([r, g, b], -1).reshape(1, -1, 3).astype(np.float64)
+    y = R.color(rgb, dict(gray=1))[0, :, 0]
+    q14 = (r.ravel() * 4899 + g.ravel() * 9617 + b.ravel() * 1868 + 8192) >> 14
+    assert (y == q14).all()
+    flt = np.rint(0.299 * r + 0.587 * g + 0.114 * b).ravel()
+    assert (flt != q14).any()   # the float formula is NOT the cv2 result everywhere
 
 
 @pytest.mark.gpu
