@@ -96,5 +96,8 @@ case "$1" in
     "200 r6_mw_0b env SSSEG_MERGE_WGRAD=0 python bench.py --no-cpu-baseline --no-fp32" \
     "200 r6_mw_1b python bench.py --no-cpu-baseline --no-fp32" \
     "600 r6_mw_tests env SSSEG_MERGE_WGRAD=0 python -u -m pytest -q -x --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_graph.py tests/test_overlap.py tests/test_determinism.py" ;;
-  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3|events|order|gq|gb|io|fe|seg|mw"; exit 2 ;;
+  wred4) bash tools/gpu_steps.sh \
+    "400 r6_wred4_1 env SSSEG_WGRAD_BATCH_REDUCE=1 python tools/full_size_steps.py --configs c4,c5 --graph" \
+    "400 r6_wred4_0 python tools/full_size_steps.py --configs c4,c5 --graph" ;;
+  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3|events|order|gq|gb|io|fe|seg|mw|wred4"; exit 2 ;;
 esac
