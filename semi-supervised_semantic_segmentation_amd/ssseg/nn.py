@@ -154,7 +154,9 @@ def batched_wgrad_reduce():
 
 
 # ---- held weight-gradient calls: two backward passes issued on two streams, their gradient writes replayed after ------
-_HOLD = {'on': False, 'tag': None, 'calls': [], 'params': False, 'adds': []}
+_HOLD = {'on': False, 'tag': None, 'calls': [], 'params': False, 'adds': [], 'streams': {},
+         # streams the replayed (merged) weight-gradient launches are spread over (SSSEG_WGRAD_BURST; 1 = this stream)
+         'burst': max(1, int(os.environ.get('SSSEG_WGRAD_BURST', '1')))}
 
 
 @contextlib.contextmanager
@@ -220,15 +222,40 @@ def replay_held(order):
     for p, tmp in adds:   # grad += tmp (tmp = the one fp32 term the kernel would have added): bitwise the same sum
         g = _grad_of(p)
         N.call('ssseg_axpby', N.dev_ptr(g), 1.0, N.dev_ptr(tmp), 1.0, N.dev_ptr(g), g.numel(), N.stream())
+    nburst = _HOLD['burst'] if not _WRED['on'] else 1
+    streams = [cur]
+    if nburst > 1:   # the merged launches are independent (one .grad each): spread them round-robin over streams
+        pool = _HOLD['streams'].setdefault(cur.device, [])
+        while len(pool) < nburst - 1:
+            pool.append(torch.cuda.Stream(device=cur.device))
+        for sd in pool[:nburst - 1]:
+            sd.wait_stream(cur)
+            streams.append(sd)
+    first = {}
     with batched_wgrad_reduce():
         with defer_wgrad():
             for tag, mod, args, kw in calls:
                 if tag == order[0]:
+                    first[id(mod)] = args
                     mod._ssseg_wgrad(*args, **kw)
+        k = 0
         for tag, mod, args, kw in calls:
             if tag == order[1]:
-                mod._ssseg_wgrad(*args, **kw)
+                sd = streams[k % len(streams)]
+                k += 1
+                if sd is not cur:
+                    for t in list(args) + list(first.get(id(mod), ())):
+                        if isinstance(t, torch.Tensor) and t.is_cuda:
+                            t.record_stream(sd)
+                            vc = _vcat_of(t)
+                            if vc is not None:
+                                vc.a.record_stream(sd)
+                                vc.b.record_stream(sd)
+                with torch.cuda.stream(sd):
+                    mod._ssseg_wgrad(*args, **kw)
         flush_wgrad()
+    for sd in streams[1:]:
+        cur.wait_stream(sd)
 
 
 # ---- deferred BN parameter gradients of the differentiated eval pass ---------------------------------------------------

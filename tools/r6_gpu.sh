@@ -99,5 +99,13 @@ case "$1" in
   wred4) bash tools/gpu_steps.sh \
     "400 r6_wred4_1 env SSSEG_WGRAD_BATCH_REDUCE=1 python tools/full_size_steps.py --configs c4,c5 --graph" \
     "400 r6_wred4_0 python tools/full_size_steps.py --configs c4,c5 --graph" ;;
-  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3|events|order|gq|gb|io|fe|seg|mw|wred4"; exit 2 ;;
+  burst) bash tools/gpu_steps.sh \
+    "600 r6_burst_tests env SSSEG_WGRAD_BURST=2 python -u -m pytest -q -x --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_graph.py tests/test_overlap.py tests/test_determinism.py" \
+    "200 r6_burst_2 env SSSEG_WGRAD_BURST=2 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_burst_1 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_burst_3 env SSSEG_WGRAD_BURST=3 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_burst_2b env SSSEG_WGRAD_BURST=2 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_burst_1b python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_burst_3b env SSSEG_WGRAD_BURST=3 python bench.py --no-cpu-baseline --no-fp32" ;;
+  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3|events|order|gq|gb|io|fe|seg|mw|wred4|burst"; exit 2 ;;
 esac
