@@ -107,5 +107,22 @@ case "$1" in
     "200 r6_burst_2b env SSSEG_WGRAD_BURST=2 python bench.py --no-cpu-baseline --no-fp32" \
     "200 r6_burst_1b python bench.py --no-cpu-baseline --no-fp32" \
     "200 r6_burst_3b env SSSEG_WGRAD_BURST=3 python bench.py --no-cpu-baseline --no-fp32" ;;
-  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3|events|order|gq|gb|io|fe|seg|mw|wred4|burst"; exit 2 ;;
+  knobs) bash tools/gpu_steps.sh \
+    "200 r6_kn_base python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_kn_kernarg env HIP_FORCE_DEV_KERNARG=1 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_kn_reps env SSSEG_TUNE_REPS=12 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_kn_w75 env SSSEG_KNOBS=10=75 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_kn_w150 env SSSEG_KNOBS=10=150 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_kn_base2 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_kn_kernarg2 env HIP_FORCE_DEV_KERNARG=0 python bench.py --no-cpu-baseline --no-fp32" ;;
+  reps) bash tools/gpu_steps.sh \
+    "200 r6_rp_12 env SSSEG_TUNE_REPS=12 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_rp_5 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_rp_24 env SSSEG_TUNE_REPS=24 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_rp_12b env SSSEG_TUNE_REPS=12 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_rp_5b python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_rp_24b env SSSEG_TUNE_REPS=24 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_rp_5c python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_rp_12c env SSSEG_TUNE_REPS=12 python bench.py --no-cpu-baseline --no-fp32" ;;
+  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3|events|order|gq|gb|io|fe|seg|mw|wred4|burst|knobs|reps"; exit 2 ;;
 esac
