@@ -124,5 +124,22 @@ case "$1" in
     "200 r6_rp_24b env SSSEG_TUNE_REPS=24 python bench.py --no-cpu-baseline --no-fp32" \
     "200 r6_rp_5c python bench.py --no-cpu-baseline --no-fp32" \
     "200 r6_rp_12c env SSSEG_TUNE_REPS=12 python bench.py --no-cpu-baseline --no-fp32" ;;
-  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3|events|order|gq|gb|io|fe|seg|mw|wred4|burst|knobs|reps"; exit 2 ;;
+  knobs2) bash tools/gpu_steps.sh \
+    "200 r6_k2_base python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_k2_k14off env SSSEG_KNOBS=14=-1 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_k2_k16 env SSSEG_KNOBS=16=-1 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_k2_k15 env SSSEG_KNOBS=15=-1 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_k2_cbwd0 env SSSEG_OVERLAP_CONSISTENCY_BWD=0 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_k2_gstat0 env SSSEG_BN_GSTAT=0 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_k2_base2 python bench.py --no-cpu-baseline --no-fp32" ;;
+  cbwd) bash tools/gpu_steps.sh \
+    "200 r6_cb_0a env SSSEG_OVERLAP_CONSISTENCY_BWD=0 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_cb_1a python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_cb_0b env SSSEG_OVERLAP_CONSISTENCY_BWD=0 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_cb_1b python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_cb_0c env SSSEG_OVERLAP_CONSISTENCY_BWD=0 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_cb_1c python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_cb_0d env SSSEG_OVERLAP_CONSISTENCY_BWD=0 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_cb_1d python bench.py --no-cpu-baseline --no-fp32" ;;
+  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3|events|order|gq|gb|io|fe|seg|mw|wred4|burst|knobs|reps|knobs2|cbwd"; exit 2 ;;
 esac
