@@ -406,8 +406,7 @@ size_t ssseg_conv_igemm_workspace_bytes(const ssseg_conv_desc* desc_host, int dt
  * knob 12: fused-statistics experiment switch (0 = normal); knob 13: pointwise kernels (0 = on, -1 = off);
  * knob 14: deterministic split-K of the LDS-DMA configs (0 = the geometry rule, default; -1 = off; 2 / 4 / 8 = forced S);
  * knob 15: the single-buffered two-blocks-per-CU halo conv, variant 28 (0 = on, -1 = off);
- * knob 16: the halo convs' 32- and 16-wide tiles on 32^2 / 16^2 maps (0 = on, -1 = 64-wide tiles only);
- * knob 17: the row-walking image-input stem kernel (0 = on, default; -1 = one output row per block).
+ * knob 16: the halo convs' 32- and 16-wide tiles on 32^2 / 16^2 maps (0 = on, -1 = 64-wide tiles only).
  * Forward variants never change results; the
  * weight-gradient knobs change the fp32 summation order of dW.  Not thread-safe. */
 int ssseg_set_knob(int id, int value);

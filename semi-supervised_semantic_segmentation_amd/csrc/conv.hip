@@ -7,7 +7,7 @@
 
 #include "conv_kernels.h"
 
-int g_knobs[18] = {0, -1, 0, 0, 0, 1, 0, 0, 0, 0, 100, 0, 0, 0, 0, 0, 0, -1};   // runtime variant switches (ssseg_set_knob)
+int g_knobs[17] = {0, -1, 0, 0, 0, 1, 0, 0, 0, 0, 100, 0, 0, 0, 0, 0, 0};   // runtime variant switches (ssseg_set_knob)
 // (knob 1, the register-staged kernel's fp32-atomic split-K, stays off: measured a net loss on the C2 step (r2u) and its
 // sums are order-dependent; knob 14 is the deterministic split-K of the LDS-DMA configs)
 thread_local int t_dsplit = 1;
@@ -449,7 +449,7 @@ bool geom_ok(const ConvGeom& g, int dt) {
 }  // namespace
 
 extern "C" int ssseg_set_knob(int id, int value) {
-  if (id < 0 || id >= 18) return SSSEG_EINVAL;
+  if (id < 0 || id >= 17) return SSSEG_EINVAL;
   if (id == 6 && value) {
     std::lock_guard<std::mutex> lk(g_variant_mu);
     g_variant.clear();

@@ -110,145 +110,8 @@ __global__ void __launch_bounds__(256) stem_conv_kernel(const T16* __restrict__ 
   store_tile_lds<T16, BM, BN, FM, FN, 256, STATS>(acc, smem, m0, n0, wave * (FM * 16), 0, lane, g, y, ep);
 }
 
-// Row-walking form (round 6, the default; knob 17 = -1 selects the kernel above): a block stages the weights once and
-// walks STEM_ROWS consecutive output rows of its 128-pixel column segment, keeping the R image rows of the current
-// output row in an LDS ring (slot = local row % R) and loading only the sy new rows per step -- issued before the
-// previous row's epilogue, so they are in flight while it stores.  The one-row kernel staged the 28 KB of weights
-// and a 7 x 262-pixel patch for every 128 x 64 output tile (~355 MB of L2 -> LDS traffic per bs-16 forward against a
-// 134 MB output).  Each row is the same tile with the same MFMA sequence and epilogue as the one-row kernel: results
-// bitwise equal (tests/test_hip_layers.py).
-constexpr int STEM_ROWS = 8;
-
-template <typename T16, int R, bool STATS>
-__global__ void __launch_bounds__(256) stem_rows_kernel(const T16* __restrict__ x, const T16* __restrict__ w4,
-                                                        T16* __restrict__ y, ConvGeom g, Epi<T16> ep, int rblocks) {
-  constexpr int FM = STEM_FM, FN = STEM_FN, BM = STEM_BM, BN = STEM_BN;
-  constexpr int BSZ = BN * R * 32 * 2;                       // weights [BN][R][32], bytes
-  constexpr int PSZ = R * STEM_PW * 8;                       // image ring [R][PW] x 8 bytes
-  constexpr int ESZ = BM * (BN * 4 + 16);                    // staged epilogue (store_tile_lds)
-  __shared__ __attribute__((aligned(16))) char smem[BSZ + PSZ + ESZ];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int n0 = blockIdx.y * BN;
-  const int cblocks = g.OW / BM;
-  const int cb = blockIdx.x % cblocks;
-  const int rb = (blockIdx.x / cblocks) % rblocks;
-  const int img = blockIdx.x / (cblocks * rblocks);
-  const int ox0 = cb * BM, oy0 = rb * STEM_ROWS;
-  const int nrows = min(STEM_ROWS, g.OH - oy0);
-  const int gq = lane >> 4, li = lane & 15;
-  const int iy00 = oy0 * g.sy + g.py, ix0 = ox0 * g.sx + g.px;   // py, px: minus the padding
-  const int pw = (BM - 1) * g.sx + g.S;                      // columns actually used
-  uint2* P = (uint2*)(smem + BSZ);
-  char* E = smem + BSZ + PSZ;
-  constexpr int KR = (STEM_PW + 255) / 256;                  // ring pixels per thread and image row
-
-  // local image row lr (input row iy00 + lr) into ring slot lr % R: loads in registers first, LDS writes after
-  auto load_row = [&](int lr, uint2 (&v)[KR]) {
-    const int iy = iy00 + lr;
-#pragma unroll
-    for (int k = 0; k < KR; ++k) {
-      const int c = t + 256 * k, ix = ix0 + c;
-      const bool ok = c < pw && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
-      const long long off = ok ? (((long long)img * g.H + iy) * g.W + ix) * g.ldx : 0;
-      v[k] = *(const uint2*)(x + off);
-      if (!ok) v[k] = make_uint2(0u, 0u);
-    }
-  };
-  auto put_row = [&](int lr, const uint2 (&v)[KR]) {
-#pragma unroll
-    for (int k = 0; k < KR; ++k) {
-      const int c = t + 256 * k;
-      if (c < pw) P[(lr % R) * STEM_PW + c] = v[k];
-    }
-  };
-
-  // weights and the first R image rows
-  constexpr int KW = (BN * R * 8 + 255) / 256;               // weight 8-byte slots per thread ([BN][R][8] slots)
-  const int SK = g.S * 4;
-  const unsigned short* wsrc = (const unsigned short*)w4;
-  uint2 wv[KW];
-#pragma unroll
-  for (int k = 0; k < KW; ++k) {
-    const int i = t + 256 * k;
-    const int q = i & 7, r = (i >> 3) % R, nn = (i >> 3) / R;
-    const int n = n0 + nn;
-    const bool v = i < BN * R * 8 && n < g.K && q < g.S;
-    wv[k] = v ? *(const uint2*)(wsrc + ((long long)n * R + r) * SK + 4 * q) : make_uint2(0u, 0u);
-  }
-  {
-    uint2 rv[R][KR];
-#pragma unroll
-    for (int r = 0; r < R; ++r) load_row(r, rv[r]);
-#pragma unroll
-    for (int r = 0; r < R; ++r) put_row(r, rv[r]);
-  }
-  uint2* B8 = (uint2*)smem;
-#pragma unroll
-  for (int k = 0; k < KW; ++k) {
-    const int i = t + 256 * k;
-    if (i < BN * R * 8) B8[i] = wv[k];
-  }
-  __syncthreads();
-  const unsigned short* Bs = (const unsigned short*)smem;
-  const bool h0 = 2 * gq < g.S, h1 = 2 * gq + 1 < g.S;
-
-  for (int j = 0; j < nrows; ++j) {
-    f32x4 acc[FN][FM];
-#pragma unroll
-    for (int i = 0; i < FN; ++i)
-#pragma unroll
-      for (int jj = 0; jj < FM; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int slot = (j * g.sy + r) % R;
-      bf16x8 af[FN], bfr[FM];
-#pragma unroll
-      for (int i = 0; i < FN; ++i) af[i] = *(const bf16x8*)(Bs + ((i * 16 + li) * R + r) * 32 + 8 * gq);
-#pragma unroll
-      for (int jj = 0; jj < FM; ++jj) {
-        const int c = (wave * (FM * 16) + jj * 16 + li) * g.sx + 2 * gq;   // ring column of tap 2gq
-        const uint2 lo = h0 ? P[slot * STEM_PW + c] : make_uint2(0u, 0u);
-        const uint2 hi = h1 ? P[slot * STEM_PW + c + 1] : make_uint2(0u, 0u);
-        bfr[jj] = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
-      }
-#pragma unroll
-      for (int i = 0; i < FN; ++i)
-#pragma unroll
-        for (int jj = 0; jj < FM; ++jj) acc[i][jj] = M16<T16>::mma(af[i], bfr[jj], acc[i][jj]);
-    }
-    // the next output row's new image rows: loads in flight during this row's epilogue (its first barrier also
-    // ends every wave's ring reads of this row, so the slots they replace are free once it returns)
-    const bool more = j + 1 < nrows;
-    uint2 nv[2][KR];
-    if (more) {
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-        if (q < g.sy) load_row((j + 1) * g.sy + R - g.sy + q, nv[q]);
-    }
-    const long long m0 = ((long long)img * g.OH + oy0 + j) * g.OW + ox0;
-    store_tile_lds<T16, BM, BN, FM, FN, 256, STATS>(acc, E, m0, n0, wave * (FM * 16), 0, lane, g, y, ep);
-    if (more) {
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-        if (q < g.sy) put_row((j + 1) * g.sy + R - g.sy + q, nv[q]);
-      __syncthreads();
-    }
-  }
-}
-
 template <typename T16, int R>
 void launch_stem(const void* x, const void* w4, void* y, const ConvGeom& g, const Epi<T16>& ep, hipStream_t s) {
-  if (g_knobs[17] == 0 && g.sy <= 2 && g.sy <= R) {
-    const int rblocks = (int)((g.OH + STEM_ROWS - 1) / STEM_ROWS);
-    const dim3 grid((unsigned)(g.N * rblocks * (g.OW / STEM_BM)), (unsigned)((g.K + STEM_BN - 1) / STEM_BN));
-    if (ep.stats)
-      hipLaunchKernelGGL((stem_rows_kernel<T16, R, true>), grid, dim3(256), 0, s, (const T16*)x, (const T16*)w4,
-                         (T16*)y, g, ep, rblocks);
-    else
-      hipLaunchKernelGGL((stem_rows_kernel<T16, R, false>), grid, dim3(256), 0, s, (const T16*)x, (const T16*)w4,
-                         (T16*)y, g, ep, rblocks);
-    return;
-  }
   const dim3 grid((unsigned)(g.M / STEM_BM), (unsigned)((g.K + STEM_BN - 1) / STEM_BN));
   if (ep.stats)
     hipLaunchKernelGGL((stem_conv_kernel<T16, R, true>), grid, dim3(256), 0, s, (const T16*)x, (const T16*)w4, (T16*)y,

@@ -833,49 +833,6 @@ def test_stem_conv_kernel(hip_device, dtype, k, s, H, W):
     del tol
 
 
-_STEM_ROWS_DEFAULT = -1   # knob 17's default in csrc/conv.hip
-
-
-@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("k,s,H,W", [(7, 2, 38, 256), (3, 2, 33, 512), (7, 1, 17, 128), (7, 2, 64, 256)])
-def test_stem_rows_kernel_bitwise(hip_device, dtype, k, s, H, W):
-    """The row-walking stem kernel (default; a block walks 8 output rows with an LDS ring of image rows) against the
-    one-row kernel (knob 17 = -1): the same tiles, MFMA sequence and epilogue, so every output -- plain, training BN
-    with fused statistics (and the running mean they produce), the eval BN's raw copy and its weight gradient -- is
-    bitwise equal; output heights not a multiple of 8 exercise the last row block."""
-    from ssseg import native as N
-    from ssseg import nn as snn
-    snn.set_compute_dtype(dtype)
-    try:
-        torch.manual_seed(5)
-        conv = snn.Conv2d(3, 64, k, s, k // 2, bias=False).to(hip_device)
-        bn = snn.BatchNorm2d(64).to(hip_device)
-        with torch.no_grad():
-            bn.weight.uniform_(0.5, 1.5)
-            bn.bias.uniform_(-0.2, 0.2)
-        xa = _act_in(torch.rand(3, 3, H, W), hip_device)
-        outs = {}
-        for knob in (-1, 0):
-            N.call('ssseg_set_knob', 17, knob)
-            with torch.no_grad():
-                y0 = conv(xa)
-                bn.train()
-                bn.reset_running_stats()
-                y1 = snn.conv_bn_act(conv, xa, bn, relu=True)
-                rm, rv = bn.running_mean.clone(), bn.running_var.clone()
-                bn.eval()
-            conv.weight.grad = None
-            y2 = snn.conv_bn_act(conv, xa.detach().clone(), bn, relu=True)
-            y2.backward(torch.ones_like(y2))
-            torch.cuda.synchronize()
-            outs[knob] = [t.detach().cpu().clone() for t in (y0, y1, rm, rv, y2, conv.weight.grad)]
-        for name, a, b in zip(('conv', 'train-bn', 'running_mean', 'running_var', 'eval-bn', 'dW'), outs[-1], outs[0]):
-            assert torch.equal(a, b), name
-    finally:
-        N.call('ssseg_set_knob', 17, _STEM_ROWS_DEFAULT)
-        snn.set_compute_dtype(torch.bfloat16)
-
-
 @pytest.mark.parametrize('cin,cout,H', [(256, 128, 8), (128, 64, 13), (64, 40, 6)])
 def test_convT_phase_launch_bitwise(hip_device, cin, cout, H):
     """ConvTranspose2d(4,2,1) forward as ONE launch over its four output phases (ssseg_conv_igemm_phases) vs one

@@ -141,13 +141,5 @@ case "$1" in
     "200 r6_cb_1c python bench.py --no-cpu-baseline --no-fp32" \
     "200 r6_cb_0d env SSSEG_OVERLAP_CONSISTENCY_BWD=0 python bench.py --no-cpu-baseline --no-fp32" \
     "200 r6_cb_1d python bench.py --no-cpu-baseline --no-fp32" ;;
-  rows) bash tools/gpu_steps.sh \
-    "300 r6_rows_tests python -u -m pytest -q -x --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_hip_layers.py -k stem" \
-    "200 r6_rows_stem1 env SSSEG_KNOBS=17=0 python tools/bench_stem.py" \
-    "200 r6_rows_stem0 env SSSEG_KNOBS=17=-1 python tools/bench_stem.py" \
-    "200 r6_rows_b1 env SSSEG_KNOBS=17=0 python bench.py --no-cpu-baseline --no-fp32" \
-    "200 r6_rows_b0 env SSSEG_KNOBS=17=-1 python bench.py --no-cpu-baseline --no-fp32" \
-    "200 r6_rows_b1b env SSSEG_KNOBS=17=0 python bench.py --no-cpu-baseline --no-fp32" \
-    "200 r6_rows_b0b env SSSEG_KNOBS=17=-1 python bench.py --no-cpu-baseline --no-fp32" ;;
-  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3|events|order|gq|gb|io|fe|seg|mw|wred4|burst|knobs|reps|knobs2|cbwd|rows"; exit 2 ;;
+  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3|events|order|gq|gb|io|fe|seg|mw|wred4|burst|knobs|reps|knobs2|cbwd"; exit 2 ;;
 esac
