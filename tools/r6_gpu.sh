@@ -2,6 +2,8 @@
 # Round-6 GPU evidence, in parts that each fit one gpurun call (tools/gpu_steps.sh: every step under its own limit,
 # stop at the first fault / time limit).
 #   bash tools/r6_gpu.sh tests | full | bench | pmc
+# Phases order / io / fe / seg / rows ran experiments whose code was removed after measuring (DESIGN.md §7 rows r6g and
+# 'Measured and rejected in round 6'); their env switches no longer exist, so they now time the default build.
 case "$1" in
   tests) bash tools/gpu_steps.sh \
     "900 r6_gputests python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider" \
