@@ -2,7 +2,7 @@
 # Round-6 GPU evidence, in parts that each fit one gpurun call (tools/gpu_steps.sh: every step under its own limit,
 # stop at the first fault / time limit).
 #   bash tools/r6_gpu.sh tests | full | bench | pmc
-# Phases order / io / fe / seg / rows ran experiments whose code was removed after measuring (DESIGN.md §7 rows r6g and
+# Phases order / io / fe / seg ran experiments whose code was removed after measuring (DESIGN.md §7 rows r6g and
 # 'Measured and rejected in round 6'); their env switches no longer exist, so they now time the default build.
 case "$1" in
   tests) bash tools/gpu_steps.sh \
@@ -143,5 +143,11 @@ case "$1" in
     "200 r6_cb_1c python bench.py --no-cpu-baseline --no-fp32" \
     "200 r6_cb_0d env SSSEG_OVERLAP_CONSISTENCY_BWD=0 python bench.py --no-cpu-baseline --no-fp32" \
     "200 r6_cb_1d python bench.py --no-cpu-baseline --no-fp32" ;;
-  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3|events|order|gq|gb|io|fe|seg|mw|wred4|burst|knobs|reps|knobs2|cbwd"; exit 2 ;;
+  hwq) bash tools/gpu_steps.sh \
+    "200 r6_hq_8 env GPU_MAX_HW_QUEUES=8 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_hq_d python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_hq_2 env GPU_MAX_HW_QUEUES=2 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_hq_8b env GPU_MAX_HW_QUEUES=8 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_hq_db python bench.py --no-cpu-baseline --no-fp32" ;;
+  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3|events|order|gq|gb|io|fe|seg|mw|wred4|burst|knobs|reps|knobs2|cbwd|hwq"; exit 2 ;;
 esac
