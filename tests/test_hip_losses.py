@@ -75,6 +75,21 @@ def test_bilinear_fwd_bwd(hip_device, shape, size, ac):
                                rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize('ac', [False, True])
+@pytest.mark.parametrize('fmt,dt', [(torch.contiguous_format, torch.float32), (torch.channels_last, torch.bfloat16)])
+def test_bilinear_identity_size_is_the_input(hip_device, ac, fmt, dt):
+    """At the input's own size interpolate_bilinear returns the input (PyTorch's CPU kernels copy there): the kernel's
+    (1, 0) weights reproduce the finite values bit for bit, and the gradient passes straight through."""
+    o = ops()
+    x = torch.randn(2, 3, 24, 40, device=hip_device).to(dt).contiguous(memory_format=fmt).requires_grad_(True)
+    y = o.interpolate_bilinear(x, (24, 40), align_corners=ac)
+    assert y is x
+    yk = o._Bilinear.apply(x.detach(), (24, 40), ac)   # the kernel at identity size
+    assert torch.equal(yk, x.detach())
+    ref = torch.nn.functional.interpolate(x.detach().float().cpu(), size=(24, 40), mode='bilinear', align_corners=ac)
+    assert torch.equal(ref, x.detach().float().cpu())
+
+
 def test_bilinear_channels_last_bf16(hip_device):
     x = torch.randn(2, 8, 16, 16, device=hip_device).to(memory_format=torch.channels_last)
     y32 = ops().interpolate_bilinear(x, (32, 32), True)

@@ -149,5 +149,10 @@ case "$1" in
     "200 r6_hq_2 env GPU_MAX_HW_QUEUES=2 python bench.py --no-cpu-baseline --no-fp32" \
     "200 r6_hq_8b env GPU_MAX_HW_QUEUES=8 python bench.py --no-cpu-baseline --no-fp32" \
     "200 r6_hq_db python bench.py --no-cpu-baseline --no-fp32" ;;
-  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3|events|order|gq|gb|io|fe|seg|mw|wred4|burst|knobs|reps|knobs2|cbwd|hwq"; exit 2 ;;
+  ident) bash tools/gpu_steps.sh \
+    "200 r6_id_1 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_id_0 env SSSEG_BILINEAR_IDENTITY=0 python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_id_1b python bench.py --no-cpu-baseline --no-fp32" \
+    "200 r6_id_0b env SSSEG_BILINEAR_IDENTITY=0 python bench.py --no-cpu-baseline --no-fp32" ;;
+  *) echo "usage: $0 tests|full|bench|quick|fix|study|probe|diag|wred|stem|pmc|full3|events|order|gq|gb|io|fe|seg|mw|wred4|burst|knobs|reps|knobs2|cbwd|hwq|ident"; exit 2 ;;
 esac
